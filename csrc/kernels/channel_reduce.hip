@@ -1,0 +1,162 @@
+// Per-(sample, channel) attribution reductions and score accumulators.
+//
+// The reference computes every score in a module hook with a chain of ATen ops
+// followed by `.detach().cpu().numpy()` and `np.concatenate` on every batch
+// (apoz.py:31-38, sensitivity.py:27-33, taylor.py:40-48). Here a single pass reads the
+// activation and/or gradient once, produces the (B, C) per-sample score slab on device,
+// and a second deterministic column pass folds it into fp64 running sums. There is no
+// host sync per batch and no float atomics (bit-reproducible results).
+#include "tp_common.h"
+
+namespace tp {
+
+enum ReduceMode : int { TAYLOR_ABS = 0, TAYLOR_SIGNED = 1, SENS_ABS = 2, APOZ_POS = 3, SUM_GRAD = 4 };
+
+template <int MODE>
+__device__ __forceinline__ float elem(float a, float g) {
+  if constexpr (MODE == TAYLOR_ABS || MODE == TAYLOR_SIGNED) return -(g * a);
+  else if constexpr (MODE == SENS_ABS) return fabsf(g);
+  else if constexpr (MODE == APOZ_POS) return a > 0.f ? 1.f : 0.f;
+  else return g;
+}
+
+template <int MODE>
+__device__ __forceinline__ float finish(float v) {
+  if constexpr (MODE == TAYLOR_ABS) return fabsf(v);
+  else return v;
+}
+
+// NCHW (rows = B*C, each row S contiguous floats). LPR lanes cooperate on one row.
+template <int MODE, int LPR, bool VEC>
+__global__ __launch_bounds__(256) void channel_reduce_nchw(const float* __restrict__ act,
+                                                           const float* __restrict__ grad,
+                                                           float* __restrict__ out, long long rows,
+                                                           int S) {
+  long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long row = gtid / LPR;
+  int lr = (int)(gtid % LPR);
+  float acc = 0.f;
+  if (row < rows) {
+    if constexpr (VEC) {
+      const int S4 = S >> 2;
+      const float4* a4 = reinterpret_cast<const float4*>(act ? act + row * S : nullptr);
+      const float4* g4 = reinterpret_cast<const float4*>(grad ? grad + row * S : nullptr);
+      for (int s = lr; s < S4; s += LPR) {
+        float4 av = make_float4(0.f, 0.f, 0.f, 0.f), gv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (MODE != SENS_ABS && MODE != SUM_GRAD) av = a4[s];
+        if constexpr (MODE != APOZ_POS) gv = g4[s];
+        acc += elem<MODE>(av.x, gv.x) + elem<MODE>(av.y, gv.y) + elem<MODE>(av.z, gv.z) +
+               elem<MODE>(av.w, gv.w);
+      }
+    } else {
+      const float* a = act ? act + row * S : nullptr;
+      const float* g = grad ? grad + row * S : nullptr;
+      for (int s = lr; s < S; s += LPR) {
+        float av = 0.f, gv = 0.f;
+        if constexpr (MODE != SENS_ABS && MODE != SUM_GRAD) av = a[s];
+        if constexpr (MODE != APOZ_POS) gv = g[s];
+        acc += elem<MODE>(av, gv);
+      }
+    }
+  }
+  if constexpr (LPR > 1) acc = group_sum<LPR>(acc);
+  if (row < rows && lr == 0) out[row] = finish<MODE>(acc);
+}
+
+// NHWC / channels_last (b, s, c): a block owns (b, 64-channel tile); 4 waves split s.
+template <int MODE>
+__global__ __launch_bounds__(256) void channel_reduce_nhwc(const float* __restrict__ act,
+                                                           const float* __restrict__ grad,
+                                                           float* __restrict__ out, int C, int S) {
+  __shared__ float part[4][64];
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sg = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < C) {
+    const long long base = (long long)b * S * C + c;
+    for (int s = sg; s < S; s += 4) {
+      float av = 0.f, gv = 0.f;
+      if constexpr (MODE != SENS_ABS && MODE != SUM_GRAD) av = act[base + (long long)s * C];
+      if constexpr (MODE != APOZ_POS) gv = grad[base + (long long)s * C];
+      acc += elem<MODE>(av, gv);
+    }
+  }
+  part[sg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (sg == 0 && c < C) {
+    float v = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+    out[(long long)b * C + c] = finish<MODE>(v);
+  }
+}
+
+template <int MODE>
+static hipError_t launch_reduce(const float* act, const float* grad, float* out, int B, int C, int S,
+                                int channels_last, hipStream_t st) {
+  if (channels_last) {
+    dim3 grid(ceil_div(C, 64), B);
+    channel_reduce_nhwc<MODE><<<grid, 256, 0, st>>>(act, grad, out, C, S);
+    return hipGetLastError();
+  }
+  long long rows = (long long)B * C;
+  const bool vec = (S % 4 == 0) && ((((uintptr_t)act) | ((uintptr_t)grad)) % 16 == 0);
+  const int Se = vec ? S / 4 : S;
+  int lpr = Se >= 64 ? 64 : (Se >= 16 ? 16 : (Se >= 4 ? 4 : 1));
+  long long threads = rows * lpr;
+  unsigned grid = ceil_div(threads, 256);
+#define TP_L(L)                                                                           \
+  if (lpr == L) {                                                                         \
+    if (vec) channel_reduce_nchw<MODE, L, true><<<grid, 256, 0, st>>>(act, grad, out, rows, S); \
+    else channel_reduce_nchw<MODE, L, false><<<grid, 256, 0, st>>>(act, grad, out, rows, S);   \
+  }
+  TP_L(64) TP_L(16) TP_L(4) TP_L(1)
+#undef TP_L
+  return hipGetLastError();
+}
+
+// acc_sum[c] += sum_b v[b, c] (and acc_sq[c] += v^2) in fp64, fixed summation order.
+__global__ __launch_bounds__(256) void column_accumulate(const float* __restrict__ v,
+                                                         double* __restrict__ acc_sum,
+                                                         double* __restrict__ acc_sq, int B, int C) {
+  __shared__ double ps[4][64];
+  __shared__ double pq[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int b = rg; b < B; b += 4) {
+      double x = (double)v[(long long)b * C + c];
+      s += x;
+      q += x * x;
+    }
+  }
+  ps[rg][threadIdx.x & 63] = s;
+  pq[rg][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    acc_sum[c] += ps[0][threadIdx.x] + ps[1][threadIdx.x] + ps[2][threadIdx.x] + ps[3][threadIdx.x];
+    if (acc_sq)
+      acc_sq[c] += pq[0][threadIdx.x] + pq[1][threadIdx.x] + pq[2][threadIdx.x] + pq[3][threadIdx.x];
+  }
+}
+
+}  // namespace tp
+
+extern "C" hipError_t tp_channel_reduce(const float* act, const float* grad, float* out, int B, int C,
+                                        int S, int mode, int channels_last, hipStream_t st) {
+  using namespace tp;
+  switch (mode) {
+    case TAYLOR_ABS: return launch_reduce<TAYLOR_ABS>(act, grad, out, B, C, S, channels_last, st);
+    case TAYLOR_SIGNED: return launch_reduce<TAYLOR_SIGNED>(act, grad, out, B, C, S, channels_last, st);
+    case SENS_ABS: return launch_reduce<SENS_ABS>(act, grad, out, B, C, S, channels_last, st);
+    case APOZ_POS: return launch_reduce<APOZ_POS>(act, grad, out, B, C, S, channels_last, st);
+    case SUM_GRAD: return launch_reduce<SUM_GRAD>(act, grad, out, B, C, S, channels_last, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+extern "C" hipError_t tp_column_accumulate(const float* v, double* acc_sum, double* acc_sq, int B, int C,
+                                           hipStream_t st) {
+  tp::column_accumulate<<<tp::ceil_div(C, 64), 256, 0, st>>>(v, acc_sum, acc_sq, B, C);
+  return hipGetLastError();
+}

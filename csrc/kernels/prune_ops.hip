@@ -1,0 +1,111 @@
+// Pruner kernels.
+//
+// * channel_fill   — `index_fill_(1, idx, value)` used by the NaN probe (pruner.py:138-142)
+//                    and by simulated-pruning ablations (nbVGG:1276).
+// * nan_channels   — "which channels of this activation carry a NaN" (pruner.py:158-162),
+//                    producing a per-channel flag vector in a single pass.
+// * gather_multi   — one launch slicing up to 8 tensors {param, grad, optimizer states}
+//                    along an axis with a shared keep-index list (pruner.py:106-112,
+//                    opt_pruner.py:17-19 issue one ATen index_select per tensor).
+#include "tp_common.h"
+
+namespace tp {
+
+__global__ void channel_fill(float* __restrict__ x, long long B, int C, long long S,
+                             const int64_t* __restrict__ idx, int nidx, float value) {
+  long long total = B * nidx * S;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    long long s = t % S;
+    long long r = t / S;
+    int i = (int)(r % nidx);
+    long long b = r / nidx;
+    x[(b * C + idx[i]) * S + s] = value;
+  }
+}
+
+// flags[c] = 1 if any x[b, c, s] is NaN. One block per channel.
+__global__ __launch_bounds__(256) void nan_channels(const float* __restrict__ x, long long B, int C,
+                                                   long long S, uint8_t* __restrict__ flags) {
+  const int c = blockIdx.x;
+  int found = 0;
+  for (long long t = threadIdx.x; t < B * S; t += blockDim.x) {
+    long long b = t / S, s = t % S;
+    float v = x[(b * C + c) * S + s];
+    found |= (v != v);
+  }
+  found = __syncthreads_or(found);
+  if (threadIdx.x == 0) flags[c] = (uint8_t)(found ? 1 : 0);
+}
+
+struct GatherDesc {
+  const void* src;
+  void* dst;
+  long long outer;
+  long long n;      // source extent along the sliced axis
+  long long inner;  // elements after the axis
+};
+
+struct GatherBatch {
+  GatherDesc d[8];
+  int count;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void gather_multi(GatherBatch batch, const int64_t* __restrict__ keep,
+                                                    long long nkeep) {
+  const GatherDesc g = batch.d[blockIdx.y];
+  const T* __restrict__ src = reinterpret_cast<const T*>(g.src);
+  T* __restrict__ dst = reinterpret_cast<T*>(g.dst);
+  const long long total = g.outer * nkeep * g.inner;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    long long i = t % g.inner;
+    long long r = t / g.inner;
+    long long j = r % nkeep;
+    long long o = r / nkeep;
+    dst[t] = src[(o * g.n + keep[j]) * g.inner + i];
+  }
+}
+
+}  // namespace tp
+
+extern "C" hipError_t tp_channel_fill(float* x, long long B, int C, long long S, const int64_t* idx,
+                                      int nidx, float value, hipStream_t st) {
+  long long total = B * nidx * S;
+  if (total == 0) return hipSuccess;
+  unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 4096);
+  tp::channel_fill<<<grid, 256, 0, st>>>(x, B, C, S, idx, nidx, value);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_nan_channels(const float* x, long long B, int C, long long S, uint8_t* flags,
+                                      hipStream_t st) {
+  if (C == 0) return hipSuccess;
+  tp::nan_channels<<<C, 256, 0, st>>>(x, B, C, S, flags);
+  return hipGetLastError();
+}
+
+// srcs/dsts/outer/n/inner arrays of length count (<= 8); elsize in {1,2,4,8} bytes.
+extern "C" hipError_t tp_gather_multi(const void* const* srcs, void* const* dsts, const long long* outer,
+                                      const long long* n, const long long* inner, int count, int elsize,
+                                      const int64_t* keep, long long nkeep, hipStream_t st) {
+  if (count <= 0 || count > 8) return hipErrorInvalidValue;
+  tp::GatherBatch b{};
+  b.count = count;
+  long long maxtot = 0;
+  for (int i = 0; i < count; ++i) {
+    b.d[i] = tp::GatherDesc{srcs[i], dsts[i], outer[i], n[i], inner[i]};
+    maxtot = std::max(maxtot, outer[i] * nkeep * inner[i]);
+  }
+  if (maxtot == 0) return hipSuccess;
+  dim3 grid((unsigned)std::min<long long>(tp::ceil_div(maxtot, 256), 2048), count);
+  switch (elsize) {
+    case 1: tp::gather_multi<uint8_t><<<grid, 256, 0, st>>>(b, keep, nkeep); break;
+    case 2: tp::gather_multi<uint16_t><<<grid, 256, 0, st>>>(b, keep, nkeep); break;
+    case 4: tp::gather_multi<uint32_t><<<grid, 256, 0, st>>>(b, keep, nkeep); break;
+    case 8: tp::gather_multi<uint64_t><<<grid, 256, 0, st>>>(b, keep, nkeep); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}

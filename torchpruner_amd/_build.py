@@ -1,0 +1,120 @@
+"""In-tree native build for the MI355X (gfx950) extension ``torchpruner_amd/_C.so``.
+
+Design
+------
+* Every ``csrc/kernels/*.hip`` file is plain HIP (no torch headers) and is compiled
+  with ``hipcc --offload-arch=gfx950`` into an object file. Kernel files export
+  host-side launcher functions that take raw device pointers + a ``hipStream_t``.
+* ``csrc/bindings.cpp`` is the only translation unit that includes torch. It
+  validates tensors (device / dtype / contiguity / shape — ops fail loudly on a
+  mismatch) and registers the ``torch.ops.tpamd.*`` operators with
+  ``TORCH_LIBRARY``.
+* Everything is linked with ``-shared`` into ``torchpruner_amd/_C.so`` against the
+  HIP runtime that ships inside torch (same soname ``libamdhip64.so.7``), so the
+  extension shares torch's streams and caching allocator.
+
+The reference has no native code at all; this replaces the
+implicit cuDNN/cuBLAS/ATen kernels its hooks trigger.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+BUILD_DIR = ROOT / "build" / "native"
+OUT = Path(__file__).resolve().parent / "_C.so"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_paths():
+    import torch
+    tdir = Path(torch.__file__).resolve().parent
+    inc = [tdir / "include", tdir / "include" / "torch" / "csrc" / "api" / "include"]
+    lib = tdir / "lib"
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _common_flags():
+    return [
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-fPIC",
+        "-std=c++17",
+        "-ffp-contract=fast",
+        "-munsafe-fp-atomics",
+        f"-I{CSRC / 'include'}",
+        "-Wno-unused-result",
+    ]
+
+
+def _needs_rebuild(src: Path, obj: Path, deps: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    if src.stat().st_mtime > t:
+        return True
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(str(c) for c in cmd), flush=True)
+    r = subprocess.run([str(c) for c in cmd], capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"native build failed: {' '.join(str(c) for c in cmd[:6])} ...")
+    return r
+
+
+def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
+    """Compile all HIP kernels + torch bindings into ``torchpruner_amd/_C.so``."""
+    inc, lib, abi = _torch_paths()
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    headers = sorted((CSRC / "include").glob("*.h"))
+    kernels = sorted((CSRC / "kernels").glob("*.hip"))
+    bindings = sorted(CSRC.glob("*.cpp"))
+
+    jobs_list = []
+    objs = []
+    for src in kernels:
+        obj = BUILD_DIR / (src.stem + ".o")
+        objs.append(obj)
+        if force or _needs_rebuild(src, obj, headers):
+            cmd = [HIPCC, *_common_flags(), f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-c", src, "-o", obj]
+            jobs_list.append(cmd)
+    for binding in bindings:
+        bobj = BUILD_DIR / (binding.stem + ".o")
+        objs.append(bobj)
+        if force or _needs_rebuild(binding, bobj, headers):
+            cmd = [HIPCC, *_common_flags(), f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                   "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+                   *[f"-I{p}" for p in inc], "-c", binding, "-o", bobj]
+            jobs_list.append(cmd)
+
+    n = jobs or min(8, os.cpu_count() or 4)
+    if jobs_list:
+        with ThreadPoolExecutor(max_workers=n) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs_list))
+
+    if force or jobs_list or not OUT.exists() or any(o.stat().st_mtime > OUT.stat().st_mtime for o in objs):
+        tmp = OUT.with_suffix(".so.tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs,
+               f"-L{lib}", f"-Wl,-rpath,{lib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip",
+               "-lamdhip64", "-o", tmp]
+        _run(cmd, verbose)
+        os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(verbose=True, force="--force" in sys.argv)
+    print(OUT)

@@ -1,0 +1,18 @@
+from .graph import (
+    ACTIVATIONS,
+    discover_cascade,
+    find_best_module_for_attributions,
+    get_resnet_pruning_graph,
+    get_vgg_pruning_graph,
+)
+from .flops import count_parameters, count_flops
+
+__all__ = [
+    "ACTIVATIONS",
+    "discover_cascade",
+    "find_best_module_for_attributions",
+    "get_resnet_pruning_graph",
+    "get_vgg_pruning_graph",
+    "count_parameters",
+    "count_flops",
+]
