@@ -1,0 +1,331 @@
+"""Attribution-metric core (reference: torchpruner/attributions/attributions.py:15-116).
+
+Same public contract as the reference — ``Metric(model, data_generator, criterion, device,
+reduction="mean", ...)`` and ``run(module, find_best_evaluation_module=False)`` returning a
+NumPy array — re-designed for MI355X:
+
+* **Device-resident accumulation.** Hooks never copy to the host. Per-sample (B, C) scores
+  are produced by the HIP channel-reduction kernels (ops.channel_reduce) and folded into
+  float64 device accumulators (ops.column_accumulate); one device->host copy per ``run()``.
+  The reference does ``.cpu().numpy()`` + ``np.concatenate`` on every batch (O(N^2) host
+  work, a device sync per batch — apoz.py:34-38, taylor.py:46-48).
+* **Data parallel.** When a process group is live, whole batches are sharded round-robin
+  over ranks (parallel.dist.ShardedBatches) and the (C+1,) accumulator is all-reduced once
+  per ``run()`` over RCCL (R1); per-sample slabs for ``reduction="none"``/callables are
+  all-gathered in global batch order (R2).
+* **Gradient capture by tensor hooks** on a fresh leaf that replaces the evaluation module's
+  output (safe with ``ReLU(inplace=True)``, which the deprecated non-full
+  ``register_backward_hook`` of the reference relies on). Parameters are frozen during the
+  pass, so backward runs only downstream of the evaluation module and only the input
+  gradients (no weight-gradient GEMMs). Scores are identical to the reference; the
+  reference's side effect of accumulating ``param.grad`` is intentionally dropped.
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+from abc import ABC, abstractmethod
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.nn.modules.conv import _ConvNd
+
+from .. import ops
+from ..parallel import dist as pdist
+from ..utils.graph import ACTIVATIONS, find_best_module_for_attributions
+
+logger = logging.getLogger("torchpruner")
+
+SUPPORTED_OUT_PRUNING_MODULES = [nn.Linear, _ConvNd]
+__all__ = ["_AttributionMetric", "SUPPORTED_OUT_PRUNING_MODULES", "ACTIVATIONS", "ScoreAccumulator"]
+
+
+class ScoreAccumulator:
+    """Per-unit score accumulator living on the metric's device.
+
+    ``stats`` mode (reduction mean/sum): float64 (C,) running sum + sample count.
+    ``samples`` mode (reduction none/callable): the per-batch (B, C) slabs, kept on device
+    and tagged with their global batch index so data-parallel gathers preserve order.
+    """
+
+    def __init__(self, reduction, device):
+        self.mode = "stats" if reduction in ("mean", "sum") else "samples"
+        self.device = torch.device(device)
+        self.sum = None
+        self.count = 0
+        self.slabs: list[tuple[int, torch.Tensor]] = []
+        self.dtype = None
+
+    def add(self, v: torch.Tensor, batch_index: int):
+        """Add a (B, C) per-sample score slab for global batch ``batch_index``."""
+        if self.dtype is None:
+            self.dtype = v.dtype
+        if self.mode == "stats":
+            if self.sum is None:
+                self.sum = torch.zeros(v.shape[1], dtype=torch.float64, device=v.device)
+            ops.column_accumulate(v, self.sum)
+            self.count += v.shape[0]
+        else:
+            self.slabs.append((batch_index, v.detach()))
+
+    def finalize(self, reduction, aggregate, collective=False, group=None):
+        """Reduce across ranks (if ``collective``) and apply ``reduction``; returns NumPy."""
+        if not collective:
+            return self._finalize_local(reduction, aggregate)
+        out_dtype = np.float32 if self.dtype in (None, torch.float32, torch.float16, torch.bfloat16) else np.float64
+        if self.mode == "stats":
+            n = self.sum.numel() if self.sum is not None else 0
+            # ranks must agree on C even if one owned no batches: share it first
+            n = pdist.all_max_int(n, group)
+            buf = torch.zeros(n + 1, dtype=torch.float64, device=self.device)
+            if self.sum is not None:
+                buf[:n] = self.sum
+            buf[n] = float(self.count)
+            pdist.all_reduce_sum_(buf, group)
+            host = buf.cpu().numpy()
+            total, count = host[:n], host[n]
+            if reduction == "mean":
+                res = total / max(count, 1.0)
+            else:
+                res = total
+            return res.astype(out_dtype)
+        rows = pdist.gather_ordered_rows(self.slabs, group)
+        return self._to_numpy_rows(rows, aggregate, out_dtype)
+
+    def _finalize_local(self, reduction, aggregate):
+        out_dtype = np.float32 if self.dtype in (None, torch.float32, torch.float16, torch.bfloat16) else np.float64
+        if self.mode == "stats":
+            total = self.sum.cpu().numpy() if self.sum is not None else np.zeros(0)
+            res = total / max(self.count, 1) if reduction == "mean" else total
+            return res.astype(out_dtype)
+        slabs = sorted(self.slabs, key=lambda s: s[0])
+        rows = torch.cat([t for _, t in slabs], 0) if slabs else torch.empty(0)
+        return self._to_numpy_rows(rows, aggregate, out_dtype)
+
+    @staticmethod
+    def _to_numpy_rows(rows, aggregate, out_dtype):
+        arr = rows.cpu().numpy()
+        if arr.dtype != out_dtype and out_dtype == np.float32:
+            arr = arr.astype(np.float32)
+        return aggregate(arr)
+
+
+class _AttributionMetric(ABC):
+    """Abstract base of every metric (reference attributions.py:15-25)."""
+
+    def __init__(self, model, data_generator, criterion, device, reduction="mean", *, group=None,
+                 shard_data=None):
+        assert reduction in ["mean", "none", "sum"] or callable(reduction), \
+            'Reduction must be a string in ["mean", "none", "sum"] or a function'
+        self.model = model
+        self.data_gen = data_generator
+        self.criterion = criterion
+        self.device = device
+        self.reduction = reduction
+        self.deterministic = False
+        self.benchmark = False
+        # Data-parallel knobs (new): process group and whether to shard the generator.
+        # shard_data=None -> shard automatically when a multi-rank group is live.
+        self.group = group
+        self.shard_data = shard_data
+
+    # ------------------------------------------------------------------ API parity
+    @abstractmethod
+    def run(self, module, **kwargs):
+        assert any(isinstance(module, t) for t in SUPPORTED_OUT_PRUNING_MODULES), \
+            f"Attributions can be computed only for the following modules {SUPPORTED_OUT_PRUNING_MODULES}"
+        return self.find_evaluation_module(module, **kwargs)
+
+    def find_evaluation_module(self, module, find_best_evaluation_module=False):
+        if find_best_evaluation_module is True:
+            return find_best_module_for_attributions(self.model, module)
+        return module
+
+    def run_all_forward(self):
+        """No-grad forward over this rank's batches; returns per-sample losses (concatenated)."""
+        self.set_deterministic()
+        losses = []
+        try:
+            with torch.no_grad():
+                for _, x, y in self._batches():
+                    losses.append(self.criterion(self.model(x), y, reduction="none"))
+        finally:
+            self.restore_deterministic()
+        return torch.cat(losses, 0) if losses else None
+
+    def run_all_forward_and_backward(self):
+        """Forward + backward (default mean reduction) over this rank's batches."""
+        self.set_deterministic()
+        try:
+            for _, x, y in self._batches():
+                loss = self.criterion(self.model(x), y)
+                loss.backward()
+        finally:
+            self.restore_deterministic()
+
+    def run_forward_partial(self, x=None, y_true=None, to_module=None, from_module=None):
+        """``model.forward_partial`` wrapper (attributions.py:70-89)."""
+        self.set_deterministic()
+        loss = None
+        try:
+            y = self.model.forward_partial(x, to_module=to_module, from_module=from_module)
+            if y_true is not None and to_module is None:
+                loss = self.criterion(y, y_true, reduction="none")
+        finally:
+            self.restore_deterministic()
+        return y, loss
+
+    def aggregate_over_samples(self, attributions):
+        """Host NumPy aggregation over axis 0 (attributions.py:91-106)."""
+        if self.reduction == "mean":
+            return np.mean(attributions, 0)
+        elif self.reduction == "sum":
+            return np.sum(attributions, 0)
+        elif self.reduction == "none":
+            return attributions
+        return self.reduction(attributions)
+
+    def set_deterministic(self):
+        self.deterministic = torch.backends.cudnn.deterministic
+        self.benchmark = torch.backends.cudnn.benchmark
+        torch.backends.cudnn.deterministic = True
+        torch.backends.cudnn.benchmark = False
+
+    def restore_deterministic(self):
+        torch.backends.cudnn.deterministic = self.deterministic
+        torch.backends.cudnn.benchmark = self.benchmark
+
+    # ------------------------------------------------------------------ engine internals
+    def _world(self):
+        return pdist.get_world_size(self.group), pdist.get_rank(self.group)
+
+    def _sharding(self) -> bool:
+        world, _ = self._world()
+        return world > 1 and (self.shard_data is None or self.shard_data)
+
+    def _batches(self):
+        """Yield ``(global_batch_index, x, y)`` on ``self.device`` for this rank's batches."""
+        world, rank = self._world()
+        it = pdist.ShardedBatches(self.data_gen, rank, world) if self._sharding() else \
+            ((i, x, y) for i, (x, y) in enumerate(self.data_gen))
+        for i, x, y in it:
+            yield i, _to(x, self.device), _to(y, self.device)
+
+    def _new_accumulator(self) -> ScoreAccumulator:
+        return ScoreAccumulator(self.reduction, self.device)
+
+    def _finalize(self, acc: ScoreAccumulator):
+        # not sharded: every rank already holds the full result, so no collective
+        return acc.finalize(self.reduction, self.aggregate_over_samples, collective=self._sharding(),
+                            group=self.group)
+
+    @contextlib.contextmanager
+    def _frozen_params(self):
+        """Temporarily stop every parameter from requiring grad (input-grad-only backward)."""
+        flags = [(p, p.requires_grad) for p in self.model.parameters()]
+        for p, _ in flags:
+            p.requires_grad_(False)
+        try:
+            yield
+        finally:
+            for p, f in flags:
+                p.requires_grad_(f)
+
+    def _has_inplace(self) -> bool:
+        return any(getattr(m, "inplace", False) for m in self.model.modules())
+
+    def _grad_capture_pass(self, eval_modules, on_grad):
+        """Forward+backward over this rank's batches capturing, for every module in
+        ``eval_modules``, its output ``a`` and ``dL/da``: ``on_grad(k, a, g, batch_index)``.
+
+        The first evaluation module to execute becomes the autograd leaf (nothing upstream
+        is differentiated); parameters are frozen so only input gradients are computed.
+        One pass serves any number of modules (the reference needs one pass per module).
+        """
+        if isinstance(eval_modules, nn.Module):
+            eval_modules = [eval_modules]
+        state = {}
+        has_inplace = self._has_inplace()
+
+        def make_hook(k, module):
+            # an activation's consumers are convs/pools/linears; a conv/linear/BN output may be
+            # consumed by an in-place activation, so hand a copy downstream in that case
+            copy_out = has_inplace and not isinstance(module, ACTIVATIONS)
+
+            def fwd_hook(_m, _inp, out):
+                idx = state["idx"]
+                if not state["leafed"]:
+                    state["leafed"] = True
+                    src = out.detach().requires_grad_(True)
+                    ret = src.clone() if (copy_out or has_inplace) else src
+                else:
+                    src = out
+                    ret = out.clone() if copy_out else None
+                act = src.detach()
+                version = act._version
+
+                def _tensor_hook(g):
+                    if act._version != version:
+                        raise RuntimeError(
+                            f"activation of {module} was modified in place after capture; "
+                            "attribute at a different module")
+                    on_grad(k, act, g, idx)
+                src.register_hook(_tensor_hook)
+                return ret
+
+            return fwd_hook
+
+        handles = [m.register_forward_hook(make_hook(k, m)) for k, m in enumerate(eval_modules)]
+        self.set_deterministic()
+        try:
+            with self._frozen_params():
+                for i, x, y in self._batches():
+                    state["idx"] = i
+                    state["leafed"] = False
+                    loss = self.criterion(self.model(x), y)
+                    loss.backward()
+        finally:
+            for h in handles:
+                h.remove()
+            self.restore_deterministic()
+
+    def _forward_capture_pass(self, eval_modules, on_out):
+        """No-grad forward pass calling ``on_out(k, output, batch_index)`` per module."""
+        state = {}
+
+        def make_hook(k):
+            def hook(_m, _inp, out):
+                on_out(k, out, state["idx"])
+            return hook
+
+        handles = [m.register_forward_hook(make_hook(k)) for k, m in enumerate(eval_modules)]
+        self.set_deterministic()
+        try:
+            with torch.no_grad():
+                for i, x, _y in self._batches():
+                    state["idx"] = i
+                    self.model(x)
+        finally:
+            for h in handles:
+                h.remove()
+            self.restore_deterministic()
+
+    def run_many(self, modules, find_best_evaluation_module=False, **kwargs):
+        """Scores for several modules. Hook-based metrics share ONE pass over the data
+        (new API; the reference runs a full pass per module). Returns a list of arrays."""
+        return [self.run(m, find_best_evaluation_module=find_best_evaluation_module, **kwargs) for m in modules]
+
+    def _eval_modules(self, modules, find_best_evaluation_module):
+        out = []
+        for m in modules:
+            assert any(isinstance(m, t) for t in SUPPORTED_OUT_PRUNING_MODULES), \
+                f"Attributions can be computed only for the following modules {SUPPORTED_OUT_PRUNING_MODULES}"
+            out.append(self.find_evaluation_module(m, find_best_evaluation_module=find_best_evaluation_module))
+        return out
+
+
+def _to(t, device):
+    if isinstance(t, torch.Tensor):
+        return t.to(device, non_blocking=True)
+    return t

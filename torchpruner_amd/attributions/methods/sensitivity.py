@@ -1,0 +1,22 @@
+"""Sensitivity: mean |dL/dz| per unit — Mittal et al. (reference: methods/sensitivity.py:5-34).
+
+Per sample: sum over trailing dims of |grad_output|, gradient of the per-batch *mean* loss
+(so scores scale with 1/batch_size, as in the reference).
+"""
+from ... import ops
+from ..base import _AttributionMetric
+
+
+class SensitivityAttributionMetric(_AttributionMetric):
+    def run(self, module, **kwargs):
+        module = super().run(module, **kwargs)
+        return self._run_modules([module])[0]
+
+    def run_many(self, modules, find_best_evaluation_module=False, **kwargs):
+        return self._run_modules(self._eval_modules(modules, find_best_evaluation_module))
+
+    def _run_modules(self, eval_modules):
+        accs = [self._new_accumulator() for _ in eval_modules]
+        self._grad_capture_pass(eval_modules,
+                                lambda k, a, g, i: accs[k].add(ops.channel_reduce(None, g, "sensitivity"), i))
+        return [self._finalize(a) for a in accs]

@@ -1,0 +1,235 @@
+"""Monte-Carlo Shapley values over output units (reference: methods/shapley_values.py:7-99).
+
+Semantics kept from the reference:
+* ``sv_samples`` permutations of the ``n`` units are drawn with NumPy's global RNG once
+  (on the first batch) and shared by every batch (shapley_values.py:45-47);
+* the contribution of unit ``pi[p-1]`` is ``(L_p - L_{p-1}) / S`` where ``L_p`` is the
+  per-sample loss with the first ``p`` units of ``pi`` zeroed at the evaluation module;
+* fast path via ``model.forward_partial`` when present, slow path (a masking forward hook
+  and full forward passes) otherwise.
+
+MI355X-native execution:
+* **Batched prefixes.** ``L_p`` for different ``p`` are independent, so K prefixes of one
+  permutation are materialised by one HIP launch as a (K*B)-sample batch
+  (``ops.prefix_mask``) and evaluated by ONE downstream forward; the K deltas are scattered
+  on device (``ops.shapley_scatter`` / ``ops.shapley_column``). The reference runs one tiny
+  forward plus one device->host copy per unit (S*n per batch, shapley_values.py:55-61).
+  K is sized from an element budget so the batch fills the GPU (288 GB HBM).
+* **Work sharding across ranks.** The S*n prefix evaluations per batch are split into
+  contiguous ranges over ranks (one boundary evaluation per range), permutations are
+  broadcast from rank 0 (R3), and the accumulators are all-reduced once per ``run()`` (R4).
+"""
+from __future__ import annotations
+
+import logging
+
+import numpy as np
+import torch
+from torch.nn.modules.batchnorm import _BatchNorm
+from torch.nn.modules.dropout import _DropoutNd
+
+from ... import ops
+from ...parallel import dist as pdist
+from ..base import _AttributionMetric
+
+logger = logging.getLogger("torchpruner")
+
+
+class ShapleyAttributionMetric(_AttributionMetric):
+    """Approximate Shapley values by permutation sampling.
+
+    Extra keyword arguments (all optional):
+      prefix_batch       fixed number K of prefixes evaluated per forward (default: auto)
+      max_eval_elements  element budget used to size K automatically
+    """
+
+    def __init__(self, *args, sv_samples=5, prefix_batch=None, max_eval_elements=1 << 27, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.samples = sv_samples
+        self.mask_indices = []
+        self.prefix_batch = prefix_batch
+        self.max_eval_elements = max_eval_elements
+
+    def run(self, module, sv_samples=None, **kwargs):
+        module = super().run(module, **kwargs)
+        sv_samples = sv_samples if sv_samples is not None else self.samples
+        if hasattr(self.model, "forward_partial"):
+            return self.run_module_with_partial(module, sv_samples)
+        logger.warning("Consider adding a 'forward_partial' method to your model to speed-up Shapley values "
+                       "computation")
+        return self.run_module(module, sv_samples)
+
+    # ------------------------------------------------------------------ helpers
+    def _prefix_chunk(self, B, per_sample):
+        if self.prefix_batch is not None:
+            return max(1, int(self.prefix_batch))
+        if self.model.training and any(isinstance(m, (_BatchNorm, _DropoutNd)) for m in self.model.modules()):
+            return 1  # batch statistics / dropout masks would mix across stacked prefixes
+        return max(1, int(self.max_eval_elements // max(1, 4 * B * per_sample)))
+
+    def _permutations(self, n, S):
+        world, rank = self._world()
+        perms = None
+        if rank == 0 or world == 1:
+            perms = np.stack([np.random.permutation(n) for _ in range(S)]) if S > 0 else np.zeros((0, n), np.int64)
+        if world > 1:
+            perms = pdist.broadcast_object(perms, 0, self.group)
+        return perms
+
+    def _segments(self, S, n):
+        """This rank's share of the flattened (permutation j, prefix p in 1..n) work."""
+        world, rank = self._world()
+        if world > 1 and self.shard_data is not False:
+            lo, hi = pdist.split_range(S * n, rank, world)
+        else:
+            lo, hi = 0, S * n
+        segs = []
+        u = lo
+        while u < hi:
+            j = u // n
+            p_lo = u % n + 1
+            p_hi = min(n, p_lo + (hi - u) - 1)
+            segs.append((j, p_lo, p_hi))
+            u += p_hi - p_lo + 1
+        return segs
+
+    @staticmethod
+    def _rank_of(perm, device):
+        n = len(perm)
+        r = torch.empty(n, dtype=torch.int32)
+        r[torch.as_tensor(perm, dtype=torch.long)] = torch.arange(n, dtype=torch.int32)
+        return r.to(device)
+
+    def _accumulate_permutation(self, perm_t, rank_t, p_lo, p_hi, base_loss, evaluate, K, S, sink):
+        """Evaluate prefixes p_lo..p_hi of one permutation and add their deltas to ``sink``."""
+        B = base_loss.shape[0]
+        prev = base_loss if p_lo == 1 else evaluate(rank_t, p_lo - 1, 1)[0]
+        cur = p_lo
+        while cur <= p_hi:
+            cnt = min(K, p_hi - cur + 1)
+            Ls = evaluate(rank_t, cur, cnt)  # (cnt, B)
+            L = torch.cat([prev.view(1, B), Ls], 0).float().contiguous()
+            sink(L, perm_t, cur - 1)
+            prev = Ls[-1]
+            cur += cnt
+
+    def _run_batches(self, module, S, prepare):
+        """Shared driver. ``prepare(x, y)`` -> (n, B, per_sample, base_loss, evaluate)."""
+        stats = self.reduction in ("mean", "sum")
+        sv_col = None
+        slabs = []
+        count = 0
+        perms = None
+        perm_ts = rank_ts = None
+        segs = None
+        with torch.no_grad():
+            # every rank iterates every batch; the prefix work (not the data) is sharded
+            for bidx, (x, y) in enumerate(self.data_gen):
+                x, y = _to(x, self.device), _to(y, self.device)
+                n, B, per_sample, base_loss, evaluate = prepare(x, y)
+                if perms is None:
+                    perms = self._permutations(n, S)
+                    perm_ts = [torch.as_tensor(p, dtype=torch.int32).to(base_loss.device) for p in perms]
+                    rank_ts = [self._rank_of(p, base_loss.device) for p in perms]
+                    segs = self._segments(S, n)
+                K = self._prefix_chunk(B, per_sample)
+                if stats:
+                    if sv_col is None:
+                        sv_col = torch.zeros(n, dtype=torch.float64, device=base_loss.device)
+                    sink = lambda L, pt, k0: ops.shapley_column(L, pt, sv_col, k0, 1.0 / S)
+                else:
+                    slab = torch.zeros(B, n, dtype=torch.float64, device=base_loss.device)
+                    slabs.append(slab)
+                    sink = lambda L, pt, k0, slab=slab: ops.shapley_scatter(L, pt, slab, 0, k0, 1.0 / S)
+                for j, p_lo, p_hi in segs:
+                    self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi, base_loss, evaluate, K, S, sink)
+                count += B
+        world, _ = self._world()
+        collective = world > 1 and self.shard_data is not False
+        if stats:
+            if sv_col is None:
+                return np.zeros(0)
+            if collective:
+                pdist.all_reduce_sum_(sv_col, self.group)
+            total = sv_col.cpu().numpy()
+            return total / max(count, 1) if self.reduction == "mean" else total
+        sv = torch.cat(slabs, 0) if slabs else torch.zeros(0, 0, dtype=torch.float64)
+        if collective:
+            pdist.all_reduce_sum_(sv, self.group)
+        return self.aggregate_over_samples(sv.cpu().numpy())
+
+    # ------------------------------------------------------------------ fast path
+    def run_module_with_partial(self, module, sv_samples):
+        """Shapley sampling with ``model.forward_partial`` (runs only downstream layers)."""
+
+        def prepare(x, y):
+            original_z, _ = self.run_forward_partial(x, to_module=module)
+            _, original_loss = self.run_forward_partial(original_z, y_true=y, from_module=module)
+            B = original_z.shape[0]
+            z = original_z.contiguous() if not original_z.is_contiguous(memory_format=torch.channels_last) \
+                else original_z
+
+            def evaluate(rank_t, p_first, cnt):
+                masked = ops.prefix_mask(z, rank_t, p_first, cnt)
+                yy = y.repeat((cnt,) + (1,) * (y.dim() - 1))
+                _, loss = self.run_forward_partial(masked, y_true=yy, from_module=module)
+                return loss.reshape(cnt, B, -1).sum(-1)
+
+            return (original_z.shape[1], B, original_z[0].numel(), original_loss.reshape(B, -1).sum(-1), evaluate)
+
+        return self._run_batches(module, sv_samples, prepare)
+
+    # ------------------------------------------------------------------ slow path
+    def run_module(self, module, samples):
+        """Shapley sampling through full forward passes and a masking forward hook."""
+        state = {"mode": "off"}
+
+        def hook(_m, _inp, out):
+            module._tp_prune_dim = out.shape[1]
+            if state["mode"] == "off":
+                return None
+            return ops.prefix_mask(out.contiguous(), state["rank"], state["p0"], state["K"])
+
+        handle = module.register_forward_hook(hook)
+        try:
+            def prepare(x, y):
+                self.set_deterministic()
+                try:
+                    state["mode"] = "off"
+                    base = self.criterion(self.model(x), y, reduction="none")
+                finally:
+                    self.restore_deterministic()
+                B = x.shape[0]
+                n = module._tp_prune_dim
+
+                def evaluate(rank_t, p_first, cnt):
+                    state.update(mode="on", rank=rank_t, p0=p_first, K=cnt)
+                    self.set_deterministic()
+                    try:
+                        yy = y.repeat((cnt,) + (1,) * (y.dim() - 1))
+                        loss = self.criterion(self.model(x), yy, reduction="none")
+                    finally:
+                        state["mode"] = "off"
+                        self.restore_deterministic()
+                    return loss.reshape(cnt, B, -1).sum(-1)
+
+                return n, B, max(1, x[0].numel()), base.reshape(B, -1).sum(-1), evaluate
+
+            return self._run_batches(module, samples, prepare)
+        finally:
+            handle.remove()
+            if hasattr(module, "_tp_prune_dim"):
+                delattr(module, "_tp_prune_dim")
+            self.mask_indices = []
+
+    def _forward_hook(self):
+        """Reference-compatible masking hook: zero ``self.mask_indices`` of the output."""
+        def _hook(module, _, output):
+            module._tp_prune_dim = output.shape[1]
+            return output.index_fill_(1, torch.tensor(self.mask_indices, dtype=torch.long,
+                                                      device=output.device), 0.0)
+        return _hook
+
+
+def _to(t, device):
+    return t.to(device, non_blocking=True) if isinstance(t, torch.Tensor) else t

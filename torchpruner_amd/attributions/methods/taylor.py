@@ -1,0 +1,27 @@
+"""First-order Taylor expansion — Molchanov et al. (reference: methods/taylor.py:6-49).
+
+Per sample: |sum over trailing dims of -(dL/dz * z)| (no abs with ``signed=True``).
+The activation and gradient are read once by one fused HIP reduction; the reference keeps a
+full activation clone per batch and leaks it on the module (taylor.py:35).
+"""
+from ... import ops
+from ..base import _AttributionMetric
+
+
+class TaylorAttributionMetric(_AttributionMetric):
+    def __init__(self, *args, signed=False, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.signed = signed
+
+    def run(self, module, **kwargs):
+        module = super().run(module, **kwargs)
+        return self._run_modules([module])[0]
+
+    def run_many(self, modules, find_best_evaluation_module=False, **kwargs):
+        return self._run_modules(self._eval_modules(modules, find_best_evaluation_module))
+
+    def _run_modules(self, eval_modules):
+        mode = "taylor_signed" if self.signed else "taylor"
+        accs = [self._new_accumulator() for _ in eval_modules]
+        self._grad_capture_pass(eval_modules, lambda k, a, g, i: accs[k].add(ops.channel_reduce(a, g, mode), i))
+        return [self._finalize(a) for a in accs]

@@ -1,0 +1,139 @@
+"""Synthetic, device-resident datasets (no torchvision / no network in this environment).
+
+The reference trains and scores on CIFAR-10 / MNIST / FashionMNIST through torchvision
+DataLoaders with ``num_workers=1`` (experiments/models/cifar10.py:80-161). Here data of the
+same shapes is generated directly on the GPU, so attribution throughput is bound by the
+engine and not by a host loader:
+
+* :class:`DeviceLoader` — a fixed (x, y) tensor pair already on device, batched without
+  copies; has ``.dataset`` (``len``) for Shapley and ``shard(rank, world)`` for
+  data-parallel runs (round-robin whole batches, no foreign batch is ever touched).
+* :class:`StreamLoader` — ImageNet-scale streams: batch ``i`` is regenerated on device from
+  ``seed + i`` each time (nothing stored), so any rank can produce exactly its batches.
+* ``teacher`` labels: ``y = argmax model(x)`` of a reference model, which gives a
+  meaningful "top-1 retained after pruning" on random-init weights (top-1 = 100% before).
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Optional
+
+import torch
+
+SHAPES = {
+    "cifar10": ((3, 32, 32), 10),
+    "mnist": ((1, 28, 28), 10),
+    "fmnist": ((1, 28, 28), 10),
+    "imagenet": ((3, 224, 224), 1000),
+}
+
+
+class _Len:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+class DeviceLoader:
+    """Iterate fixed on-device tensors in batches (like a non-shuffling DataLoader)."""
+
+    def __init__(self, x: torch.Tensor, y: torch.Tensor, batch_size: int, drop_last: bool = False):
+        assert x.shape[0] == y.shape[0]
+        self.x, self.y = x, y
+        self.batch_size = batch_size
+        self.drop_last = drop_last
+        self.dataset = _Len(x.shape[0])
+
+    def __len__(self):
+        n = self.x.shape[0]
+        return n // self.batch_size if self.drop_last else math.ceil(n / self.batch_size)
+
+    def _batch(self, i):
+        s = i * self.batch_size
+        return self.x[s:s + self.batch_size], self.y[s:s + self.batch_size]
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self._batch(i)
+
+    def shard(self, rank: int, world: int):
+        for i in range(rank, len(self), world):
+            x, y = self._batch(i)
+            yield i, x, y
+
+
+class StreamLoader:
+    """Deterministic on-device stream of ``num_batches`` random batches (nothing stored)."""
+
+    def __init__(self, num_batches: int, batch_size: int, shape, num_classes: int, device, seed: int = 0,
+                 labeler: Optional[Callable] = None, channels_last: bool = False):
+        self.num_batches = num_batches
+        self.batch_size = batch_size
+        self.shape = tuple(shape)
+        self.num_classes = num_classes
+        self.device = torch.device(device)
+        self.seed = seed
+        self.labeler = labeler
+        self.channels_last = channels_last
+        self.dataset = _Len(num_batches * batch_size)
+
+    def __len__(self):
+        return self.num_batches
+
+    def _batch(self, i):
+        g = torch.Generator(device=self.device)
+        g.manual_seed(self.seed * 1_000_003 + i)
+        x = torch.randn((self.batch_size,) + self.shape, generator=g, device=self.device)
+        if self.channels_last and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        if self.labeler is not None:
+            y = self.labeler(x)
+        else:
+            y = torch.randint(0, self.num_classes, (self.batch_size,), generator=g, device=self.device)
+        return x, y
+
+    def __iter__(self):
+        for i in range(self.num_batches):
+            yield self._batch(i)
+
+    def shard(self, rank: int, world: int):
+        for i in range(rank, self.num_batches, world):
+            x, y = self._batch(i)
+            yield i, x, y
+
+
+def synthetic_dataset(name: str, n: int, device="cpu", seed: int = 0, teacher: Optional[torch.nn.Module] = None,
+                      batch_for_teacher: int = 1024):
+    """Return ``(x, y)`` of ``n`` samples shaped like dataset ``name`` on ``device``.
+
+    With ``teacher`` the labels are the teacher's eval-mode argmax predictions.
+    """
+    shape, nc = SHAPES[name]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn((n,) + shape, generator=g).to(device)
+    if teacher is None:
+        y = torch.randint(0, nc, (n,), generator=g).to(device)
+    else:
+        y = teacher_labels(teacher, x, batch_for_teacher)
+    return x, y
+
+
+@torch.no_grad()
+def teacher_labels(model: torch.nn.Module, x: torch.Tensor, batch: int = 1024) -> torch.Tensor:
+    was = model.training
+    model.eval()
+    out = []
+    for s in range(0, x.shape[0], batch):
+        out.append(model(x[s:s + batch]).argmax(1))
+    model.train(was)
+    return torch.cat(out, 0)
+
+
+def loaders(name: str, n_train: int, n_val: int, batch_size: int, val_batch_size: int, device="cpu", seed: int = 0,
+            teacher=None):
+    """(train_loader, val_loader) of synthetic on-device data shaped like ``name``."""
+    xt, yt = synthetic_dataset(name, n_train, device, seed, teacher)
+    xv, yv = synthetic_dataset(name, n_val, device, seed + 1, teacher)
+    return DeviceLoader(xt, yt, batch_size), DeviceLoader(xv, yv, val_batch_size)

@@ -1,0 +1,20 @@
+"""Distributed runtime: RCCL-over-xGMI data parallelism for attribution and finetuning."""
+from .dist import (
+    DistContext,
+    ShardedBatches,
+    all_reduce_sum_,
+    barrier,
+    broadcast_object,
+    broadcast_tensor_,
+    gather_ordered_rows,
+    get_rank,
+    get_world_size,
+    init_distributed,
+    is_dist,
+    split_range,
+)
+
+__all__ = [
+    "DistContext", "ShardedBatches", "all_reduce_sum_", "barrier", "broadcast_object", "broadcast_tensor_",
+    "gather_ordered_rows", "get_rank", "get_world_size", "init_distributed", "is_dist", "split_range",
+]

@@ -116,6 +116,15 @@ def broadcast_tensor_(t: torch.Tensor, src: int = 0, group=None) -> torch.Tensor
     return t
 
 
+def all_max_int(v: int, group=None) -> int:
+    """Max of a Python int over ranks (used to agree on shapes when a rank saw no data)."""
+    if get_world_size(group) == 1:
+        return int(v)
+    vals = [None] * get_world_size(group)
+    dist.all_gather_object(vals, int(v), group=group)
+    return max(vals)
+
+
 def barrier(group=None):
     if get_world_size(group) > 1:
         dist.barrier(group=group)
