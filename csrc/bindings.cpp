@@ -84,6 +84,39 @@ void column_accumulate(const at::Tensor& v, at::Tensor& acc_sum, const c10::opti
                                     (int)v.size(1), cur_stream()));
 }
 
+// For every i: v = |T[i]| (or T[i]); acc[i] += v.sum(0) (acc[i] may be empty = skip);
+// after: 0 leave T, 1 write v back, 2 zero T. One launch per 16 tensors.
+void score_fold_(at::TensorList T, at::TensorList acc, bool take_abs, int64_t after) {
+  TORCH_CHECK(T.size() == acc.size(), "one accumulator per score tensor");
+  if (T.empty()) return;
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(T[0].device());
+  std::vector<float*> tp;
+  std::vector<double*> ap;
+  std::vector<int> bs, cs;
+  auto flush = [&]() {
+    if (tp.empty()) return;
+    TP_CHECK_HIP(tp_score_fold_multi(tp.data(), ap.data(), bs.data(), cs.data(), (int)tp.size(), take_abs ? 1 : 0,
+                                     (int)after, cur_stream()));
+    tp.clear(); ap.clear(); bs.clear(); cs.clear();
+  };
+  for (size_t i = 0; i < T.size(); ++i) {
+    check_cuda_f32(T[i], "T");
+    TORCH_CHECK(T[i].dim() == 2 && T[i].is_contiguous(), "T must be contiguous (B, C)");
+    double* a = nullptr;
+    if (acc[i].defined() && acc[i].numel() > 0) {
+      TORCH_CHECK(acc[i].scalar_type() == at::kDouble && acc[i].is_contiguous() && acc[i].numel() == T[i].size(1),
+                  "acc must be a contiguous float64 (C,) tensor");
+      a = acc[i].data_ptr<double>();
+    }
+    tp.push_back(T[i].data_ptr<float>());
+    ap.push_back(a);
+    bs.push_back((int)T[i].size(0));
+    cs.push_back((int)T[i].size(1));
+    if (tp.size() == 16) flush();
+  }
+  flush();
+}
+
 void channel_fill_(at::Tensor& x, const at::Tensor& idx, double value) {
   check_cuda_f32(x, "x");
   TORCH_CHECK(x.is_contiguous(), "channel_fill_ needs a contiguous NC* tensor");
@@ -218,6 +251,7 @@ TORCH_LIBRARY(tpamd, m) {
   m.def("channel_reduce(Tensor? act, Tensor? grad, int mode) -> Tensor");
   m.def("column_accumulate(Tensor v, Tensor(a!) acc_sum, Tensor(b!)? acc_sq) -> ()");
   m.def("channel_fill_(Tensor(a!) x, Tensor idx, float value) -> ()");
+  m.def("score_fold_(Tensor(a!)[] T, Tensor(b!)[] acc, bool take_abs, int after) -> ()");
   m.def("nan_channels(Tensor x) -> Tensor");
   m.def("gather_multi(Tensor[] srcs, int[] axes, Tensor keep) -> Tensor[]");
   m.def("prefix_mask(Tensor z, Tensor rank, int p0, int K) -> Tensor");
@@ -231,6 +265,7 @@ TORCH_LIBRARY_IMPL(tpamd, CUDA, m) {
   m.impl("channel_reduce", &channel_reduce);
   m.impl("column_accumulate", &column_accumulate);
   m.impl("channel_fill_", &channel_fill_);
+  m.impl("score_fold_", &score_fold_);
   m.impl("nan_channels", &nan_channels);
   m.impl("gather_multi", &gather_multi);
   m.impl("prefix_mask", &prefix_mask);

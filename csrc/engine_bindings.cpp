@@ -1,7 +1,164 @@
-// torch.ops.tpamd.* registrations for the fused conv/GEMM engine kernels.
+// torch.ops.tpamd.* registrations for the fused conv / GEMM engine kernels (conv_mfma.hip).
 #include <torch/library.h>
 #include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hip/hip_runtime.h>
+
 #include "tp_launchers.h"
 
-void register_engine_ops_def(torch::Library& m) {}
-void register_engine_ops_impl(torch::Library& m) {}
+extern "C" {
+hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w, int B, int H, int W, int Cin,
+                         int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits, const float* scale,
+                         const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
+                         float* taylor, int HWo, float* ws, hipStream_t st);
+hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
+                                int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
+}
+
+namespace {
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define TP_CHECK_HIP(expr)                                                                  \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    TORCH_CHECK(_e == hipSuccess, "tpamd conv launch failed: ", hipGetErrorString(_e));     \
+  } while (0)
+
+void need(const at::Tensor& t, const char* name, int64_t dim) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat, name, " must be a float32 GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(dim < 0 || t.dim() == dim, name, " must have ", dim, " dims, got ", t.dim());
+}
+
+const float* opt_ptr(const c10::optional<at::Tensor>& t, int64_t n, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  need(*t, name, 1);
+  TORCH_CHECK(t->numel() == n, name, " must have ", n, " elements");
+  return t->data_ptr<float>();
+}
+
+enum { EPI_FWD = 0, EPI_FWD_POOL = 1, EPI_BWD = 2 };
+
+int64_t splits_ws(int64_t splits, int64_t K) {
+  const int64_t kt = K / 32;
+  splits = std::max<int64_t>(1, std::min<int64_t>(splits, kt));
+  const int64_t per = (kt + splits - 1) / splits;
+  return (kt + per - 1) / per;
+}
+
+// Forward conv / linear: x (B,H,W,Cin) NHWC, w (Cout, K) with K = ks*ks*Cin.
+// Returns out (B,H,W,Cout) or pooled (B,H/2,W/2,Cout) + argmax bytes.
+std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w,
+                                            const c10::optional<at::Tensor>& scale,
+                                            const c10::optional<at::Tensor>& shift, bool relu, bool pool, int64_t ks,
+                                            int64_t cfg, int64_t splits) {
+  need(x, "x", 4);
+  need(w, "w", 2);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
+  TORCH_CHECK(ks == 1 || ks == 3, "ks must be 1 or 3");
+  TORCH_CHECK(w.size(1) == ks * ks * Cin, "weight K mismatch: ", w.size(1), " vs ", ks * ks * Cin);
+  TORCH_CHECK(Cin % 32 == 0, "Cin must be a multiple of 32");
+  TORCH_CHECK(!pool || (H % 2 == 0 && W % 2 == 0), "pooling needs even H, W");
+  TORCH_CHECK(cfg >= 0 && cfg <= 3, "bad tile config");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const float* sc = opt_ptr(scale, Cout, "scale");
+  const float* sh = opt_ptr(shift, Cout, "shift");
+  at::Tensor out, am;
+  if (pool) {
+    out = at::empty({B, H / 2, W / 2, Cout}, x.options());
+    am = at::empty({B, H / 2, W / 2, Cout}, x.options().dtype(at::kByte));
+  } else {
+    out = at::empty({B, H, W, Cout}, x.options());
+  }
+  const int64_t sp = splits_ws(splits, ks * ks * Cin);
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * H * W * Cout}, x.options());
+  TP_CHECK_HIP(tp_conv_igemm(x.data_ptr<float>(), nullptr, w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin,
+                             (int)Cout, (int)ks, pool ? 1 : 0, 0, pool ? EPI_FWD_POOL : EPI_FWD, (int)cfg, (int)sp, sc,
+                             sh, relu ? 1 : 0, out.data_ptr<float>(), pool ? am.data_ptr<uint8_t>() : nullptr, nullptr,
+                             nullptr, (int)(H * W), sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+  return {out, am};
+}
+
+// dgrad + fused consumer epilogue.
+// g: grad w.r.t. the conv output, (B,H,W,Cout); or, with g_argmax, the masked grad at pooled
+//    resolution (B,H/2,W/2,Cout) whose full-resolution form is implied by the argmax bytes.
+// wt: flipped/transposed weight (Cin, ks*ks*Cout). act: activation at the conv input (B,H,W,Cin).
+// taylor (B,Cin) fp32 accumulated atomically with sum_hw -(dL/dact * act) (nullable).
+// Returns dL/d(pre-activation) * bn_scale masked by act>0 (B,H,W,Cin), or an empty tensor.
+at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_argmax, const at::Tensor& wt,
+                      const at::Tensor& act, const c10::optional<at::Tensor>& bn_scale,
+                      const c10::optional<at::Tensor>& taylor, bool want_out, int64_t ks, int64_t cfg,
+                      int64_t splits) {
+  need(g, "g", 4);
+  need(wt, "wt", 2);
+  need(act, "act", 4);
+  const bool unpool = g_argmax.has_value() && g_argmax->defined();
+  const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3);
+  const int64_t Cout = g.size(3);
+  if (unpool) {
+    TORCH_CHECK(g.size(1) * 2 == H && g.size(2) * 2 == W, "pooled grad shape mismatch");
+    TORCH_CHECK(g_argmax->scalar_type() == at::kByte && g_argmax->sizes() == g.sizes() && g_argmax->is_contiguous(),
+                "g_argmax must be uint8 with g's shape");
+  } else {
+    TORCH_CHECK(g.size(1) == H && g.size(2) == W, "grad shape mismatch");
+  }
+  TORCH_CHECK(g.size(0) == B, "batch mismatch");
+  TORCH_CHECK(wt.size(0) == Cin && wt.size(1) == ks * ks * Cout, "wt must be (Cin, ks*ks*Cout)");
+  TORCH_CHECK(Cout % 32 == 0, "Cout must be a multiple of 32 for dgrad");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
+  float* tay = nullptr;
+  if (taylor.has_value() && taylor->defined()) {
+    TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
+                    taylor->numel() == B * Cin,
+                "taylor must be a contiguous float32 (B, Cin) GPU tensor");
+    tay = taylor->data_ptr<float>();
+  }
+  at::Tensor out;
+  if (want_out) out = at::empty({B, H, W, Cin}, g.options());
+  const int64_t sp = splits_ws(splits, ks * ks * Cout);
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
+  TP_CHECK_HIP(tp_conv_igemm(g.data_ptr<float>(), unpool ? g_argmax->data_ptr<uint8_t>() : nullptr,
+                             wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, (int)ks, 0,
+                             unpool ? 1 : 0, EPI_BWD, (int)cfg, (int)sp, sc, nullptr, 0,
+                             want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(), tay,
+                             (int)(H * W), sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+  return out;
+}
+
+// First conv layer (tiny Cin) on the VALU: NCHW input -> NHWC output, BN affine + ReLU fused.
+at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor& scale, const at::Tensor& shift,
+                      bool relu) {
+  need(x, "x", 4);
+  need(w, "w", 4);
+  const int64_t B = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = w.size(0);
+  TORCH_CHECK(w.size(1) == Cin && w.size(2) == 3 && w.size(3) == 3, "w must be (Cout, Cin, 3, 3)");
+  need(scale, "scale", 1);
+  need(shift, "shift", 1);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  auto out = at::empty({B, H, W, Cout}, x.options());
+  TP_CHECK_HIP(tp_conv_first_direct(x.data_ptr<float>(), w.data_ptr<float>(), scale.data_ptr<float>(),
+                                    shift.data_ptr<float>(), out.data_ptr<float>(), (int)B, (int)Cin, (int)H, (int)W,
+                                    (int)Cout, relu ? 1 : 0, cur_stream()));
+  return out;
+}
+
+}  // namespace
+
+void register_engine_ops_def(torch::Library& m) {
+  m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
+        "int splits) -> (Tensor, Tensor)");
+  m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
+        "bool want_out, int ks, int cfg, int splits) -> Tensor");
+  m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
+}
+
+void register_engine_ops_impl(torch::Library& m) {
+  m.impl("conv_fwd", &conv_fwd);
+  m.impl("conv_dgrad", &conv_dgrad);
+  m.impl("conv_first", &conv_first);
+}

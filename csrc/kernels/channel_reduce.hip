@@ -140,7 +140,57 @@ __global__ __launch_bounds__(256) void column_accumulate(const float* __restrict
   }
 }
 
+// Multi-layer score fold used by the fused engine after each backward: for every layer l,
+// v = |T_l[b,c]| (or signed); acc_l[c] += sum_b v; then T_l[b,c] <- v (keep per-sample slab)
+// or 0 (persistent arena ready for the next batch). One launch for all layers.
+struct ScoreDesc {
+  float* T;
+  double* acc;
+  int B;
+  int C;
+};
+struct ScoreBatch {
+  ScoreDesc d[16];
+};
+
+__global__ __launch_bounds__(256) void score_fold_multi(ScoreBatch batch, int take_abs, int after) {
+  __shared__ double ps[4][64];
+  const ScoreDesc s = batch.d[blockIdx.y];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  if (blockIdx.x * 64 >= s.C) return;  // uniform per block
+  double acc = 0.0;
+  if (c < s.C) {
+    for (int b = rg; b < s.B; b += 4) {
+      float* p = s.T + (long long)b * s.C + c;
+      float v = *p;
+      if (take_abs) v = fabsf(v);
+      acc += (double)v;
+      if (after == 1) *p = v;        // keep the processed per-sample value
+      else if (after == 2) *p = 0.f; // zero for the next batch
+    }
+  }
+  ps[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0 && c < s.C && s.acc)
+    s.acc[c] += ps[0][threadIdx.x] + ps[1][threadIdx.x] + ps[2][threadIdx.x] + ps[3][threadIdx.x];
+}
+
 }  // namespace tp
+
+extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, const int* B, const int* C, int count,
+                                          int take_abs, int after, hipStream_t st) {
+  if (count <= 0 || count > 16) return hipErrorInvalidValue;
+  tp::ScoreBatch b{};
+  int maxc = 0;
+  for (int i = 0; i < count; ++i) {
+    b.d[i] = tp::ScoreDesc{T[i], acc[i], B[i], C[i]};
+    maxc = std::max(maxc, C[i]);
+  }
+  dim3 grid(tp::ceil_div(maxc, 64), count);
+  tp::score_fold_multi<<<grid, 256, 0, st>>>(b, take_abs, after);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t tp_channel_reduce(const float* act, const float* grad, float* out, int B, int C,
                                         int S, int mode, int channels_last, hipStream_t st) {

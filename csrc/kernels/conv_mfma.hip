@@ -1,0 +1,526 @@
+// Implicit-GEMM 3x3 / 1x1 convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32) with
+// fused epilogues — the compute core of the fused attribution engine (SURVEY.md §2.5 K1/K2/K4,
+// K5 eval-mode BN folded, K6 NaN-propagating ReLU, K7 2x2 max-pool, K9c Taylor reduction).
+//
+// Layout: activations NHWC (channels contiguous), weights [Cout][KS][KS][Cin] = [n][k] with
+// k = (kh*KS + kw)*Cin + ci. GEMM view: M = B*H*W output pixels, N = Cout, K = KS*KS*Cin.
+// stride 1, padding (KS-1)/2 (the VGG / classifier shapes). dgrad of such a conv is the same
+// conv of dL/dy with flipped, transposed weights, so one kernel serves forward and backward.
+//
+// Tiling: 256 threads = 4 waves; block tile BM x BN, wave tile WM x WN made of 32x32 MFMA
+// tiles; K staged through double-buffered LDS in BK=32 slices (one conv tap, 32 channels).
+// Inside a K-slice lane (i, h) feeds k = h*16 + s at MFMA step s (any bijection works as long
+// as A and B agree), so each lane reads its 16 operands with 4 ds_read_b128 per fragment from
+// rows padded to 36 floats (144 B = 9 bank slots: conflict-free for ds_read_b128 groups).
+//
+// M ordering: plain (b, oh, ow) or POOLED_M (b, oh/2, ow/2, dy, dx). With POOLED_M the four
+// pixels of every 2x2 pooling window are rows 4g..4g+3 of a 32x32 MFMA tile, which the
+// accumulator layout (row = (r&3) + 8(r>>2) + 4(lane>>5)) places in ONE lane's registers
+// r = 4g..4g+3 — the max-pool is four in-register max operations.
+#include "tp_common.h"
+
+namespace tp {
+
+enum Epi : int {
+  EPI_FWD = 0,       // y = relu?(acc*scale[n] + shift[n]) stored NHWC
+  EPI_FWD_POOL = 1,  // + 2x2 max-pool: pooled value + argmax byte
+  EPI_BWD = 2,       // dgrad epilogue: Taylor partial of the consumer's activation, masked/scaled grad
+  EPI_PARTIAL = 3,   // raw split-K partial slab (epilogue applied by conv_epilogue)
+};
+
+struct ConvArgs {
+  // operands
+  const float* x;           // A source: NHWC [B][H][W][Cin] (or pooled grad [B][H/2][W/2][Cin] if UNPOOL)
+  const uint8_t* x_argmax;  // UNPOOL: argmax bytes of the pooled grad
+  const float* w;           // [N][K]
+  // shape
+  int B, H, W, Cin, N, K;   // K = KS*KS*Cin
+  int M;                    // B*H*W
+  int k_tiles_per_split;
+  // epilogue
+  const float* scale;       // [N] (EPI_FWD*) or BN scale of the consumer layer (EPI_BWD)
+  const float* shift;       // [N]
+  int relu;                 // EPI_FWD*: apply ReLU
+  float* out;               // EPI_FWD: [M][N]; POOL: [M/4][N]; BWD: masked grad [M][N] (nullable); PARTIAL: slab
+  uint8_t* out_argmax;      // POOL: [M/4][N]
+  const float* act;         // EPI_BWD: activation [M][N] the grad refers to
+  float* taylor;            // EPI_BWD: [B][N] fp32 per-sample sums (atomic), nullable
+  int HWo;                  // EPI_BWD: pixels per image at the grad's resolution
+};
+
+template <int BM, int BN, int WM, int WN>
+struct Tile {
+  static constexpr int BK = 32;
+  static constexpr int LDK = BK + 4;  // padded row (floats)
+  static constexpr int WAVES_N = BN / WN;
+  static constexpr int TM = WM / 32, TN = WN / 32;
+  static constexpr int A_CHUNKS = BM * BK / 4 / 256;  // float4 per thread per slice
+  static constexpr int B_CHUNKS = BN * BK / 4 / 256;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static_assert(A_CHUNKS >= 1 && B_CHUNKS >= 1, "tile too small");
+};
+
+__device__ __forceinline__ void pix_of(int m, int H, int W, bool pooled, int& b, int& oh, int& ow) {
+  const int HW = H * W;
+  b = m / HW;
+  const int r = m - b * HW;
+  if (pooled) {
+    const int w2 = W >> 1;
+    const int j = r >> 2, q = r & 3;
+    oh = (j / w2) * 2 + (q >> 1);
+    ow = (j % w2) * 2 + (q & 1);
+  } else {
+    oh = r / W;
+    ow = r - oh * W;
+  }
+}
+
+// Bijective XCD-aware remap: consecutive logical tiles share an XCD (blocks b, b+8 share one).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs p) {
+  using T = Tile<BM, BN, WM, WN>;
+  constexpr int BK = T::BK, LDK = T::LDK;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
+  constexpr int STAGE = (BM + BN) * LDK;  // floats per pipeline stage: A rows then B rows
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int n_tiles = (p.N + BN - 1) / BN;
+  const int m_tiles = (p.M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / n_tiles) * BM;
+  const int n0 = (tile % n_tiles) * BN;
+  if (m0 >= m_tiles * BM) return;
+  const int split = blockIdx.y;
+  const int kt_total = p.K / BK;
+  const int kt_begin = split * p.k_tiles_per_split;
+  const int kt_end = min(kt_total, kt_begin + p.k_tiles_per_split);
+  const int cin_tiles = p.Cin / BK;
+
+  // ---- per-thread A rows (pixel coordinates are loop invariant) --------------------------
+  int a_b[T::A_CHUNKS], a_oh[T::A_CHUNKS], a_ow[T::A_CHUNKS], a_c4[T::A_CHUNKS], a_row[T::A_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < T::A_CHUNKS; ++i) {
+    const int id = tid + i * 256;
+    a_row[i] = id / (BK / 4);
+    a_c4[i] = id % (BK / 4);
+    const int m = m0 + a_row[i];
+    if (m < p.M) {
+      pix_of(m, p.H, p.W, POOLED_M, a_b[i], a_oh[i], a_ow[i]);
+    } else {
+      a_b[i] = -1;
+      a_oh[i] = a_ow[i] = 0;
+    }
+  }
+  int b_row[T::B_CHUNKS], b_c4[T::B_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < T::B_CHUNKS; ++i) {
+    const int id = tid + i * 256;
+    b_row[i] = id / (BK / 4);
+    b_c4[i] = id % (BK / 4);
+  }
+
+  float4 ra[T::A_CHUNKS], rb[T::B_CHUNKS];
+
+  auto load_tile = [&](int kt) {
+    const int tap = kt / cin_tiles;
+    const int c0 = (kt - tap * cin_tiles) * BK;
+    const int dh = tap / KS - (KS - 1) / 2, dw = tap % KS - (KS - 1) / 2;
+#pragma unroll
+    for (int i = 0; i < T::A_CHUNKS; ++i) {
+      const int ih = a_oh[i] + dh, iw = a_ow[i] + dw;
+      const bool ok = a_b[i] >= 0 && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) {
+        const int c = c0 + a_c4[i] * 4;
+        if constexpr (UNPOOL) {
+          const int H2 = p.H >> 1, W2 = p.W >> 1;
+          const long long off = (((long long)a_b[i] * H2 + (ih >> 1)) * W2 + (iw >> 1)) * p.Cin + c;
+          const float4 g = *reinterpret_cast<const float4*>(p.x + off);
+          const uchar4 am = *reinterpret_cast<const uchar4*>(p.x_argmax + off);
+          const uint8_t q = (uint8_t)(((ih & 1) << 1) | (iw & 1));
+          v.x = am.x == q ? g.x : 0.f;
+          v.y = am.y == q ? g.y : 0.f;
+          v.z = am.z == q ? g.z : 0.f;
+          v.w = am.w == q ? g.w : 0.f;
+        } else {
+          const long long off = (((long long)a_b[i] * p.H + ih) * p.W + iw) * p.Cin + c;
+          v = *reinterpret_cast<const float4*>(p.x + off);
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_CHUNKS; ++i) {
+      const int n = n0 + b_row[i];
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n < p.N) v = *reinterpret_cast<const float4*>(p.w + (long long)n * p.K + kt * BK + b_c4[i] * 4);
+      rb[i] = v;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < T::A_CHUNKS; ++i)
+      *reinterpret_cast<float4*>(smem + buf * STAGE + a_row[i] * LDK + a_c4[i] * 4) = ra[i];
+#pragma unroll
+    for (int i = 0; i < T::B_CHUNKS; ++i)
+      *reinterpret_cast<float4*>(smem + buf * STAGE + (BM + b_row[i]) * LDK + b_c4[i] * 4) = rb[i];
+  };
+
+  f32x16 acc[T::TM][T::TN];
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int wm0 = (wave / T::WAVES_N) * WM;
+  const int wn0 = (wave % T::WAVES_N) * WN;
+  const int li = lane & 31, lh = lane >> 5;
+
+  if (kt_begin < kt_end) {
+    load_tile(kt_begin);
+    store_tile(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      const bool more = kt + 1 < kt_end;
+      if (more) load_tile(kt + 1);  // global loads in flight under the MFMAs below
+      const float* a_base = smem + buf * STAGE + (wm0 + li) * LDK + lh * 16;
+      const float* b_base = smem + buf * STAGE + (BM + wn0 + li) * LDK + lh * 16;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float4 af[T::TM], bf[T::TN];
+#pragma unroll
+        for (int i = 0; i < T::TM; ++i) af[i] = *reinterpret_cast<const float4*>(a_base + i * 32 * LDK + c * 4);
+#pragma unroll
+        for (int j = 0; j < T::TN; ++j) bf[j] = *reinterpret_cast<const float4*>(b_base + j * 32 * LDK + c * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+            for (int j = 0; j < T::TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+        }
+      }
+      if (more) store_tile(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // ---- epilogue --------------------------------------------------------------------------
+#pragma unroll
+  for (int j = 0; j < T::TN; ++j) {
+    const int n = n0 + wn0 + j * 32 + li;
+    const bool nok = n < p.N;
+    float sc = 1.f, sh = 0.f;
+    if constexpr (EPI == EPI_FWD || EPI == EPI_FWD_POOL || EPI == EPI_BWD) {
+      if (nok) {
+        sc = p.scale ? p.scale[n] : 1.f;
+        if constexpr (EPI != EPI_BWD) sh = p.shift ? p.shift[n] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i) {
+      const int mt = m0 + wm0 + i * 32;
+      if constexpr (EPI == EPI_FWD_POOL) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int m = mt + 8 * g + 4 * lh;  // first row of this pooling window
+          float best = 0.f;
+          int arg = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float v = acc[i][j][4 * g + q] * sc + sh;
+            if (p.relu) v = nan_relu(v);
+            if (q == 0 || v > best || (v != v && best == best)) {
+              best = v;
+              arg = q;
+            }
+          }
+          if (nok && m < p.M) {
+            const long long o = (long long)(m >> 2) * p.N + n;
+            p.out[o] = best;
+            p.out_argmax[o] = (uint8_t)arg;
+          }
+        }
+      } else if constexpr (EPI == EPI_BWD) {
+        int cur_b = -1;
+        float tsum = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int m = mt + 8 * g + 4 * lh + q;
+            if (nok && m < p.M) {
+              const long long o = (long long)m * p.N + n;
+              const float gval = acc[i][j][4 * g + q];
+              const float a = p.act[o];
+              if (p.taylor) {
+                const int b = m / p.HWo;
+                if (b != cur_b) {
+                  if (cur_b >= 0) atomicAdd(p.taylor + (long long)cur_b * p.N + n, tsum);
+                  cur_b = b;
+                  tsum = 0.f;
+                }
+                tsum += -(gval * a);
+              }
+              if (p.out) p.out[o] = a > 0.f ? gval * sc : 0.f;
+            }
+          }
+        }
+        if (p.taylor && cur_b >= 0) atomicAdd(p.taylor + (long long)cur_b * p.N + n, tsum);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mt + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (nok && m < p.M) {
+            float v = acc[i][j][r];
+            if constexpr (EPI == EPI_FWD) {
+              v = v * sc + sh;
+              if (p.relu) v = nan_relu(v);
+              p.out[(long long)m * p.N + n] = v;
+            } else {  // EPI_PARTIAL
+              p.out[((long long)split * p.M + m) * p.N + n] = v;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// Split-K combine + epilogue (deterministic order over the slabs), one thread per output
+// element (or per pooled element).
+template <int EPI>
+__global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __restrict__ slabs, int splits) {
+  const long long MN = (long long)p.M * p.N;
+  if constexpr (EPI == EPI_FWD_POOL) {
+    const long long total = MN / 4;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+      const int n = (int)(t % p.N);
+      const long long mp = t / p.N;
+      const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
+      float best = 0.f;
+      int arg = 0;
+      for (int q = 0; q < 4; ++q) {
+        const long long o = (mp * 4 + q) * p.N + n;
+        float v = 0.f;
+        for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
+        v = v * sc + sh;
+        if (p.relu) v = nan_relu(v);
+        if (q == 0 || v > best || (v != v && best == best)) {
+          best = v;
+          arg = q;
+        }
+      }
+      p.out[t] = best;
+      p.out_argmax[t] = (uint8_t)arg;
+    }
+  } else {
+    for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < MN;
+         o += (long long)gridDim.x * blockDim.x) {
+      const int n = (int)(o % p.N);
+      float v = 0.f;
+      for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
+      if constexpr (EPI == EPI_FWD) {
+        const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
+        v = v * sc + sh;
+        if (p.relu) v = nan_relu(v);
+        p.out[o] = v;
+      } else {  // EPI_BWD
+        const float a = p.act[o];
+        if (p.taylor) atomicAdd(p.taylor + (o / p.N / p.HWo) * p.N + n, -(v * a));
+        if (p.out) p.out[o] = a > 0.f ? v * (p.scale ? p.scale[n] : 1.f) : 0.f;
+      }
+    }
+  }
+}
+
+// First layer: direct conv on the VALU (Cin is tiny), NCHW fp32 input -> NHWC output with the
+// BN-eval affine and ReLU fused. A thread owns one output pixel x 4 channels, so COUT/4
+// consecutive lanes write one pixel's contiguous NHWC row (coalesced 16-B stores); the
+// Cin*9 input taps of a pixel are shared through L1 by those lanes.
+template <int COUT>
+__global__ __launch_bounds__(256) void conv_first_direct(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, float* __restrict__ out,
+                                                         int B, int Cin, int H, int W, int relu) {
+  constexpr int G = COUT / 4;
+  extern __shared__ float4 wsh4[];  // [Cin*9][G] float4 (4 output channels per entry)
+  const int KK = Cin * 9;
+  float* wsh = reinterpret_cast<float*>(wsh4);
+  for (int t = threadIdx.x; t < KK * COUT; t += blockDim.x) {
+    const int n = t % COUT, k = t / COUT;  // w is [COUT][Cin][3][3]
+    wsh[t] = w[n * KK + k];
+  }
+  __syncthreads();
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long pix = gt / G;
+  const int grp = (int)(gt % G);
+  if (pix >= (long long)B * H * W) return;
+  const int b = (int)(pix / (H * W));
+  const int r = (int)(pix % (H * W));
+  const int oh = r / W, ow = r % W;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int c = 0; c < Cin; ++c) {
+    const float* xc = x + ((long long)b * Cin + c) * H * W;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ih = oh + kh - 1, iw = ow + kw - 1;
+        const float v = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xc[ih * W + iw] : 0.f;
+        const float4 wk = wsh4[((c * 3 + kh) * 3 + kw) * G + grp];
+        acc.x = fmaf(v, wk.x, acc.x);
+        acc.y = fmaf(v, wk.y, acc.y);
+        acc.z = fmaf(v, wk.z, acc.z);
+        acc.w = fmaf(v, wk.w, acc.w);
+      }
+    }
+  }
+  const int n = grp * 4;
+  float4 v;
+  v.x = acc.x * scale[n] + shift[n];
+  v.y = acc.y * scale[n + 1] + shift[n + 1];
+  v.z = acc.z * scale[n + 2] + shift[n + 2];
+  v.w = acc.w * scale[n + 3] + shift[n + 3];
+  if (relu) {
+    v.x = nan_relu(v.x);
+    v.y = nan_relu(v.y);
+    v.z = nan_relu(v.z);
+    v.w = nan_relu(v.w);
+  }
+  *reinterpret_cast<float4*>(out + pix * COUT + n) = v;
+}
+
+}  // namespace tp
+
+// ------------------------------------------------------------------------------------------
+// Host launchers
+// ------------------------------------------------------------------------------------------
+namespace {
+
+using tp::ConvArgs;
+
+template <int BM, int BN, int WM, int WN, int KS, bool PM, bool UP, int EPI>
+hipError_t launch_cfg(const ConvArgs& a, int splits, hipStream_t st) {
+  const int m_tiles = (a.M + BM - 1) / BM, n_tiles = (a.N + BN - 1) / BN;
+  dim3 grid(m_tiles * n_tiles, splits);
+  tp::conv_igemm<BM, BN, WM, WN, KS, PM, UP, EPI><<<grid, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+// cfg: 0 = 128x128 (waves 2x2 of 64x64), 1 = 256x64 (4x1 of 64x64), 2 = 64x64 (2x2 of 32x32),
+//      3 = 128x64 (2x2 of 64x32)
+template <int KS, bool PM, bool UP, int EPI>
+hipError_t launch_any(int cfg, const ConvArgs& a, int splits, hipStream_t st) {
+  switch (cfg) {
+    case 0: return launch_cfg<128, 128, 64, 64, KS, PM, UP, EPI>(a, splits, st);
+    case 1: return launch_cfg<256, 64, 64, 64, KS, PM, UP, EPI>(a, splits, st);
+    case 2: return launch_cfg<64, 64, 32, 32, KS, PM, UP, EPI>(a, splits, st);
+    case 3: return launch_cfg<128, 64, 64, 32, KS, PM, UP, EPI>(a, splits, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int KS>
+hipError_t dispatch_epi(int cfg, int epi, bool pooled_m, bool unpool, const ConvArgs& a, int splits,
+                        hipStream_t st) {
+  using namespace tp;
+  if (epi == EPI_FWD_POOL) {
+    if (!pooled_m || unpool) return hipErrorInvalidValue;
+    return launch_any<KS, true, false, EPI_FWD_POOL>(cfg, a, splits, st);
+  }
+  if (epi == EPI_PARTIAL) {
+    if (pooled_m) return unpool ? launch_any<KS, true, true, EPI_PARTIAL>(cfg, a, splits, st)
+                                : launch_any<KS, true, false, EPI_PARTIAL>(cfg, a, splits, st);
+    return unpool ? launch_any<KS, false, true, EPI_PARTIAL>(cfg, a, splits, st)
+                  : launch_any<KS, false, false, EPI_PARTIAL>(cfg, a, splits, st);
+  }
+  if (pooled_m) return hipErrorInvalidValue;
+  if (epi == EPI_FWD) return unpool ? launch_any<KS, false, true, EPI_FWD>(cfg, a, splits, st)
+                                    : launch_any<KS, false, false, EPI_FWD>(cfg, a, splits, st);
+  if (epi == EPI_BWD) return unpool ? launch_any<KS, false, true, EPI_BWD>(cfg, a, splits, st)
+                                    : launch_any<KS, false, false, EPI_BWD>(cfg, a, splits, st);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// Main entry. ``ws`` is a workspace of splits*M*N floats when splits > 1.
+extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w, int B, int H, int W,
+                                    int Cin, int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits,
+                                    const float* scale, const float* shift, int relu, float* out,
+                                    uint8_t* out_argmax, const float* act, float* taylor, int HWo, float* ws,
+                                    hipStream_t st) {
+  using namespace tp;
+  if (Cin % 32 != 0) return hipErrorInvalidValue;
+  ConvArgs a{};
+  a.x = x;
+  a.x_argmax = x_argmax;
+  a.w = w;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.N = Cout;
+  a.K = ks * ks * Cin;
+  a.M = B * H * W;
+  const int kt = a.K / 32;
+  splits = std::max(1, std::min(splits, kt));
+  a.k_tiles_per_split = (kt + splits - 1) / splits;
+  splits = (kt + a.k_tiles_per_split - 1) / a.k_tiles_per_split;
+  a.scale = scale;
+  a.shift = shift;
+  a.relu = relu;
+  a.out = out;
+  a.out_argmax = out_argmax;
+  a.act = act;
+  a.taylor = taylor;
+  a.HWo = HWo;
+  if (splits == 1 || epi == EPI_PARTIAL) {
+    ConvArgs b = a;
+    if (epi == EPI_PARTIAL) b.out = ws ? ws : out;
+    return ks == 3 ? dispatch_epi<3>(cfg, epi, pooled_m, unpool, b, splits, st)
+                   : dispatch_epi<1>(cfg, epi, pooled_m, unpool, b, splits, st);
+  }
+  // split-K: partial slabs then a deterministic combine + epilogue
+  ConvArgs b = a;
+  b.out = ws;
+  hipError_t e = ks == 3 ? dispatch_epi<3>(cfg, EPI_PARTIAL, pooled_m, unpool, b, splits, st)
+                         : dispatch_epi<1>(cfg, EPI_PARTIAL, pooled_m, unpool, b, splits, st);
+  if (e != hipSuccess) return e;
+  const long long MN = (long long)a.M * a.N;
+  const long long work = epi == EPI_FWD_POOL ? MN / 4 : MN;
+  unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
+  if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
+  else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
+  else if (epi == EPI_BWD) conv_epilogue<EPI_BWD><<<grid, 256, 0, st>>>(a, ws, splits);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift,
+                                           float* out, int B, int Cin, int H, int W, int Cout, int relu,
+                                           hipStream_t st) {
+  const long long pix = (long long)B * H * W;
+  const unsigned grid = tp::ceil_div(pix * (Cout / 4), 256);
+  const size_t lds = (size_t)Cin * 9 * Cout * sizeof(float);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  if (Cout == 64) tp::conv_first_direct<64><<<grid, 256, lds, st>>>(x, w, scale, shift, out, B, Cin, H, W, relu);
+  else if (Cout == 32) tp::conv_first_direct<32><<<grid, 256, lds, st>>>(x, w, scale, shift, out, B, Cin, H, W, relu);
+  else if (Cout == 16) tp::conv_first_direct<16><<<grid, 256, lds, st>>>(x, w, scale, shift, out, B, Cin, H, W, relu);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}

@@ -1,0 +1,181 @@
+"""Fused conv/GEMM kernels (csrc/kernels/conv_mfma.hip) vs plain PyTorch fp32 references, and
+the fused VGG engine vs the generic hook path."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # B, H, W, Cin, Cout
+    (4, 32, 32, 64, 64),
+    (3, 16, 16, 128, 128),
+    (5, 8, 8, 256, 256),
+    (6, 4, 4, 512, 512),
+    (16, 2, 2, 512, 512),
+    (2, 6, 10, 32, 96),
+]
+
+
+def _rand(*shape, gen):
+    return torch.randn(*shape, generator=gen)
+
+
+def _ref_fwd(x_nhwc, w, scale, shift, relu, pool):
+    x = x_nhwc.permute(0, 3, 1, 2).double()
+    y = F.conv2d(x, w.double(), padding=w.shape[-1] // 2)
+    y = y * scale.double().view(1, -1, 1, 1) + shift.double().view(1, -1, 1, 1)
+    if relu:
+        y = y.clamp_min(0)
+    am = None
+    if pool:
+        y, idx = F.max_pool2d(y, 2, return_indices=True)
+        H = x.shape[2]
+        W = x.shape[3]
+        ih, iw = idx // W, idx % W
+        am = ((ih % 2) * 2 + (iw % 2)).permute(0, 2, 3, 1)
+    return y.permute(0, 2, 3, 1).float(), am
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("pool", [False, True])
+def test_conv_fwd(cuda, shape, cfg, splits, pool):
+    from torchpruner_amd import ops
+    T = ops.require()
+    B, H, W, Cin, Cout = shape
+    g = torch.Generator().manual_seed(hash((shape, cfg)) % 1000)
+    x = _rand(B, H, W, Cin, gen=g)
+    w = _rand(Cout, Cin, 3, 3, gen=g) * (2.0 / (9 * Cin)) ** 0.5
+    scale = _rand(Cout, gen=g).abs() + 0.5
+    shift = _rand(Cout, gen=g) * 0.1
+    ref, am_ref = _ref_fwd(x, w, scale, shift, True, pool)
+    wk = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous()
+    out, am = T.conv_fwd(x.to(cuda), wk.to(cuda), scale.to(cuda), shift.to(cuda), True, pool, 3, cfg, splits)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-4)
+    if pool:
+        # argmax must point at the max (ties are measure-zero for random data)
+        assert (am.cpu().long() == am_ref).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("B,K,N", [(37, 512, 512), (37, 512, 10), (256, 512, 512), (8, 4096, 96)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_linear_fwd(cuda, B, K, N, relu):
+    from torchpruner_amd import ops
+    T = ops.require()
+    g = torch.Generator().manual_seed(B + K + N)
+    x = _rand(B, K, gen=g)
+    w = _rand(N, K, gen=g) / K ** 0.5
+    b = _rand(N, gen=g)
+    ref = F.linear(x.double(), w.double(), b.double())
+    if relu:
+        ref = ref.clamp_min(0)
+    for cfg in (0, 2, 3):
+        out, _ = T.conv_fwd(x.view(B, 1, 1, K).to(cuda), w.to(cuda), None, b.to(cuda), relu, False, 1, cfg, 2)
+        torch.testing.assert_close(out.view(B, N).cpu(), ref.float(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("cfg", [0, 2, 3])
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("unpool", [False, True])
+def test_conv_dgrad_taylor(cuda, shape, cfg, splits, unpool):
+    from torchpruner_amd import ops
+    T = ops.require()
+    B, H, W, Cin, Cout = shape  # conv maps Cin -> Cout; dgrad goes back to Cin
+    g = torch.Generator().manual_seed(7 + hash(shape) % 100)
+    w = _rand(Cout, Cin, 3, 3, gen=g) * (1.0 / (9 * Cin)) ** 0.5
+    act = torch.relu(_rand(B, H, W, Cin, gen=g))  # post-ReLU activation at the conv input
+    bn_scale = _rand(Cin, gen=g).abs() + 0.5
+    if unpool:
+        gp = _rand(B, H // 2, W // 2, Cout, gen=g)
+        am = torch.randint(0, 4, (B, H // 2, W // 2, Cout), generator=g, dtype=torch.uint8)
+        gfull = torch.zeros(B, H, W, Cout)
+        for q in range(4):
+            dy, dx = q // 2, q % 2
+            gfull[:, dy::2, dx::2, :] = torch.where(am == q, gp, torch.zeros(()))
+    else:
+        gfull = _rand(B, H, W, Cout, gen=g)
+    # reference: dL/dx of the conv, Taylor of act, masked/scaled grad
+    dx = torch.nn.grad.conv2d_input((B, Cin, H, W), w.double(), gfull.permute(0, 3, 1, 2).double(), padding=1)
+    dx = dx.permute(0, 2, 3, 1)
+    tay_ref = (-(dx * act.double())).sum((1, 2))
+    out_ref = torch.where(act > 0, dx * bn_scale.double(), torch.zeros((), dtype=torch.float64))
+    wt = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, -1).contiguous()
+    tay = torch.zeros(B, Cin, device=cuda)
+    gin = (gp if unpool else gfull).to(cuda)
+    out = T.conv_dgrad(gin, am.to(cuda) if unpool else None, wt.to(cuda), act.to(cuda), bn_scale.to(cuda), tay,
+                       True, 3, cfg, splits)
+    torch.testing.assert_close(out.cpu(), out_ref.float(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(tay.cpu(), tay_ref.float(), rtol=1e-4, atol=1e-3)
+
+
+def test_conv_first(cuda):
+    from torchpruner_amd import ops
+    T = ops.require()
+    g = torch.Generator().manual_seed(3)
+    x = _rand(5, 3, 32, 32, gen=g)
+    w = _rand(64, 3, 3, 3, gen=g) * 0.3
+    s = _rand(64, gen=g).abs()
+    t = _rand(64, gen=g)
+    ref = (F.conv2d(x.double(), w.double(), padding=1) * s.double().view(1, -1, 1, 1)
+           + t.double().view(1, -1, 1, 1)).clamp_min(0).permute(0, 2, 3, 1)
+    out = T.conv_first(x.to(cuda), w.to(cuda), s.to(cuda), t.to(cuda), True)
+    torch.testing.assert_close(out.cpu(), ref.float(), rtol=1e-4, atol=1e-4)
+
+
+def test_nan_propagation(cuda):
+    """The pruner's NaN probe relies on NaN surviving conv+ReLU+pool (SURVEY §7.3 hard part 2)."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    x = torch.randn(2, 4, 4, 32)
+    x[:, 1, 1, 5] = float("nan")
+    w = torch.randn(32, 32 * 9) * 0.1
+    out, am = T.conv_fwd(x.to(cuda), w.to(cuda), None, None, True, True, 3, 2, 1)
+    assert torch.isnan(out.cpu()[:, 0, 0]).all()  # the window covering the NaN's receptive field
+
+
+def test_engine_taylor_matches_generic_path(cuda):
+    from torchpruner_amd import TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.models import prunable_vgg16
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(0)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    lins = [model.classifier[1], model.classifier[4]]
+    x = torch.randn(48, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (48,), device=cuda)
+    dl = DeviceLoader(x, y, 16)
+    ev = [find_best_module_for_attributions(model, m) for m in convs + lins]
+    assert maybe_engine(model, ev, F.cross_entropy, cuda) is not None
+    # fp64 CPU oracle of the same attribution
+    import copy
+    m64 = copy.deepcopy(model).double().cpu()
+    c64 = [m for m in m64.features if isinstance(m, torch.nn.Conv2d)] + [m64.classifier[1], m64.classifier[4]]
+    dl64 = DeviceLoader(x.double().cpu(), y.cpu(), 16)
+    for signed in (False, True):
+        for red in ("mean", "none"):
+            fused = TaylorAttributionMetric(model, dl, F.cross_entropy, cuda, signed=signed, reduction=red).run_many(
+                convs + lins, find_best_evaluation_module=True)
+            os.environ["TORCHPRUNER_BACKEND"] = "torch"
+            try:
+                generic = TaylorAttributionMetric(model, dl, F.cross_entropy, cuda, signed=signed,
+                                                  reduction=red).run_many(convs + lins, True)
+                exact = TaylorAttributionMetric(m64, dl64, F.cross_entropy, "cpu", signed=signed,
+                                                reduction=red).run_many(c64, True)
+            finally:
+                del os.environ["TORCHPRUNER_BACKEND"]
+            for a, b, e in zip(fused, generic, exact):
+                scale = np.abs(e).max() + 1e-30
+                err_fused = np.abs(a - e).max() / scale
+                err_generic = np.abs(b - e).max() / scale
+                print(f"signed={signed} red={red} fused_err={err_fused:.2e} miopen_err={err_generic:.2e}")
+                # deep ReLU nets amplify rounding through mask flips; the fused fp32 MFMA path must
+                # be at least as close to fp64 as MIOpen's fp32 (Winograd) path
+                assert err_fused < (5e-3 if red == "mean" else 2e-2), (err_fused, err_generic)
+                assert err_fused <= 1.5 * err_generic + 1e-5, (err_fused, err_generic)

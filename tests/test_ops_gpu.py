@@ -106,3 +106,21 @@ def test_cross_entropy(cuda, nc):
     l, g = ops.cross_entropy(x.to(cuda), t.to(cuda), 1 / 37, True)
     torch.testing.assert_close(l.cpu(), l_ref, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(g.cpu(), g_ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("after", [0, 1, 2])
+@pytest.mark.parametrize("take_abs", [False, True])
+def test_score_fold(cuda, after, take_abs):
+    g = torch.Generator().manual_seed(after)
+    Ts = [torch.randn(7, c, generator=g) for c in (3, 64, 130, 512)] * 5  # 20 slabs -> 2 launches
+    ref_T = [t.abs() if take_abs else t.clone() for t in Ts]
+    acc_ref = [torch.full((t.shape[1],), 0.5, dtype=torch.float64) + r.double().sum(0) for t, r in zip(Ts, ref_T)]
+    Td = [t.to(cuda) for t in Ts]
+    accs = [torch.full((t.shape[1],), 0.5, dtype=torch.float64, device=cuda) for t in Ts]
+    accs[3] = None
+    ops.score_fold_(Td, accs, take_abs, after)
+    for i, (t, a) in enumerate(zip(Td, accs)):
+        if a is not None:
+            torch.testing.assert_close(a.cpu(), acc_ref[i])
+        exp = Ts[i] if after == 0 else (ref_T[i] if after == 1 else torch.zeros_like(Ts[i]))
+        torch.testing.assert_close(t.cpu(), exp)

@@ -57,6 +57,13 @@ class ScoreAccumulator:
         self.slabs: list[tuple[int, torch.Tensor]] = []
         self.dtype = None
 
+    def ensure_sum(self, C: int, device) -> torch.Tensor:
+        """The fp64 (C,) running sum (allocated on first use) for kernels that fold into it."""
+        if self.sum is None:
+            self.sum = torch.zeros(C, dtype=torch.float64, device=device)
+            self.dtype = torch.float32
+        return self.sum
+
     def add(self, v: torch.Tensor, batch_index: int):
         """Add a (B, C) per-sample score slab for global batch ``batch_index``."""
         if self.dtype is None:

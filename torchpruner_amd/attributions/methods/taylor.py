@@ -5,6 +5,7 @@ The activation and gradient are read once by one fused HIP reduction; the refere
 full activation clone per batch and leaks it on the module (taylor.py:35).
 """
 from ... import ops
+from ...engine import maybe_engine
 from ..base import _AttributionMetric
 
 
@@ -23,5 +24,32 @@ class TaylorAttributionMetric(_AttributionMetric):
     def _run_modules(self, eval_modules):
         mode = "taylor_signed" if self.signed else "taylor"
         accs = [self._new_accumulator() for _ in eval_modules]
-        self._grad_capture_pass(eval_modules, lambda k, a, g, i: accs[k].add(ops.channel_reduce(a, g, mode), i))
+        fused = maybe_engine(self.model, eval_modules, self.criterion, self.device)
+        if fused is not None:
+            # native path: one fused forward + input-grad backward scores every module, then
+            # ONE fold launch turns all layers' per-sample sums into |.| and fp64 accumulators
+            engine, blocks = fused
+            owner = {}
+            for k, b in enumerate(blocks):
+                owner.setdefault(b, k)
+            uniq = sorted(owner)
+            stats = accs[0].mode == "stats"
+            for i, x, y in self._batches():
+                B = x.shape[0]
+                if stats:
+                    arena = engine.score_arena(B, uniq, x.device)
+                    engine.taylor(x, y, set(uniq), arena)
+                    sums = [accs[owner[b]].ensure_sum(arena[b].shape[1], x.device) for b in uniq]
+                    ops.score_fold_([arena[b] for b in uniq], sums, not self.signed, 2)
+                    for b in uniq:
+                        accs[owner[b]].count += B
+                else:
+                    res = engine.taylor(x, y, set(uniq))
+                    ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), not self.signed, 1)
+                    for b in uniq:
+                        accs[owner[b]].add(res[b], i)
+            accs = [accs[owner[b]] for b in blocks]
+        else:
+            self._grad_capture_pass(eval_modules,
+                                    lambda k, a, g, i: accs[k].add(ops.channel_reduce(a, g, mode), i))
         return [self._finalize(a) for a in accs]

@@ -1,0 +1,381 @@
+"""Fused attribution engine for conv chains (VGG-style CNNs and MLP heads) on MI355X.
+
+The reference scores one module per full forward+backward pass, through PyTorch hooks, with
+the conv/BN/ReLU/pool ops as separate cuDNN/ATen kernels (attributions.py:58-68,
+taylor.py:18-49). This engine lowers an eval-mode chain
+
+    [Conv3x3 -> BN -> ReLU (-> MaxPool2x2)]*  -> flatten -> [Dropout] Linear [ReLU] ...
+
+into a handful of HIP kernels per layer and computes Taylor scores for EVERY layer in ONE
+forward + input-gradient-only backward:
+
+forward   conv_first (VALU direct conv, NCHW->NHWC) then conv_fwd per layer: implicit-GEMM
+          fp32 MFMA with BN folded into a per-channel affine, NaN-propagating ReLU and the
+          2x2 max-pool fused in the epilogue (pooled value + argmax byte stored; the
+          full-resolution activation never touches HBM).
+loss      fused softmax cross-entropy: per-sample loss and dL/dlogits in one kernel.
+backward  conv_dgrad per layer: the same GEMM on flipped/transposed weights; its epilogue
+          reads the consumer activation once and emits (a) the Taylor partial
+          sum_hw -(dL/da * a) per (sample, channel) and (b) dL/d(pre-activation) masked by
+          the ReLU and scaled by the BN scale. Max-pool backward is fused into the NEXT
+          dgrad's operand loader (unpool by argmax on the fly).
+          No weight gradients, no autograd graph, no activation clones, no host syncs.
+
+Numerics: fp32 end to end (MFMA f32 is a bit-exact fp32 FMA chain); BN folding and GEMM
+summation order differ from cuDNN/MIOpen only at rounding level.
+"""
+from __future__ import annotations
+
+import math
+import weakref
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+# tile configs of conv_mfma.hip: 0=128x128, 1=256x64, 2=64x64, 3=128x64
+_CU = 256
+
+
+def _pick_cfg(M: int, N: int, K: int):
+    """Choose (tile cfg, split-K) so a launch has enough workgroups for 256 CUs."""
+    cands = [(0, 128, 128), (3, 128, 64), (1, 256, 64), (2, 64, 64)]
+    best = None
+    for cfg, bm, bn in cands:
+        if N <= 64 and bn == 128:
+            continue
+        tiles = math.ceil(M / bm) * math.ceil(N / bn)
+        splits = 1
+        kt = K // 32
+        while tiles * splits < 2 * _CU and splits * 2 <= kt // 4 and splits < 16:
+            splits *= 2
+        waste = (math.ceil(M / bm) * bm * math.ceil(N / bn) * bn) / (M * N)
+        # prefer big tiles when the grid is full anyway; small tiles / split-K otherwise
+        score = (min(tiles * splits, 2 * _CU) / (2 * _CU)) / waste * (1.0 if bm * bn >= 128 * 64 else 0.85)
+        score *= 1.0 if splits == 1 else 0.9
+        if best is None or score > best[0]:
+            best = (score, cfg, splits)
+    return best[1], best[2]
+
+
+@dataclass
+class ConvBlock:
+    conv: nn.Conv2d
+    bn: Optional[nn.BatchNorm2d]
+    relu: Optional[nn.Module]
+    pool: Optional[nn.MaxPool2d]
+    first: bool = False
+
+
+@dataclass
+class LinearBlock:
+    linear: nn.Linear
+    relu: Optional[nn.Module]
+
+
+@dataclass
+class Plan:
+    convs: list = field(default_factory=list)
+    linears: list = field(default_factory=list)
+
+    def eval_module_of(self, i):
+        blk = self.blocks[i]
+        return blk.relu
+
+    @property
+    def blocks(self):
+        return self.convs + self.linears
+
+
+def _stages(model):
+    if hasattr(model, "_stages"):
+        return list(model._stages())
+    if isinstance(model, nn.Sequential):
+        return list(model.children())
+    return None
+
+
+def build_plan(model: nn.Module):
+    """Lower ``model`` to a Plan, or return (None, reason)."""
+    stages = _stages(model)
+    if stages is None:
+        return None, "model has no linear stage list (forward_partial chain or nn.Sequential)"
+    plan = Plan()
+    i = 0
+    n = len(stages)
+    while i < n and isinstance(stages[i], nn.Conv2d):
+        conv = stages[i]
+        if conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1) or \
+                conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros":
+            return None, f"unsupported conv {conv}"
+        i += 1
+        bn = relu = pool = None
+        if i < n and isinstance(stages[i], nn.BatchNorm2d):
+            bn = stages[i]
+            i += 1
+        if i < n and isinstance(stages[i], nn.ReLU):
+            relu = stages[i]
+            i += 1
+        if relu is None:
+            return None, "conv block without ReLU"
+        if i < n and isinstance(stages[i], nn.MaxPool2d):
+            pool = stages[i]
+            k = pool.kernel_size if isinstance(pool.kernel_size, int) else pool.kernel_size[0]
+            s = pool.stride if isinstance(pool.stride, int) else pool.stride[0]
+            if k != 2 or s != 2 or pool.padding not in (0, (0, 0)) or pool.dilation not in (1, (1, 1)) \
+                    or pool.ceil_mode:
+                return None, f"unsupported pool {pool}"
+            i += 1
+        first = len(plan.convs) == 0
+        if first and (conv.in_channels % 32 != 0):
+            if pool is not None or conv.out_channels not in (16, 32, 64):
+                return None, "first conv must be unpooled with 16/32/64 outputs"
+        elif conv.in_channels % 32 != 0:
+            return None, "conv input channels must be a multiple of 32"
+        plan.convs.append(ConvBlock(conv, bn, relu, pool, first=first and conv.in_channels % 32 != 0))
+    if not plan.convs:
+        return None, "no conv stack"
+    # flatten
+    if i < n and (isinstance(stages[i], nn.Flatten) or getattr(stages[i], "__name__", "") == "_flatten"):
+        i += 1
+    else:
+        return None, "expected flatten after the conv stack"
+    while i < n:
+        st = stages[i]
+        if isinstance(st, nn.Dropout):
+            i += 1
+            continue
+        if isinstance(st, nn.Linear):
+            i += 1
+            relu = None
+            if i < n and isinstance(stages[i], nn.ReLU):
+                relu = stages[i]
+                i += 1
+            plan.linears.append(LinearBlock(st, relu))
+            continue
+        return None, f"unsupported classifier stage {st}"
+    if not plan.linears or any(b.relu is None for b in plan.linears[:-1]) or plan.linears[-1].relu is not None:
+        return None, "classifier must be Linear(+ReLU) blocks ending in a plain Linear"
+    if plan.linears[0].linear.in_features != plan.convs[-1].conv.out_channels:
+        return None, "features must end at 1x1 spatial resolution"
+    return plan, ""
+
+
+class FusedChainEngine:
+    """Executes a Plan with the HIP kernels. Weights are re-packed lazily whenever a
+    parameter changes identity, storage or version (e.g. after pruning / training)."""
+
+    def __init__(self, model: nn.Module, plan: Plan):
+        self.plan = plan
+        self._key = None
+        self._packed = None
+        self._arenas = {}
+
+    # ------------------------------------------------------------------ weights
+    def _params_key(self):
+        key = []
+        for b in self.plan.convs:
+            for t in (b.conv.weight, b.conv.bias) + ((b.bn.weight, b.bn.bias, b.bn.running_mean, b.bn.running_var)
+                                                     if b.bn is not None else ()):
+                if t is not None:
+                    key.append((t.data_ptr(), t._version, tuple(t.shape)))
+        for b in self.plan.linears:
+            for t in (b.linear.weight, b.linear.bias):
+                if t is not None:
+                    key.append((t.data_ptr(), t._version, tuple(t.shape)))
+        return tuple(key)
+
+    @torch.no_grad()
+    def _pack(self):
+        key = self._params_key()
+        if key == self._key:
+            return self._packed
+        convs = []
+        for b in self.plan.convs:
+            w = b.conv.weight.detach().float()
+            cout = w.shape[0]
+            bias = b.conv.bias.detach().float() if b.conv.bias is not None else torch.zeros(cout, device=w.device)
+            if b.bn is not None:
+                inv = torch.rsqrt(b.bn.running_var.float() + b.bn.eps)
+                g = b.bn.weight.float() if b.bn.weight is not None else torch.ones_like(inv)
+                beta = b.bn.bias.float() if b.bn.bias is not None else torch.zeros_like(inv)
+                scale = g * inv
+                shift = (bias - b.bn.running_mean.float()) * scale + beta
+            else:
+                scale = torch.ones(cout, device=w.device)
+                shift = bias
+            entry = {"scale": scale.contiguous(), "shift": shift.contiguous(), "pool": b.pool is not None}
+            if b.first:
+                entry["w_first"] = w.contiguous()
+            else:
+                entry["w"] = w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous()  # [n][(kh,kw,ci)]
+            # dgrad operand: flipped taps, transposed channels -> [ci][(kh,kw,co)]
+            entry["wt"] = w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1).contiguous()
+            convs.append(entry)
+        lins = []
+        for b in self.plan.linears:
+            w = b.linear.weight.detach().float()
+            n_out = w.shape[0]
+            bias = b.linear.bias.detach().float() if b.linear.bias is not None else torch.zeros(n_out, device=w.device)
+            pad = (-n_out) % 32
+            wt = w.t()
+            if pad:
+                wt = torch.cat([wt, torch.zeros(wt.shape[0], pad, device=w.device)], 1)
+            lins.append({"w": w.contiguous(), "bias": bias.contiguous(), "wt": wt.contiguous(), "pad": pad,
+                         "relu": b.relu is not None})
+        self._packed = {"convs": convs, "lins": lins}
+        self._key = key
+        return self._packed
+
+    # ------------------------------------------------------------------ execution
+    def forward(self, x: torch.Tensor):
+        """Forward pass; returns (logits, saved) where saved holds what backward needs."""
+        T = ops.require()
+        P = self._pack()
+        B = x.shape[0]
+        acts = []  # per conv: (activation NHWC (pooled if pool), argmax or None)
+        h = None
+        for ci, (blk, e) in enumerate(zip(self.plan.convs, P["convs"])):
+            if ci == 0 and blk.first:
+                h = T.conv_first(x.float().contiguous(), e["w_first"], e["scale"], e["shift"], True)
+                acts.append((h, None))
+                continue
+            if ci == 0:
+                h = x.float().permute(0, 2, 3, 1).contiguous()
+            M = h.shape[0] * h.shape[1] * h.shape[2]
+            cfg, sp = _pick_cfg(M, e["scale"].numel(), e["w"].shape[1])
+            out, am = T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
+            h = out
+            acts.append((out, am if e["pool"] else None))
+        feats = h.reshape(B, 1, 1, -1)
+        lin_acts = [feats]
+        for li, e in enumerate(P["lins"]):
+            cfg, sp = _pick_cfg(B, e["w"].shape[0], e["w"].shape[1])
+            out, _ = T.conv_fwd(lin_acts[-1], e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp)
+            lin_acts.append(out)
+        logits = lin_acts[-1].reshape(B, -1)
+        return logits, {"acts": acts, "lin_acts": lin_acts}
+
+    def score_arena(self, B: int, want, device):
+        """Persistent zeroed (B, C) score slabs for the blocks in ``want`` (one allocation).
+        The caller must leave them zeroed (ops.score_fold_ with after=2) for reuse."""
+        key = (B, tuple(sorted(want)), str(device))
+        arena = self._arenas.get(key)
+        if arena is None:
+            widths = {b: self._block_width(b) for b in sorted(want)}
+            flat = torch.zeros(B * sum(widths.values()), device=device)
+            arena, off = {}, 0
+            for b, c in widths.items():
+                arena[b] = flat[off:off + B * c].view(B, c)
+                off += B * c
+            self._arenas[key] = arena
+        return arena
+
+    def _block_width(self, b):
+        blocks = self.plan.blocks
+        blk = blocks[b]
+        return blk.conv.out_channels if isinstance(blk, ConvBlock) else blk.linear.out_features
+
+    def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None):
+        """One fused forward+backward; returns {block index: (B, C) per-sample signed Taylor
+        sums sum_hw -(dL/da * a)} for every requested block (conv blocks first, then
+        linear blocks; the final linear has none)."""
+        T = ops.require()
+        P = self._pack()
+        nconv, nlin = len(self.plan.convs), len(self.plan.linears)
+        if want is None:
+            want = set(range(nconv + nlin - 1))
+        if arena is None:
+            arena = {b: torch.zeros(x.shape[0], self._block_width(b), device=x.device) for b in want}
+        logits, saved = self.forward(x)
+        B = logits.shape[0]
+        _, g = ops.cross_entropy(logits, y, 1.0 / B, True)
+        lin_acts = saved["lin_acts"]
+        acts = saved["acts"]
+        res = {}
+        # classifier (dgrad of linear j produces the grad at its input = output of block j-1)
+        e_last = P["lins"][-1]
+        if e_last["pad"]:
+            g = torch.cat([g, torch.zeros(B, e_last["pad"], device=g.device)], 1)
+        g = g.reshape(B, 1, 1, -1).contiguous()
+        for j in range(nlin - 1, -1, -1):
+            e = P["lins"][j]
+            act = lin_acts[j]  # input of linear j
+            blk_index = nconv + j - 1  # the block whose output is `act`
+            taylor = None
+            if blk_index in want:
+                taylor = arena[blk_index]
+                res[blk_index] = taylor
+            bn_scale = P["convs"][-1]["scale"] if j == 0 else None
+            cfg, sp = _pick_cfg(B, act.shape[3], e["wt"].shape[1])
+            g = T.conv_dgrad(g, None, e["wt"], act, bn_scale, taylor, True, 1, cfg, sp)
+        # conv stack: g is dL/d(pre-activation of conv nconv-1) * bn_scale, at the
+        # (pooled, if pooled) output resolution of that block
+        for ci in range(nconv - 1, 0, -1):
+            e = P["convs"][ci]
+            prev_act = acts[ci - 1][0]
+            _, am = acts[ci]
+            taylor = None
+            if (ci - 1) in want:
+                taylor = arena[ci - 1]
+                res[ci - 1] = taylor
+            H, W = prev_act.shape[1], prev_act.shape[2]
+            M = B * H * W
+            cfg, sp = _pick_cfg(M, prev_act.shape[3], e["wt"].shape[1])
+            need_out = ci - 1 > 0
+            g = T.conv_dgrad(g, am, e["wt"], prev_act, P["convs"][ci - 1]["scale"], taylor, need_out, 3, cfg, sp)
+        return res
+
+
+def criterion_is_cross_entropy(criterion, device) -> bool:
+    """Numerically probe whether ``criterion(out, y[, reduction])`` is plain mean cross-entropy."""
+    try:
+        g = torch.Generator(device="cpu").manual_seed(1234)
+        logits = (torch.randn(6, 5, generator=g) * 2).to(device)
+        y = torch.randint(0, 5, (6,), generator=g).to(device)
+        ref = F.cross_entropy(logits, y)
+        got = criterion(logits, y)
+        return bool(torch.allclose(got.float(), ref.float(), rtol=1e-5, atol=1e-6))
+    except Exception:
+        return False
+
+
+def maybe_engine(model, eval_modules, criterion, device):
+    """Return (engine, block indices of eval_modules) when the fused path applies, else None."""
+    dev = torch.device(device) if not isinstance(device, torch.device) else device
+    if dev.type != "cuda" or ops.backend() == "torch" or not ops.available():
+        return None
+    if model.training:
+        return None
+    if any(p.dtype != torch.float32 for p in model.parameters()):
+        return None
+    plan, _reason = build_plan(model)
+    if plan is None:
+        return None
+    idx = []
+    blocks = plan.blocks
+    for m in eval_modules:
+        found = None
+        for k, b in enumerate(blocks[:-1]):
+            if b.relu is m:
+                found = k
+                break
+        if found is None:
+            return None
+        idx.append(found)
+    if not criterion_is_cross_entropy(criterion, dev):
+        return None
+    eng = _ENGINES.get(model)
+    if eng is None or len(eng.plan.blocks) != len(plan.blocks) or any(
+            a.conv is not b.conv if isinstance(a, ConvBlock) else a.linear is not b.linear
+            for a, b in zip(eng.plan.blocks, plan.blocks)):
+        eng = FusedChainEngine(model, plan)
+        _ENGINES[model] = eng
+    return eng, idx
+
+
+_ENGINES: "weakref.WeakKeyDictionary[nn.Module, FusedChainEngine]" = weakref.WeakKeyDictionary()

@@ -14,7 +14,7 @@ from ._native import available, backend, load, require, use_native
 
 __all__ = [
     "available", "backend", "load", "require", "use_native",
-    "REDUCE_MODES", "channel_reduce", "column_accumulate", "channel_fill_", "nan_channels",
+    "REDUCE_MODES", "channel_reduce", "column_accumulate", "score_fold_", "channel_fill_", "nan_channels",
     "gather_multi", "prefix_mask", "shapley_scatter", "shapley_column", "cross_entropy",
 ]
 
@@ -79,6 +79,26 @@ def column_accumulate(v: torch.Tensor, acc_sum: torch.Tensor, acc_sq: torch.Tens
     acc_sum += v64.sum(0)
     if acc_sq is not None:
         acc_sq += (v64 * v64).sum(0)
+
+
+def score_fold_(Ts: Sequence[torch.Tensor], accs: Sequence[torch.Tensor | None], take_abs: bool, after: int) -> None:
+    """For each (B, C) score slab T: v = |T| (or T); acc += v.sum(0) in float64 (acc may be
+    None); then ``after`` = 0 leaves T, 1 writes v back into T, 2 zeroes T. One launch for
+    up to 16 slabs (the fused engine folds every layer's scores at once)."""
+    if len(Ts) == 0:
+        return
+    if use_native(*Ts):
+        empty = torch.empty(0, dtype=torch.float64, device=Ts[0].device)
+        require().score_fold_(list(Ts), [a if a is not None else empty for a in accs], bool(take_abs), int(after))
+        return
+    for T, a in zip(Ts, accs):
+        v = T.abs() if take_abs else T
+        if a is not None:
+            a += v.double().sum(0)
+        if after == 1:
+            T.copy_(v)
+        elif after == 2:
+            T.zero_()
 
 
 def channel_fill_(x: torch.Tensor, idx, value: float) -> torch.Tensor:
