@@ -61,7 +61,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
   TORCH_CHECK(w.size(1) == ks * ks * Cin, "weight K mismatch: ", w.size(1), " vs ", ks * ks * Cin);
   TORCH_CHECK(Cin % 32 == 0, "Cin must be a multiple of 32");
   TORCH_CHECK(!pool || (H % 2 == 0 && W % 2 == 0), "pooling needs even H, W");
-  TORCH_CHECK(cfg >= 0 && cfg <= 3, "bad tile config");
+  TORCH_CHECK(cfg >= 0 && cfg <= 6, "bad tile config");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   const float* sc = opt_ptr(scale, Cout, "scale");
   const float* sh = opt_ptr(shift, Cout, "shift");

@@ -19,6 +19,25 @@ namespace tp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Raw buffer loads (offset >= num_records returns 0 in hardware). Declared against the LLVM
+// intrinsics directly: the clang __builtin_amdgcn_raw_buffer_load_b128 of ROCm 7.2 lowers to a
+// single-dword load on gfx950.
+__device__ f32x4 buf_load_f32x4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ unsigned buf_load_u32(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
+
+// Buffer descriptor for a flat range of ``bytes`` (stride 0, raw addressing). Build it only
+// from wave-uniform values (kernel arguments) so it lives in SGPRs.
+__device__ __forceinline__ i32x4 make_rsrc(const void* p, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  i32x4 r;
+  r.x = (int)(unsigned)a;
+  r.y = (int)((a >> 32) & 0xffffu);
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

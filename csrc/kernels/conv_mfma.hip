@@ -21,6 +21,8 @@
 
 namespace tp {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 enum Epi : int {
   EPI_FWD = 0,       // y = relu?(acc*scale[n] + shift[n]) stored NHWC
   EPI_FWD_POOL = 1,  // + 2x2 max-pool: pooled value + argmax byte
@@ -37,6 +39,7 @@ struct ConvArgs {
   int B, H, W, Cin, N, K;   // K = KS*KS*Cin
   int M;                    // B*H*W
   int k_tiles_per_split;
+  long long x_elems;        // elements of the A source tensor (buffer-descriptor bound)
   // epilogue
   const float* scale;       // [N] (EPI_FWD*) or BN scale of the consumer layer (EPI_BWD)
   const float* shift;       // [N]
@@ -54,11 +57,15 @@ struct Tile {
   static constexpr int LDK = BK + 4;  // padded row (floats)
   static constexpr int WAVES_N = BN / WN;
   static constexpr int TM = WM / 32, TN = WN / 32;
-  static constexpr int A_CHUNKS = BM * BK / 4 / 256;  // float4 per thread per slice
-  static constexpr int B_CHUNKS = BN * BK / 4 / 256;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static constexpr int NW = (BM / WM) * (BN / WN);  // waves per block
+  static constexpr int NT = 64 * NW;                 // threads per block
+  static constexpr int A_CHUNKS = BM * BK / 4 / NT;  // float4 per thread per slice
+  static constexpr int B_CHUNKS = BN * BK / 4 / NT;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per block");
   static_assert(A_CHUNKS >= 1 && B_CHUNKS >= 1, "tile too small");
 };
+
+constexpr int tile_threads(int bm, int bn, int wm, int wn) { return 64 * (bm / wm) * (bn / wn); }
 
 __device__ __forceinline__ void pix_of(int m, int H, int W, bool pooled, int& b, int& oh, int& ow) {
   const int HW = H * W;
@@ -83,7 +90,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI>
-__global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs p) {
+__global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, WM, WN) / 128) void conv_igemm(ConvArgs p) {
   using T = Tile<BM, BN, WM, WN>;
   constexpr int BK = T::BK, LDK = T::LDK;
   __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
@@ -103,27 +110,47 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs p) {
   const int kt_end = min(kt_total, kt_begin + p.k_tiles_per_split);
   const int cin_tiles = p.Cin / BK;
 
-  // ---- per-thread A rows (pixel coordinates are loop invariant) --------------------------
-  int a_b[T::A_CHUNKS], a_oh[T::A_CHUNKS], a_ow[T::A_CHUNKS], a_c4[T::A_CHUNKS], a_row[T::A_CHUNKS];
+  // ---- per-thread A rows: loop-invariant offsets + a bitmask of in-bounds taps ----------
+  // Loads go through buffer descriptors: an out-of-range offset returns zeros in hardware,
+  // so conv padding and ragged M/N edges cost one v_cndmask instead of a branch per load.
+  constexpr unsigned OOB = 0x80000000u;
+  const i32x4 xr = make_rsrc(p.x, (unsigned)(p.x_elems * 4));
+  const i32x4 wr = make_rsrc(p.w, (unsigned)(p.N * p.K * 4));
+  const i32x4 amr = make_rsrc(p.x_argmax, UNPOOL ? (unsigned)p.x_elems : 0u);
+
+  int a_off[T::A_CHUNKS], a_row[T::A_CHUNKS], a_c4[T::A_CHUNKS];
+  unsigned a_mask[T::A_CHUNKS];
+  int a_oh[T::A_CHUNKS], a_ow[T::A_CHUNKS];
 #pragma unroll
   for (int i = 0; i < T::A_CHUNKS; ++i) {
-    const int id = tid + i * 256;
+    const int id = tid + i * T::NT;
     a_row[i] = id / (BK / 4);
     a_c4[i] = id % (BK / 4);
     const int m = m0 + a_row[i];
+    int b = 0, oh = 0, ow = 0;
+    unsigned mask = 0;
     if (m < p.M) {
-      pix_of(m, p.H, p.W, POOLED_M, a_b[i], a_oh[i], a_ow[i]);
-    } else {
-      a_b[i] = -1;
-      a_oh[i] = a_ow[i] = 0;
+      pix_of(m, p.H, p.W, POOLED_M, b, oh, ow);
+#pragma unroll
+      for (int t = 0; t < KS * KS; ++t) {
+        const int ih = oh + t / KS - (KS - 1) / 2, iw = ow + t % KS - (KS - 1) / 2;
+        if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) mask |= 1u << t;
+      }
     }
+    a_mask[i] = mask;
+    a_oh[i] = oh;
+    a_ow[i] = ow;
+    if constexpr (UNPOOL) a_off[i] = b * (p.H >> 1) * (p.W >> 1) * p.Cin + a_c4[i] * 4;
+    else a_off[i] = ((b * p.H + oh) * p.W + ow) * p.Cin + a_c4[i] * 4;
   }
-  int b_row[T::B_CHUNKS], b_c4[T::B_CHUNKS];
+  int b_off[T::B_CHUNKS], b_row[T::B_CHUNKS], b_c4[T::B_CHUNKS];
 #pragma unroll
   for (int i = 0; i < T::B_CHUNKS; ++i) {
-    const int id = tid + i * 256;
+    const int id = tid + i * T::NT;
     b_row[i] = id / (BK / 4);
     b_c4[i] = id % (BK / 4);
+    const int n = n0 + b_row[i];
+    b_off[i] = n < p.N ? (n * p.K + b_c4[i] * 4) * 4 : -1;
   }
 
   float4 ra[T::A_CHUNKS], rb[T::B_CHUNKS];
@@ -134,34 +161,32 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs p) {
     const int dh = tap / KS - (KS - 1) / 2, dw = tap % KS - (KS - 1) / 2;
 #pragma unroll
     for (int i = 0; i < T::A_CHUNKS; ++i) {
-      const int ih = a_oh[i] + dh, iw = a_ow[i] + dw;
-      const bool ok = a_b[i] >= 0 && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) {
-        const int c = c0 + a_c4[i] * 4;
-        if constexpr (UNPOOL) {
-          const int H2 = p.H >> 1, W2 = p.W >> 1;
-          const long long off = (((long long)a_b[i] * H2 + (ih >> 1)) * W2 + (iw >> 1)) * p.Cin + c;
-          const float4 g = *reinterpret_cast<const float4*>(p.x + off);
-          const uchar4 am = *reinterpret_cast<const uchar4*>(p.x_argmax + off);
-          const uint8_t q = (uint8_t)(((ih & 1) << 1) | (iw & 1));
-          v.x = am.x == q ? g.x : 0.f;
-          v.y = am.y == q ? g.y : 0.f;
-          v.z = am.z == q ? g.z : 0.f;
-          v.w = am.w == q ? g.w : 0.f;
-        } else {
-          const long long off = (((long long)a_b[i] * p.H + ih) * p.W + iw) * p.Cin + c;
-          v = *reinterpret_cast<const float4*>(p.x + off);
-        }
+      const bool ok = (a_mask[i] >> tap) & 1u;
+      if constexpr (UNPOOL) {
+        const int ih = a_oh[i] + dh, iw = a_ow[i] + dw;
+        const int off = a_off[i] + ((ih >> 1) * (p.W >> 1) + (iw >> 1)) * p.Cin + c0;
+        const unsigned vo = ok ? (unsigned)off * 4u : OOB;
+        const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
+        const unsigned am = buf_load_u32(amr, (int)(ok ? (unsigned)off : OOB), 0, 0);
+        const unsigned q = (unsigned)(((ih & 1) << 1) | (iw & 1));
+        float4 v;
+        v.x = ((am >> 0) & 0xffu) == q ? g[0] : 0.f;
+        v.y = ((am >> 8) & 0xffu) == q ? g[1] : 0.f;
+        v.z = ((am >> 16) & 0xffu) == q ? g[2] : 0.f;
+        v.w = ((am >> 24) & 0xffu) == q ? g[3] : 0.f;
+        ra[i] = v;
+      } else {
+        const int delta = (dh * p.W + dw) * p.Cin + c0;  // wave-uniform
+        const unsigned vo = ok ? (unsigned)(a_off[i] + delta) * 4u : OOB;
+        const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
+        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
       }
-      ra[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < T::B_CHUNKS; ++i) {
-      const int n = n0 + b_row[i];
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (n < p.N) v = *reinterpret_cast<const float4*>(p.w + (long long)n * p.K + kt * BK + b_c4[i] * 4);
-      rb[i] = v;
+      const unsigned vo = b_off[i] >= 0 ? (unsigned)(b_off[i] + kt * BK * 4) : OOB;
+      const f32x4 g = buf_load_f32x4(wr, (int)vo, 0, 0);
+      rb[i] = make_float4(g[0], g[1], g[2], g[3]);
     }
   };
   auto store_tile = [&](int buf) {
@@ -195,21 +220,32 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs p) {
       if (more) load_tile(kt + 1);  // global loads in flight under the MFMAs below
       const float* a_base = smem + buf * STAGE + (wm0 + li) * LDK + lh * 16;
       const float* b_base = smem + buf * STAGE + (BM + wn0 + li) * LDK + lh * 16;
+      // software-pipelined fragment reads: chunk c+1 is read while chunk c feeds the MFMAs
+      float4 af[2][T::TM], bf[2][T::TN];
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i) af[0][i] = *reinterpret_cast<const float4*>(a_base + i * 32 * LDK);
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) bf[0][j] = *reinterpret_cast<const float4*>(b_base + j * 32 * LDK);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        float4 af[T::TM], bf[T::TN];
+        if (c < 3) {
 #pragma unroll
-        for (int i = 0; i < T::TM; ++i) af[i] = *reinterpret_cast<const float4*>(a_base + i * 32 * LDK + c * 4);
+          for (int i = 0; i < T::TM; ++i)
+            af[(c + 1) & 1][i] = *reinterpret_cast<const float4*>(a_base + i * 32 * LDK + (c + 1) * 4);
 #pragma unroll
-        for (int j = 0; j < T::TN; ++j) bf[j] = *reinterpret_cast<const float4*>(b_base + j * 32 * LDK + c * 4);
+          for (int j = 0; j < T::TN; ++j)
+            bf[(c + 1) & 1][j] = *reinterpret_cast<const float4*>(b_base + j * 32 * LDK + (c + 1) * 4);
+        }
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
 #pragma unroll
           for (int i = 0; i < T::TM; ++i)
 #pragma unroll
             for (int j = 0; j < T::TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[c & 1][i][s], bf[c & 1][j][s], acc[i][j], 0, 0, 0);
         }
+        __builtin_amdgcn_s_setprio(0);
       }
       if (more) store_tile(buf ^ 1);
       __syncthreads();
@@ -417,17 +453,21 @@ template <int BM, int BN, int WM, int WN, int KS, bool PM, bool UP, int EPI>
 hipError_t launch_cfg(const ConvArgs& a, int splits, hipStream_t st) {
   const int m_tiles = (a.M + BM - 1) / BM, n_tiles = (a.N + BN - 1) / BN;
   dim3 grid(m_tiles * n_tiles, splits);
-  tp::conv_igemm<BM, BN, WM, WN, KS, PM, UP, EPI><<<grid, 256, 0, st>>>(a);
+  tp::conv_igemm<BM, BN, WM, WN, KS, PM, UP, EPI><<<grid, tp::Tile<BM, BN, WM, WN>::NT, 0, st>>>(a);
   return hipGetLastError();
 }
 
 // cfg: 0 = 128x128 (waves 2x2 of 64x64), 1 = 256x64 (4x1 of 64x64), 2 = 64x64 (2x2 of 32x32),
+//      4 = 128x128 (8 waves 2x4 of 64x32), 5 = 256x64 (8 waves 4x2 of 64x32), 6 = 128x64 (8 waves 4x2 of 32x32),
 //      3 = 128x64 (2x2 of 64x32)
 template <int KS, bool PM, bool UP, int EPI>
 hipError_t launch_any(int cfg, const ConvArgs& a, int splits, hipStream_t st) {
   switch (cfg) {
     case 0: return launch_cfg<128, 128, 64, 64, KS, PM, UP, EPI>(a, splits, st);
     case 1: return launch_cfg<256, 64, 64, 64, KS, PM, UP, EPI>(a, splits, st);
+    case 4: return launch_cfg<128, 128, 64, 32, KS, PM, UP, EPI>(a, splits, st);  // 8 waves
+    case 5: return launch_cfg<256, 64, 64, 32, KS, PM, UP, EPI>(a, splits, st);   // 8 waves
+    case 6: return launch_cfg<128, 64, 32, 32, KS, PM, UP, EPI>(a, splits, st);   // 8 waves
     case 2: return launch_cfg<64, 64, 32, 32, KS, PM, UP, EPI>(a, splits, st);
     case 3: return launch_cfg<128, 64, 64, 32, KS, PM, UP, EPI>(a, splits, st);
   }
@@ -477,6 +517,9 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   a.N = Cout;
   a.K = ks * ks * Cin;
   a.M = B * H * W;
+  a.x_elems = unpool ? (long long)B * (H / 2) * (W / 2) * Cin : (long long)B * H * W * Cin;
+  // buffer descriptors address 32-bit byte offsets
+  if (a.x_elems * 4 >= (1ll << 31) || (long long)Cout * a.K * 4 >= (1ll << 31)) return hipErrorInvalidValue;
   const int kt = a.K / 32;
   splits = std::max(1, std::min(splits, kt));
   a.k_tiles_per_split = (kt + splits - 1) / splits;

@@ -1,0 +1,100 @@
+"""Micro-benchmark of the fused conv kernels on the VGG16-CIFAR layer shapes (fwd + dgrad).
+
+    python -m torchpruner_amd.bench.conv_kernels [--batch 256] [--iters 20] [--json out.json]
+
+Reports time and TFLOP/s per layer (2*M*N*K / t) for the tile config the engine would pick,
+and optionally every config (``--all-cfg``), so kernel changes can be A/B'd in one process.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+
+import torch
+
+from torchpruner_amd import ops
+from torchpruner_amd.engine.fused_chain import _pick_cfg
+
+# (H, W, Cin, Cout, pool) of the 12 MFMA convs of VGG16 on 32x32 inputs
+VGG16_LAYERS = [
+    (32, 32, 64, 64, True),
+    (16, 16, 64, 128, False),
+    (16, 16, 128, 128, True),
+    (8, 8, 128, 256, False),
+    (8, 8, 256, 256, False),
+    (8, 8, 256, 256, True),
+    (4, 4, 256, 512, False),
+    (4, 4, 512, 512, False),
+    (4, 4, 512, 512, True),
+    (2, 2, 512, 512, False),
+    (2, 2, 512, 512, False),
+    (2, 2, 512, 512, True),
+]
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(iters):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--all-cfg", action="store_true")
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    T = ops.require()
+    dev = torch.device("cuda")
+    B = args.batch
+    rows = []
+    tot_f = tot_t = 0.0
+    for li, (H, W, Cin, Cout, pool) in enumerate(VGG16_LAYERS):
+        x = torch.randn(B, H, W, Cin, device=dev)
+        w = torch.randn(Cout, 9 * Cin, device=dev) * 0.02
+        wt = torch.randn(Cin, 9 * Cout, device=dev) * 0.02
+        sc = torch.ones(Cout, device=dev)
+        sh = torch.zeros(Cout, device=dev)
+        M, flops = B * H * W, 2.0 * B * H * W * Cout * 9 * Cin
+        act = torch.relu(torch.randn(B, H, W, Cin, device=dev))
+        scin = torch.ones(Cin, device=dev)
+        tay = torch.zeros(B, Cin, device=dev)
+        if pool:
+            g = torch.randn(B, H // 2, W // 2, Cout, device=dev)
+            am = torch.randint(0, 4, (B, H // 2, W // 2, Cout), device=dev, dtype=torch.uint8)
+        else:
+            g = torch.randn(B, H, W, Cout, device=dev)
+            am = None
+        cfgs = [0, 1, 2, 3, 4, 5, 6] if args.all_cfg else [None]
+        for cfg in cfgs:
+            fc, fs = _pick_cfg(M, Cout, 9 * Cin)
+            bc, bs = _pick_cfg(M, Cin, 9 * Cout)
+            if cfg is not None:
+                fc = bc = cfg
+            tf = timeit(lambda: T.conv_fwd(x, w, sc, sh, True, pool, 3, fc, fs), args.iters)
+            tb = timeit(lambda: T.conv_dgrad(g, am, wt, act, scin, tay, True, 3, bc, bs), args.iters)
+            r = {"layer": li + 1, "shape": [B, H, W, Cin, Cout], "pool": pool, "fwd_cfg": [fc, fs], "bwd_cfg": [bc, bs],
+                 "fwd_us": round(tf, 1), "bwd_us": round(tb, 1), "fwd_tflops": round(flops / tf / 1e6, 1),
+                 "bwd_tflops": round(flops / tb / 1e6, 1)}
+            rows.append(r)
+            if cfg is None:
+                tot_f += 2 * flops
+                tot_t += tf + tb
+            print(f"L{li+1:2d} {H:2d}x{W:<2d} {Cin:3d}->{Cout:3d} pool={int(pool)} cfg f{fc}/{fs} b{bc}/{bs}: "
+                  f"fwd {tf:7.1f} us {flops/tf/1e6:6.1f} TF | dgrad {tb:7.1f} us {flops/tb/1e6:6.1f} TF", flush=True)
+    if tot_t:
+        print(f"TOTAL {tot_t:.1f} us, {tot_f / tot_t / 1e6:.1f} TF/s average")
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump({"batch": B, "rows": rows, "total_us": tot_t}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

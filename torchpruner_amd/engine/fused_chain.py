@@ -27,6 +27,7 @@ summation order differ from cuDNN/MIOpen only at rounding level.
 from __future__ import annotations
 
 import math
+import os
 import weakref
 from dataclasses import dataclass, field
 from typing import Optional
@@ -37,29 +38,82 @@ import torch.nn.functional as F
 
 from .. import ops
 
-# tile configs of conv_mfma.hip: 0=128x128, 1=256x64, 2=64x64, 3=128x64
+# tile configs of conv_mfma.hip: 0=128x128, 1=256x64, 2=64x64, 3=128x64 (4 waves);
+# 4=128x128, 5=256x64, 6=128x64 (8 waves)
 _CU = 256
+_TILES = {0: (128, 128), 1: (256, 64), 2: (64, 64), 3: (128, 64), 4: (128, 128), 5: (256, 64), 6: (128, 64)}
+
+
+def _splits_for(M, N, K, bm, bn):
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    splits, kt = 1, K // 32
+    while tiles * splits < 2 * _CU and splits * 2 <= kt // 4 and splits < 16:
+        splits *= 2
+    return splits
 
 
 def _pick_cfg(M: int, N: int, K: int):
-    """Choose (tile cfg, split-K) so a launch has enough workgroups for 256 CUs."""
-    cands = [(0, 128, 128), (3, 128, 64), (1, 256, 64), (2, 64, 64)]
+    """Heuristic (tile cfg, split-K) so a launch has enough workgroups for 256 CUs."""
     best = None
-    for cfg, bm, bn in cands:
+    for cfg in (0, 3, 1, 2):
+        bm, bn = _TILES[cfg]
         if N <= 64 and bn == 128:
             continue
         tiles = math.ceil(M / bm) * math.ceil(N / bn)
-        splits = 1
-        kt = K // 32
-        while tiles * splits < 2 * _CU and splits * 2 <= kt // 4 and splits < 16:
-            splits *= 2
+        splits = _splits_for(M, N, K, bm, bn)
         waste = (math.ceil(M / bm) * bm * math.ceil(N / bn) * bn) / (M * N)
-        # prefer big tiles when the grid is full anyway; small tiles / split-K otherwise
         score = (min(tiles * splits, 2 * _CU) / (2 * _CU)) / waste * (1.0 if bm * bn >= 128 * 64 else 0.85)
         score *= 1.0 if splits == 1 else 0.9
         if best is None or score > best[0]:
             best = (score, cfg, splits)
     return best[1], best[2]
+
+
+class Autotuner:
+    """Per-shape choice of (tile cfg, split-K) by timing every candidate once on the real
+    operands (the analogue of cudnn.benchmark; disable with TORCHPRUNER_AUTOTUNE=0)."""
+
+    def __init__(self):
+        self.cache = {}
+        self.enabled = os.environ.get("TORCHPRUNER_AUTOTUNE", "1") != "0"
+
+    def candidates(self, M, N, K):
+        out = []
+        for cfg, (bm, bn) in _TILES.items():
+            if N <= 64 and bn == 128:
+                continue
+            sp = _splits_for(M, N, K, bm, bn)
+            out.append((cfg, sp))
+            if sp > 1:
+                out.append((cfg, max(1, sp // 2)))
+        return out
+
+    def choose(self, key, M, N, K, run):
+        """``run(cfg, splits)`` launches the op once (must be side-effect free)."""
+        hit = self.cache.get(key)
+        if hit is not None:
+            return hit
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
+            res = _pick_cfg(M, N, K)
+            self.cache[key] = res
+            return res
+        best = None
+        for cand in self.candidates(M, N, K):
+            run(*cand)  # warm
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(2):
+                run(*cand)
+            e1.record()
+            e1.synchronize()
+            t = e0.elapsed_time(e1)
+            if best is None or t < best[0]:
+                best = (t, cand)
+        self.cache[key] = best[1]
+        return best[1]
+
+
+TUNER = Autotuner()
 
 
 @dataclass
@@ -247,15 +301,22 @@ class FusedChainEngine:
             if ci == 0:
                 h = x.float().permute(0, 2, 3, 1).contiguous()
             M = h.shape[0] * h.shape[1] * h.shape[2]
-            cfg, sp = _pick_cfg(M, e["scale"].numel(), e["w"].shape[1])
+            N, K = e["scale"].numel(), e["w"].shape[1]
+            hh = h
+            cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"]), M, N, K,
+                                   lambda c, s_, e=e, hh=hh: T.conv_fwd(hh, e["w"], e["scale"], e["shift"], True,
+                                                                      e["pool"], 3, c, s_))
             out, am = T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
             h = out
             acts.append((out, am if e["pool"] else None))
         feats = h.reshape(B, 1, 1, -1)
         lin_acts = [feats]
         for li, e in enumerate(P["lins"]):
-            cfg, sp = _pick_cfg(B, e["w"].shape[0], e["w"].shape[1])
-            out, _ = T.conv_fwd(lin_acts[-1], e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp)
+            xin = lin_acts[-1]
+            cfg, sp = TUNER.choose(("lin", tuple(xin.shape), e["w"].shape[0]), B, e["w"].shape[0], e["w"].shape[1],
+                                   lambda c, s_, e=e, xin=xin: T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"],
+                                                                        False, 1, c, s_))
+            out, _ = T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp)
             lin_acts.append(out)
         logits = lin_acts[-1].reshape(B, -1)
         return logits, {"acts": acts, "lin_acts": lin_acts}
@@ -311,7 +372,10 @@ class FusedChainEngine:
                 taylor = arena[blk_index]
                 res[blk_index] = taylor
             bn_scale = P["convs"][-1]["scale"] if j == 0 else None
-            cfg, sp = _pick_cfg(B, act.shape[3], e["wt"].shape[1])
+            gg = g
+            cfg, sp = TUNER.choose(("lin_bwd", tuple(g.shape), tuple(act.shape)), B, act.shape[3], e["wt"].shape[1],
+                                   lambda c, s_, e=e, gg=gg, act=act, bn=bn_scale: T.conv_dgrad(
+                                       gg, None, e["wt"], act, bn, None, True, 1, c, s_))
             g = T.conv_dgrad(g, None, e["wt"], act, bn_scale, taylor, True, 1, cfg, sp)
         # conv stack: g is dL/d(pre-activation of conv nconv-1) * bn_scale, at the
         # (pooled, if pooled) output resolution of that block
@@ -325,9 +389,14 @@ class FusedChainEngine:
                 res[ci - 1] = taylor
             H, W = prev_act.shape[1], prev_act.shape[2]
             M = B * H * W
-            cfg, sp = _pick_cfg(M, prev_act.shape[3], e["wt"].shape[1])
             need_out = ci - 1 > 0
-            g = T.conv_dgrad(g, am, e["wt"], prev_act, P["convs"][ci - 1]["scale"], taylor, need_out, 3, cfg, sp)
+            sc_prev = P["convs"][ci - 1]["scale"]
+            gg = g
+            cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None), M,
+                                   prev_act.shape[3], e["wt"].shape[1],
+                                   lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out: T.conv_dgrad(
+                                       gg, am, e["wt"], pa, sc, None, no, 3, c, s_))
+            g = T.conv_dgrad(g, am, e["wt"], prev_act, sc_prev, taylor, need_out, 3, cfg, sp)
         return res
 
 
