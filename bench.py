@@ -3,16 +3,17 @@
 
 Workload (BASELINE.json config #2, scaled to N GPUs):
 * VGG16-BN / CIFAR-10 shape (reference experiments/models/cifar10.py:62-77), random-init
-  weights, eval mode, fp32 compute (the reference's precision).
+  weights briefly trained (untimed, ``--train-steps``) on a synthetic CIFAR-shaped prototype
+  task so that top-1 is meaningful; eval mode; fp32 compute (the reference's precision).
 * One step = Taylor attribution of one batch of B images *for every conv layer* (all 13
   units a 50%-filter prune needs), evaluated after BN+ReLU (``find_best_evaluation_module``),
   through the public API ``TaylorAttributionMetric.run_many``.
 * Data parallel: one process per GPU (torchrun), whole batches sharded per rank, scores
   all-reduced over RCCL at the end of ``run_many`` (inside the timed region).
 * Weak scaling: B images per GPU per step; ``value`` = total images/s over all GPUs.
-* After timing (untimed): prune 50% of every conv layer's filters by the measured scores and
-  report top-1 agreement with the unpruned model on held-out synthetic images
-  (labels = the unpruned model's predictions, so top-1 before pruning is 100%).
+* After timing (untimed): prune 50% of every conv layer's filters by the measured scores
+  (one shot, no finetuning) and report held-out top-1 before/after, plus the same prune with
+  Random scores as a reference point.
 * ``--baseline``: also time the reference-semantics eager implementation (one full pass per
   layer, clone + non-full backward hook, full backward, per-batch host numpy concat) on the
   same GPU for a few batches (rank 0), reported as ``eager_reference_img_s``.
@@ -34,7 +35,7 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from torchpruner_amd import Pruner, TaylorAttributionMetric, get_vgg_pruning_graph  # noqa: E402
-from torchpruner_amd.data import DeviceLoader, teacher_labels  # noqa: E402
+from torchpruner_amd.data import DeviceLoader, PrototypeTask  # noqa: E402
 from torchpruner_amd.models import prunable_vgg16  # noqa: E402
 from torchpruner_amd.parallel import dist as pdist  # noqa: E402
 from torchpruner_amd.utils import find_best_module_for_attributions  # noqa: E402
@@ -45,12 +46,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 256)),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 512)),
                     help="images per GPU per step")
     ap.add_argument("--baseline", action="store_true", help="also time the reference-semantics eager path")
     ap.add_argument("--baseline-batches", type=int, default=2)
     ap.add_argument("--no-prune", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--train-steps", type=int, default=int(os.environ.get("BENCH_TRAIN_STEPS", 150)),
+                    help="untimed SGD steps on the synthetic task before scoring (0 = random init)")
     return ap.parse_args()
 
 
@@ -59,12 +62,58 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def make_batches(model, n_batches, B, device, seed):
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    x = torch.randn(n_batches * B, 3, 32, 32, generator=g, device=device)
-    y = teacher_labels(model, x, batch=1024)
-    return x, y
+def train_teacher(model, task, steps, device, seed):
+    """Untimed: a few hundred SGD steps (reference optimizer settings, cifar10.py:95-99) on the
+    synthetic prototype task; all ranks end with rank 0's weights."""
+    if steps > 0:
+        opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-4)
+        sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=0.05, total_steps=steps)
+        model.train()
+        for i in range(steps):
+            x, y = task.sample(128, seed * 100_003 + i)
+            opt.zero_grad(set_to_none=True)
+            F.cross_entropy(model(x), y).backward()
+            opt.step()
+            sched.step()
+    model.eval()
+    model.zero_grad(set_to_none=True)
+    if pdist.get_world_size() > 1:
+        with torch.no_grad():
+            for t in list(model.parameters()) + list(model.buffers()):
+                pdist.broadcast_tensor_(t.data, 0)
+
+
+@torch.no_grad()
+def layerwise_top1(model, convs, scores, x, y, frac=0.5):
+    """Reference layerwise-robustness protocol (nbVGG:1233-1285) at one point: for each conv
+    layer alone, zero the ``frac`` lowest-scored channels after its BN+ReLU; mean top-1."""
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    accs = []
+    for conv, s in zip(convs, scores):
+        idx = torch.as_tensor(np.argsort(s, kind="stable")[: int(len(s) * frac)], device=x.device)
+        ev = find_best_module_for_attributions(model, conv)
+        h = ev.register_forward_hook(lambda m, i, o, idx=idx: o.index_fill(1, idx, 0.0))
+        try:
+            accs.append(top1(model, x, y))
+        finally:
+            h.remove()
+    return float(np.mean(accs))
+
+
+@torch.no_grad()
+def top1(model, x, y):
+    model.eval()
+    return float((model(x).argmax(1) == y).float().mean())
+
+
+def prune_half(model, scores_by_conv, dev):
+    pruner = Pruner(model, (3, 32, 32), dev)
+    for module, cascade in get_vgg_pruning_graph(model):
+        s = scores_by_conv.get(id(module))
+        if s is None:
+            continue
+        idx = np.argsort(s, kind="stable")[: len(s) // 2]
+        pruner.prune_model(module, idx, cascading_modules=cascade)
 
 
 def timed_run(metric, convs, world):
@@ -90,13 +139,17 @@ def main():
     assert dev.type == "cuda", "bench.py needs a GPU"
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
-    model = prunable_vgg16().to(dev).eval()
+    model = prunable_vgg16().to(dev)
+    task = PrototypeTask((3, 32, 32), 10, noise=2.0, seed=args.seed, device=dev)
+    t0 = time.perf_counter()
+    train_teacher(model, task, args.train_steps, dev, args.seed)
+    log(f"[bench] teacher: {args.train_steps} SGD steps in {time.perf_counter() - t0:.1f}s (untimed)")
     convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
     B = args.batch
 
     # every rank builds the same global data set; each processes its own whole batches
-    xw, yw = make_batches(model, max(args.warmup, 1) * world, B, dev, args.seed + 1)
-    xt, yt = make_batches(model, args.steps * world, B, dev, args.seed + 2)
+    xw, yw = task.sample(max(args.warmup, 1) * world * B, args.seed + 1)
+    xt, yt = task.sample(args.steps * world * B, args.seed + 2)
     warm = TaylorAttributionMetric(model, DeviceLoader(xw, yw, B), F.cross_entropy, dev)
     metric = TaylorAttributionMetric(model, DeviceLoader(xt, yt, B), F.cross_entropy, dev)
 
@@ -119,7 +172,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (CIFAR-10 shape, random-init VGG16-BN, teacher labels)",
+        "data": "synthetic (CIFAR-10-shaped prototype task; random-init VGG16-BN briefly trained, untimed)",
         "config": {
             "model": "VGG16-BN (CIFAR-10, reference classifier)",
             "global_batch": B * world,
@@ -151,20 +204,30 @@ def main():
         log(f"[bench] reference-semantics eager: {nb * B / bt:.0f} img/s per GPU")
 
     if not args.no_prune:
-        # untimed: one-shot 50% filter pruning of every conv layer by the Taylor scores
-        xv, yv = make_batches(model, 1, 1000, dev, args.seed + 3)
-        conv_scores = {id(c): s for c, s in zip(convs, scores)}
-        pruner = Pruner(model, (3, 32, 32), dev)
-        for module, cascade in get_vgg_pruning_graph(model):
-            if id(module) not in conv_scores:
-                continue
-            s = conv_scores[id(module)]
-            idx = np.argsort(s, kind="stable")[: len(s) // 2]
-            pruner.prune_model(module, idx, cascading_modules=cascade)
-        with torch.no_grad():
-            acc = (model(xv).argmax(1) == yv).float().mean().item()
-        result["top1_retained_at_50pct"] = round(acc, 4)
-        log(f"[bench] top-1 retained after 50% conv-filter pruning: {acc:.4f}")
+        # untimed: one-shot 50% filter pruning of every conv layer (no finetuning)
+        import copy
+        xv, yv = task.sample(2000, args.seed + 3)
+        before = top1(model, xv, yv)
+        rng = np.random.RandomState(args.seed)
+        lw_taylor = layerwise_top1(model, convs, scores, xv, yv)
+        lw_random = layerwise_top1(model, convs, [rng.random_sample(c.out_channels) for c in convs], xv, yv)
+        result["top1_layerwise_50pct_taylor"] = round(lw_taylor, 4)
+        result["top1_layerwise_50pct_random"] = round(lw_random, 4)
+        log(f"[bench] layerwise 50% (one layer at a time, mean over 13): Taylor {lw_taylor:.4f}, "
+            f"Random {lw_random:.4f}")
+        rnd = copy.deepcopy(model)
+        prune_half(model, {id(c): s for c, s in zip(convs, scores)}, dev)
+        after = top1(model, xv, yv)
+        rconvs = [m for m in rnd.features if isinstance(m, torch.nn.Conv2d)]
+        rng = np.random.RandomState(args.seed)
+        prune_half(rnd, {id(c): rng.random_sample(c.out_channels) for c in rconvs}, dev)
+        after_rnd = top1(rnd, xv, yv)
+        result["top1_before"] = round(before, 4)
+        result["top1_oneshot_all_layers_50pct_taylor"] = round(after, 4)
+        result["top1_retained_at_50pct"] = round(lw_taylor / max(before, 1e-9), 4)
+        result["top1_oneshot_all_layers_50pct_random"] = round(after_rnd, 4)
+        log(f"[bench] top-1 before {before:.4f}; after one-shot 50% prune of ALL conv layers (no finetune): "
+            f"Taylor {after:.4f}, Random {after_rnd:.4f}")
 
     if rank == 0:
         print(json.dumps(result), flush=True)

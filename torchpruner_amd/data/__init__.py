@@ -1,4 +1,4 @@
 """Synthetic on-device datasets shaped like the reference's CIFAR-10 / MNIST / ImageNet."""
-from .synthetic import SHAPES, DeviceLoader, StreamLoader, loaders, synthetic_dataset, teacher_labels
+from .synthetic import SHAPES, DeviceLoader, PrototypeTask, StreamLoader, loaders, synthetic_dataset, teacher_labels
 
-__all__ = ["SHAPES", "DeviceLoader", "StreamLoader", "loaders", "synthetic_dataset", "teacher_labels"]
+__all__ = ["SHAPES", "DeviceLoader", "PrototypeTask", "StreamLoader", "loaders", "synthetic_dataset", "teacher_labels"]

@@ -131,6 +131,39 @@ def teacher_labels(model: torch.nn.Module, x: torch.Tensor, batch: int = 1024) -
     return torch.cat(out, 0)
 
 
+class PrototypeTask:
+    """A learnable synthetic classification task of a given image shape.
+
+    Class ``c`` has a fixed smooth prototype image ``P_c`` (low-resolution Gaussian noise,
+    bilinearly upsampled, unit variance); a sample is ``P_y + noise * N(0, 1)``. A CNN learns
+    it in a few hundred steps, which makes "top-1 retained after pruning" meaningful without
+    any dataset download (random-init networks predict one class for every input).
+    """
+
+    def __init__(self, shape=(3, 32, 32), num_classes=10, noise=1.0, seed=0, device="cpu", low_res=8):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        c, h, w = shape
+        low = torch.randn(num_classes, c, low_res, low_res, generator=g)
+        protos = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=False)
+        protos = (protos - protos.mean((1, 2, 3), keepdim=True)) / protos.std((1, 2, 3), keepdim=True)
+        self.protos = protos.to(device)
+        self.noise = noise
+        self.num_classes = num_classes
+        self.shape = tuple(shape)
+        self.device = torch.device(device)
+
+    def sample(self, n: int, seed: int):
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        y = torch.randint(0, self.num_classes, (n,), generator=g, device=self.device)
+        x = self.protos[y] + self.noise * torch.randn((n,) + self.shape, generator=g, device=self.device)
+        return x, y
+
+    def loader(self, n: int, batch_size: int, seed: int) -> "DeviceLoader":
+        x, y = self.sample(n, seed)
+        return DeviceLoader(x, y, batch_size)
+
+
 def loaders(name: str, n_train: int, n_val: int, batch_size: int, val_batch_size: int, device="cpu", seed: int = 0,
             teacher=None):
     """(train_loader, val_loader) of synthetic on-device data shaped like ``name``."""

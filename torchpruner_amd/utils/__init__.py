@@ -6,6 +6,7 @@ from .graph import (
     get_vgg_pruning_graph,
 )
 from .flops import count_parameters, count_flops
+from .train import test, train
 
 __all__ = [
     "ACTIVATIONS",
@@ -15,4 +16,6 @@ __all__ = [
     "get_vgg_pruning_graph",
     "count_parameters",
     "count_flops",
+    "train",
+    "test",
 ]
