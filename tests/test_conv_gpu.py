@@ -179,3 +179,55 @@ def test_engine_taylor_matches_generic_path(cuda):
                 # be at least as close to fp64 as MIOpen's fp32 (Winograd) path
                 assert err_fused < (5e-3 if red == "mean" else 2e-2), (err_fused, err_generic)
                 assert err_fused <= 1.5 * err_generic + 1e-5, (err_fused, err_generic)
+
+
+@pytest.mark.parametrize("layer", [1, 5, 12, 14])
+def test_engine_shapley_matches_generic_path(cuda, layer):
+    """Fused prefix evaluation (pooled-activation masking, fused downstream forward) gives the
+    same Shapley values as the reference-style forward_partial path, same permutations."""
+    from torchpruner_amd import ShapleyAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(0)
+    model = prunable_vgg16().to(cuda).eval()
+    prunable = [m for m in model.features if isinstance(m, torch.nn.Conv2d)] + [model.classifier[1],
+                                                                                 model.classifier[4]]
+    module = prunable[layer]
+    x = torch.randn(12, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (12,), device=cuda)
+    dl = DeviceLoader(x, y, 6)
+    import copy
+    m64 = copy.deepcopy(model).double().cpu()
+    p64 = [m for m in m64.features if isinstance(m, torch.nn.Conv2d)] + [m64.classifier[1], m64.classifier[4]]
+    dl64 = DeviceLoader(x.double().cpu(), y.cpu(), 6)
+    res = []
+    for backend, mdl, mod, d, dd in (("hip", model, module, cuda, dl), ("torch", model, module, cuda, dl),
+                                     ("torch", m64, p64[layer], "cpu", dl64)):
+        os.environ["TORCHPRUNER_BACKEND"] = backend
+        try:
+            np.random.seed(11)
+            res.append(ShapleyAttributionMetric(mdl, dd, F.cross_entropy, d, sv_samples=2,
+                                                reduction="none").run(mod, find_best_evaluation_module=True))
+        finally:
+            del os.environ["TORCHPRUNER_BACKEND"]
+    scale = np.abs(res[2]).max() + 1e-12
+    err_fused = np.abs(res[0] - res[2]).max() / scale
+    err_generic = np.abs(res[1] - res[2]).max() / scale
+    print(f"layer {layer}: fused_err={err_fused:.2e} miopen_err={err_generic:.2e}")
+    # Shapley deltas of a random-init deep ReLU net are ill-conditioned (ReLU-mask flips);
+    # both fp32 paths sit in the same error class w.r.t. fp64
+    assert err_fused <= 3 * err_generic + 2e-3, (err_fused, err_generic)
+    # the engine's partial forward itself is exact to fp32 rounding: masked prefix losses
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    engine, (k,) = maybe_engine(model, [find_best_module_for_attributions(model, module)], F.cross_entropy, cuda)
+    zk, _ = engine.forward(x, stop_after=k)
+    keep = torch.rand(zk.shape[3], device=cuda) > 0.3
+    got = engine.loss_from(k, zk * keep.view(1, 1, 1, -1), y)
+    ev64 = find_best_module_for_attributions(m64, p64[layer])
+    with torch.no_grad():
+        z64 = m64.forward_partial(x.double().cpu(), to_module=ev64)
+        shape = (1, -1) + (1,) * (z64.dim() - 2)
+        ref = F.cross_entropy(m64.forward_partial(z64 * keep.cpu().double().view(shape), from_module=ev64),
+                              y.cpu(), reduction="none")
+    torch.testing.assert_close(got.double().cpu(), ref, rtol=1e-4, atol=1e-5)

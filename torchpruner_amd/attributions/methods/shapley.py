@@ -29,6 +29,7 @@ from torch.nn.modules.batchnorm import _BatchNorm
 from torch.nn.modules.dropout import _DropoutNd
 
 from ... import ops
+from ...engine import maybe_engine
 from ...parallel import dist as pdist
 from ..base import _AttributionMetric
 
@@ -43,7 +44,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
       max_eval_elements  element budget used to size K automatically
     """
 
-    def __init__(self, *args, sv_samples=5, prefix_batch=None, max_eval_elements=1 << 27, **kwargs):
+    def __init__(self, *args, sv_samples=5, prefix_batch=None, max_eval_elements=1 << 29, **kwargs):
         super().__init__(*args, **kwargs)
         self.samples = sv_samples
         self.mask_indices = []
@@ -53,6 +54,9 @@ class ShapleyAttributionMetric(_AttributionMetric):
     def run(self, module, sv_samples=None, **kwargs):
         module = super().run(module, **kwargs)
         sv_samples = sv_samples if sv_samples is not None else self.samples
+        fused = self._fused_prepare(module)
+        if fused is not None:
+            return self._run_batches(module, sv_samples, fused)
         if hasattr(self.model, "forward_partial"):
             return self.run_module_with_partial(module, sv_samples)
         logger.warning("Consider adding a 'forward_partial' method to your model to speed-up Shapley values "
@@ -157,6 +161,33 @@ class ShapleyAttributionMetric(_AttributionMetric):
         if collective:
             pdist.all_reduce_sum_(sv, self.group)
         return self.aggregate_over_samples(sv.cpu().numpy())
+
+    # ------------------------------------------------------------------ native path
+    def _fused_prepare(self, module):
+        """Prefix evaluation on the fused HIP engine (eval-mode VGG-style chains, CE loss):
+        the evaluation module's activation is produced once per batch, K prefix-masked copies
+        are stacked by one kernel and pushed through the remaining fused layers in ONE forward.
+        Masking a post-ReLU activation commutes with the following 2x2 max-pool, so the
+        engine masks its pooled output (4x less data) with identical results."""
+        fused = maybe_engine(self.model, [module], self.criterion, self.device)
+        if fused is None:
+            return None
+        engine, (k,) = fused
+
+        def prepare(x, y):
+            zk, _ = engine.forward(x, stop_after=k)  # engine layout (B, H, W, C)
+            B = zk.shape[0]
+            z_cl = zk.permute(0, 3, 1, 2)  # (B, C, H, W) view, channels_last strides
+            base = engine.loss_from(k, zk, y)
+
+            def evaluate(rank_t, p_first, cnt):
+                masked = ops.prefix_mask(z_cl, rank_t, p_first, cnt)  # (cnt*B, C, H, W) channels_last
+                loss = engine.loss_from(k, masked.permute(0, 2, 3, 1), y.repeat(cnt))
+                return loss.view(cnt, B)
+
+            return zk.shape[3], B, zk[0].numel(), base, evaluate
+
+        return prepare
 
     # ------------------------------------------------------------------ fast path
     def run_module_with_partial(self, module, sv_samples):

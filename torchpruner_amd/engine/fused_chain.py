@@ -286,8 +286,26 @@ class FusedChainEngine:
         return self._packed
 
     # ------------------------------------------------------------------ execution
-    def forward(self, x: torch.Tensor):
-        """Forward pass; returns (logits, saved) where saved holds what backward needs."""
+    def _conv(self, T, e, h):
+        M = h.shape[0] * h.shape[1] * h.shape[2]
+        N, K = e["scale"].numel(), e["w"].shape[1]
+        cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"]), M, N, K,
+                               lambda c, s_, e=e, hh=h: T.conv_fwd(hh, e["w"], e["scale"], e["shift"], True,
+                                                                  e["pool"], 3, c, s_))
+        return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
+
+    def _linear(self, T, e, xin):
+        B = xin.shape[0]
+        cfg, sp = TUNER.choose(("lin", tuple(xin.shape), e["w"].shape[0]), B, e["w"].shape[0], e["w"].shape[1],
+                               lambda c, s_, e=e, xin=xin: T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"],
+                                                                    False, 1, c, s_))
+        out, _ = T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp)
+        return out
+
+    def forward(self, x: torch.Tensor, stop_after: Optional[int] = None):
+        """Forward pass; returns (logits, saved) where saved holds what backward needs.
+        With ``stop_after=k`` returns (output of block k in engine layout, saved) instead:
+        NHWC (pooled when the block pools) for conv blocks, (B,1,1,N) for linear blocks."""
         T = ops.require()
         P = self._pack()
         B = x.shape[0]
@@ -296,30 +314,41 @@ class FusedChainEngine:
         for ci, (blk, e) in enumerate(zip(self.plan.convs, P["convs"])):
             if ci == 0 and blk.first:
                 h = T.conv_first(x.float().contiguous(), e["w_first"], e["scale"], e["shift"], True)
-                acts.append((h, None))
-                continue
-            if ci == 0:
-                h = x.float().permute(0, 2, 3, 1).contiguous()
-            M = h.shape[0] * h.shape[1] * h.shape[2]
-            N, K = e["scale"].numel(), e["w"].shape[1]
-            hh = h
-            cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"]), M, N, K,
-                                   lambda c, s_, e=e, hh=hh: T.conv_fwd(hh, e["w"], e["scale"], e["shift"], True,
-                                                                      e["pool"], 3, c, s_))
-            out, am = T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
-            h = out
-            acts.append((out, am if e["pool"] else None))
-        feats = h.reshape(B, 1, 1, -1)
-        lin_acts = [feats]
+                am = None
+            else:
+                if ci == 0:
+                    h = x.float().permute(0, 2, 3, 1).contiguous()
+                h, am = self._conv(T, e, h)
+            acts.append((h, am if e["pool"] else None))
+            if stop_after == ci:
+                return h, {"acts": acts}
+        lin_acts = [h.reshape(B, 1, 1, -1)]
+        nconv = len(self.plan.convs)
         for li, e in enumerate(P["lins"]):
-            xin = lin_acts[-1]
-            cfg, sp = TUNER.choose(("lin", tuple(xin.shape), e["w"].shape[0]), B, e["w"].shape[0], e["w"].shape[1],
-                                   lambda c, s_, e=e, xin=xin: T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"],
-                                                                        False, 1, c, s_))
-            out, _ = T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp)
-            lin_acts.append(out)
+            lin_acts.append(self._linear(T, e, lin_acts[-1]))
+            if stop_after == nconv + li:
+                return lin_acts[-1], {"acts": acts, "lin_acts": lin_acts}
         logits = lin_acts[-1].reshape(B, -1)
         return logits, {"acts": acts, "lin_acts": lin_acts}
+
+    def forward_from(self, k: int, h: torch.Tensor) -> torch.Tensor:
+        """Logits of the network given the output ``h`` of block ``k`` (engine layout)."""
+        T = ops.require()
+        P = self._pack()
+        nconv = len(self.plan.convs)
+        B = h.shape[0]
+        for ci in range(k + 1, nconv):
+            h, _ = self._conv(T, P["convs"][ci], h)
+        if k < nconv:
+            h = h.reshape(B, 1, 1, -1)
+        for li in range(max(0, k + 1 - nconv), len(P["lins"])):
+            h = self._linear(T, P["lins"][li], h)
+        return h.reshape(B, -1)
+
+    def loss_from(self, k: int, h: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """Per-sample cross-entropy of the network continued from block ``k``'s output."""
+        loss, _ = ops.cross_entropy(self.forward_from(k, h), y, 1.0, False)
+        return loss
 
     def score_arena(self, B: int, want, device):
         """Persistent zeroed (B, C) score slabs for the blocks in ``want`` (one allocation).
