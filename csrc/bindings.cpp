@@ -62,9 +62,13 @@ at::Tensor channel_reduce(const c10::optional<at::Tensor>& act, const c10::optio
   TORCH_CHECK(!need_g || grad.has_value(), "mode ", mode, " needs the gradient");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ref.device());
   auto out = at::empty({s.B, s.C}, ref.options());
+  const int wse = tp_channel_reduce_ws_elems((int)s.B, (int)s.C, (int)s.S, s.cl ? 1 : 0);
+  at::Tensor ws;
+  if (wse > 0) ws = at::empty({wse}, ref.options());
   TP_CHECK_HIP(tp_channel_reduce(need_a ? act->data_ptr<float>() : nullptr,
-                                 need_g ? grad->data_ptr<float>() : nullptr, out.data_ptr<float>(), (int)s.B,
-                                 (int)s.C, (int)s.S, (int)mode, s.cl ? 1 : 0, cur_stream()));
+                                 need_g ? grad->data_ptr<float>() : nullptr, out.data_ptr<float>(),
+                                 wse > 0 ? ws.data_ptr<float>() : nullptr, (int)s.B, (int)s.C, (int)s.S, (int)mode,
+                                 s.cl ? 1 : 0, cur_stream()));
   return out;
 }
 

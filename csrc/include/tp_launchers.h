@@ -5,8 +5,9 @@
 
 extern "C" {
 // channel_reduce.hip
-hipError_t tp_channel_reduce(const float* act, const float* grad, float* out, int B, int C, int S, int mode,
-                             int channels_last, hipStream_t st);
+hipError_t tp_channel_reduce(const float* act, const float* grad, float* out, float* ws, int B, int C, int S,
+                             int mode, int channels_last, hipStream_t st);
+int tp_channel_reduce_ws_elems(int B, int C, int S, int channels_last);
 hipError_t tp_column_accumulate(const float* v, double* acc_sum, double* acc_sq, int B, int C, hipStream_t st);
 // prune_ops.hip
 hipError_t tp_channel_fill(float* x, long long B, int C, long long S, const int64_t* idx, int nidx, float value,

@@ -12,6 +12,9 @@ namespace tp {
 
 enum ReduceMode : int { TAYLOR_ABS = 0, TAYLOR_SIGNED = 1, SENS_ABS = 2, APOZ_POS = 3, SUM_GRAD = 4 };
 
+// spatial chunks of the NHWC reduction (>= ~512 positions each, at most 64)
+__host__ __device__ inline int nhwc_chunks(int S) { return S <= 1024 ? 1 : (S / 512 > 64 ? 64 : S / 512); }
+
 template <int MODE>
 __device__ __forceinline__ float elem(float a, float g) {
   if constexpr (MODE == TAYLOR_ABS || MODE == TAYLOR_SIGNED) return -(g * a);
@@ -63,19 +66,23 @@ __global__ __launch_bounds__(256) void channel_reduce_nchw(const float* __restri
   if (row < rows && lr == 0) out[row] = finish<MODE>(acc);
 }
 
-// NHWC / channels_last (b, s, c): a block owns (b, 64-channel tile); 4 waves split s.
+// NHWC / channels_last (b, s, c): a block owns (b, 64-channel tile, spatial chunk); 4 waves
+// split the chunk. With several chunks (large feature maps: 112x112 = 12,544 positions) each
+// block writes a partial to ``ws`` [b][chunk][c] and nhwc_finish sums the chunks in order.
 template <int MODE>
 __global__ __launch_bounds__(256) void channel_reduce_nhwc(const float* __restrict__ act,
                                                            const float* __restrict__ grad,
-                                                           float* __restrict__ out, int C, int S) {
+                                                           float* __restrict__ out, float* __restrict__ ws,
+                                                           int C, int S, int chunk) {
   __shared__ float part[4][64];
   const int b = blockIdx.y;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sg = threadIdx.x >> 6;
+  const int s0 = blockIdx.z * chunk, s1 = min(S, s0 + chunk);
   float acc = 0.f;
   if (c < C) {
     const long long base = (long long)b * S * C + c;
-    for (int s = sg; s < S; s += 4) {
+    for (int s = s0 + sg; s < s1; s += 4) {
       float av = 0.f, gv = 0.f;
       if constexpr (MODE != SENS_ABS && MODE != SUM_GRAD) av = act[base + (long long)s * C];
       if constexpr (MODE != APOZ_POS) gv = grad[base + (long long)s * C];
@@ -86,16 +93,31 @@ __global__ __launch_bounds__(256) void channel_reduce_nhwc(const float* __restri
   __syncthreads();
   if (sg == 0 && c < C) {
     float v = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
-    out[(long long)b * C + c] = finish<MODE>(v);
+    if (gridDim.z == 1) out[(long long)b * C + c] = finish<MODE>(v);
+    else ws[((long long)b * gridDim.z + blockIdx.z) * C + c] = v;
   }
 }
 
 template <int MODE>
-static hipError_t launch_reduce(const float* act, const float* grad, float* out, int B, int C, int S,
+__global__ __launch_bounds__(256) void nhwc_finish(const float* __restrict__ ws, float* __restrict__ out, int B,
+                                                   int C, int chunks) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)B * C) return;
+  const long long b = t / C, c = t % C;
+  float v = 0.f;
+  for (int k = 0; k < chunks; ++k) v += ws[(b * chunks + k) * C + c];
+  out[t] = finish<MODE>(v);
+}
+
+template <int MODE>
+static hipError_t launch_reduce(const float* act, const float* grad, float* out, float* ws, int B, int C, int S,
                                 int channels_last, hipStream_t st) {
   if (channels_last) {
-    dim3 grid(ceil_div(C, 64), B);
-    channel_reduce_nhwc<MODE><<<grid, 256, 0, st>>>(act, grad, out, C, S);
+    const int chunks = ws ? nhwc_chunks(S) : 1;
+    const int chunk = (S + chunks - 1) / chunks;
+    dim3 grid(ceil_div(C, 64), B, chunks);
+    channel_reduce_nhwc<MODE><<<grid, 256, 0, st>>>(act, grad, out, ws, C, S, chunk);
+    if (chunks > 1) nhwc_finish<MODE><<<ceil_div((long long)B * C, 256), 256, 0, st>>>(ws, out, B, C, chunks);
     return hipGetLastError();
   }
   long long rows = (long long)B * C;
@@ -192,15 +214,20 @@ extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, c
   return hipGetLastError();
 }
 
-extern "C" hipError_t tp_channel_reduce(const float* act, const float* grad, float* out, int B, int C,
+extern "C" int tp_channel_reduce_ws_elems(int B, int C, int S, int channels_last) {
+  const int k = channels_last ? tp::nhwc_chunks(S) : 1;
+  return k > 1 ? B * C * k : 0;
+}
+
+extern "C" hipError_t tp_channel_reduce(const float* act, const float* grad, float* out, float* ws, int B, int C,
                                         int S, int mode, int channels_last, hipStream_t st) {
   using namespace tp;
   switch (mode) {
-    case TAYLOR_ABS: return launch_reduce<TAYLOR_ABS>(act, grad, out, B, C, S, channels_last, st);
-    case TAYLOR_SIGNED: return launch_reduce<TAYLOR_SIGNED>(act, grad, out, B, C, S, channels_last, st);
-    case SENS_ABS: return launch_reduce<SENS_ABS>(act, grad, out, B, C, S, channels_last, st);
-    case APOZ_POS: return launch_reduce<APOZ_POS>(act, grad, out, B, C, S, channels_last, st);
-    case SUM_GRAD: return launch_reduce<SUM_GRAD>(act, grad, out, B, C, S, channels_last, st);
+    case TAYLOR_ABS: return launch_reduce<TAYLOR_ABS>(act, grad, out, ws, B, C, S, channels_last, st);
+    case TAYLOR_SIGNED: return launch_reduce<TAYLOR_SIGNED>(act, grad, out, ws, B, C, S, channels_last, st);
+    case SENS_ABS: return launch_reduce<SENS_ABS>(act, grad, out, ws, B, C, S, channels_last, st);
+    case APOZ_POS: return launch_reduce<APOZ_POS>(act, grad, out, ws, B, C, S, channels_last, st);
+    case SUM_GRAD: return launch_reduce<SUM_GRAD>(act, grad, out, ws, B, C, S, channels_last, st);
   }
   return hipErrorInvalidValue;
 }

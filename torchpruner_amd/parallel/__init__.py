@@ -18,3 +18,6 @@ __all__ = [
     "DistContext", "ShardedBatches", "all_reduce_sum_", "barrier", "broadcast_object", "broadcast_tensor_",
     "gather_ordered_rows", "get_rank", "get_world_size", "init_distributed", "is_dist", "split_range",
 ]
+from .ddp import PrunableDDP, params_in_sync, prune_and_rewrap  # noqa: E402
+
+__all__ += ["PrunableDDP", "params_in_sync", "prune_and_rewrap"]

@@ -1,0 +1,79 @@
+"""Prune-aware DistributedDataParallel (SURVEY.md §2.6 R6/R7, §2.7 "DDP for finetune").
+
+``torch.nn.parallel.DistributedDataParallel`` sizes its gradient buckets (and, with
+``gradient_as_bucket_view``, the ``.grad`` storage) from the parameter shapes at construction.
+Structured pruning changes those shapes in place (Pruner keeps Parameter identity), so the
+wrapper must be rebuilt after every prune: :class:`PrunableDDP` does that, re-broadcasting
+the (already identical, see Pruner's index broadcast R5) parameters from rank 0 (R7).
+
+Gradient all-reduce runs on RCCL over xGMI. xGMI is point-to-point (7 links x ~153 GB/s per
+MI355X); RCCL's ring/tree channels are per-link bound, so large buckets amortise the
+per-collective latency while the first bucket still overlaps the tail of backward. The
+default ``bucket_cap_mb=64`` puts a ResNet-50 (~102 MB of fp32 gradients) in 2 buckets.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+from torch.nn.parallel import DistributedDataParallel as DDP
+
+from . import dist as pdist
+
+
+class PrunableDDP(nn.Module):
+    """Wraps ``module`` in DDP when a multi-rank process group is live (identity otherwise)
+    and rebuilds the wrapper on :meth:`rewrap` after pruning."""
+
+    def __init__(self, module: nn.Module, device=None, bucket_cap_mb: float = 64.0, **ddp_kwargs):
+        super().__init__()
+        self.module = module
+        self.device = device
+        self.bucket_cap_mb = bucket_cap_mb
+        self.ddp_kwargs = ddp_kwargs
+        self._ddp = None
+        self.rewrap()
+
+    @property
+    def distributed(self) -> bool:
+        return pdist.get_world_size() > 1
+
+    def rewrap(self):
+        """(Re)build the DDP wrapper for the current parameter shapes."""
+        self._ddp = None
+        if not self.distributed:
+            return self
+        dev = self.device
+        kw = dict(self.ddp_kwargs)
+        if dev is not None and torch.device(dev).type == "cuda":
+            kw.setdefault("device_ids", [torch.device(dev).index or 0])
+        kw.setdefault("broadcast_buffers", True)
+        self._ddp = DDP(self.module, bucket_cap_mb=self.bucket_cap_mb, **kw)
+        return self
+
+    def forward(self, *args, **kwargs):
+        if self._ddp is None:
+            return self.module(*args, **kwargs)
+        return self._ddp(*args, **kwargs)
+
+
+def prune_and_rewrap(pruner, wrapper: PrunableDDP, module, indices, cascading_modules):
+    """Prune ``module`` (+ cascade) on the unwrapped model, then rebuild the DDP buckets."""
+    pruner.prune_model(module, indices, cascading_modules=cascading_modules)
+    wrapper.rewrap()
+
+
+def params_in_sync(model: nn.Module, group=None) -> bool:
+    """True when every parameter is bitwise identical across ranks (debug / tests)."""
+    if pdist.get_world_size(group) == 1:
+        return True
+    ok = True
+    for p in model.parameters():
+        t = p.detach().float().flatten()
+        ref = t.clone()
+        pdist.broadcast_tensor_(ref, 0, group)
+        ok = ok and bool(torch.equal(ref, t))
+    flag = torch.tensor([1.0 if ok else 0.0], device=next(model.parameters()).device)
+    vals = [None] * pdist.get_world_size(group)
+    import torch.distributed as dist
+    dist.all_gather_object(vals, float(flag.item()), group=group)
+    return all(v == 1.0 for v in vals)

@@ -20,6 +20,7 @@ Differences (deliberate fixes):
 from __future__ import annotations
 
 import logging
+import os
 
 import numpy as np
 import torch
@@ -203,7 +204,9 @@ class Pruner:
 
     def _run_forward(self, x=None):
         d, b = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
-        torch.backends.cudnn.deterministic = True
+        # see _AttributionMetric.set_deterministic for the ROCm/MIOpen exception
+        if torch.version.hip is None or os.environ.get("TORCHPRUNER_DETERMINISTIC", "0") == "1":
+            torch.backends.cudnn.deterministic = True
         torch.backends.cudnn.benchmark = False
         was_training = self.model.training
         self.model.eval()
