@@ -123,7 +123,7 @@ class _AttributionMetric(ABC):
     """Abstract base of every metric (reference attributions.py:15-25)."""
 
     def __init__(self, model, data_generator, criterion, device, reduction="mean", *, group=None,
-                 shard_data=None):
+                 shard_data=None, checkpoint=None, checkpoint_every=50):
         assert reduction in ["mean", "none", "sum"] or callable(reduction), \
             'Reduction must be a string in ["mean", "none", "sum"] or a function'
         self.model = model
@@ -137,6 +137,12 @@ class _AttributionMetric(ABC):
         # shard_data=None -> shard automatically when a multi-rank group is live.
         self.group = group
         self.shard_data = shard_data
+        # Resume support (new): accumulators + processed batch indices are persisted every
+        # ``checkpoint_every`` batches to ``checkpoint`` (a per-rank path in DP runs).
+        self.checkpoint = checkpoint
+        self.checkpoint_every = checkpoint_every
+        self._ckpt = None
+        self._run_accs = None
 
     # ------------------------------------------------------------------ API parity
     @abstractmethod
@@ -227,11 +233,36 @@ class _AttributionMetric(ABC):
         world, rank = self._world()
         it = pdist.ShardedBatches(self.data_gen, rank, world) if self._sharding() else \
             ((i, x, y) for i, (x, y) in enumerate(self.data_gen))
+        ck = self._ckpt
         for i, x, y in it:
+            if ck is not None and i in ck.done:
+                continue  # processed before an interruption
             yield i, _to(x, self.device), _to(y, self.device)
+            if ck is not None:  # the consumer finished batch i before asking for the next one
+                ck.step(self._run_accs, i)
 
     def _new_accumulator(self) -> ScoreAccumulator:
         return ScoreAccumulator(self.reduction, self.device)
+
+    def _begin_run(self, accs, eval_modules):
+        """Attach (and restore) the resumable checkpoint of this run, if configured."""
+        self._run_accs = accs
+        self._ckpt = None
+        if self.checkpoint:
+            from ..checkpoint import AttributionCheckpoint
+            names = {id(m): n for n, m in self.model.named_modules()}
+            key = "|".join([type(self).__name__, str(self.reduction), str(getattr(self, "signed", ""))] +
+                           [names.get(id(m), type(m).__name__) for m in eval_modules])
+            world, rank = self._world()
+            path = self.checkpoint if world == 1 else f"{self.checkpoint}.rank{rank}"
+            self._ckpt = AttributionCheckpoint(path, key, self.checkpoint_every)
+            self._ckpt.restore(accs)
+
+    def _end_run(self):
+        if self._ckpt is not None:
+            self._ckpt.save(self._run_accs)
+        self._ckpt = None
+        self._run_accs = None
 
     def _finalize(self, acc: ScoreAccumulator):
         # not sharded: every rank already holds the full result, so no collective

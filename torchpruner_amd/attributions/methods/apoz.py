@@ -19,5 +19,10 @@ class APoZAttributionMetric(_AttributionMetric):
 
     def _run_modules(self, eval_modules):
         accs = [self._new_accumulator() for _ in eval_modules]
-        self._forward_capture_pass(eval_modules, lambda k, out, i: accs[k].add(ops.channel_reduce(out, None, "apoz"), i))
+        self._begin_run(accs, eval_modules)
+        try:
+            self._forward_capture_pass(eval_modules,
+                                       lambda k, out, i: accs[k].add(ops.channel_reduce(out, None, "apoz"), i))
+        finally:
+            self._end_run()
         return [self._finalize(a) for a in accs]

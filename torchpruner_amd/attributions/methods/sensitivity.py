@@ -17,6 +17,10 @@ class SensitivityAttributionMetric(_AttributionMetric):
 
     def _run_modules(self, eval_modules):
         accs = [self._new_accumulator() for _ in eval_modules]
-        self._grad_capture_pass(eval_modules,
-                                lambda k, a, g, i: accs[k].add(ops.channel_reduce(None, g, "sensitivity"), i))
+        self._begin_run(accs, eval_modules)
+        try:
+            self._grad_capture_pass(eval_modules,
+                                    lambda k, a, g, i: accs[k].add(ops.channel_reduce(None, g, "sensitivity"), i))
+        finally:
+            self._end_run()
         return [self._finalize(a) for a in accs]

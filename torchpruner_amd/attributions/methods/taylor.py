@@ -24,6 +24,13 @@ class TaylorAttributionMetric(_AttributionMetric):
     def _run_modules(self, eval_modules):
         mode = "taylor_signed" if self.signed else "taylor"
         accs = [self._new_accumulator() for _ in eval_modules]
+        self._begin_run(accs, eval_modules)
+        try:
+            return self._run_loop(eval_modules, accs, mode)
+        finally:
+            self._end_run()
+
+    def _run_loop(self, eval_modules, accs, mode):
         fused = maybe_engine(self.model, eval_modules, self.criterion, self.device)
         if fused is not None:
             # native path: one fused forward + input-grad backward scores every module, then
