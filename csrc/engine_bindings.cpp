@@ -14,6 +14,9 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
                          float* taylor, int HWo, float* ws, hipStream_t st);
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
+hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
+                        int unpool, int epi, int splits, const float* scale, const float* shift, int relu, float* out,
+                        uint8_t* out_argmax, const float* act, float* taylor, float* ws, hipStream_t st);
 }
 
 namespace {
@@ -147,6 +150,90 @@ at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor
   return out;
 }
 
+int64_t wino_splits(int64_t splits, int64_t C) {
+  const int64_t chunks = C / 8;
+  splits = std::max<int64_t>(1, std::min<int64_t>(splits, chunks));
+  const int64_t per = (chunks + splits - 1) / splits;
+  return (chunks + per - 1) / per;
+}
+
+void need_u(const at::Tensor& u, int64_t C, int64_t K) {
+  need(u, "u", 3);
+  TORCH_CHECK(u.size(0) == 16 && u.size(1) == C && u.size(2) == K, "u must be (16, C, K) = (16, ", C, ", ", K,
+              "), got ", u.sizes());
+}
+
+// Winograd F(2x2,3x3) forward: x (B,H,W,C) NHWC, u (16, C, K) from winograd_weights().
+std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::Tensor& u,
+                                                 const c10::optional<at::Tensor>& scale,
+                                                 const c10::optional<at::Tensor>& shift, bool relu, bool pool,
+                                                 int64_t splits) {
+  need(x, "x", 4);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(2);
+  need_u(u, C, K);
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "Winograd F(2x2,3x3) needs even H, W");
+  TORCH_CHECK(C % 8 == 0 && K % 32 == 0, "Winograd needs C % 8 == 0 and K % 32 == 0");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const float* sc = opt_ptr(scale, K, "scale");
+  const float* sh = opt_ptr(shift, K, "shift");
+  at::Tensor out, am;
+  if (pool) {
+    out = at::empty({B, H / 2, W / 2, K}, x.options());
+    am = at::empty({B, H / 2, W / 2, K}, x.options().dtype(at::kByte));
+  } else {
+    out = at::empty({B, H, W, K}, x.options());
+  }
+  const int64_t sp = wino_splits(splits, C);
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * H * W * K}, x.options());
+  TP_CHECK_HIP(tp_conv_wino(x.data_ptr<float>(), nullptr, u.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)K,
+                            0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
+                            pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr,
+                            sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+  return {out, am};
+}
+
+// Winograd dgrad with the conv_dgrad epilogue contract; ut = winograd_weights of the
+// flipped/transposed kernel, (16, Cout, Cin).
+at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_argmax, const at::Tensor& ut,
+                           const at::Tensor& act, const c10::optional<at::Tensor>& bn_scale,
+                           const c10::optional<at::Tensor>& taylor, bool want_out, int64_t splits) {
+  need(g, "g", 4);
+  need(act, "act", 4);
+  const bool unpool = g_argmax.has_value() && g_argmax->defined();
+  const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
+  need_u(ut, Cout, Cin);
+  if (unpool) {
+    TORCH_CHECK(g.size(1) * 2 == H && g.size(2) * 2 == W, "pooled grad shape mismatch");
+    TORCH_CHECK(g_argmax->scalar_type() == at::kByte && g_argmax->sizes() == g.sizes() && g_argmax->is_contiguous(),
+                "g_argmax must be uint8 with g's shape");
+  } else {
+    TORCH_CHECK(g.size(1) == H && g.size(2) == W, "grad shape mismatch");
+  }
+  TORCH_CHECK(g.size(0) == B, "batch mismatch");
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "Winograd F(2x2,3x3) needs even H, W");
+  TORCH_CHECK(Cout % 8 == 0 && Cin % 32 == 0, "Winograd dgrad needs Cout % 8 == 0 and Cin % 32 == 0");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
+  float* tay = nullptr;
+  if (taylor.has_value() && taylor->defined()) {
+    TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
+                    taylor->numel() == B * Cin,
+                "taylor must be a contiguous float32 (B, Cin) GPU tensor");
+    tay = taylor->data_ptr<float>();
+  }
+  at::Tensor out;
+  if (want_out) out = at::empty({B, H, W, Cin}, g.options());
+  const int64_t sp = wino_splits(splits, Cout);
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
+  TP_CHECK_HIP(tp_conv_wino(g.data_ptr<float>(), unpool ? g_argmax->data_ptr<uint8_t>() : nullptr,
+                            ut.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, unpool ? 1 : 0, EPI_BWD,
+                            (int)sp, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
+                            act.data_ptr<float>(), tay, sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+  return out;
+}
+
 }  // namespace
 
 void register_engine_ops_def(torch::Library& m) {
@@ -155,10 +242,16 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
         "bool want_out, int ks, int cfg, int splits) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
+  m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits) "
+        "-> (Tensor, Tensor)");
+  m.def("conv_wino_dgrad(Tensor g, Tensor? g_argmax, Tensor ut, Tensor act, Tensor? bn_scale, "
+        "Tensor(a!)? taylor, bool want_out, int splits) -> Tensor");
 }
 
 void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_fwd", &conv_fwd);
   m.impl("conv_dgrad", &conv_dgrad);
   m.impl("conv_first", &conv_first);
+  m.impl("conv_wino_fwd", &conv_wino_fwd);
+  m.impl("conv_wino_dgrad", &conv_wino_dgrad);
 }

@@ -175,15 +175,16 @@ struct ScoreBatch {
   ScoreDesc d[16];
 };
 
-__global__ __launch_bounds__(256) void score_fold_multi(ScoreBatch batch, int take_abs, int after) {
-  __shared__ double ps[4][64];
+__global__ __launch_bounds__(1024) void score_fold_multi(ScoreBatch batch, int take_abs, int after) {
+  constexpr int RG = 16;  // row groups per block (the fold is latency bound: few columns, many rows)
+  __shared__ double ps[RG][64];
   const ScoreDesc s = batch.d[blockIdx.y];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rg = threadIdx.x >> 6;
   if (blockIdx.x * 64 >= s.C) return;  // uniform per block
   double acc = 0.0;
   if (c < s.C) {
-    for (int b = rg; b < s.B; b += 4) {
+    for (int b = rg; b < s.B; b += RG) {
       float* p = s.T + (long long)b * s.C + c;
       float v = *p;
       if (take_abs) v = fabsf(v);
@@ -194,8 +195,12 @@ __global__ __launch_bounds__(256) void score_fold_multi(ScoreBatch batch, int ta
   }
   ps[rg][threadIdx.x & 63] = acc;
   __syncthreads();
-  if (rg == 0 && c < s.C && s.acc)
-    s.acc[c] += ps[0][threadIdx.x] + ps[1][threadIdx.x] + ps[2][threadIdx.x] + ps[3][threadIdx.x];
+  if (rg == 0 && c < s.C && s.acc) {
+    double t = 0.0;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) t += ps[g][threadIdx.x];
+    s.acc[c] += t;
+  }
 }
 
 }  // namespace tp
@@ -210,7 +215,7 @@ extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, c
     maxc = std::max(maxc, C[i]);
   }
   dim3 grid(tp::ceil_div(maxc, 64), count);
-  tp::score_fold_multi<<<grid, 256, 0, st>>>(b, take_abs, after);
+  tp::score_fold_multi<<<grid, 1024, 0, st>>>(b, take_abs, after);
   return hipGetLastError();
 }
 

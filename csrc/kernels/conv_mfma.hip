@@ -392,8 +392,11 @@ __global__ __launch_bounds__(256) void conv_first_direct(const float* __restrict
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, float* __restrict__ out,
                                                          int B, int Cin, int H, int W, int relu) {
-  constexpr int G = COUT / 4;
-  extern __shared__ float4 wsh4[];  // [Cin*9][G] float4 (4 output channels per entry)
+  // a thread owns one pixel x CPT channels: each loaded input tap feeds CPT FMAs (the
+  // 4-channel version was instruction-issue bound: one global + one LDS load per 4 FMAs)
+  constexpr int CPT = COUT >= 16 ? 16 : COUT;
+  constexpr int G = COUT / CPT;
+  extern __shared__ float4 wsh4[];  // [Cin*9][COUT/4] float4
   const int KK = Cin * 9;
   float* wsh = reinterpret_cast<float*>(wsh4);
   for (int t = threadIdx.x; t < KK * COUT; t += blockDim.x) {
@@ -408,7 +411,9 @@ __global__ __launch_bounds__(256) void conv_first_direct(const float* __restrict
   const int b = (int)(pix / (H * W));
   const int r = (int)(pix % (H * W));
   const int oh = r / W, ow = r % W;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float acc[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) acc[j] = 0.f;
   for (int c = 0; c < Cin; ++c) {
     const float* xc = x + ((long long)b * Cin + c) * H * W;
 #pragma unroll
@@ -417,27 +422,35 @@ __global__ __launch_bounds__(256) void conv_first_direct(const float* __restrict
       for (int kw = 0; kw < 3; ++kw) {
         const int ih = oh + kh - 1, iw = ow + kw - 1;
         const float v = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xc[ih * W + iw] : 0.f;
-        const float4 wk = wsh4[((c * 3 + kh) * 3 + kw) * G + grp];
-        acc.x = fmaf(v, wk.x, acc.x);
-        acc.y = fmaf(v, wk.y, acc.y);
-        acc.z = fmaf(v, wk.z, acc.z);
-        acc.w = fmaf(v, wk.w, acc.w);
+        const float4* wk = wsh4 + ((c * 3 + kh) * 3 + kw) * (COUT / 4) + grp * (CPT / 4);
+#pragma unroll
+        for (int q = 0; q < CPT / 4; ++q) {
+          const float4 ww = wk[q];
+          acc[4 * q] = fmaf(v, ww.x, acc[4 * q]);
+          acc[4 * q + 1] = fmaf(v, ww.y, acc[4 * q + 1]);
+          acc[4 * q + 2] = fmaf(v, ww.z, acc[4 * q + 2]);
+          acc[4 * q + 3] = fmaf(v, ww.w, acc[4 * q + 3]);
+        }
       }
     }
   }
-  const int n = grp * 4;
-  float4 v;
-  v.x = acc.x * scale[n] + shift[n];
-  v.y = acc.y * scale[n + 1] + shift[n + 1];
-  v.z = acc.z * scale[n + 2] + shift[n + 2];
-  v.w = acc.w * scale[n + 3] + shift[n + 3];
-  if (relu) {
-    v.x = nan_relu(v.x);
-    v.y = nan_relu(v.y);
-    v.z = nan_relu(v.z);
-    v.w = nan_relu(v.w);
+  const int n0 = grp * CPT;
+#pragma unroll
+  for (int q = 0; q < CPT / 4; ++q) {
+    const int n = n0 + 4 * q;
+    float4 v;
+    v.x = acc[4 * q] * scale[n] + shift[n];
+    v.y = acc[4 * q + 1] * scale[n + 1] + shift[n + 1];
+    v.z = acc[4 * q + 2] * scale[n + 2] + shift[n + 2];
+    v.w = acc[4 * q + 3] * scale[n + 3] + shift[n + 3];
+    if (relu) {
+      v.x = nan_relu(v.x);
+      v.y = nan_relu(v.y);
+      v.z = nan_relu(v.z);
+      v.w = nan_relu(v.w);
+    }
+    *reinterpret_cast<float4*>(out + pix * COUT + n) = v;
   }
-  *reinterpret_cast<float4*>(out + pix * COUT + n) = v;
 }
 
 }  // namespace tp
@@ -554,11 +567,42 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   return hipGetLastError();
 }
 
+// Split combine + epilogue for slabs produced elsewhere (Winograd partials): slab layout
+// [splits][M][K], pooled M order for epi == fwd+pool.
+extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
+                                              const float* scale, const float* shift, int relu, float* out,
+                                              uint8_t* out_argmax, const float* act, float* taylor,
+                                              hipStream_t st) {
+  using namespace tp;
+  ConvArgs a{};
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.N = K;
+  a.M = B * H * W;
+  a.scale = scale;
+  a.shift = shift;
+  a.relu = relu;
+  a.out = out;
+  a.out_argmax = out_argmax;
+  a.act = act;
+  a.taylor = taylor;
+  a.HWo = H * W;
+  const long long MN = (long long)a.M * a.N;
+  const long long work = epi == EPI_FWD_POOL ? MN / 4 : MN;
+  unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
+  if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
+  else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
+  else if (epi == EPI_BWD) conv_epilogue<EPI_BWD><<<grid, 256, 0, st>>>(a, ws, splits);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 extern "C" hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift,
                                            float* out, int B, int Cin, int H, int W, int Cout, int relu,
                                            hipStream_t st) {
   const long long pix = (long long)B * H * W;
-  const unsigned grid = tp::ceil_div(pix * (Cout / 4), 256);
+  const unsigned grid = tp::ceil_div(pix * (Cout >= 16 ? Cout / 16 : 1), 256);
   const size_t lds = (size_t)Cin * 9 * Cout * sizeof(float);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   if (Cout == 64) tp::conv_first_direct<64><<<grid, 256, lds, st>>>(x, w, scale, shift, out, B, Cin, H, W, relu);

@@ -231,3 +231,83 @@ def test_engine_shapley_matches_generic_path(cuda, layer):
         ref = F.cross_entropy(m64.forward_partial(z64 * keep.cpu().double().view(shape), from_module=ev64),
                               y.cpu(), reduction="none")
     torch.testing.assert_close(got.double().cpu(), ref, rtol=1e-4, atol=1e-5)
+
+
+# ---------------------------------------------------------------- Winograd F(2x2,3x3)
+WINO_SHAPES = [  # B, H, W, Cin, Cout
+    (4, 32, 32, 64, 64),
+    (3, 16, 16, 128, 256),
+    (5, 8, 8, 256, 256),
+    (6, 4, 4, 512, 512),
+    (16, 2, 2, 512, 512),
+    (2, 6, 10, 40, 96),
+    (3, 18, 14, 64, 32),
+]
+
+
+@pytest.mark.parametrize("shape", WINO_SHAPES)
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("pool", [False, True])
+def test_wino_fwd(cuda, shape, splits, pool):
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import winograd_weights
+    T = ops.require()
+    B, H, W, Cin, Cout = shape
+    g = torch.Generator().manual_seed(11 + hash(shape) % 1000)
+    x = _rand(B, H, W, Cin, gen=g)
+    w = _rand(Cout, Cin, 3, 3, gen=g) * (2.0 / (9 * Cin)) ** 0.5
+    scale = _rand(Cout, gen=g).abs() + 0.5
+    shift = _rand(Cout, gen=g) * 0.1
+    ref, am_ref = _ref_fwd(x, w, scale, shift, True, pool)
+    u = winograd_weights(w.to(cuda))
+    out, am = T.conv_wino_fwd(x.to(cuda), u, scale.to(cuda), shift.to(cuda), True, pool, splits)
+    torch.testing.assert_close(out.cpu(), ref, rtol=3e-4, atol=3e-4)
+    if pool:
+        assert (am.cpu().long() == am_ref).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("shape", WINO_SHAPES)
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("unpool", [False, True])
+def test_wino_dgrad_taylor(cuda, shape, splits, unpool):
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import winograd_weights
+    T = ops.require()
+    B, H, W, Cin, Cout = shape
+    if Cin % 32:
+        pytest.skip("dgrad output channels must be a multiple of 32")
+    g = torch.Generator().manual_seed(5 + hash(shape) % 100)
+    w = _rand(Cout, Cin, 3, 3, gen=g) * (1.0 / (9 * Cin)) ** 0.5
+    act = torch.relu(_rand(B, H, W, Cin, gen=g))
+    bn_scale = _rand(Cin, gen=g).abs() + 0.5
+    if unpool:
+        gp = _rand(B, H // 2, W // 2, Cout, gen=g)
+        am = torch.randint(0, 4, (B, H // 2, W // 2, Cout), generator=g, dtype=torch.uint8)
+        gfull = torch.zeros(B, H, W, Cout)
+        for q in range(4):
+            dy, dx = q // 2, q % 2
+            gfull[:, dy::2, dx::2, :] = torch.where(am == q, gp, torch.zeros(()))
+    else:
+        gfull = _rand(B, H, W, Cout, gen=g)
+    dx = torch.nn.grad.conv2d_input((B, Cin, H, W), w.double(), gfull.permute(0, 3, 1, 2).double(), padding=1)
+    dx = dx.permute(0, 2, 3, 1)
+    tay_ref = (-(dx * act.double())).sum((1, 2))
+    out_ref = torch.where(act > 0, dx * bn_scale.double(), torch.zeros((), dtype=torch.float64))
+    ut = winograd_weights(w.flip(2, 3).transpose(0, 1).to(cuda))
+    tay = torch.zeros(B, Cin, device=cuda)
+    gin = (gp if unpool else gfull).to(cuda)
+    out = T.conv_wino_dgrad(gin, am.to(cuda) if unpool else None, ut, act.to(cuda), bn_scale.to(cuda), tay, True,
+                            splits)
+    torch.testing.assert_close(out.cpu(), out_ref.float(), rtol=3e-4, atol=3e-4)
+    torch.testing.assert_close(tay.cpu(), tay_ref.float(), rtol=3e-4, atol=3e-3)
+
+
+def test_wino_nan_propagation(cuda):
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import winograd_weights
+    T = ops.require()
+    x = torch.randn(2, 4, 4, 32)
+    x[:, 1, 1, 5] = float("nan")
+    u = winograd_weights(torch.randn(32, 32, 3, 3).to(cuda) * 0.1)
+    out, am = T.conv_wino_fwd(x.to(cuda), u, None, None, True, True, 1)
+    assert torch.isnan(out.cpu()[:, 0, 0]).all()

@@ -13,7 +13,7 @@ import json
 import torch
 
 from torchpruner_amd import ops
-from torchpruner_amd.engine.fused_chain import _pick_cfg
+from torchpruner_amd.engine.fused_chain import _pick_cfg, _wino_splits, winograd_weights
 
 # (H, W, Cin, Cout, pool) of the 12 MFMA convs of VGG16 on 32x32 inputs
 VGG16_LAYERS = [
@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--all-cfg", action="store_true")
+    ap.add_argument("--wino", action="store_true", help="also time the Winograd kernel (splits sweep)")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     T = ops.require()
@@ -89,6 +90,20 @@ def main():
                 tot_t += tf + tb
             print(f"L{li+1:2d} {H:2d}x{W:<2d} {Cin:3d}->{Cout:3d} pool={int(pool)} cfg f{fc}/{fs} b{bc}/{bs}: "
                   f"fwd {tf:7.1f} us {flops/tf/1e6:6.1f} TF | dgrad {tb:7.1f} us {flops/tb/1e6:6.1f} TF", flush=True)
+        if args.wino:
+            # TF/s columns are direct-conv-equivalent FLOPs (2*M*N*9*C) / time
+            u = winograd_weights(w.view(Cout, 3, 3, Cin).permute(0, 3, 1, 2))
+            ut = winograd_weights(wt.view(Cin, 3, 3, Cout).permute(0, 3, 1, 2))
+            P = B * (H // 2) * (W // 2)
+            base_f, base_b = _wino_splits(P, Cout, Cin), _wino_splits(P, Cin, Cout)
+            for sf, sb in sorted({(base_f, base_b), (1, 1), (max(1, base_f // 2), max(1, base_b // 2)),
+                                  (base_f * 2, base_b * 2)}):
+                tf = timeit(lambda: T.conv_wino_fwd(x, u, sc, sh, True, pool, sf), args.iters)
+                tb = timeit(lambda: T.conv_wino_dgrad(g, am, ut, act, scin, tay, True, sb), args.iters)
+                rows.append({"layer": li + 1, "wino": True, "splits": [sf, sb], "fwd_us": round(tf, 1),
+                             "bwd_us": round(tb, 1)})
+                print(f"    wino splits f{sf}/b{sb}: fwd {tf:7.1f} us {flops/tf/1e6:6.1f} TFe | "
+                      f"dgrad {tb:7.1f} us {flops/tb/1e6:6.1f} TFe", flush=True)
     if tot_t:
         print(f"TOTAL {tot_t:.1f} us, {tot_f / tot_t / 1e6:.1f} TF/s average")
     if args.json:

@@ -42,6 +42,36 @@ from .. import ops
 # 4=128x128, 5=256x64, 6=128x64 (8 waves)
 _CU = 256
 _TILES = {0: (128, 128), 1: (256, 64), 2: (64, 64), 3: (128, 64), 4: (128, 128), 5: (256, 64), 6: (128, 64)}
+WINO = -1  # pseudo tile cfg: fused Winograd F(2x2,3x3) kernel (winograd.hip)
+
+# Winograd F(2x2,3x3) weight transform G g G^T
+_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+
+
+@torch.no_grad()
+def winograd_weights(w: torch.Tensor) -> torch.Tensor:
+    """(K, C, 3, 3) conv weight -> (16, C, K) transformed weights U[xi][c][k] = (G g G^T)[xi]
+    in the layout winograd.hip stages into LDS: within every 32-channel block of K the
+    output channel j + 16*n is stored at position 2*j + n (one 64-bit LDS read feeds both
+    MFMA column tiles of a lane). Computed in fp64, rounded once to fp32."""
+    K, C = w.shape[0], w.shape[1]
+    assert w.shape[2:] == (3, 3) and K % 32 == 0, "winograd_weights needs 3x3 kernels and K % 32 == 0"
+    G = torch.tensor(_G, dtype=torch.float64, device=w.device)
+    u = torch.einsum("ia,kcab,jb->ijck", G, w.double(), G).reshape(16, C, K)
+    u = u.reshape(16, C, K // 32, 2, 16).transpose(3, 4).reshape(16, C, K)
+    return u.float().contiguous()
+
+
+def _wino_ok(H, W, C, K):
+    return H % 2 == 0 and W % 2 == 0 and C % 8 == 0 and K % 32 == 0 and H * W >= 16
+
+
+def _wino_splits(P, K, C):
+    tiles = math.ceil(P / 64) * (K // 32)
+    splits, chunks = 1, C // 8
+    while tiles * splits < 2 * _CU and splits * 2 <= chunks // 4 and splits < 16:
+        splits *= 2
+    return splits
 
 
 def _splits_for(M, N, K, bm, bn):
@@ -77,8 +107,12 @@ class Autotuner:
         self.cache = {}
         self.enabled = os.environ.get("TORCHPRUNER_AUTOTUNE", "1") != "0"
 
-    def candidates(self, M, N, K):
+    def candidates(self, M, N, K, wino=None):
+        """``wino``: (P tiles, C) when the Winograd kernel applies to this conv."""
         out = []
+        if wino is not None:
+            sp = _wino_splits(wino[0], N, wino[1])
+            out += [(WINO, sp)] + ([(WINO, max(1, sp // 2))] if sp > 1 else [])
         for cfg, (bm, bn) in _TILES.items():
             if N <= 64 and bn == 128:
                 continue
@@ -88,17 +122,17 @@ class Autotuner:
                 out.append((cfg, max(1, sp // 2)))
         return out
 
-    def choose(self, key, M, N, K, run):
+    def choose(self, key, M, N, K, run, wino=None):
         """``run(cfg, splits)`` launches the op once (must be side-effect free)."""
         hit = self.cache.get(key)
         if hit is not None:
             return hit
         if not self.enabled or torch.cuda.is_current_stream_capturing():
-            res = _pick_cfg(M, N, K)
+            res = (WINO, _wino_splits(wino[0], N, wino[1])) if wino is not None else _pick_cfg(M, N, K)
             self.cache[key] = res
             return res
         best = None
-        for cand in self.candidates(M, N, K):
+        for cand in self.candidates(M, N, K, wino):
             run(*cand)  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -228,6 +262,7 @@ class FusedChainEngine:
         self._key = None
         self._packed = None
         self._arenas = {}
+        self.use_wino = os.environ.get("TORCHPRUNER_WINOGRAD", "1") != "0"
 
     # ------------------------------------------------------------------ weights
     def _params_key(self):
@@ -269,6 +304,11 @@ class FusedChainEngine:
                 entry["w"] = w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous()  # [n][(kh,kw,ci)]
             # dgrad operand: flipped taps, transposed channels -> [ci][(kh,kw,co)]
             entry["wt"] = w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1).contiguous()
+            if self.use_wino:
+                if not b.first and cout % 32 == 0 and w.shape[1] % 8 == 0:
+                    entry["u"] = winograd_weights(w)
+                if w.shape[1] % 32 == 0 and cout % 8 == 0:
+                    entry["ut"] = winograd_weights(w.flip(2, 3).transpose(0, 1))
             convs.append(entry)
         lins = []
         for b in self.plan.linears:
@@ -286,13 +326,26 @@ class FusedChainEngine:
         return self._packed
 
     # ------------------------------------------------------------------ execution
-    def _conv(self, T, e, h):
-        M = h.shape[0] * h.shape[1] * h.shape[2]
-        N, K = e["scale"].numel(), e["w"].shape[1]
-        cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"]), M, N, K,
-                               lambda c, s_, e=e, hh=h: T.conv_fwd(hh, e["w"], e["scale"], e["shift"], True,
-                                                                  e["pool"], 3, c, s_))
+    @staticmethod
+    def _conv_run(T, e, h, cfg, sp):
+        if cfg == WINO:
+            return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp)
         return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
+
+    def _conv(self, T, e, h):
+        B, H, W, C = h.shape
+        M = B * H * W
+        N, K = e["scale"].numel(), e["w"].shape[1]
+        wino = (B * (H // 2) * (W // 2), C) if "u" in e and _wino_ok(H, W, C, N) else None
+        cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"], wino is not None), M, N, K,
+                               lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino)
+        return self._conv_run(T, e, h, cfg, sp)
+
+    @staticmethod
+    def _dgrad_run(T, e, g, am, act, sc, taylor, want_out, cfg, sp):
+        if cfg == WINO:
+            return T.conv_wino_dgrad(g, am, e["ut"], act, sc, taylor, want_out, sp)
+        return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp)
 
     def _linear(self, T, e, xin):
         B = xin.shape[0]
@@ -421,11 +474,13 @@ class FusedChainEngine:
             need_out = ci - 1 > 0
             sc_prev = P["convs"][ci - 1]["scale"]
             gg = g
-            cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None), M,
-                                   prev_act.shape[3], e["wt"].shape[1],
-                                   lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out: T.conv_dgrad(
-                                       gg, am, e["wt"], pa, sc, None, no, 3, c, s_))
-            g = T.conv_dgrad(g, am, e["wt"], prev_act, sc_prev, taylor, need_out, 3, cfg, sp)
+            Cin, Cg = prev_act.shape[3], g.shape[3]
+            wino = (B * (H // 2) * (W // 2), Cg) if "ut" in e and _wino_ok(H, W, Cg, Cin) else None
+            cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None),
+                                   M, Cin, e["wt"].shape[1],
+                                   lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out:
+                                   self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_), wino)
+            g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp)
         return res
 
 
