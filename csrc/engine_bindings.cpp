@@ -15,8 +15,8 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
-                        int unpool, int epi, int splits, const float* scale, const float* shift, int relu, float* out,
-                        uint8_t* out_argmax, const float* act, float* taylor, float* ws, hipStream_t st);
+                        int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
+                        float* out, uint8_t* out_argmax, const float* act, float* taylor, float* ws, hipStream_t st);
 }
 
 namespace {
@@ -159,17 +159,18 @@ int64_t wino_splits(int64_t splits, int64_t C) {
 
 void need_u(const at::Tensor& u, int64_t C, int64_t K) {
   need(u, "u", 3);
-  TORCH_CHECK(u.size(0) == 16 && u.size(1) == C && u.size(2) == K, "u must be (16, C, K) = (16, ", C, ", ", K,
-              "), got ", u.sizes());
+  TORCH_CHECK(C % 8 == 0 && K % 32 == 0 && u.size(0) == C / 8 && u.size(1) == K / 32 && u.size(2) == 4096,
+              "u must be the Winograd U images (C/8, K/32, 4096) = (", C / 8, ", ", K / 32, ", 4096), got ",
+              u.sizes());
 }
 
 // Winograd F(2x2,3x3) forward: x (B,H,W,C) NHWC, u (16, C, K) from winograd_weights().
 std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::Tensor& u,
                                                  const c10::optional<at::Tensor>& scale,
                                                  const c10::optional<at::Tensor>& shift, bool relu, bool pool,
-                                                 int64_t splits) {
+                                                 int64_t splits, bool staged) {
   need(x, "x", 4);
-  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(2);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
   need_u(u, C, K);
   TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "Winograd F(2x2,3x3) needs even H, W");
   TORCH_CHECK(C % 8 == 0 && K % 32 == 0, "Winograd needs C % 8 == 0 and K % 32 == 0");
@@ -187,7 +188,8 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * H * W * K}, x.options());
   TP_CHECK_HIP(tp_conv_wino(x.data_ptr<float>(), nullptr, u.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)K,
-                            0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
+                            0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, staged ? 1 : 0, sc, sh, relu ? 1 : 0,
+                            out.data_ptr<float>(),
                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr,
                             sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
   return {out, am};
@@ -197,7 +199,7 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
 // flipped/transposed kernel, (16, Cout, Cin).
 at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_argmax, const at::Tensor& ut,
                            const at::Tensor& act, const c10::optional<at::Tensor>& bn_scale,
-                           const c10::optional<at::Tensor>& taylor, bool want_out, int64_t splits) {
+                           const c10::optional<at::Tensor>& taylor, bool want_out, int64_t splits, bool staged) {
   need(g, "g", 4);
   need(act, "act", 4);
   const bool unpool = g_argmax.has_value() && g_argmax->defined();
@@ -229,7 +231,7 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
   if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
   TP_CHECK_HIP(tp_conv_wino(g.data_ptr<float>(), unpool ? g_argmax->data_ptr<uint8_t>() : nullptr,
                             ut.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, unpool ? 1 : 0, EPI_BWD,
-                            (int)sp, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
+                            (int)sp, staged ? 1 : 0, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
                             act.data_ptr<float>(), tay, sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
   return out;
 }
@@ -242,10 +244,10 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
         "bool want_out, int ks, int cfg, int splits) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
-  m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits) "
-        "-> (Tensor, Tensor)");
+  m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
+        "bool staged=True) -> (Tensor, Tensor)");
   m.def("conv_wino_dgrad(Tensor g, Tensor? g_argmax, Tensor ut, Tensor act, Tensor? bn_scale, "
-        "Tensor(a!)? taylor, bool want_out, int splits) -> Tensor");
+        "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True) -> Tensor");
 }
 
 void register_engine_ops_impl(torch::Library& m) {

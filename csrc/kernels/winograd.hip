@@ -4,17 +4,35 @@
 //
 //   * a wave owns 16 output tiles (2x2 pixels each) x 32 output channels x all 16 transform
 //     points xi; its 16*2 accumulator tiles (16x16, 4 regs) live in registers;
-//   * per 8-channel chunk each lane loads the 4x4 input patch of "its" tile (MFMA A-row =
-//     lane&15) for 2 channels (A-k = lane>>4), forms V = B^T d B in registers (32 adds per
-//     channel) and feeds the 16 V values straight into 16 MFMAs as the A operand;
-//   * the transformed weights U = G g G^T ([16][C][K], K interleaved per 32-block) are staged
-//     in LDS per block (shared by its 4 waves) and read as the B operand;
+//   * per 8-channel chunk each lane fetches the 4x4 input patch of "its" tile (MFMA A-row =
+//     lane&15) for 2 channels (A-k = lane>>4), forms V = B^T d B in registers (packed fp32
+//     adds, both channels at once) and feeds the 16 V values straight into the MFMAs as the
+//     A operand;
+//   * the transformed weights U = G g G^T are pre-arranged on the host into the exact 16-KB
+//     LDS image of one (8-channel chunk, 32-output-channel block) and DMA'd into LDS with
+//     `buffer_load_dwordx4 ... lds` (no staging VGPRs); the image is XOR-arranged so every
+//     B-operand ds_read_b64 is bank-conflict free;
+//   * input path (XMODE):
+//       X_DIRECT  each lane loads its 16 patch pixels straight from HBM/L2 (prefetched one
+//                 chunk ahead). Simple, any shape, but 4x overlapping patches make the
+//                 texture-address path the bottleneck (TA busy ~60%, PMC);
+//       X_UNPOOL  the same, rebuilding the full-resolution dgrad input from the pooled
+//                 gradient + argmax bytes (a 4x4 patch spans 3x3 pooled cells);
+//       X_STAGED  the block's input REGION (its 64 tiles' union, halos shared) is DMA'd once
+//                 per chunk into a double-buffered, source-swizzled LDS image, and lanes read
+//                 their patches with conflict-free ds_read_b64: ~3x fewer bytes through the
+//                 TA and 1/5 of the load instructions;
+//       X_STAGED_UNPOOL  the same for the dgrad of a pooled layer: the POOLED gradient region
+//                 (16-B DMA) and its argmax bytes (4-B DMA) are staged, and each lane rebuilds
+//                 its full-resolution 4x4 patch from the 3x3 pooled cells it spans;
 //   * the epilogue applies Y = A^T m A in registers. A 2x2 Winograd output tile IS a 2x2
 //     max-pool window, so pooling is 3 max ops on values the lane already holds; BN affine,
 //     ReLU, Taylor partials and the masked gradient are fused exactly as in conv_mfma.hip.
-//   * UNPOOL: the dgrad input is rebuilt on the fly from the pooled gradient + argmax bytes
-//     (a 4x4 full-resolution patch spans 3x3 pooled cells).
 #include "tp_common.h"
+
+#include <map>
+#include <mutex>
+#include <tuple>
 
 namespace tp {
 
@@ -23,11 +41,17 @@ __device__ f32x2 buf_load_f32x2(i32x4 rsrc, int voffset, int soffset, int aux) _
 __device__ unsigned short buf_load_u16(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i16");
 
 enum WEpi : int { W_FWD = 0, W_FWD_POOL = 1, W_BWD = 2, W_PARTIAL = 3 };
+enum XMode : int { X_DIRECT = 0, X_UNPOOL = 1, X_STAGED = 2, X_STAGED_UNPOOL = 3 };
+
+constexpr int W_TK = 32;             // output channels per block
+constexpr int W_CH = 8;              // input channels per chunk
+constexpr int W_UIMG = 4096;         // floats of one U image (16 xi x 8 c x 32 k)
+constexpr int W_XS = 6144;           // floats of one staged input image (24 KiB)
 
 struct WinoArgs {
-  const float* x;           // NHWC (B,H,W,C), or pooled grad (B,H/2,W/2,C) when UNPOOL
-  const uint8_t* x_argmax;  // UNPOOL: argmax bytes of the pooled grad
-  const float* u;           // [16][C][K] transformed weights, K interleaved per 32-block
+  const float* x;           // NHWC (B,H,W,C), or pooled grad (B,H/2,W/2,C) for X_UNPOOL
+  const uint8_t* x_argmax;  // X_UNPOOL: argmax bytes of the pooled grad
+  const float* u;           // U images [C/8][K/32][4096]
   int B, H, W, C, K;
   int P;                    // output tiles = B*(H/2)*(W/2)
   int c_per_split;
@@ -40,6 +64,11 @@ struct WinoArgs {
   const float* act;
   float* taylor;
   int pooled_m;             // W_PARTIAL: write the slab in pooled M order (b, th, tw, q)
+  // X_STAGED region geometry: a block's 64 tiles = n_img images x R tile rows each
+  int n_img, R, RW, IP;     // RW: row pitch (pixels), IP: image pitch (pixels)
+  int rounds;               // 256-slot DMA rounds per staged image
+  // X_STAGED_UNPOOL: pooled region pitches; argmax image rounds and its byte offset
+  int arounds, aoff;
 };
 
 __device__ __forceinline__ int xcd_remap_w(int bid, int nwg) {
@@ -48,9 +77,12 @@ __device__ __forceinline__ int xcd_remap_w(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-// V = B^T d B for one channel (d row-major 4x4), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
-__device__ __forceinline__ void input_transform(const float d[16], float v[16]) {
-  float t[16];
+// staged-image slot swizzle (an involution; keeps 4-slot groups): linear slot L = 2*pixel + half
+__host__ __device__ __forceinline__ int xswz(int L) { return L ^ ((L >> 4) & 3); }
+
+// V = B^T d B on two channels at once, B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
+__device__ __forceinline__ void input_transform2(const f32x2 d[16], f32x2 v[16]) {
+  f32x2 t[16];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     t[0 * 4 + j] = d[0 * 4 + j] - d[2 * 4 + j];
@@ -82,147 +114,17 @@ __device__ __forceinline__ void output_transform(const float m[16], float y[4]) 
   }
 }
 
-template <int EPI, bool UNPOOL>
-__global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
-  constexpr int TK = 32, CH = 8, LDU = 48;       // LDU: 2*48 = 32 mod 64 -> conflict-free b64 reads
-  constexpr int STAGE = 16 * CH * LDU;           // floats per U stage
-  __shared__ __attribute__((aligned(16))) float us[2 * STAGE];
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = lane & 15, g = lane >> 4;
-  const int n_k = (p.K + TK - 1) / TK;
-  const int tile = xcd_remap_w(blockIdx.x, gridDim.x);
-  const int k0 = (tile % n_k) * TK;
-  const int pw0 = (tile / n_k) * 64 + wave * 16;  // first tile of this wave
+// one 16-B-per-lane LDS-DMA: lane l's 16 bytes land at lds_base + 16*l
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, float* lds_base, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)lds_base, 16, voff, soff, 0, 0);
+}
+
+// ---- epilogue: output tiles pw0 + 4g + r, channels k0 + j + 16n ------------------------
+template <int EPI>
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16][2], int pw0, int k0, int g, int j) {
   const int H2 = p.H >> 1, W2 = p.W >> 1, T_img = H2 * W2;
-  const int c_begin = blockIdx.y * p.c_per_split;
-  const int c_end = min(p.C, c_begin + p.c_per_split);
-
-  const i32x4 xr = make_rsrc(p.x, (unsigned)(p.x_elems * 4));
-  const i32x4 ar = make_rsrc(p.x_argmax, UNPOOL ? (unsigned)p.x_elems : 0u);
-  const i32x4 ur = make_rsrc(p.u, (unsigned)(16u * p.C * p.K * 4u));
-  constexpr unsigned OOB = 0x80000000u;
-
-  // ---- the input tile of this lane (A row j) ------------------------------------------
-  const int pin = pw0 + j;
-  int b = 0, th = 0, tw = 0;
-  const bool tok = pin < p.P;
-  if (tok) {
-    b = pin / T_img;
-    const int r = pin - b * T_img;
-    th = r / W2;
-    tw = r - th * W2;
-  }
-  // offsets (elements, channel 0) and validity of the 16 patch pixels (or 9 pooled cells)
-  int poff[16];
-  unsigned pmask = 0;
-  if constexpr (!UNPOOL) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ih = 2 * th - 1 + r, iw = 2 * tw - 1 + q;
-        const bool ok = tok && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-        poff[r * 4 + q] = ((b * p.H + ih) * p.W + iw) * p.C;
-        pmask |= (ok ? 1u : 0u) << (r * 4 + q);
-      }
-  } else {
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int ph = th - 1 + r, pq = tw - 1 + q;
-        const bool ok = tok && ph >= 0 && ph < H2 && pq >= 0 && pq < W2;
-        poff[r * 3 + q] = ((b * H2 + ph) * W2 + pq) * p.C;
-        pmask |= (ok ? 1u : 0u) << (r * 3 + q);
-      }
-  }
-
-  // ---- U staging: thread -> (row = xi*CH + c, half of the 32 k's) ---------------------
-  const int srow = threadIdx.x >> 1, shalf = threadIdx.x & 1;
-  const int s_xi = srow / CH, s_c = srow % CH;
-  float4 ru[4];
-  auto load_u = [&](int c0) {
-    const unsigned base = (unsigned)((s_xi * p.C + c0 + s_c) * p.K + k0 + shalf * 16) * 4u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x4 v = buf_load_f32x4(ur, (int)(base + 16u * i), 0, 0);
-      ru[i] = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  };
-  auto store_u = [&](int buf) {
-    float* dst = us + buf * STAGE + srow * LDU + shalf * 16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(dst + 4 * i) = ru[i];
-  };
-
-  f32x4 acc[16][2];
-#pragma unroll
-  for (int x = 0; x < 16; ++x)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (c_begin < c_end) {
-    load_u(c_begin);
-    store_u(0);
-    __syncthreads();
-    int buf = 0;
-    for (int c0 = c_begin; c0 < c_end; c0 += CH) {
-      const bool more = c0 + CH < c_end;
-      if (more) load_u(c0 + CH);
-      // patch values for channels c0+2g, c0+2g+1
-      float d0[16], d1[16];
-      const int cc = c0 + 2 * g;
-      if constexpr (!UNPOOL) {
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          const unsigned vo = ((pmask >> t) & 1u) ? (unsigned)(poff[t] + cc) * 4u : OOB;
-          const f32x2 v = buf_load_f32x2(xr, (int)vo, 0, 0);
-          d0[t] = v[0];
-          d1[t] = v[1];
-        }
-      } else {
-        float g0[9], g1[9];
-        unsigned am[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const bool ok = (pmask >> t) & 1u;
-          const f32x2 v = buf_load_f32x2(xr, (int)(ok ? (unsigned)(poff[t] + cc) * 4u : OOB), 0, 0);
-          g0[t] = v[0];
-          g1[t] = v[1];
-          am[t] = buf_load_u16(ar, (int)(ok ? (unsigned)(poff[t] + cc) : OOB), 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int cell = ((r + 1) >> 1) * 3 + ((q + 1) >> 1);
-            const unsigned want = (unsigned)((((r + 1) & 1) << 1) | ((q + 1) & 1));
-            d0[r * 4 + q] = (am[cell] & 0xffu) == want ? g0[cell] : 0.f;
-            d1[r * 4 + q] = ((am[cell] >> 8) & 0xffu) == want ? g1[cell] : 0.f;
-          }
-      }
-      const float* ub = us + buf * STAGE;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        float v[16];
-        input_transform(e == 0 ? d0 : d1, v);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int x = 0; x < 16; ++x) {
-          const float2 w2 = *reinterpret_cast<const float2*>(ub + (x * CH + 2 * g + e) * LDU + 2 * j);
-          acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[x], w2.x, acc[x][0], 0, 0, 0);
-          acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[x], w2.y, acc[x][1], 0, 0, 0);
-        }
-        __builtin_amdgcn_s_setprio(0);
-      }
-      if (more) store_u(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
-    }
-  }
-
-  // ---- epilogue: output tiles pw0 + 4g + r, channels k0 + j + 16n ----------------------
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
     const int k = k0 + j + 16 * n;
@@ -293,18 +195,382 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   }
 }
 
+template <int EPI, int XMODE>
+__global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
+  constexpr bool STAGED = XMODE == X_STAGED || XMODE == X_STAGED_UNPOOL, UNPOOL = XMODE == X_UNPOOL;
+  // separate objects per buffer so the compiler's LDS-DMA alias tracking can tell them apart
+  __shared__ __attribute__((aligned(16))) float us0[W_UIMG];
+  __shared__ __attribute__((aligned(16))) float us1[W_UIMG];
+  __shared__ __attribute__((aligned(16))) float xs0[STAGED ? W_XS : 4];
+  __shared__ __attribute__((aligned(16))) float xs1[STAGED ? W_XS : 4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int n_k = p.K / W_TK;
+  const int tile = xcd_remap_w(blockIdx.x, gridDim.x);
+  const int kb = tile % n_k, k0 = kb * W_TK;
+  const int blk_p = tile / n_k;
+  const int pw0 = blk_p * 64 + wave * 16;  // first tile of this wave
+  const int H2 = p.H >> 1, W2 = p.W >> 1, T_img = H2 * W2;
+  const int c_begin = blockIdx.y * p.c_per_split;
+  const int c_end = min(p.C, c_begin + p.c_per_split);
+  constexpr unsigned OOB = 0x80000000u;
+
+  const __amdgpu_buffer_rsrc_t urs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, (int)(16u * p.C * p.K * 4u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0,
+                                                                        (int)(p.x_elems * 4), 0x00020000);
+  const i32x4 xr = make_rsrc(p.x, (unsigned)(p.x_elems * 4));
+  const i32x4 ar = make_rsrc(p.x_argmax, UNPOOL ? (unsigned)p.x_elems : 0u);
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.x_argmax, (short)0, XMODE == X_STAGED_UNPOOL ? (int)p.x_elems : 0, 0x00020000);
+
+  // ---- this lane's input tile (A row j) ------------------------------------------------
+  const int pin = pw0 + j;
+  int b = 0, th = 0, tw = 0;
+  const bool tok = pin < p.P;
+  if (tok) {
+    b = pin / T_img;
+    const int r = pin - b * T_img;
+    th = r / W2;
+    tw = r - th * W2;
+  }
+
+  // X_DIRECT / X_UNPOOL: per-lane pixel offsets; X_STAGED: per-lane LDS byte offsets
+  int poff[16];
+  int aoffs[XMODE == X_STAGED_UNPOOL ? 9 : 1];
+  unsigned pmask = 0;
+  // X_STAGED: this thread's DMA source offsets (bytes, channel 0) for each 256-slot round
+  constexpr int MAX_ROUNDS = W_XS * 4 / 16 / 256;  // 6
+  unsigned xsrc[STAGED ? MAX_ROUNDS : 1];
+  if constexpr (XMODE == X_DIRECT) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ih = 2 * th - 1 + r, iw = 2 * tw - 1 + q;
+        const bool ok = tok && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        poff[r * 4 + q] = ((b * p.H + ih) * p.W + iw) * p.C;
+        pmask |= (ok ? 1u : 0u) << (r * 4 + q);
+      }
+  } else if constexpr (XMODE == X_UNPOOL) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int ph = th - 1 + r, pq = tw - 1 + q;
+        const bool ok = tok && ph >= 0 && ph < H2 && pq >= 0 && pq < W2;
+        poff[r * 3 + q] = ((b * H2 + ph) * W2 + pq) * p.C;
+        pmask |= (ok ? 1u : 0u) << (r * 3 + q);
+      }
+  } else if constexpr (XMODE == X_STAGED) {
+    // block region: images b0 .. b0+n_img-1, input rows 2*th0-1 .. 2*th0+2R, cols -1 .. W
+    const int t0 = blk_p * 64;
+    const int b0 = t0 / T_img;
+    const int th0 = (t0 - b0 * T_img) / W2;
+    const int RH = 2 * p.R + 2, RWc = p.W + 2;
+    // lane's patch in region coordinates (clamped for tail lanes: results are discarded)
+    const int im = tok ? b - b0 : 0, rr0 = tok ? 2 * (th - th0) : 0, cc0 = tok ? 2 * tw : 0;
+    const int pix0 = im * p.IP + rr0 * p.RW + cc0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int L = 2 * (pix0 + r * p.RW + q) + (g >> 1);
+        poff[r * 4 + q] = xswz(L) * 16 + (g & 1) * 8;
+      }
+#pragma unroll
+    for (int i = 0; i < MAX_ROUNDS; ++i) {
+      const int s = i * 256 + tid;
+      const int L = xswz(s);
+      const int pix = L >> 1, h = L & 1;
+      const int imr = pix / p.IP, rem = pix - imr * p.IP;
+      const int rr = rem / p.RW, cc = rem - rr * p.RW;
+      const int bb = b0 + imr, ih = 2 * th0 - 1 + rr, iw = cc - 1;
+      const bool ok = i < p.rounds && imr < p.n_img && rr < RH && cc < RWc && bb < p.B && ih >= 0 &&
+                      ih < p.H && iw >= 0 && iw < p.W;
+      xsrc[i] = ok ? (unsigned)((((bb * p.H + ih) * p.W + iw) * p.C) * 4 + h * 16) : OOB;
+    }
+  } else {  // X_STAGED_UNPOOL: pooled rows th0-1 .. th0+R, pooled cols -1 .. W2
+    const int t0 = blk_p * 64;
+    const int b0 = t0 / T_img;
+    const int th0 = (t0 - b0 * T_img) / W2;
+    const int PRH = p.R + 2, PRWc = W2 + 2;
+    const int im = tok ? b - b0 : 0, pr0 = tok ? th - th0 : 0, pc0 = tok ? tw : 0;
+    const int cell0 = im * p.IP + pr0 * p.RW + pc0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int cell = cell0 + r * p.RW + q;
+        poff[r * 3 + q] = xswz(2 * cell + (g >> 1)) * 16 + (g & 1) * 8;  // value (2 floats)
+        aoffs[r * 3 + q] = p.aoff + cell * 8 + 2 * g;                   // argmax (2 bytes)
+      }
+#pragma unroll
+    for (int i = 0; i < MAX_ROUNDS; ++i) {
+      // rounds [0, rounds): value slots (16 B), [rounds, rounds + arounds): argmax units (4 B)
+      const bool val = i < p.rounds;
+      const int s = val ? i * 256 + tid : (i - p.rounds) * 256 + tid;
+      const int L = val ? xswz(s) : s;
+      const int cell = L >> 1, h = L & 1;
+      const int imr = cell / p.IP, rem = cell - imr * p.IP;
+      const int pr = rem / p.RW, pc = rem - pr * p.RW;
+      const int bb = b0 + imr, ph = th0 - 1 + pr, pw = pc - 1;
+      const bool ok = i < p.rounds + p.arounds && imr < p.n_img && pr < PRH && pc < PRWc && bb < p.B &&
+                      ph >= 0 && ph < H2 && pw >= 0 && pw < W2;
+      const unsigned e0 = (unsigned)(((bb * H2 + ph) * W2 + pw) * p.C);
+      xsrc[i] = ok ? (val ? e0 * 4 + h * 16 : e0 + h * 4) : OOB;
+    }
+  }
+
+  // ---- staging (LDS-DMA): U image of chunk c0 (+ the input region when STAGED) ---------
+  auto stage = [&](int c0, float* ud, float* xd) {
+    const unsigned ubase = (unsigned)(((c0 / W_CH) * n_k + kb) * W_UIMG) * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ubase);
+    if constexpr (XMODE == X_STAGED) {
+#pragma unroll
+      for (int i = 0; i < MAX_ROUNDS; ++i)
+        if (i < p.rounds) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
+    } else if constexpr (XMODE == X_STAGED_UNPOOL) {
+#pragma unroll
+      for (int i = 0; i < MAX_ROUNDS; ++i) {
+        if (i < p.rounds) {
+          dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
+        } else if (i < p.rounds + p.arounds) {
+          float* ab = reinterpret_cast<float*>(reinterpret_cast<char*>(xd) + p.aoff) + (i - p.rounds) * 256 +
+                      wave * 64;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (lds_ptr_t)ab, 4, xsrc[i], (unsigned)c0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // X_DIRECT/X_UNPOOL raw operands, prefetched one chunk ahead
+  f32x2 xin[STAGED ? 1 : (UNPOOL ? 9 : 16)];
+  unsigned amr[UNPOOL ? 9 : 1];
+  auto issue_x = [&](int c0) {
+    const int cc = c0 + 2 * g;
+    if constexpr (XMODE == X_DIRECT) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+        xin[t] = buf_load_f32x2(xr, (int)(((pmask >> t) & 1u) ? (unsigned)(poff[t] + cc) * 4u : OOB), 0, 0);
+    } else if constexpr (XMODE == X_UNPOOL) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const bool ok = (pmask >> t) & 1u;
+        xin[t] = buf_load_f32x2(xr, (int)(ok ? (unsigned)(poff[t] + cc) * 4u : OOB), 0, 0);
+        amr[t] = buf_load_u16(ar, (int)(ok ? (unsigned)(poff[t] + cc) : OOB), 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[16][2];
+#pragma unroll
+  for (int x = 0; x < 16; ++x)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[x][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // B-operand read offset of this lane inside a U image: k = j + 16n at 2 adjacent floats,
+  // channel c = 2g + e; the g-slot is XORed with j>>3 so lanes j and j+8 use other banks
+  const int uoff = j * 8 + 2 * (g ^ ((j >> 3) << 1));
+
+  auto compute = [&](int c0, const float* ub, const float* xb, float* ud_next, float* xd_next, bool more) {
+    f32x2 v[16];
+    {
+      f32x2 d[16];
+      if constexpr (XMODE == X_STAGED) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+          d[t] = *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(xb) + poff[t]);
+      } else if constexpr (XMODE == X_STAGED_UNPOOL) {
+        f32x2 cv[9];
+        unsigned ca[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          cv[t] = *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(xb) + poff[t]);
+          ca[t] = *reinterpret_cast<const unsigned short*>(reinterpret_cast<const char*>(xb) + aoffs[t]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cell = ((r + 1) >> 1) * 3 + ((q + 1) >> 1);
+            const unsigned want = (unsigned)((((r + 1) & 1) << 1) | ((q + 1) & 1));
+            d[r * 4 + q][0] = (ca[cell] & 0xffu) == want ? cv[cell][0] : 0.f;
+            d[r * 4 + q][1] = ((ca[cell] >> 8) & 0xffu) == want ? cv[cell][1] : 0.f;
+          }
+      } else if constexpr (XMODE == X_DIRECT) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) d[t] = xin[t];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cell = ((r + 1) >> 1) * 3 + ((q + 1) >> 1);
+            const unsigned want = (unsigned)((((r + 1) & 1) << 1) | ((q + 1) & 1));
+            d[r * 4 + q][0] = (amr[cell] & 0xffu) == want ? xin[cell][0] : 0.f;
+            d[r * 4 + q][1] = ((amr[cell] >> 8) & 0xffu) == want ? xin[cell][1] : 0.f;
+          }
+      }
+      input_transform2(d, v);
+    }
+    if (more) {
+      stage(c0 + W_CH, ud_next, xd_next);
+      if constexpr (!STAGED) issue_x(c0 + W_CH);
+    }
+    const float* ul = ub + uoff;
+    constexpr int AHEAD = 4;
+    float2 wq[AHEAD];
+#pragma unroll
+    for (int s = 0; s < AHEAD; ++s)
+      wq[s] = *reinterpret_cast<const float2*>(ul + ((s & 15) * 2 + (s >> 4)) * 128);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const int x = s & 15, e = s >> 4;
+      const float2 w2 = wq[s % AHEAD];
+      if (s + AHEAD < 32) {
+        const int s2 = s + AHEAD;
+        wq[s % AHEAD] = *reinterpret_cast<const float2*>(ul + ((s2 & 15) * 2 + (s2 >> 4)) * 128);
+      }
+      acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[x][e], w2.x, acc[x][0], 0, 0, 0);
+      acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[x][e], w2.y, acc[x][1], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __syncthreads();  // drains this chunk's DMA for the next one and orders buffer reuse
+  };
+
+  if (c_begin < c_end) {
+    if constexpr (!STAGED) issue_x(c_begin);
+    stage(c_begin, us0, xs0);
+    __syncthreads();
+    for (int c0 = c_begin; c0 < c_end; c0 += 2 * W_CH) {
+      compute(c0, us0, xs0, us1, xs1, c0 + W_CH < c_end);
+      if (c0 + W_CH < c_end) compute(c0 + W_CH, us1, xs1, us0, xs0, c0 + 2 * W_CH < c_end);
+    }
+  }
+  wino_epilogue<EPI>(p, acc, pw0, k0, g, j);
+}
+
+// ---------------------------------------------------------------------------------------
+// host: staged-region geometry (bank-conflict-minimising pitches) per (B, H, W)
+// ---------------------------------------------------------------------------------------
+struct XGeom {
+  bool ok = false;
+  int n_img = 0, R = 0, RW = 0, IP = 0, rounds = 0, arounds = 0, aoff = 0;
+};
+
+// extra LDS cycles of the patch ds_read_b64s of one block (2 x 32-lane groups, banks mod 64);
+// pooled: 3x3 pooled cells per lane (staged unpool) instead of 4x4 pixels
+static int staged_conflicts(int W2, int T_img, int RW, int IP, bool pooled) {
+  const int span = pooled ? 3 : 4, step = pooled ? 1 : 2;
+  int total = 0;
+  for (int wave = 0; wave < 4; ++wave)
+    for (int r = 0; r < span; ++r)
+      for (int q = 0; q < span; ++q)
+        for (int half = 0; half < 2; ++half) {
+          int words[64];
+          int n = 0;
+          for (int jj = 0; jj < 16; ++jj)
+            for (int gg = 2 * half; gg < 2 * half + 2; ++gg) {
+              const int t = wave * 16 + jj;
+              const int im = T_img >= 64 ? 0 : t / T_img;
+              const int rem = T_img >= 64 ? t : t % T_img;
+              const int th = rem / W2, tw = rem % W2;
+              const int pix = im * IP + (step * th + r) * RW + step * tw + q;
+              const int w0 = xswz(2 * pix + (gg >> 1)) * 4 + (gg & 1) * 2;
+              words[n++] = w0;
+              words[n++] = w0 + 1;
+            }
+          for (int bank = 0; bank < 64; ++bank) {
+            int distinct[64];
+            int nd = 0;
+            for (int a = 0; a < n; ++a) {
+              if ((words[a] & 63) != bank) continue;
+              bool seen = false;
+              for (int z = 0; z < nd; ++z) seen |= distinct[z] == words[a];
+              if (!seen) distinct[nd++] = words[a];
+            }
+            if (nd > 1) total += nd - 1;
+          }
+        }
+  return total;
+}
+
+static XGeom staged_geometry(int H, int W, bool pooled) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, bool>, XGeom> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({H, W, pooled});
+  if (it != cache.end()) return it->second;
+  XGeom gm;
+  const int H2 = H / 2, W2 = W / 2, T_img = H2 * W2;
+  int n_img = 0, R = 0;
+  if (T_img >= 64 && T_img % 64 == 0 && 64 % W2 == 0) {
+    n_img = 1;
+    R = 64 / W2;
+  } else if (T_img >= 4 && 64 % T_img == 0) {
+    n_img = 64 / T_img;
+    R = H2;
+  }
+  if (n_img) {
+    // region rows x cols: full resolution (2R+2) x (W+2); pooled (R+2) x (W/2+2)
+    const int RH = pooled ? R + 2 : 2 * R + 2, RWc = pooled ? W2 + 2 : W + 2;
+    int best = -1;
+    for (int RW = RWc; RW < RWc + 16; ++RW)
+      for (int IP = RH * RW; IP < RH * RW + (n_img > 1 ? 32 : 1); ++IP) {
+        const int items = 2 * ((n_img - 1) * IP + RH * RW);  // 16-B value slots (= 4-B argmax units)
+        const int rounds = (items + 255) / 256;
+        const int arounds = pooled ? rounds : 0;
+        const int bytes = rounds * 256 * 16 + arounds * 256 * 4;
+        if (bytes > W_XS * 4 || rounds + arounds > W_XS * 4 / 16 / 256) continue;
+        const int c = staged_conflicts(W2, T_img, RW, IP, pooled);
+        const int cost = c * 4 + rounds;  // conflicts first, then DMA volume
+        if (best < 0 || cost < best) {
+          best = cost;
+          gm.ok = true;
+          gm.n_img = n_img;
+          gm.R = R;
+          gm.RW = RW;
+          gm.IP = IP;
+          gm.rounds = rounds;
+          gm.arounds = arounds;
+          gm.aoff = rounds * 256 * 16;
+        }
+      }
+  }
+  cache[{H, W, pooled}] = gm;
+  return gm;
+}
+
 }  // namespace tp
 
 // Winograd conv: same operand/epilogue contract as tp_conv_igemm (3x3, stride 1, pad 1),
-// ``u`` = transformed weights. epi: 0 fwd, 1 fwd+pool, 2 bwd (dgrad epilogue). H, W even,
-// C % 8 == 0, K % 32 == 0. splits > 1 -> partial slabs in ``ws`` + conv_epilogue combine.
+// ``u`` = U images from winograd_weights(). epi: 0 fwd, 1 fwd+pool, 2 bwd (dgrad epilogue).
+// H, W even, C % 8 == 0, K % 32 == 0. splits > 1 -> partial slabs in ``ws`` + combine.
+// staged: 1 = LDS-staged input region when the shape allows it (else direct loads).
 extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
                                               const float* scale, const float* shift, int relu, float* out,
                                               uint8_t* out_argmax, const float* act, float* taylor,
                                               hipStream_t st);
 
+extern "C" int tp_wino_staged_ok(int H, int W, int unpool) {
+  return tp::staged_geometry(H, W, unpool != 0).ok ? 1 : 0;
+}
+
+// host-side introspection (tests, tuning): {ok, n_img, R, RW, IP, rounds, arounds, aoff, conflicts}
+extern "C" void tp_wino_geometry(int H, int W, int unpool, int* out9) {
+  const tp::XGeom g = tp::staged_geometry(H, W, unpool != 0);
+  const int vals[9] = {g.ok, g.n_img, g.R, g.RW, g.IP, g.rounds, g.arounds, g.aoff,
+                       g.ok ? tp::staged_conflicts(W / 2, (H / 2) * (W / 2), g.RW, g.IP, unpool != 0) : -1};
+  for (int i = 0; i < 9; ++i) out9[i] = vals[i];
+}
+
 extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W,
-                                   int C, int K, int unpool, int epi, int splits, const float* scale,
+                                   int C, int K, int unpool, int epi, int splits, int staged, const float* scale,
                                    const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
                                    float* taylor, float* ws, hipStream_t st) {
   using namespace tp;
@@ -332,24 +598,44 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.out_argmax = out_argmax;
   a.act = act;
   a.taylor = taylor;
+  int xmode = unpool ? X_UNPOOL : X_DIRECT;
+  if (staged) {
+    const XGeom gm = staged_geometry(H, W, unpool != 0);
+    if (gm.ok) {
+      xmode = unpool ? X_STAGED_UNPOOL : X_STAGED;
+      a.n_img = gm.n_img;
+      a.R = gm.R;
+      a.RW = gm.RW;
+      a.IP = gm.IP;
+      a.rounds = gm.rounds;
+      a.arounds = gm.arounds;
+      a.aoff = gm.aoff;
+    }
+  }
   const int n_p = (a.P + 63) / 64, n_k = K / 32;
   dim3 grid(n_p * n_k, splits);
+  int e_launch = epi;
   if (splits > 1) {
     if (!ws) return hipErrorInvalidValue;
-    WinoArgs pa = a;
-    pa.out = ws;
-    pa.pooled_m = epi == W_FWD_POOL ? 1 : 0;
-    if (unpool) wino_f2x3<W_PARTIAL, true><<<grid, 256, 0, st>>>(pa);
-    else wino_f2x3<W_PARTIAL, false><<<grid, 256, 0, st>>>(pa);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return tp_conv_epilogue_slabs(ws, splits, B, H, W, K, epi, scale, shift, relu, out, out_argmax, act, taylor, st);
+    a.out = ws;
+    a.pooled_m = epi == W_FWD_POOL ? 1 : 0;
+    e_launch = W_PARTIAL;
   }
-#define TP_W(E, U) wino_f2x3<E, U><<<grid, 256, 0, st>>>(a)
-  if (epi == W_FWD) { if (unpool) TP_W(W_FWD, true); else TP_W(W_FWD, false); }
-  else if (epi == W_FWD_POOL) { if (unpool) return hipErrorInvalidValue; TP_W(W_FWD_POOL, false); }
-  else if (epi == W_BWD) { if (unpool) TP_W(W_BWD, true); else TP_W(W_BWD, false); }
-  else return hipErrorInvalidValue;
+#define TP_W(E)                                                                                 \
+  do {                                                                                          \
+    if (xmode == X_STAGED) wino_f2x3<E, X_STAGED><<<grid, 256, 0, st>>>(a);                    \
+    else if (xmode == X_STAGED_UNPOOL) wino_f2x3<E, X_STAGED_UNPOOL><<<grid, 256, 0, st>>>(a);  \
+    else if (xmode == X_UNPOOL) wino_f2x3<E, X_UNPOOL><<<grid, 256, 0, st>>>(a);               \
+    else wino_f2x3<E, X_DIRECT><<<grid, 256, 0, st>>>(a);                                      \
+  } while (0)
+  if (e_launch == W_FWD) TP_W(W_FWD);
+  else if (e_launch == W_FWD_POOL) {
+    if (unpool) return hipErrorInvalidValue;
+    TP_W(W_FWD_POOL);
+  } else if (e_launch == W_BWD) TP_W(W_BWD);
+  else TP_W(W_PARTIAL);
 #undef TP_W
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || splits == 1) return e;
+  return tp_conv_epilogue_slabs(ws, splits, B, H, W, K, epi, scale, shift, relu, out, out_argmax, act, taylor, st);
 }

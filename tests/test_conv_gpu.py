@@ -234,8 +234,11 @@ def test_engine_shapley_matches_generic_path(cuda, layer):
 
 
 # ---------------------------------------------------------------- Winograd F(2x2,3x3)
-WINO_SHAPES = [  # B, H, W, Cin, Cout
+WINO_SHAPES = [  # B, H, W, Cin, Cout (staged-region modes: rows for W/2 | 64, images for (H/2)(W/2) | 64)
     (4, 32, 32, 64, 64),
+    (3, 64, 32, 32, 64),
+    (2, 16, 64, 32, 32),
+    (7, 8, 8, 64, 32),
     (3, 16, 16, 128, 256),
     (5, 8, 8, 256, 256),
     (6, 4, 4, 512, 512),
@@ -248,7 +251,8 @@ WINO_SHAPES = [  # B, H, W, Cin, Cout
 @pytest.mark.parametrize("shape", WINO_SHAPES)
 @pytest.mark.parametrize("splits", [1, 3])
 @pytest.mark.parametrize("pool", [False, True])
-def test_wino_fwd(cuda, shape, splits, pool):
+@pytest.mark.parametrize("staged", [False, True])
+def test_wino_fwd(cuda, shape, splits, pool, staged):
     from torchpruner_amd import ops
     from torchpruner_amd.engine.fused_chain import winograd_weights
     T = ops.require()
@@ -260,7 +264,7 @@ def test_wino_fwd(cuda, shape, splits, pool):
     shift = _rand(Cout, gen=g) * 0.1
     ref, am_ref = _ref_fwd(x, w, scale, shift, True, pool)
     u = winograd_weights(w.to(cuda))
-    out, am = T.conv_wino_fwd(x.to(cuda), u, scale.to(cuda), shift.to(cuda), True, pool, splits)
+    out, am = T.conv_wino_fwd(x.to(cuda), u, scale.to(cuda), shift.to(cuda), True, pool, splits, staged)
     torch.testing.assert_close(out.cpu(), ref, rtol=3e-4, atol=3e-4)
     if pool:
         assert (am.cpu().long() == am_ref).float().mean() > 0.999
@@ -269,7 +273,8 @@ def test_wino_fwd(cuda, shape, splits, pool):
 @pytest.mark.parametrize("shape", WINO_SHAPES)
 @pytest.mark.parametrize("splits", [1, 4])
 @pytest.mark.parametrize("unpool", [False, True])
-def test_wino_dgrad_taylor(cuda, shape, splits, unpool):
+@pytest.mark.parametrize("staged", [False, True])
+def test_wino_dgrad_taylor(cuda, shape, splits, unpool, staged):
     from torchpruner_amd import ops
     from torchpruner_amd.engine.fused_chain import winograd_weights
     T = ops.require()
@@ -297,7 +302,7 @@ def test_wino_dgrad_taylor(cuda, shape, splits, unpool):
     tay = torch.zeros(B, Cin, device=cuda)
     gin = (gp if unpool else gfull).to(cuda)
     out = T.conv_wino_dgrad(gin, am.to(cuda) if unpool else None, ut, act.to(cuda), bn_scale.to(cuda), tay, True,
-                            splits)
+                            splits, staged)
     torch.testing.assert_close(out.cpu(), out_ref.float(), rtol=3e-4, atol=3e-4)
     torch.testing.assert_close(tay.cpu(), tay_ref.float(), rtol=3e-4, atol=3e-3)
 

@@ -10,11 +10,20 @@ BT = torch.tensor([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], d
 AT = torch.tensor([[1, 1, 1, 0], [0, 1, -1, -1]], dtype=torch.float64)
 
 
-def _wino_conv(x, u_il):
-    """x (B,C,H,W) fp64; u_il (16, C, K) in the kernel's interleaved layout."""
+def _decode_images(img):
+    """(C/8, K/32, 4096) U images -> (4, 4, C, K)."""
+    CB, KB = img.shape[0], img.shape[1]
+    t = img.double().reshape(CB, KB, 16, 2, 16, 4, 2).clone()  # (cb, kb, xi, e, j, gs, n)
+    t[:, :, :, :, 8:] = t[:, :, :, :, 8:, [2, 3, 0, 1]]
+    t = t.permute(2, 0, 5, 3, 1, 6, 4)  # (xi, cb, g, e, kb, n, j)
+    return t.reshape(4, 4, CB * 8, KB * 32)
+
+
+def _wino_conv(x, u_img):
+    """x (B,C,H,W) fp64; u_img = winograd_weights() images."""
     B, C, H, W = x.shape
-    K = u_il.shape[2]
-    u = u_il.double().reshape(16, C, K // 32, 16, 2).transpose(3, 4).reshape(4, 4, C, K)
+    u = _decode_images(u_img)
+    K = u.shape[3]
     xp = F.pad(x, (1, 1, 1, 1))
     patches = xp.unfold(2, 4, 2).unfold(3, 4, 2)  # (B, C, H/2, W/2, 4, 4)
     V = torch.einsum("ir,bcpqrs,js->bpqijc", BT, patches, BT)
@@ -28,7 +37,7 @@ def test_winograd_layout_matches_conv2d():
     x = torch.randn(2, 8, 6, 10, generator=g, dtype=torch.float64)
     w = torch.randn(64, 8, 3, 3, generator=g, dtype=torch.float64)
     u = winograd_weights(w.float())
-    assert u.shape == (16, 8, 64)
+    assert u.shape == (1, 2, 4096)
     ref = F.conv2d(x, w, padding=1)
     got = _wino_conv(x, u)
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)

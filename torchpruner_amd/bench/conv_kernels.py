@@ -96,14 +96,15 @@ def main():
             ut = winograd_weights(wt.view(Cin, 3, 3, Cout).permute(0, 3, 1, 2))
             P = B * (H // 2) * (W // 2)
             base_f, base_b = _wino_splits(P, Cout, Cin), _wino_splits(P, Cin, Cout)
-            for sf, sb in sorted({(base_f, base_b), (1, 1), (max(1, base_f // 2), max(1, base_b // 2)),
-                                  (base_f * 2, base_b * 2)}):
-                tf = timeit(lambda: T.conv_wino_fwd(x, u, sc, sh, True, pool, sf), args.iters)
-                tb = timeit(lambda: T.conv_wino_dgrad(g, am, ut, act, scin, tay, True, sb), args.iters)
-                rows.append({"layer": li + 1, "wino": True, "splits": [sf, sb], "fwd_us": round(tf, 1),
-                             "bwd_us": round(tb, 1)})
-                print(f"    wino splits f{sf}/b{sb}: fwd {tf:7.1f} us {flops/tf/1e6:6.1f} TFe | "
-                      f"dgrad {tb:7.1f} us {flops/tb/1e6:6.1f} TFe", flush=True)
+            for staged in (False, True):
+                for sf, sb in sorted({(base_f, base_b), (1, 1), (max(1, base_f // 2), max(1, base_b // 2)),
+                                      (base_f * 2, base_b * 2)}):
+                    tf = timeit(lambda: T.conv_wino_fwd(x, u, sc, sh, True, pool, sf, staged), args.iters)
+                    tb = timeit(lambda: T.conv_wino_dgrad(g, am, ut, act, scin, tay, True, sb, staged), args.iters)
+                    rows.append({"layer": li + 1, "wino": "lds" if staged else "direct", "splits": [sf, sb],
+                                 "fwd_us": round(tf, 1), "bwd_us": round(tb, 1)})
+                    print(f"    wino-{'lds' if staged else 'dir'} splits f{sf}/b{sb}: fwd {tf:7.1f} us "
+                          f"{flops/tf/1e6:6.1f} TFe | dgrad {tb:7.1f} us {flops/tb/1e6:6.1f} TFe", flush=True)
     if tot_t:
         print(f"TOTAL {tot_t:.1f} us, {tot_f / tot_t / 1e6:.1f} TF/s average")
     if args.json:

@@ -42,7 +42,8 @@ from .. import ops
 # 4=128x128, 5=256x64, 6=128x64 (8 waves)
 _CU = 256
 _TILES = {0: (128, 128), 1: (256, 64), 2: (64, 64), 3: (128, 64), 4: (128, 128), 5: (256, 64), 6: (128, 64)}
-WINO = -1  # pseudo tile cfg: fused Winograd F(2x2,3x3) kernel (winograd.hip)
+WINO = -1  # pseudo tile cfg: fused Winograd F(2x2,3x3) kernel (winograd.hip), direct patch loads
+WINO_LDS = -2  # the same with the block input region staged through LDS
 
 # Winograd F(2x2,3x3) weight transform G g G^T
 _G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
@@ -50,20 +51,25 @@ _G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
 
 @torch.no_grad()
 def winograd_weights(w: torch.Tensor) -> torch.Tensor:
-    """(K, C, 3, 3) conv weight -> (16, C, K) transformed weights U[xi][c][k] = (G g G^T)[xi]
-    in the layout winograd.hip stages into LDS: within every 32-channel block of K the
-    output channel j + 16*n is stored at position 2*j + n (one 64-bit LDS read feeds both
-    MFMA column tiles of a lane). Computed in fp64, rounded once to fp32."""
+    """(K, C, 3, 3) conv weight -> U = G g G^T arranged as the LDS images winograd.hip DMAs:
+    (C/8, K/32, 4096), one 16-KB image per (8-input-channel chunk, 32-output-channel block).
+    Inside an image, word ((xi*2 + e)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + n holds
+    U[xi][c = 8*cb + 2g + e][k = 32*kb + j + 16n]: one ds_read_b64 feeds both MFMA column
+    tiles of lane (j, g) and the XOR keeps lanes j, j+8 on different banks.
+    Computed in fp64, rounded once to fp32."""
     K, C = w.shape[0], w.shape[1]
-    assert w.shape[2:] == (3, 3) and K % 32 == 0, "winograd_weights needs 3x3 kernels and K % 32 == 0"
+    assert w.shape[2:] == (3, 3) and K % 32 == 0 and C % 8 == 0, \
+        "winograd_weights needs 3x3 kernels, K % 32 == 0 and C % 8 == 0"
     G = torch.tensor(_G, dtype=torch.float64, device=w.device)
-    u = torch.einsum("ia,kcab,jb->ijck", G, w.double(), G).reshape(16, C, K)
-    u = u.reshape(16, C, K // 32, 2, 16).transpose(3, 4).reshape(16, C, K)
-    return u.float().contiguous()
+    u = torch.einsum("ia,kcab,jb->ijck", G, w.double(), G).reshape(16, C // 8, 4, 2, K // 32, 2, 16)
+    # (xi, cb, g, e, kb, n, j) -> (cb, kb, xi, e, j, g, n)
+    img = u.permute(1, 4, 0, 3, 6, 2, 5).contiguous()
+    img[:, :, :, :, 8:] = img[:, :, :, :, 8:, [2, 3, 0, 1]]
+    return img.reshape(C // 8, K // 32, 4096).float().contiguous()
 
 
 def _wino_ok(H, W, C, K):
-    return H % 2 == 0 and W % 2 == 0 and C % 8 == 0 and K % 32 == 0 and H * W >= 16
+    return H % 2 == 0 and W % 2 == 0 and C % 8 == 0 and K % 32 == 0
 
 
 def _wino_splits(P, K, C):
@@ -112,7 +118,8 @@ class Autotuner:
         out = []
         if wino is not None:
             sp = _wino_splits(wino[0], N, wino[1])
-            out += [(WINO, sp)] + ([(WINO, max(1, sp // 2))] if sp > 1 else [])
+            for kind in (WINO, WINO_LDS):
+                out += [(kind, sp)] + ([(kind, max(1, sp // 2))] if sp > 1 else [])
         for cfg, (bm, bn) in _TILES.items():
             if N <= 64 and bn == 128:
                 continue
@@ -128,7 +135,7 @@ class Autotuner:
         if hit is not None:
             return hit
         if not self.enabled or torch.cuda.is_current_stream_capturing():
-            res = (WINO, _wino_splits(wino[0], N, wino[1])) if wino is not None else _pick_cfg(M, N, K)
+            res = (WINO_LDS, _wino_splits(wino[0], N, wino[1])) if wino is not None else _pick_cfg(M, N, K)
             self.cache[key] = res
             return res
         best = None
@@ -328,8 +335,8 @@ class FusedChainEngine:
     # ------------------------------------------------------------------ execution
     @staticmethod
     def _conv_run(T, e, h, cfg, sp):
-        if cfg == WINO:
-            return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp)
+        if cfg in (WINO, WINO_LDS):
+            return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS)
         return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
 
     def _conv(self, T, e, h):
@@ -343,8 +350,8 @@ class FusedChainEngine:
 
     @staticmethod
     def _dgrad_run(T, e, g, am, act, sc, taylor, want_out, cfg, sp):
-        if cfg == WINO:
-            return T.conv_wino_dgrad(g, am, e["ut"], act, sc, taylor, want_out, sp)
+        if cfg in (WINO, WINO_LDS):
+            return T.conv_wino_dgrad(g, am, e["ut"], act, sc, taylor, want_out, sp, cfg == WINO_LDS)
         return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp)
 
     def _linear(self, T, e, xin):
