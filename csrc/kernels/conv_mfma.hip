@@ -363,22 +363,45 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       p.out[t] = best;
       p.out_argmax[t] = (uint8_t)arg;
     }
-  } else {
+  } else if constexpr (EPI == EPI_FWD) {
     for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < MN;
          o += (long long)gridDim.x * blockDim.x) {
       const int n = (int)(o % p.N);
       float v = 0.f;
       for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
-      if constexpr (EPI == EPI_FWD) {
-        const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
-        v = v * sc + sh;
-        if (p.relu) v = nan_relu(v);
-        p.out[o] = v;
-      } else {  // EPI_BWD
+      const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
+      v = v * sc + sh;
+      if (p.relu) v = nan_relu(v);
+      p.out[o] = v;
+    }
+  } else if (p.HWo > 64) {  // EPI_BWD, large images: element-parallel, atomic Taylor sums
+    for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < MN;
+         o += (long long)gridDim.x * blockDim.x) {
+      const int n = (int)(o % p.N);
+      float v = 0.f;
+      for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
+      const float a = p.act[o];
+      if (p.taylor) atomicAdd(p.taylor + (o / p.N / p.HWo) * p.N + n, -(v * a));
+      if (p.out) p.out[o] = a > 0.f ? v * (p.scale ? p.scale[n] : 1.f) : 0.f;
+    }
+  } else {  // EPI_BWD, small images: one thread per (image, channel) walks the image's
+            // pixels, so the Taylor sum is a plain deterministic += (no atomics)
+    const long long BN = (long long)(p.M / p.HWo) * p.N;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < BN;
+         t += (long long)gridDim.x * blockDim.x) {
+      const int n = (int)(t % p.N);
+      const long long b = t / p.N;
+      const float sc = p.scale ? p.scale[n] : 1.f;
+      float tsum = 0.f;
+      for (int px = 0; px < p.HWo; ++px) {
+        const long long o = (b * p.HWo + px) * p.N + n;
+        float v = 0.f;
+        for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
         const float a = p.act[o];
-        if (p.taylor) atomicAdd(p.taylor + (o / p.N / p.HWo) * p.N + n, -(v * a));
-        if (p.out) p.out[o] = a > 0.f ? v * (p.scale ? p.scale[n] : 1.f) : 0.f;
+        tsum += -(v * a);
+        if (p.out) p.out[o] = a > 0.f ? v * sc : 0.f;
       }
+      if (p.taylor) p.taylor[t] += tsum;
     }
   }
 }
@@ -558,7 +581,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
                          : dispatch_epi<1>(cfg, EPI_PARTIAL, pooled_m, unpool, b, splits, st);
   if (e != hipSuccess) return e;
   const long long MN = (long long)a.M * a.N;
-  const long long work = epi == EPI_FWD_POOL ? MN / 4 : MN;
+  const long long work = epi == EPI_FWD_POOL ? MN / 4 : (epi == EPI_BWD && a.HWo <= 64 ? MN / a.HWo : MN);
   unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
   if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
   else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
@@ -589,7 +612,7 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
   a.taylor = taylor;
   a.HWo = H * W;
   const long long MN = (long long)a.M * a.N;
-  const long long work = epi == EPI_FWD_POOL ? MN / 4 : MN;
+  const long long work = epi == EPI_FWD_POOL ? MN / 4 : (epi == EPI_BWD && a.HWo <= 64 ? MN / a.HWo : MN);
   unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
   if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
   else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);

@@ -122,9 +122,21 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, float* lds_base
 }
 
 // ---- epilogue: output tiles pw0 + 4g + r, channels k0 + j + 16n ------------------------
+// red: >= 65*32 floats of LDS, free for reuse (W_BWD Taylor: per-block reduction so each
+// block issues ONE global atomic per (image, channel) instead of one per lane and image run;
+// cross-XCD float atomics are the slow part of the dgrad epilogue otherwise).
 template <int EPI>
-__device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16][2], int pw0, int k0, int g, int j) {
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16][2], int pw0, int k0, int g, int j,
+                                              int blk_p, float* red) {
   const int H2 = p.H >> 1, W2 = p.W >> 1, T_img = H2 * W2;
+  const int b_first = (blk_p * 64) / T_img;
+  const int n_red = min(65, (blk_p * 64 + 63) / T_img - b_first + 1);
+  if constexpr (EPI == W_BWD) {
+    if (p.taylor) {
+      for (int t = threadIdx.x; t < n_red * W_TK; t += blockDim.x) red[t] = 0.f;
+      __syncthreads();
+    }
+  }
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
     const int k = k0 + j + 16 * n;
@@ -178,7 +190,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
             const float a = p.act[pix * p.K + k];
             if (p.taylor) {
               if (bb != cur_b) {
-                if (cur_b >= 0) atomicAdd(p.taylor + (long long)cur_b * p.K + k, tsum);
+                if (cur_b >= 0) atomicAdd(red + (cur_b - b_first) * W_TK + j + 16 * n, tsum);
                 cur_b = bb;
                 tsum = 0.f;
               }
@@ -190,7 +202,16 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
       }
     }
     if constexpr (EPI == W_BWD) {
-      if (p.taylor && cur_b >= 0) atomicAdd(p.taylor + (long long)cur_b * p.K + k, tsum);
+      if (p.taylor && cur_b >= 0) atomicAdd(red + (cur_b - b_first) * W_TK + j + 16 * n, tsum);
+    }
+  }
+  if constexpr (EPI == W_BWD) {
+    if (p.taylor) {
+      __syncthreads();
+      for (int t = threadIdx.x; t < n_red * W_TK; t += blockDim.x) {
+        const int bb = b_first + t / W_TK, k = k0 + t % W_TK;
+        if (bb < p.B && k < p.K) atomicAdd(p.taylor + (long long)bb * p.K + k, red[t]);
+      }
     }
   }
 }
@@ -452,7 +473,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       if (c0 + W_CH < c_end) compute(c0 + W_CH, us1, xs1, us0, xs0, c0 + 2 * W_CH < c_end);
     }
   }
-  wino_epilogue<EPI>(p, acc, pw0, k0, g, j);
+  wino_epilogue<EPI>(p, acc, pw0, k0, g, j, blk_p, us0);
 }
 
 // ---------------------------------------------------------------------------------------
