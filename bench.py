@@ -125,9 +125,7 @@ def timed_run(metric, convs, world):
     pdist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = pdist.all_max_float(dt)
     return scores, dt
 
 

@@ -57,12 +57,17 @@ def init_distributed(backend: str | None = None, device: str | None = None) -> D
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = (device != "cpu") and torch.cuda.is_available()
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # TORCHPRUNER_SHARE_GPU=1 maps ranks onto the visible devices round-robin: a rehearsal
+        # mode for multi-rank runs on a 1-GPU box (pair it with TORCHPRUNER_DIST_BACKEND=gloo,
+        # RCCL refuses two ranks on one device)
+        dev_index = local_rank % torch.cuda.device_count() if os.environ.get("TORCHPRUNER_SHARE_GPU") == "1" \
+            else local_rank
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
     else:
         dev = torch.device("cpu")
     if backend is None:
-        backend = "nccl" if use_cuda else "gloo"
+        backend = os.environ.get("TORCHPRUNER_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     if world > 1 and not is_dist():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
@@ -123,6 +128,17 @@ def all_max_int(v: int, group=None) -> int:
     vals = [None] * get_world_size(group)
     dist.all_gather_object(vals, int(v), group=group)
     return max(vals)
+
+
+def all_max_float(x: float, group=None) -> float:
+    """MAX of a Python float over ranks (any backend)."""
+    if get_world_size(group) == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dev = _comm_device(t, group)
+    t = t.to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
 
 
 def barrier(group=None):
