@@ -88,34 +88,38 @@ void column_accumulate(const at::Tensor& v, at::Tensor& acc_sum, const c10::opti
                                     (int)v.size(1), cur_stream()));
 }
 
-// For every i: v = |T[i]| (or T[i]); acc[i] += v.sum(0) (acc[i] may be empty = skip);
-// after: 0 leave T, 1 write v back, 2 zero T. One launch per 16 tensors.
+// For every i: T[i] is (B, C) or (R, B, C) partial slots summed in slot order;
+// v = |sum| (or sum); acc[i] += v.sum(0) (acc[i] may be empty = skip);
+// after: 0 leave T, 1 write v back (slot 0; other slots zeroed), 2 zero T. One launch per 16 tensors.
 void score_fold_(at::TensorList T, at::TensorList acc, bool take_abs, int64_t after) {
   TORCH_CHECK(T.size() == acc.size(), "one accumulator per score tensor");
   if (T.empty()) return;
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(T[0].device());
   std::vector<float*> tp;
   std::vector<double*> ap;
-  std::vector<int> bs, cs;
+  std::vector<int> bs, cs, rs;
   auto flush = [&]() {
     if (tp.empty()) return;
-    TP_CHECK_HIP(tp_score_fold_multi(tp.data(), ap.data(), bs.data(), cs.data(), (int)tp.size(), take_abs ? 1 : 0,
-                                     (int)after, cur_stream()));
-    tp.clear(); ap.clear(); bs.clear(); cs.clear();
+    TP_CHECK_HIP(tp_score_fold_multi(tp.data(), ap.data(), bs.data(), cs.data(), rs.data(), (int)tp.size(),
+                                     take_abs ? 1 : 0, (int)after, cur_stream()));
+    tp.clear(); ap.clear(); bs.clear(); cs.clear(); rs.clear();
   };
   for (size_t i = 0; i < T.size(); ++i) {
     check_cuda_f32(T[i], "T");
-    TORCH_CHECK(T[i].dim() == 2 && T[i].is_contiguous(), "T must be contiguous (B, C)");
+    TORCH_CHECK((T[i].dim() == 2 || T[i].dim() == 3) && T[i].is_contiguous(),
+                "T must be contiguous (B, C) or (R, B, C) partial slots");
+    const int64_t nb = T[i].size(-2), nc = T[i].size(-1), nr = T[i].dim() == 3 ? T[i].size(0) : 1;
     double* a = nullptr;
     if (acc[i].defined() && acc[i].numel() > 0) {
-      TORCH_CHECK(acc[i].scalar_type() == at::kDouble && acc[i].is_contiguous() && acc[i].numel() == T[i].size(1),
+      TORCH_CHECK(acc[i].scalar_type() == at::kDouble && acc[i].is_contiguous() && acc[i].numel() == nc,
                   "acc must be a contiguous float64 (C,) tensor");
       a = acc[i].data_ptr<double>();
     }
     tp.push_back(T[i].data_ptr<float>());
     ap.push_back(a);
-    bs.push_back((int)T[i].size(0));
-    cs.push_back((int)T[i].size(1));
+    bs.push_back((int)nb);
+    cs.push_back((int)nc);
+    rs.push_back((int)nr);
     if (tp.size() == 16) flush();
   }
   flush();

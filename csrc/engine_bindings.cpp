@@ -14,6 +14,7 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
                          float* taylor, int HWo, float* ws, hipStream_t st);
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
+int tp_wino_taylor_slots(int H, int W);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* ws, hipStream_t st);
@@ -116,8 +117,8 @@ at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_ar
   float* tay = nullptr;
   if (taylor.has_value() && taylor->defined()) {
     TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
-                    taylor->numel() == B * Cin,
-                "taylor must be a contiguous float32 (B, Cin) GPU tensor");
+                    taylor->numel() > 0 && taylor->numel() % (B * Cin) == 0,
+                "taylor must be a contiguous float32 (B, Cin) or (R, B, Cin) GPU tensor (slot 0 is written)");
     tay = taylor->data_ptr<float>();
   }
   at::Tensor out;
@@ -219,9 +220,11 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
   const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
   float* tay = nullptr;
   if (taylor.has_value() && taylor->defined()) {
+    const int64_t R = tp_wino_taylor_slots((int)H, (int)W);
     TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
-                    taylor->numel() == B * Cin,
-                "taylor must be a contiguous float32 (B, Cin) GPU tensor");
+                    taylor->numel() == R * B * Cin,
+                "taylor must be a contiguous float32 (R, B, Cin) GPU tensor with R = ", R,
+                " partial slots (winograd_taylor_slots)");
     tay = taylor->data_ptr<float>();
   }
   at::Tensor out;
@@ -238,7 +241,10 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
 
 }  // namespace
 
+int64_t wino_taylor_slots(int64_t H, int64_t W) { return tp_wino_taylor_slots((int)H, (int)W); }
+
 void register_engine_ops_def(torch::Library& m) {
+  m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits) -> (Tensor, Tensor)");
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "

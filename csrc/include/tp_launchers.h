@@ -33,5 +33,5 @@ void register_engine_ops_def(torch::Library& m);
 void register_engine_ops_impl(torch::Library& m);
 #endif
 
-extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, const int* B, const int* C, int count,
-                                          int take_abs, int after, hipStream_t st);
+extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, const int* B, const int* C,
+                                          const int* R, int count, int take_abs, int after, hipStream_t st);

@@ -166,10 +166,11 @@ __global__ __launch_bounds__(256) void column_accumulate(const float* __restrict
 // v = |T_l[b,c]| (or signed); acc_l[c] += sum_b v; then T_l[b,c] <- v (keep per-sample slab)
 // or 0 (persistent arena ready for the next batch). One launch for all layers.
 struct ScoreDesc {
-  float* T;
+  float* T;     // (R, B, C): R partial slots per score (summed in slot order: deterministic)
   double* acc;
   int B;
   int C;
+  int R;
 };
 struct ScoreBatch {
   ScoreDesc d[16];
@@ -184,13 +185,19 @@ __global__ __launch_bounds__(1024) void score_fold_multi(ScoreBatch batch, int t
   if (blockIdx.x * 64 >= s.C) return;  // uniform per block
   double acc = 0.0;
   if (c < s.C) {
+    const long long slot = (long long)s.B * s.C;
     for (int b = rg; b < s.B; b += RG) {
       float* p = s.T + (long long)b * s.C + c;
       float v = *p;
+      for (int r = 1; r < s.R; ++r) v += p[r * slot];
       if (take_abs) v = fabsf(v);
       acc += (double)v;
-      if (after == 1) *p = v;        // keep the processed per-sample value
-      else if (after == 2) *p = 0.f; // zero for the next batch
+      if (after == 1) {  // keep the processed per-sample value (in slot 0)
+        *p = v;
+        for (int r = 1; r < s.R; ++r) p[r * slot] = 0.f;
+      } else if (after == 2) {  // zero for the next batch
+        for (int r = 0; r < s.R; ++r) p[r * slot] = 0.f;
+      }
     }
   }
   ps[rg][threadIdx.x & 63] = acc;
@@ -205,13 +212,13 @@ __global__ __launch_bounds__(1024) void score_fold_multi(ScoreBatch batch, int t
 
 }  // namespace tp
 
-extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, const int* B, const int* C, int count,
-                                          int take_abs, int after, hipStream_t st) {
+extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, const int* B, const int* C,
+                                          const int* R, int count, int take_abs, int after, hipStream_t st) {
   if (count <= 0 || count > 16) return hipErrorInvalidValue;
   tp::ScoreBatch b{};
   int maxc = 0;
   for (int i = 0; i < count; ++i) {
-    b.d[i] = tp::ScoreDesc{T[i], acc[i], B[i], C[i]};
+    b.d[i] = tp::ScoreDesc{T[i], acc[i], B[i], C[i], R[i]};
     maxc = std::max(maxc, C[i]);
   }
   dim3 grid(tp::ceil_div(maxc, 64), count);

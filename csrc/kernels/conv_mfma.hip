@@ -374,16 +374,8 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       if (p.relu) v = nan_relu(v);
       p.out[o] = v;
     }
-  } else if (p.HWo > 64) {  // EPI_BWD, large images: element-parallel, atomic Taylor sums
-    for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < MN;
-         o += (long long)gridDim.x * blockDim.x) {
-      const int n = (int)(o % p.N);
-      float v = 0.f;
-      for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
-      const float a = p.act[o];
-      if (p.taylor) atomicAdd(p.taylor + (o / p.N / p.HWo) * p.N + n, -(v * a));
-      if (p.out) p.out[o] = a > 0.f ? v * (p.scale ? p.scale[n] : 1.f) : 0.f;
-    }
+  } else if (p.HWo > 64) {
+    // EPI_BWD, large images: handled by conv_epilogue_bwd_img (block per image x 64 channels)
   } else {  // EPI_BWD, small images: one thread per (image, channel) walks the image's
             // pixels, so the Taylor sum is a plain deterministic += (no atomics)
     const long long BN = (long long)(p.M / p.HWo) * p.N;
@@ -403,6 +395,38 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       }
       if (p.taylor) p.taylor[t] += tsum;
     }
+  }
+}
+
+// Split-combine + dgrad epilogue for large images without atomics: a 1024-thread block owns
+// (image b, 64 channels); 16 pixel groups stride over the image, and the Taylor partials are
+// combined in LDS in a fixed order (bit-reproducible).
+__global__ __launch_bounds__(1024) void conv_epilogue_bwd_img(ConvArgs p, const float* __restrict__ slabs,
+                                                               int splits) {
+  __shared__ float red[16][64];
+  const long long MN = (long long)p.M * p.N;
+  const int b = blockIdx.y;
+  const int c = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  float tsum = 0.f;
+  if (n < p.N) {
+    const float sc = p.scale ? p.scale[n] : 1.f;
+    for (int px = pg; px < p.HWo; px += 16) {
+      const long long o = ((long long)b * p.HWo + px) * p.N + n;
+      float v = 0.f;
+      for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
+      const float a = p.act[o];
+      tsum += -(v * a);
+      if (p.out) p.out[o] = a > 0.f ? v * sc : 0.f;
+    }
+  }
+  red[pg][c] = tsum;
+  __syncthreads();
+  if (pg == 0 && n < p.N && p.taylor) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c];
+    p.taylor[(long long)b * p.N + n] += t;
   }
 }
 
@@ -585,6 +609,8 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
   if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
   else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
+  else if (epi == EPI_BWD && a.HWo > 64)
+    conv_epilogue_bwd_img<<<dim3((unsigned)ceil_div(a.N, 64), (unsigned)(a.M / a.HWo)), 1024, 0, st>>>(a, ws, splits);
   else if (epi == EPI_BWD) conv_epilogue<EPI_BWD><<<grid, 256, 0, st>>>(a, ws, splits);
   else return hipErrorInvalidValue;
   return hipGetLastError();
@@ -616,6 +642,8 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
   unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
   if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
   else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
+  else if (epi == EPI_BWD && a.HWo > 64)
+    conv_epilogue_bwd_img<<<dim3((unsigned)ceil_div(a.N, 64), (unsigned)(a.M / a.HWo)), 1024, 0, st>>>(a, ws, splits);
   else if (epi == EPI_BWD) conv_epilogue<EPI_BWD><<<grid, 256, 0, st>>>(a, ws, splits);
   else return hipErrorInvalidValue;
   return hipGetLastError();

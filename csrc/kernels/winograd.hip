@@ -69,6 +69,7 @@ struct WinoArgs {
   int rounds;               // 256-slot DMA rounds per staged image
   // X_STAGED_UNPOOL: pooled region pitches; argmax image rounds and its byte offset
   int arounds, aoff;
+  int tay_slots;            // W_BWD: partial slots R of the (R, B, K) taylor slab
 };
 
 __device__ __forceinline__ int xcd_remap_w(int bid, int nwg) {
@@ -122,21 +123,26 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, float* lds_base
 }
 
 // ---- epilogue: output tiles pw0 + 4g + r, channels k0 + j + 16n ------------------------
-// red: >= 65*32 floats of LDS, free for reuse (W_BWD Taylor: per-block reduction so each
-// block issues ONE global atomic per (image, channel) instead of one per lane and image run;
-// cross-XCD float atomics are the slow part of the dgrad epilogue otherwise).
+// Taylor partials (W_BWD) without atomics: every lane stores its (tile, channel) partial
+// sum_q -(dL/da * a) into LDS (one writer per entry), the block sums the tiles of each image in
+// tile order, and writes that block sum into slot (block index within the image) of the
+// (R, B, K) taylor slab — a single-writer +=; score_fold sums the R slots in slot order. The
+// result is bit-reproducible run to run (no float atomics anywhere on the engine's Taylor path).
+// red: >= 64*32 floats of LDS free for reuse.
+__host__ __device__ inline int wino_taylor_slots(int H, int W) {
+  const int T_img = (H / 2) * (W / 2);
+  if (T_img <= 0) return 1;
+  if (T_img % 64 == 0) return T_img / 64;
+  if (64 % T_img == 0) return 1;
+  return (T_img + 63) / 64 + 1;
+}
+
 template <int EPI>
 __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16][2], int pw0, int k0, int g, int j,
                                               int blk_p, float* red) {
   const int H2 = p.H >> 1, W2 = p.W >> 1, T_img = H2 * W2;
-  const int b_first = (blk_p * 64) / T_img;
-  const int n_red = min(65, (blk_p * 64 + 63) / T_img - b_first + 1);
-  if constexpr (EPI == W_BWD) {
-    if (p.taylor) {
-      for (int t = threadIdx.x; t < n_red * W_TK; t += blockDim.x) red[t] = 0.f;
-      __syncthreads();
-    }
-  }
+  const int t0 = blk_p * 64;
+  const int tl_base = (pw0 - t0) + 4 * g;  // block-local index of this lane's first output tile
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
     const int k = k0 + j + 16 * n;
@@ -146,71 +152,72 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
       sc = p.scale ? p.scale[k] : 1.f;
       if (EPI != W_BWD) sh = p.shift ? p.shift[k] : 0.f;
     }
-    int cur_b = -1;
-    float tsum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int pt = pw0 + 4 * g + r;
-      if (!kok || pt >= p.P) continue;
-      float m[16], y[4];
+      float tsum = 0.f;
+      if (kok && pt < p.P) {
+        float m[16], y[4];
 #pragma unroll
-      for (int x = 0; x < 16; ++x) m[x] = acc[x][n][r];
-      output_transform(m, y);
-      const int bb = pt / T_img;
-      const int rr = pt - bb * T_img;
-      const int oh2 = rr / W2, ow2 = rr - oh2 * W2;
-      if constexpr (EPI == W_FWD_POOL) {
-        float best = 0.f;
-        int arg = 0;
+        for (int x = 0; x < 16; ++x) m[x] = acc[x][n][r];
+        output_transform(m, y);
+        const int bb = pt / T_img;
+        const int rr = pt - bb * T_img;
+        const int oh2 = rr / W2, ow2 = rr - oh2 * W2;
+        if constexpr (EPI == W_FWD_POOL) {
+          float best = 0.f;
+          int arg = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float v = y[q] * sc + sh;
-          if (p.relu) v = nan_relu(v);
-          if (q == 0 || v > best || (v != v && best == best)) {
-            best = v;
-            arg = q;
-          }
-        }
-        const long long o = (long long)pt * p.K + k;
-        p.out[o] = best;
-        p.out_argmax[o] = (uint8_t)arg;
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int oh = 2 * oh2 + (q >> 1), ow = 2 * ow2 + (q & 1);
-          const long long pix = ((long long)bb * p.H + oh) * p.W + ow;
-          if constexpr (EPI == W_FWD) {
+          for (int q = 0; q < 4; ++q) {
             float v = y[q] * sc + sh;
             if (p.relu) v = nan_relu(v);
-            p.out[pix * p.K + k] = v;
-          } else if constexpr (EPI == W_PARTIAL) {
-            const long long mrow = p.pooled_m ? (long long)pt * 4 + q : pix;
-            p.out[((long long)blockIdx.y * p.B * p.H * p.W + mrow) * p.K + k] = y[q];
-          } else {  // W_BWD
-            const float a = p.act[pix * p.K + k];
-            if (p.taylor) {
-              if (bb != cur_b) {
-                if (cur_b >= 0) atomicAdd(red + (cur_b - b_first) * W_TK + j + 16 * n, tsum);
-                cur_b = bb;
-                tsum = 0.f;
-              }
-              tsum += -(y[q] * a);
+            if (q == 0 || v > best || (v != v && best == best)) {
+              best = v;
+              arg = q;
             }
-            if (p.out) p.out[pix * p.K + k] = a > 0.f ? y[q] * sc : 0.f;
+          }
+          const long long o = (long long)pt * p.K + k;
+          p.out[o] = best;
+          p.out_argmax[o] = (uint8_t)arg;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int oh = 2 * oh2 + (q >> 1), ow = 2 * ow2 + (q & 1);
+            const long long pix = ((long long)bb * p.H + oh) * p.W + ow;
+            if constexpr (EPI == W_FWD) {
+              float v = y[q] * sc + sh;
+              if (p.relu) v = nan_relu(v);
+              p.out[pix * p.K + k] = v;
+            } else if constexpr (EPI == W_PARTIAL) {
+              const long long mrow = p.pooled_m ? (long long)pt * 4 + q : pix;
+              p.out[((long long)blockIdx.y * p.B * p.H * p.W + mrow) * p.K + k] = y[q];
+            } else {  // W_BWD
+              const float a = p.act[pix * p.K + k];
+              tsum += -(y[q] * a);
+              if (p.out) p.out[pix * p.K + k] = a > 0.f ? y[q] * sc : 0.f;
+            }
           }
         }
       }
-    }
-    if constexpr (EPI == W_BWD) {
-      if (p.taylor && cur_b >= 0) atomicAdd(red + (cur_b - b_first) * W_TK + j + 16 * n, tsum);
+      if constexpr (EPI == W_BWD) {
+        if (p.taylor) red[(tl_base + r) * W_TK + j + 16 * n] = tsum;
+      }
     }
   }
   if constexpr (EPI == W_BWD) {
     if (p.taylor) {
       __syncthreads();
-      for (int t = threadIdx.x; t < n_red * W_TK; t += blockDim.x) {
-        const int bb = b_first + t / W_TK, k = k0 + t % W_TK;
-        if (bb < p.B && k < p.K) atomicAdd(p.taylor + (long long)bb * p.K + k, red[t]);
+      const int b_first = t0 / T_img;
+      const int t_last = min(t0 + 64, p.P) - 1;
+      const int n_img = t_last / T_img - b_first + 1;
+      for (int t = threadIdx.x; t < n_img * W_TK; t += blockDim.x) {
+        const int bb = b_first + t / W_TK, kk = t % W_TK, k = k0 + kk;
+        if (bb >= p.B || k >= p.K) continue;
+        const int lo = max(bb * T_img, t0) - t0, hi = min((bb + 1) * T_img - 1, t_last) - t0;
+        float sum = 0.f;
+        for (int tl = lo; tl <= hi; ++tl) sum += red[tl * W_TK + kk];
+        const int slot = blk_p - (bb * T_img) / 64;
+        if (slot < p.tay_slots) p.taylor[((long long)slot * p.B + bb) * p.K + k] += sum;
       }
     }
   }
@@ -578,6 +585,8 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
                                               uint8_t* out_argmax, const float* act, float* taylor,
                                               hipStream_t st);
 
+extern "C" int tp_wino_taylor_slots(int H, int W) { return tp::wino_taylor_slots(H, W); }
+
 extern "C" int tp_wino_staged_ok(int H, int W, int unpool) {
   return tp::staged_geometry(H, W, unpool != 0).ok ? 1 : 0;
 }
@@ -619,6 +628,7 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.out_argmax = out_argmax;
   a.act = act;
   a.taylor = taylor;
+  a.tay_slots = wino_taylor_slots(H, W);
   int xmode = unpool ? X_UNPOOL : X_DIRECT;
   if (staged) {
     const XGeom gm = staged_geometry(H, W, unpool != 0);

@@ -1,4 +1,4 @@
-"""Multi-process data-parallel attribution on the gloo backend (world_size 2 and 3, CPU).
+"""Multi-process data-parallel attribution on the gloo backend (world_size 2, 3, 4, 8; CPU).
 
 Checks that sharded runs reproduce the single-process scores: Taylor/Sensitivity/APoZ with
 whole-batch round-robin sharding (R1/R2), Shapley with prefix-work sharding (R3/R4), and
@@ -72,7 +72,7 @@ def _worker(rank, world, port, path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_dp_matches_single_process(world):
     ref = _compute()
     port = _free_port()
@@ -80,9 +80,24 @@ def test_dp_matches_single_process(world):
         path = os.path.join(td, "out.pt")
         mp.spawn(_worker, args=(world, port, path), nprocs=world, join=True)
         got = torch.load(path, weights_only=False)
-    for k in ["taylor", "taylor_none", "sens_sum", "sv", "sv_none"]:
+    # fp64 device accumulators: the sharded reductions agree with one process to <= 1e-6
+    # relative; Shapley prefix losses are re-batched per rank (rounding level)
+    for k in ["taylor", "taylor_none", "sens_sum"]:
+        np.testing.assert_allclose(got[k], ref[k], rtol=1e-6, atol=1e-9, err_msg=k)
+    for k in ["sv", "sv_none"]:
         np.testing.assert_allclose(got[k], ref[k], rtol=1e-5, atol=1e-8, err_msg=k)
     for a, b in zip(got["apoz_many"], ref["apoz_many"]):
         np.testing.assert_allclose(a, b, rtol=1e-6)
     assert got["taylor_none"].shape == (22, 5)
     np.testing.assert_array_equal(got["pruned_w"], ref["pruned_w"])  # rank 0 indices [0, 3] everywhere
+
+
+def test_repeat_runs_bit_identical():
+    """Same seed, same world size -> bit-identical scores (no atomics on the CPU paths)."""
+    a, b = _compute(), _compute()
+    for k in a:
+        if isinstance(a[k], list):
+            for x, y in zip(a[k], b[k]):
+                np.testing.assert_array_equal(x, y, err_msg=k)
+        else:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)

@@ -111,6 +111,24 @@ def test_cross_entropy(cuda, nc):
 
 @pytest.mark.parametrize("after", [0, 1, 2])
 @pytest.mark.parametrize("take_abs", [False, True])
+def test_score_fold_slots(cuda, after, take_abs):
+    """(R, B, C) partial slots: summed in slot order, then |.|, fp64 accumulate, keep/zero."""
+    g = torch.Generator().manual_seed(10 + after)
+    Ts = [torch.randn(r, 9, c, generator=g) for r, c in ((1, 5), (4, 64), (3, 130))] + [torch.randn(6, 33,
+                                                                                                  generator=g)]
+    cpu = [t.clone() for t in Ts]
+    acc_cpu = [torch.zeros(t.shape[-1], dtype=torch.float64) for t in Ts]
+    ops.score_fold_(cpu, acc_cpu, take_abs, after)  # PyTorch reference (CPU tensors)
+    Td = [t.to(cuda) for t in Ts]
+    accs = [torch.zeros(t.shape[-1], dtype=torch.float64, device=cuda) for t in Ts]
+    ops.score_fold_(Td, accs, take_abs, after)
+    for t, r, a, ar in zip(Td, cpu, accs, acc_cpu):
+        torch.testing.assert_close(a.cpu(), ar)
+        torch.testing.assert_close(t.cpu(), r)
+
+
+@pytest.mark.parametrize("after", [0, 1, 2])
+@pytest.mark.parametrize("take_abs", [False, True])
 def test_score_fold(cuda, after, take_abs):
     g = torch.Generator().manual_seed(after)
     Ts = [torch.randn(7, c, generator=g) for c in (3, 64, 130, 512)] * 5  # 20 slabs -> 2 launches

@@ -50,3 +50,28 @@ def test_winograd_dgrad_weights():
     ut = winograd_weights(w.flip(2, 3).transpose(0, 1).float())  # (16, 32, 64)
     ref = torch.nn.grad.conv2d_input((2, 64, 4, 6), w, gy, padding=1)
     torch.testing.assert_close(_wino_conv(gy, ut), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_taylor_slots_cover_every_block():
+    """Every 64-tile block touching an image maps to a distinct slot < taylor_slots(H, W)."""
+    from torchpruner_amd.engine.fused_chain import taylor_slots
+    for H, W in [(32, 32), (16, 16), (8, 8), (4, 4), (2, 2), (6, 10), (18, 14), (64, 32), (28, 28)]:
+        T = (H // 2) * (W // 2)
+        R = taylor_slots(H, W)
+        for b in range(7):
+            first = (b * T) // 64
+            last = ((b + 1) * T - 1) // 64
+            assert last - first + 1 <= R, (H, W, b)
+
+
+def test_score_fold_slots_cpu_reference():
+    import torch
+    from torchpruner_amd import ops
+    g = torch.Generator().manual_seed(0)
+    T = torch.randn(3, 5, 4, generator=g)
+    ref = T.sum(0).abs()
+    acc = torch.zeros(4, dtype=torch.float64)
+    ops.score_fold_([T], [acc], True, 1)
+    torch.testing.assert_close(acc, ref.double().sum(0))
+    torch.testing.assert_close(T[0], ref)
+    assert torch.count_nonzero(T[1:]) == 0

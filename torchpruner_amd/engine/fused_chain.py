@@ -68,6 +68,20 @@ def winograd_weights(w: torch.Tensor) -> torch.Tensor:
     return img.reshape(C // 8, K // 32, 4096).float().contiguous()
 
 
+def taylor_slots(H: int, W: int) -> int:
+    """Partial slots R of the (R, B, C) Taylor slab the Winograd dgrad writes for an activation
+    of spatial size H x W (one slot per 64-tile block covering an image; mirrors
+    wino_taylor_slots() in winograd.hip). score_fold sums the slots in order."""
+    T = (H // 2) * (W // 2)
+    if T <= 0:
+        return 1
+    if T % 64 == 0:
+        return T // 64
+    if 64 % T == 0:
+        return 1
+    return (T + 63) // 64 + 1
+
+
 def _wino_ok(H, W, C, K):
     return H % 2 == 0 and W % 2 == 0 and C % 8 == 0 and K % 32 == 0
 
@@ -113,13 +127,17 @@ class Autotuner:
         self.cache = {}
         self.enabled = os.environ.get("TORCHPRUNER_AUTOTUNE", "1") != "0"
 
-    def candidates(self, M, N, K, wino=None):
-        """``wino``: (P tiles, C) when the Winograd kernel applies to this conv."""
+    def candidates(self, M, N, K, wino=None, wino_only=False):
+        """``wino``: (P tiles, C) when the Winograd kernel applies to this conv; ``wino_only``
+        drops the implicit-GEMM configs (conv dgrad: the Winograd epilogue's Taylor sums are
+        atomic-free and bit-reproducible, the GEMM's are not)."""
         out = []
         if wino is not None:
             sp = _wino_splits(wino[0], N, wino[1])
             for kind in (WINO, WINO_LDS):
                 out += [(kind, sp)] + ([(kind, max(1, sp // 2))] if sp > 1 else [])
+            if wino_only:
+                return out
         for cfg, (bm, bn) in _TILES.items():
             if N <= 64 and bn == 128:
                 continue
@@ -129,7 +147,7 @@ class Autotuner:
                 out.append((cfg, max(1, sp // 2)))
         return out
 
-    def choose(self, key, M, N, K, run, wino=None):
+    def choose(self, key, M, N, K, run, wino=None, wino_only=False):
         """``run(cfg, splits)`` launches the op once (must be side-effect free)."""
         hit = self.cache.get(key)
         if hit is not None:
@@ -139,7 +157,7 @@ class Autotuner:
             self.cache[key] = res
             return res
         best = None
-        for cand in self.candidates(M, N, K, wino):
+        for cand in self.candidates(M, N, K, wino, wino_only and wino is not None):
             run(*cand)  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -410,20 +428,48 @@ class FusedChainEngine:
         loss, _ = ops.cross_entropy(self.forward_from(k, h), y, 1.0, False)
         return loss
 
-    def score_arena(self, B: int, want, device):
-        """Persistent zeroed (B, C) score slabs for the blocks in ``want`` (one allocation).
-        The caller must leave them zeroed (ops.score_fold_ with after=2) for reuse."""
-        key = (B, tuple(sorted(want)), str(device))
+    def _block_hw(self, b, H0, W0):
+        """Spatial size of block b's output activation for an H0 x W0 input."""
+        H, W = H0, W0
+        for i, blk in enumerate(self.plan.convs):
+            if blk.pool is not None:
+                H, W = H // 2, W // 2
+            if i == b:
+                return H, W
+        return 1, 1
+
+    def _arena_shapes(self, B, want, H0, W0):
+        shapes = {}
+        nconv = len(self.plan.convs)
+        for b in sorted(want):
+            c = self._block_width(b)
+            if b < nconv:
+                shapes[b] = (taylor_slots(*self._block_hw(b, H0, W0)), B, c)
+            else:
+                shapes[b] = (B, c)
+        return shapes
+
+    def score_arena(self, B: int, want, device, hw=(32, 32)):
+        """Persistent zeroed score slabs for the blocks in ``want`` (one allocation): (R, B, C)
+        partial slots for conv blocks (see taylor_slots), (B, C) for linear blocks. The caller
+        must leave them zeroed (ops.score_fold_ with after=2) for reuse."""
+        key = (B, tuple(sorted(want)), str(device), tuple(hw))
         arena = self._arenas.get(key)
         if arena is None:
-            widths = {b: self._block_width(b) for b in sorted(want)}
-            flat = torch.zeros(B * sum(widths.values()), device=device)
+            shapes = self._arena_shapes(B, want, *hw)
+            flat = torch.zeros(sum(math.prod(sh) for sh in shapes.values()), device=device)
             arena, off = {}, 0
-            for b, c in widths.items():
-                arena[b] = flat[off:off + B * c].view(B, c)
-                off += B * c
+            for b, sh in shapes.items():
+                n = math.prod(sh)
+                arena[b] = flat[off:off + n].view(sh)
+                off += n
             self._arenas[key] = arena
         return arena
+
+    @staticmethod
+    def per_sample(t: torch.Tensor) -> torch.Tensor:
+        """(B, C) view of a folded score slab (slot 0 of an (R, B, C) arena entry)."""
+        return t[0] if t.dim() == 3 else t
 
     def _block_width(self, b):
         blocks = self.plan.blocks
@@ -431,16 +477,18 @@ class FusedChainEngine:
         return blk.conv.out_channels if isinstance(blk, ConvBlock) else blk.linear.out_features
 
     def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None):
-        """One fused forward+backward; returns {block index: (B, C) per-sample signed Taylor
-        sums sum_hw -(dL/da * a)} for every requested block (conv blocks first, then
-        linear blocks; the final linear has none)."""
+        """One fused forward+backward; returns {block index: per-sample signed Taylor sums
+        sum_hw -(dL/da * a)} for every requested block (conv blocks first, then linear blocks;
+        the final linear has none) as (R, B, C) partial slots for conv blocks (sum over R, or
+        fold with ops.score_fold_) and (B, C) for linear blocks. Deterministic: no atomics."""
         T = ops.require()
         P = self._pack()
         nconv, nlin = len(self.plan.convs), len(self.plan.linears)
         if want is None:
             want = set(range(nconv + nlin - 1))
         if arena is None:
-            arena = {b: torch.zeros(x.shape[0], self._block_width(b), device=x.device) for b in want}
+            arena = {b: torch.zeros(sh, device=x.device)
+                     for b, sh in self._arena_shapes(x.shape[0], want, x.shape[2], x.shape[3]).items()}
         logits, saved = self.forward(x)
         B = logits.shape[0]
         _, g = ops.cross_entropy(logits, y, 1.0 / B, True)
@@ -486,7 +534,7 @@ class FusedChainEngine:
             cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None),
                                    M, Cin, e["wt"].shape[1],
                                    lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out:
-                                   self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_), wino)
+                                   self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_), wino, wino_only=True)
             g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp)
         return res
 

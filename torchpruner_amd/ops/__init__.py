@@ -82,9 +82,10 @@ def column_accumulate(v: torch.Tensor, acc_sum: torch.Tensor, acc_sq: torch.Tens
 
 
 def score_fold_(Ts: Sequence[torch.Tensor], accs: Sequence[torch.Tensor | None], take_abs: bool, after: int) -> None:
-    """For each (B, C) score slab T: v = |T| (or T); acc += v.sum(0) in float64 (acc may be
-    None); then ``after`` = 0 leaves T, 1 writes v back into T, 2 zeroes T. One launch for
-    up to 16 slabs (the fused engine folds every layer's scores at once)."""
+    """For each (B, C) score slab T — or (R, B, C) partial slots, summed in slot order first —
+    v = |T| (or T); acc += v.sum(0) in float64 (acc may be None); then ``after`` = 0 leaves T,
+    1 writes v back into T (slot 0, other slots zeroed), 2 zeroes T. One launch for up to 16
+    slabs (the fused engine folds every layer's scores at once)."""
     if len(Ts) == 0:
         return
     if use_native(*Ts):
@@ -92,11 +93,16 @@ def score_fold_(Ts: Sequence[torch.Tensor], accs: Sequence[torch.Tensor | None],
         require().score_fold_(list(Ts), [a if a is not None else empty for a in accs], bool(take_abs), int(after))
         return
     for T, a in zip(Ts, accs):
-        v = T.abs() if take_abs else T
+        tot = T.sum(0) if T.dim() == 3 else T
+        v = tot.abs() if take_abs else tot
         if a is not None:
             a += v.double().sum(0)
         if after == 1:
-            T.copy_(v)
+            if T.dim() == 3:
+                T[1:].zero_()
+                T[0].copy_(v)
+            else:
+                T.copy_(v)
         elif after == 2:
             T.zero_()
 
