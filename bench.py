@@ -52,8 +52,11 @@ def parse():
     ap.add_argument("--baseline-batches", type=int, default=2)
     ap.add_argument("--no-prune", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--train-steps", type=int, default=int(os.environ.get("BENCH_TRAIN_STEPS", 150)),
+    ap.add_argument("--train-steps", type=int, default=int(os.environ.get("BENCH_TRAIN_STEPS", 300)),
                     help="untimed SGD steps on the synthetic task before scoring (0 = random init)")
+    ap.add_argument("--task-noise", type=float, default=4.0,
+                    help="per-pixel noise of the synthetic prototype task (4.0: the teacher is not saturated, "
+                         "so loss gradients are informative; see profiles/taylor_quality_sweep.txt)")
     return ap.parse_args()
 
 
@@ -138,7 +141,7 @@ def main():
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
     model = prunable_vgg16().to(dev)
-    task = PrototypeTask((3, 32, 32), 10, noise=2.0, seed=args.seed, device=dev)
+    task = PrototypeTask((3, 32, 32), 10, noise=args.task_noise, seed=args.seed, device=dev)
     t0 = time.perf_counter()
     train_teacher(model, task, args.train_steps, dev, args.seed)
     log(f"[bench] teacher: {args.train_steps} SGD steps in {time.perf_counter() - t0:.1f}s (untimed)")
@@ -208,11 +211,12 @@ def main():
         before = top1(model, xv, yv)
         rng = np.random.RandomState(args.seed)
         lw_taylor = layerwise_top1(model, convs, scores, xv, yv)
-        lw_random = layerwise_top1(model, convs, [rng.random_sample(c.out_channels) for c in convs], xv, yv)
+        lw_random = float(np.mean([layerwise_top1(model, convs, [rng.random_sample(c.out_channels) for c in convs],
+                                                  xv, yv) for _ in range(3)]))
         result["top1_layerwise_50pct_taylor"] = round(lw_taylor, 4)
         result["top1_layerwise_50pct_random"] = round(lw_random, 4)
         log(f"[bench] layerwise 50% (one layer at a time, mean over 13): Taylor {lw_taylor:.4f}, "
-            f"Random {lw_random:.4f}")
+            f"Random {lw_random:.4f} (mean of 3 draws)")
         rnd = copy.deepcopy(model)
         prune_half(model, {id(c): s for c, s in zip(convs, scores)}, dev)
         after = top1(model, xv, yv)

@@ -40,6 +40,8 @@ const float* opt_ptr(const c10::optional<at::Tensor>& t, int64_t n, const char* 
   if (!t.has_value() || !t->defined()) return nullptr;
   need(*t, name, 1);
   TORCH_CHECK(t->numel() == n, name, " must have ", n, " elements");
+  // the epilogues read per-channel vectors as float4
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr<float>()) % 16 == 0, name, " must be 16-byte aligned");
   return t->data_ptr<float>();
 }
 
