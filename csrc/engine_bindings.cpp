@@ -15,6 +15,7 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
 int tp_wino_taylor_slots(int H, int W);
+hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C, int H, int W, int Cp, hipStream_t st);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* ws, hipStream_t st);
@@ -245,8 +246,21 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
 
 int64_t wino_taylor_slots(int64_t H, int64_t W) { return tp_wino_taylor_slots((int)H, (int)W); }
 
+// NCHW -> NHWC with the channel dim zero-padded to Cp (first-layer input of the MFMA kernels).
+at::Tensor nchw_to_nhwc_pad(const at::Tensor& x, int64_t Cp) {
+  need(x, "x", 4);
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(Cp >= C && Cp % 4 == 0, "Cp must be >= C and a multiple of 4");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({B, H, W, Cp}, x.options());
+  TP_CHECK_HIP(tp_nchw_to_nhwc_pad(x.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)C, (int)H, (int)W, (int)Cp,
+                                   cur_stream()));
+  return y;
+}
+
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
+  m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits) -> (Tensor, Tensor)");
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
@@ -263,5 +277,6 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_dgrad", &conv_dgrad);
   m.impl("conv_first", &conv_first);
   m.impl("conv_wino_fwd", &conv_wino_fwd);
+  m.impl("nchw_to_nhwc_pad", &nchw_to_nhwc_pad);
   m.impl("conv_wino_dgrad", &conv_wino_dgrad);
 }

@@ -176,37 +176,74 @@ struct ScoreBatch {
   ScoreDesc d[16];
 };
 
+// One block per (score tensor, 256-column chunk); threads = (row group, column quad). Columns
+// are read as float4 when C % 4 == 0 (scalar otherwise); narrow tensors get more row groups so
+// the per-thread serial chain stays short (the fold is latency bound). Row-group partials are
+// combined in LDS in a fixed order: deterministic.
 __global__ __launch_bounds__(1024) void score_fold_multi(ScoreBatch batch, int take_abs, int after) {
-  constexpr int RG = 16;  // row groups per block (the fold is latency bound: few columns, many rows)
-  __shared__ double ps[RG][64];
+  __shared__ double ps[4096];
   const ScoreDesc s = batch.d[blockIdx.y];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;
-  if (blockIdx.x * 64 >= s.C) return;  // uniform per block
-  double acc = 0.0;
-  if (c < s.C) {
-    const long long slot = (long long)s.B * s.C;
+  const int c_base = blockIdx.x * 256;
+  if (c_base >= s.C) return;  // uniform per block
+  const bool vec = (s.C & 3) == 0;
+  const int cols = min(256, s.C - c_base);
+  const int nq = vec ? (cols + 3) / 4 : min(cols, 256);  // column units (quads or scalars)
+  const int RG = min(1024 / nq, 64);
+  const int rg = threadIdx.x / nq, cu = threadIdx.x % nq;
+  const int w = vec ? 4 : 1;  // columns per unit
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  const long long slot = (long long)s.B * s.C;
+  if (rg < RG) {
+    const int c = c_base + cu * w;
     for (int b = rg; b < s.B; b += RG) {
       float* p = s.T + (long long)b * s.C + c;
-      float v = *p;
-      for (int r = 1; r < s.R; ++r) v += p[r * slot];
-      if (take_abs) v = fabsf(v);
-      acc += (double)v;
-      if (after == 1) {  // keep the processed per-sample value (in slot 0)
-        *p = v;
-        for (int r = 1; r < s.R; ++r) p[r * slot] = 0.f;
-      } else if (after == 2) {  // zero for the next batch
-        for (int r = 0; r < s.R; ++r) p[r * slot] = 0.f;
+      if (vec) {
+        float4 v = *reinterpret_cast<float4*>(p);
+        for (int r = 1; r < s.R; ++r) {
+          const float4 u = *reinterpret_cast<const float4*>(p + r * slot);
+          v.x += u.x;
+          v.y += u.y;
+          v.z += u.z;
+          v.w += u.w;
+        }
+        if (take_abs) {
+          v.x = fabsf(v.x);
+          v.y = fabsf(v.y);
+          v.z = fabsf(v.z);
+          v.w = fabsf(v.w);
+        }
+        a[0] += (double)v.x;
+        a[1] += (double)v.y;
+        a[2] += (double)v.z;
+        a[3] += (double)v.w;
+        if (after == 1) {  // keep the processed per-sample value (in slot 0)
+          *reinterpret_cast<float4*>(p) = v;
+          for (int r = 1; r < s.R; ++r) *reinterpret_cast<float4*>(p + r * slot) = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else if (after == 2) {  // zero for the next batch
+          for (int r = 0; r < s.R; ++r) *reinterpret_cast<float4*>(p + r * slot) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      } else {
+        float v = *p;
+        for (int r = 1; r < s.R; ++r) v += p[r * slot];
+        if (take_abs) v = fabsf(v);
+        a[0] += (double)v;
+        if (after == 1) {
+          *p = v;
+          for (int r = 1; r < s.R; ++r) p[r * slot] = 0.f;
+        } else if (after == 2) {
+          for (int r = 0; r < s.R; ++r) p[r * slot] = 0.f;
+        }
       }
     }
+    for (int i = 0; i < w; ++i) ps[rg * (nq * w) + cu * w + i] = a[i];
   }
-  ps[rg][threadIdx.x & 63] = acc;
   __syncthreads();
-  if (rg == 0 && c < s.C && s.acc) {
-    double t = 0.0;
-#pragma unroll
-    for (int g = 0; g < RG; ++g) t += ps[g][threadIdx.x];
-    s.acc[c] += t;
+  if (s.acc) {
+    for (int col = threadIdx.x; col < cols; col += blockDim.x) {
+      double t = 0.0;
+      for (int g = 0; g < RG; ++g) t += ps[g * (nq * w) + col];
+      s.acc[c_base + col] += t;
+    }
   }
 }
 
@@ -221,7 +258,7 @@ extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, c
     b.d[i] = tp::ScoreDesc{T[i], acc[i], B[i], C[i], R[i]};
     maxc = std::max(maxc, C[i]);
   }
-  dim3 grid(tp::ceil_div(maxc, 64), count);
+  dim3 grid(tp::ceil_div(maxc, 256), count);
   tp::score_fold_multi<<<grid, 1024, 0, st>>>(b, take_abs, after);
   return hipGetLastError();
 }

@@ -662,3 +662,34 @@ extern "C" hipError_t tp_conv_first_direct(const float* x, const float* w, const
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
+
+// NCHW (B, C, H, W) -> NHWC (B, H, W, Cp) with channels C..Cp-1 zero (Cp % 4 == 0): the
+// first layer's input in the layout the Winograd / implicit-GEMM kernels read (float4 stores).
+namespace tp {
+__global__ __launch_bounds__(256) void nchw_to_nhwc_pad(const float* __restrict__ x, float* __restrict__ y, int B,
+                                                        int C, int HW, int Cp) {
+  const long long total = (long long)B * HW * (Cp / 4);
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % (Cp / 4));
+    const long long pix = t / (Cp / 4);
+    const long long b = pix / HW, s = pix - b * HW;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c4 * 4 + i;
+      v[i] = c < C ? x[(b * C + c) * HW + s] : 0.f;
+    }
+    *reinterpret_cast<float4*>(y + pix * Cp + c4 * 4) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+}  // namespace tp
+
+extern "C" hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C, int H, int W, int Cp,
+                                          hipStream_t st) {
+  if (Cp % 4 != 0 || Cp < C) return hipErrorInvalidValue;
+  const long long total = (long long)B * H * W * (Cp / 4);
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::nchw_to_nhwc_pad<<<grid, 256, 0, st>>>(x, y, B, C, H * W, Cp);
+  return hipGetLastError();
+}

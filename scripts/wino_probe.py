@@ -6,7 +6,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torchpruner_amd import ops  # noqa: E402
-from torchpruner_amd.engine.fused_chain import winograd_weights  # noqa: E402
+from torchpruner_amd.engine.fused_chain import taylor_slots, winograd_weights  # noqa: E402
 
 T = ops.require()
 dev = torch.device("cuda")
@@ -21,7 +21,7 @@ for (H, W, C, K) in [(32, 32, 64, 64), (16, 16, 128, 128)]:
     gp = torch.randn(B, H // 2, W // 2, K, device=dev)
     am = torch.randint(0, 4, (B, H // 2, W // 2, K), device=dev, dtype=torch.uint8)
     act = torch.relu(torch.randn(B, H, W, C, device=dev))
-    tay = torch.zeros(B, C, device=dev)
+    tay = torch.zeros(taylor_slots(H, W), B, C, device=dev)
     scin = torch.ones(C, device=dev)
     for _ in range(3):
         T.conv_wino_fwd(x, u, sc, sh, True, True, 1, True)

@@ -341,3 +341,25 @@ def test_wino_nan_propagation(cuda):
     u = winograd_weights(torch.randn(32, 32, 3, 3).to(cuda) * 0.1)
     out, am = T.conv_wino_fwd(x.to(cuda), u, None, None, True, True, 1)
     assert torch.isnan(out.cpu()[:, 0, 0]).all()
+
+
+@pytest.mark.parametrize("staged", [False, True])
+def test_first_layer_winograd(cuda, staged):
+    """Tiny-Cin first layer: NCHW -> NHWC-8 pad + Winograd == fp64 conv + BN affine + ReLU."""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import winograd_weights
+    T = ops.require()
+    g = torch.Generator().manual_seed(4)
+    x = _rand(6, 3, 32, 32, gen=g)
+    w = _rand(64, 3, 3, 3, gen=g) * 0.3
+    s = _rand(64, gen=g).abs()
+    t = _rand(64, gen=g)
+    ref = (F.conv2d(x.double(), w.double(), padding=1) * s.double().view(1, -1, 1, 1)
+           + t.double().view(1, -1, 1, 1)).clamp_min(0).permute(0, 2, 3, 1)
+    xp = T.nchw_to_nhwc_pad(x.to(cuda), 8)
+    assert xp.shape == (6, 32, 32, 8)
+    torch.testing.assert_close(xp[..., :3].cpu(), x.permute(0, 2, 3, 1))
+    assert torch.count_nonzero(xp[..., 3:]) == 0
+    u = winograd_weights(F.pad(w, (0, 0, 0, 0, 0, 5)).to(cuda))
+    out, _ = T.conv_wino_fwd(xp, u, s.to(cuda), t.to(cuda), True, False, 1, staged)
+    torch.testing.assert_close(out.cpu(), ref.float(), rtol=3e-4, atol=3e-4)

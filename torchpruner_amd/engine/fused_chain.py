@@ -147,17 +147,21 @@ class Autotuner:
                 out.append((cfg, max(1, sp // 2)))
         return out
 
-    def choose(self, key, M, N, K, run, wino=None, wino_only=False):
-        """``run(cfg, splits)`` launches the op once (must be side-effect free)."""
+    def choose(self, key, M, N, K, run, wino=None, wino_only=False, cands=None):
+        """``run(cfg, splits)`` launches the op once (must be side-effect free); ``cands``
+        overrides the candidate list (first entry = the fallback when tuning is off)."""
         hit = self.cache.get(key)
         if hit is not None:
             return hit
         if not self.enabled or torch.cuda.is_current_stream_capturing():
-            res = (WINO_LDS, _wino_splits(wino[0], N, wino[1])) if wino is not None else _pick_cfg(M, N, K)
+            if cands is not None:
+                res = cands[0]
+            else:
+                res = (WINO_LDS, _wino_splits(wino[0], N, wino[1])) if wino is not None else _pick_cfg(M, N, K)
             self.cache[key] = res
             return res
         best = None
-        for cand in self.candidates(M, N, K, wino, wino_only and wino is not None):
+        for cand in (cands if cands is not None else self.candidates(M, N, K, wino, wino_only and wino is not None)):
             run(*cand)  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -325,6 +329,9 @@ class FusedChainEngine:
             entry = {"scale": scale.contiguous(), "shift": shift.contiguous(), "pool": b.pool is not None}
             if b.first:
                 entry["w_first"] = w.contiguous()
+                if self.use_wino and w.shape[1] <= 8 and cout % 32 == 0:
+                    # tiny-Cin first layer on the Winograd MFMA kernel: input padded to 8 channels
+                    entry["u_first"] = winograd_weights(F.pad(w, (0, 0, 0, 0, 0, 8 - w.shape[1])))
             else:
                 entry["w"] = w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous()  # [n][(kh,kw,ci)]
             # dgrad operand: flipped taps, transposed channels -> [ci][(kh,kw,co)]
@@ -351,6 +358,26 @@ class FusedChainEngine:
         return self._packed
 
     # ------------------------------------------------------------------ execution
+    FIRST_DIRECT = -10  # pseudo cfg: VALU direct first-layer kernel
+
+    def _first_run(self, T, e, xf, cfg, sp):
+        if cfg == self.FIRST_DIRECT:
+            return T.conv_first(xf, e["w_first"], e["scale"], e["shift"], True)
+        xp = T.nchw_to_nhwc_pad(xf, 8)
+        out, _ = T.conv_wino_fwd(xp, e["u_first"], e["scale"], e["shift"], True, False, sp, cfg == WINO_LDS)
+        return out
+
+    def _first(self, T, e, x):
+        xf = x.float().contiguous()
+        B, _, H, W = xf.shape
+        N = e["scale"].numel()
+        if "u_first" not in e or not _wino_ok(H, W, 8, N):
+            return T.conv_first(xf, e["w_first"], e["scale"], e["shift"], True)
+        cands = [(WINO_LDS, 1), (self.FIRST_DIRECT, 1), (WINO, 1)]
+        cfg, sp = TUNER.choose(("first", tuple(xf.shape), N), B * H * W, N, 27, lambda c, s_, e=e, xf=xf:
+                               self._first_run(T, e, xf, c, s_), cands=cands)
+        return self._first_run(T, e, xf, cfg, sp)
+
     @staticmethod
     def _conv_run(T, e, h, cfg, sp):
         if cfg in (WINO, WINO_LDS):
@@ -391,7 +418,7 @@ class FusedChainEngine:
         h = None
         for ci, (blk, e) in enumerate(zip(self.plan.convs, P["convs"])):
             if ci == 0 and blk.first:
-                h = T.conv_first(x.float().contiguous(), e["w_first"], e["scale"], e["shift"], True)
+                h = self._first(T, e, x)
                 am = None
             else:
                 if ci == 0:
