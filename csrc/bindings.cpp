@@ -100,8 +100,10 @@ void score_fold_(at::TensorList T, at::TensorList acc, bool take_abs, int64_t af
   std::vector<int> bs, cs, rs;
   auto flush = [&]() {
     if (tp.empty()) return;
+    const int n_ws = tp_score_fold_ws_elems(bs.data(), cs.data(), (int)tp.size());
+    at::Tensor ws = at::empty({std::max(n_ws, 1)}, T[0].options().dtype(at::kDouble));
     TP_CHECK_HIP(tp_score_fold_multi(tp.data(), ap.data(), bs.data(), cs.data(), rs.data(), (int)tp.size(),
-                                     take_abs ? 1 : 0, (int)after, cur_stream()));
+                                     take_abs ? 1 : 0, (int)after, ws.data_ptr<double>(), cur_stream()));
     tp.clear(); ap.clear(); bs.clear(); cs.clear(); rs.clear();
   };
   for (size_t i = 0; i < T.size(); ++i) {

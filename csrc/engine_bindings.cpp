@@ -11,7 +11,9 @@ extern "C" {
 hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w, int B, int H, int W, int Cin,
                          int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
-                         float* taylor, int HWo, float* ws, hipStream_t st);
+                         float* taylor, int HWo, int tay_group, float* ws, hipStream_t st);
+hipError_t tp_maxpool2_nhwc(const float* x, float* y, uint8_t* am, int B, int H, int W, int C, hipStream_t st);
+hipError_t tp_unpool2_nhwc(const float* g, const uint8_t* am, float* out, int B, int H, int W, int C, hipStream_t st);
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
 int tp_wino_taylor_slots(int H, int W);
@@ -85,7 +87,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
   TP_CHECK_HIP(tp_conv_igemm(x.data_ptr<float>(), nullptr, w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin,
                              (int)Cout, (int)ks, pool ? 1 : 0, 0, pool ? EPI_FWD_POOL : EPI_FWD, (int)cfg, (int)sp, sc,
                              sh, relu ? 1 : 0, out.data_ptr<float>(), pool ? am.data_ptr<uint8_t>() : nullptr, nullptr,
-                             nullptr, (int)(H * W), sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                             nullptr, (int)(H * W), 0, sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
   return {out, am};
 }
 
@@ -98,7 +100,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
 at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_argmax, const at::Tensor& wt,
                       const at::Tensor& act, const c10::optional<at::Tensor>& bn_scale,
                       const c10::optional<at::Tensor>& taylor, bool want_out, int64_t ks, int64_t cfg,
-                      int64_t splits) {
+                      int64_t splits, int64_t tay_group) {
   need(g, "g", 4);
   need(wt, "wt", 2);
   need(act, "act", 4);
@@ -115,6 +117,7 @@ at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_ar
   TORCH_CHECK(g.size(0) == B, "batch mismatch");
   TORCH_CHECK(wt.size(0) == Cin && wt.size(1) == ks * ks * Cout, "wt must be (Cin, ks*ks*Cout)");
   TORCH_CHECK(Cout % 32 == 0, "Cout must be a multiple of 32 for dgrad");
+  TORCH_CHECK(tay_group >= 0 && (tay_group == 0 || Cin % tay_group == 0), "tay_group must divide Cin");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
   const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
   float* tay = nullptr;
@@ -133,7 +136,7 @@ at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_ar
                              wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, (int)ks, 0,
                              unpool ? 1 : 0, EPI_BWD, (int)cfg, (int)sp, sc, nullptr, 0,
                              want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(), tay,
-                             (int)(H * W), sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                             (int)(H * W), (int)tay_group, sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
   return out;
 }
 
@@ -225,8 +228,8 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
   if (taylor.has_value() && taylor->defined()) {
     const int64_t R = tp_wino_taylor_slots((int)H, (int)W);
     TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
-                    taylor->numel() == R * B * Cin,
-                "taylor must be a contiguous float32 (R, B, Cin) GPU tensor with R = ", R,
+                    taylor->numel() % (B * Cin) == 0 && taylor->numel() >= R * B * Cin,
+                "taylor must be a contiguous float32 (R', B, Cin) GPU tensor with R' >= ", R,
                 " partial slots (winograd_taylor_slots)");
     tay = taylor->data_ptr<float>();
   }
@@ -246,6 +249,31 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
 
 int64_t wino_taylor_slots(int64_t H, int64_t W) { return tp_wino_taylor_slots((int)H, (int)W); }
 
+// NHWC 2x2/stride-2 max-pool (NaN-propagating) -> (pooled, argmax bytes)
+std::tuple<at::Tensor, at::Tensor> maxpool2_nhwc(const at::Tensor& x) {
+  need(x, "x", 4);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "maxpool2 needs even H, W");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({B, H / 2, W / 2, C}, x.options());
+  auto am = at::empty({B, H / 2, W / 2, C}, x.options().dtype(at::kByte));
+  TP_CHECK_HIP(tp_maxpool2_nhwc(x.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(), (int)B, (int)H,
+                                (int)W, (int)C, cur_stream()));
+  return {y, am};
+}
+
+// inverse of maxpool2_nhwc: scatter the pooled gradient to the argmax positions
+at::Tensor unpool2_nhwc(const at::Tensor& g, const at::Tensor& am) {
+  need(g, "g", 4);
+  TORCH_CHECK(am.scalar_type() == at::kByte && am.sizes() == g.sizes() && am.is_contiguous(), "am must match g");
+  const int64_t B = g.size(0), H = g.size(1) * 2, W = g.size(2) * 2, C = g.size(3);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  auto out = at::empty({B, H, W, C}, g.options());
+  TP_CHECK_HIP(tp_unpool2_nhwc(g.data_ptr<float>(), am.data_ptr<uint8_t>(), out.data_ptr<float>(), (int)B, (int)H,
+                               (int)W, (int)C, cur_stream()));
+  return out;
+}
+
 // NCHW -> NHWC with the channel dim zero-padded to Cp (first-layer input of the MFMA kernels).
 at::Tensor nchw_to_nhwc_pad(const at::Tensor& x, int64_t Cp) {
   need(x, "x", 4);
@@ -261,10 +289,12 @@ at::Tensor nchw_to_nhwc_pad(const at::Tensor& x, int64_t Cp) {
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
+  m.def("maxpool2_nhwc(Tensor x) -> (Tensor, Tensor)");
+  m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits) -> (Tensor, Tensor)");
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
-        "bool want_out, int ks, int cfg, int splits) -> Tensor");
+        "bool want_out, int ks, int cfg, int splits, int tay_group=0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
         "bool staged=True) -> (Tensor, Tensor)");
@@ -278,5 +308,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_first", &conv_first);
   m.impl("conv_wino_fwd", &conv_wino_fwd);
   m.impl("nchw_to_nhwc_pad", &nchw_to_nhwc_pad);
+  m.impl("maxpool2_nhwc", &maxpool2_nhwc);
+  m.impl("unpool2_nhwc", &unpool2_nhwc);
   m.impl("conv_wino_dgrad", &conv_wino_dgrad);
 }

@@ -33,5 +33,7 @@ void register_engine_ops_def(torch::Library& m);
 void register_engine_ops_impl(torch::Library& m);
 #endif
 
+extern "C" int tp_score_fold_ws_elems(const int* B, const int* C, int count);
 extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, const int* B, const int* C,
-                                          const int* R, int count, int take_abs, int after, hipStream_t st);
+                                          const int* R, int count, int take_abs, int after, double* ws,
+                                          hipStream_t st);

@@ -176,26 +176,31 @@ struct ScoreBatch {
   ScoreDesc d[16];
 };
 
-// One block per (score tensor, 256-column chunk); threads = (row group, column quad). Columns
-// are read as float4 when C % 4 == 0 (scalar otherwise); narrow tensors get more row groups so
-// the per-thread serial chain stays short (the fold is latency bound). Row-group partials are
-// combined in LDS in a fixed order: deterministic.
-__global__ __launch_bounds__(1024) void score_fold_multi(ScoreBatch batch, int take_abs, int after) {
+// Pass 1: one block per (score tensor, 256-column chunk, chunk of FOLD_ROWS rows); threads =
+// (row group, column unit: a float4 quad when C % 4 == 0, else a scalar). Each block writes its
+// fp64 column partials to ws[tensor][row chunk][C]. Pass 2 adds the row-chunk partials in
+// order into acc. Both passes use fixed summation orders: deterministic.
+constexpr int FOLD_ROWS = 32;
+
+__global__ __launch_bounds__(1024) void score_fold_rows(ScoreBatch batch, int take_abs, int after, double* ws,
+                                                         int ldc, int n_rchunks) {
   __shared__ double ps[4096];
   const ScoreDesc s = batch.d[blockIdx.y];
   const int c_base = blockIdx.x * 256;
-  if (c_base >= s.C) return;  // uniform per block
+  const int r0 = blockIdx.z * FOLD_ROWS;
+  if (c_base >= s.C || r0 >= s.B) return;  // uniform per block
+  const int r1 = min(s.B, r0 + FOLD_ROWS);
   const bool vec = (s.C & 3) == 0;
   const int cols = min(256, s.C - c_base);
-  const int nq = vec ? (cols + 3) / 4 : min(cols, 256);  // column units (quads or scalars)
-  const int RG = min(1024 / nq, 64);
+  const int nq = vec ? (cols + 3) / 4 : min(cols, 256);
+  const int RG = min(1024 / nq, FOLD_ROWS);
   const int rg = threadIdx.x / nq, cu = threadIdx.x % nq;
-  const int w = vec ? 4 : 1;  // columns per unit
+  const int w = vec ? 4 : 1;
   double a[4] = {0.0, 0.0, 0.0, 0.0};
   const long long slot = (long long)s.B * s.C;
   if (rg < RG) {
     const int c = c_base + cu * w;
-    for (int b = rg; b < s.B; b += RG) {
+    for (int b = r0 + rg; b < r1; b += RG) {
       float* p = s.T + (long long)b * s.C + c;
       if (vec) {
         float4 v = *reinterpret_cast<float4*>(p);
@@ -242,24 +247,52 @@ __global__ __launch_bounds__(1024) void score_fold_multi(ScoreBatch batch, int t
     for (int col = threadIdx.x; col < cols; col += blockDim.x) {
       double t = 0.0;
       for (int g = 0; g < RG; ++g) t += ps[g * (nq * w) + col];
-      s.acc[c_base + col] += t;
+      ws[((long long)blockIdx.y * n_rchunks + blockIdx.z) * ldc + c_base + col] = t;
     }
   }
 }
 
+__global__ __launch_bounds__(256) void score_fold_final(ScoreBatch batch, const double* ws, int ldc, int n_rchunks) {
+  const ScoreDesc s = batch.d[blockIdx.y];
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (!s.acc || c >= s.C) return;
+  const int nr = (s.B + FOLD_ROWS - 1) / FOLD_ROWS;
+  double t = 0.0;
+  for (int z = 0; z < nr; ++z) t += ws[((long long)blockIdx.y * n_rchunks + z) * ldc + c];
+  s.acc[c] += t;
+}
+
 }  // namespace tp
 
+extern "C" int tp_score_fold_ws_elems(const int* B, const int* C, int count) {
+  int maxc = 0, maxb = 0;
+  for (int i = 0; i < count; ++i) {
+    maxc = std::max(maxc, C[i]);
+    maxb = std::max(maxb, B[i]);
+  }
+  return count * tp::ceil_div(maxb, tp::FOLD_ROWS) * maxc;
+}
+
+// ws: tp_score_fold_ws_elems doubles
 extern "C" hipError_t tp_score_fold_multi(float* const* T, double* const* acc, const int* B, const int* C,
-                                          const int* R, int count, int take_abs, int after, hipStream_t st) {
+                                          const int* R, int count, int take_abs, int after, double* ws,
+                                          hipStream_t st) {
   if (count <= 0 || count > 16) return hipErrorInvalidValue;
   tp::ScoreBatch b{};
-  int maxc = 0;
+  int maxc = 0, maxb = 0;
+  bool any_acc = false;
   for (int i = 0; i < count; ++i) {
     b.d[i] = tp::ScoreDesc{T[i], acc[i], B[i], C[i], R[i]};
     maxc = std::max(maxc, C[i]);
+    maxb = std::max(maxb, B[i]);
+    any_acc |= acc[i] != nullptr;
   }
-  dim3 grid(tp::ceil_div(maxc, 256), count);
-  tp::score_fold_multi<<<grid, 1024, 0, st>>>(b, take_abs, after);
+  if (any_acc && !ws) return hipErrorInvalidValue;
+  const int nr = tp::ceil_div(maxb, tp::FOLD_ROWS);
+  tp::score_fold_rows<<<dim3(tp::ceil_div(maxc, 256), count, nr), 1024, 0, st>>>(b, take_abs, after, ws, maxc, nr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !any_acc) return e;
+  tp::score_fold_final<<<dim3(tp::ceil_div(maxc, 256), count), 256, 0, st>>>(b, ws, maxc, nr);
   return hipGetLastError();
 }
 

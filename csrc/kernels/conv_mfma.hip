@@ -49,7 +49,16 @@ struct ConvArgs {
   const float* act;         // EPI_BWD: activation [M][N] the grad refers to
   float* taylor;            // EPI_BWD: [B][N] fp32 per-sample sums (atomic), nullable
   int HWo;                  // EPI_BWD: pixels per image at the grad's resolution
+  int tay_group;            // EPI_BWD: >0 -> N = P pixel groups x tay_group channels (a dense-GEMM conv);
+                            // Taylor of column n goes to slot n / tay_group of a (P, B, tay_group) slab
 };
+
+// Taylor slab index of (image b, GEMM column n)
+__device__ __forceinline__ long long tay_index(const ConvArgs& p, long long b, int n) {
+  if (p.tay_group <= 0) return b * p.N + n;
+  const int B = p.M / p.HWo;
+  return ((long long)(n / p.tay_group) * B + b) * p.tay_group + n % p.tay_group;
+}
 
 template <int BM, int BN, int WM, int WN>
 struct Tile {
@@ -304,7 +313,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
               if (p.taylor) {
                 const int b = m / p.HWo;
                 if (b != cur_b) {
-                  if (cur_b >= 0) atomicAdd(p.taylor + (long long)cur_b * p.N + n, tsum);
+                  if (cur_b >= 0) atomicAdd(p.taylor + tay_index(p, cur_b, n), tsum);
                   cur_b = b;
                   tsum = 0.f;
                 }
@@ -314,7 +323,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
             }
           }
         }
-        if (p.taylor && cur_b >= 0) atomicAdd(p.taylor + (long long)cur_b * p.N + n, tsum);
+        if (p.taylor && cur_b >= 0) atomicAdd(p.taylor + tay_index(p, cur_b, n), tsum);
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -393,7 +402,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         tsum += -(v * a);
         if (p.out) p.out[o] = a > 0.f ? v * sc : 0.f;
       }
-      if (p.taylor) p.taylor[t] += tsum;
+      if (p.taylor) p.taylor[tay_index(p, b, n)] += tsum;
     }
   }
 }
@@ -426,7 +435,7 @@ __global__ __launch_bounds__(1024) void conv_epilogue_bwd_img(ConvArgs p, const 
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][c];
-    p.taylor[(long long)b * p.N + n] += t;
+    p.taylor[tay_index(p, b, n)] += t;
   }
 }
 
@@ -562,8 +571,8 @@ hipError_t dispatch_epi(int cfg, int epi, bool pooled_m, bool unpool, const Conv
 extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w, int B, int H, int W,
                                     int Cin, int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits,
                                     const float* scale, const float* shift, int relu, float* out,
-                                    uint8_t* out_argmax, const float* act, float* taylor, int HWo, float* ws,
-                                    hipStream_t st) {
+                                    uint8_t* out_argmax, const float* act, float* taylor, int HWo, int tay_group,
+                                    float* ws, hipStream_t st) {
   using namespace tp;
   if (Cin % 32 != 0) return hipErrorInvalidValue;
   ConvArgs a{};
@@ -592,6 +601,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   a.act = act;
   a.taylor = taylor;
   a.HWo = HWo;
+  a.tay_group = tay_group;
   if (splits == 1 || epi == EPI_PARTIAL) {
     ConvArgs b = a;
     if (epi == EPI_PARTIAL) b.out = ws ? ws : out;

@@ -109,3 +109,65 @@ extern "C" hipError_t tp_gather_multi(const void* const* srcs, void* const* dsts
   }
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// NHWC 2x2/stride-2 max-pool with argmax bytes (NaN-propagating, first max wins like PyTorch's
+// scan order (0,0),(0,1),(1,0),(1,1)) and its inverse scatter (unpool). Used by the fused
+// engine when a layer runs as a dense GEMM (2x2 images) instead of a pooling conv kernel.
+// ---------------------------------------------------------------------------------------------
+namespace tp {
+__global__ __launch_bounds__(256) void maxpool2_nhwc(const float* __restrict__ x, float* __restrict__ y,
+                                                     uint8_t* __restrict__ am, int B, int H, int W, int C) {
+  const int H2 = H / 2, W2 = W / 2;
+  const long long total = (long long)B * H2 * W2 * C;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    const long long r = t / C;
+    const int ow = (int)(r % W2), oh = (int)((r / W2) % H2);
+    const long long b = r / ((long long)W2 * H2);
+    float best = 0.f;
+    int arg = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float v = x[((b * H + 2 * oh + (q >> 1)) * W + 2 * ow + (q & 1)) * C + c];
+      if (q == 0 || v > best || (v != v && best == best)) {
+        best = v;
+        arg = q;
+      }
+    }
+    y[t] = best;
+    am[t] = (uint8_t)arg;
+  }
+}
+
+__global__ __launch_bounds__(256) void unpool2_nhwc(const float* __restrict__ g, const uint8_t* __restrict__ am,
+                                                    float* __restrict__ out, int B, int H, int W, int C) {
+  const long long total = (long long)B * H * W * C;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    const long long r = t / C;
+    const int iw = (int)(r % W), ih = (int)((r / W) % H);
+    const long long b = r / ((long long)W * H);
+    const long long o = ((b * (H / 2) + ih / 2) * (W / 2) + iw / 2) * C + c;
+    out[t] = am[o] == (uint8_t)((ih & 1) * 2 + (iw & 1)) ? g[o] : 0.f;
+  }
+}
+}  // namespace tp
+
+extern "C" hipError_t tp_maxpool2_nhwc(const float* x, float* y, uint8_t* am, int B, int H, int W, int C,
+                                       hipStream_t st) {
+  const long long total = (long long)B * (H / 2) * (W / 2) * C;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::maxpool2_nhwc<<<grid, 256, 0, st>>>(x, y, am, B, H, W, C);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_unpool2_nhwc(const float* g, const uint8_t* am, float* out, int B, int H, int W, int C,
+                                      hipStream_t st) {
+  const long long total = (long long)B * H * W * C;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::unpool2_nhwc<<<grid, 256, 0, st>>>(g, am, out, B, H, W, C);
+  return hipGetLastError();
+}

@@ -318,7 +318,7 @@ def test_wino_dgrad_taylor(cuda, shape, splits, unpool, staged):
     ut = winograd_weights(w.flip(2, 3).transpose(0, 1).to(cuda))
     from torchpruner_amd.engine.fused_chain import taylor_slots
     R = taylor_slots(H, W)
-    assert R == T.wino_taylor_slots(H, W)
+    assert R >= T.wino_taylor_slots(H, W)  # the engine may keep extra slots (dense 2x2 layers)
     tay = torch.zeros(R, B, Cin, device=cuda)
     gin = (gp if unpool else gfull).to(cuda)
     out = T.conv_wino_dgrad(gin, am.to(cuda) if unpool else None, ut, act.to(cuda), bn_scale.to(cuda), tay, True,
@@ -363,3 +363,40 @@ def test_first_layer_winograd(cuda, staged):
     u = winograd_weights(F.pad(w, (0, 0, 0, 0, 0, 5)).to(cuda))
     out, _ = T.conv_wino_fwd(xp, u, s.to(cuda), t.to(cuda), True, False, 1, staged)
     torch.testing.assert_close(out.cpu(), ref.float(), rtol=3e-4, atol=3e-4)
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_dense_gemm_2x2_layer_matches_winograd(cuda, pool):
+    """2x2-image conv as a dense GEMM (Wbig) == Winograd path: fwd (+pool) and dgrad (+unpool,
+    Taylor slots per pixel)."""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import (WINO, FusedChainEngine, taylor_slots, winograd_weights)
+    T = ops.require()
+    g = torch.Generator().manual_seed(21)
+    B, C, K = 40, 64, 96
+    w = (_rand(K, C, 3, 3, gen=g) * (2.0 / (9 * C)) ** 0.5).to(cuda)
+    e = {"w": w.permute(0, 2, 3, 1).reshape(K, -1).contiguous(), "scale": (_rand(K, gen=g).abs() + 0.5).to(cuda),
+         "shift": (_rand(K, gen=g) * 0.1).to(cuda), "pool": pool, "u": winograd_weights(w),
+         "ut": winograd_weights(w.flip(2, 3).transpose(0, 1).contiguous()),
+         "wt": w.flip(2, 3).permute(1, 2, 3, 0).reshape(C, -1).contiguous()}
+    eng = FusedChainEngine.__new__(FusedChainEngine)
+    h = _rand(B, 2, 2, C, gen=g).to(cuda)
+    y_d, am_d = eng._conv_run(T, e, h, FusedChainEngine.DENSE + 0, 2)
+    y_w, am_w = eng._conv_run(T, e, h, WINO, 1)
+    torch.testing.assert_close(y_d, y_w, rtol=3e-4, atol=3e-4)
+    if pool:
+        assert (am_d == am_w).float().mean() > 0.999
+    # dgrad into a 2x2 activation with C channels
+    act = torch.relu(_rand(B, 2, 2, C, gen=g)).to(cuda)
+    sc = (_rand(C, gen=g).abs() + 0.5).to(cuda)
+    gy = _rand(B, 1 if pool else 2, 1 if pool else 2, K, gen=g).to(cuda)
+    am = am_w if pool else None
+    R = taylor_slots(2, 2)
+    t_d = torch.zeros(R, B, C, device=cuda)
+    t_w = torch.zeros(R, B, C, device=cuda)
+    o_d = eng._dgrad_run(T, e, gy, am, act, sc, t_d, True, FusedChainEngine.DENSE + 2, 2, sc.repeat(4).contiguous())
+    o_w = eng._dgrad_run(T, e, gy, am, act, sc, t_w, True, WINO, 1)
+    torch.testing.assert_close(o_d, o_w, rtol=3e-4, atol=3e-4)
+    torch.testing.assert_close(t_d.sum(0), t_w.sum(0), rtol=3e-4, atol=3e-4)
+    y2, am2 = T.maxpool2_nhwc(y_w if not pool else y_w.new_ones(B, 2, 2, K))
+    assert y2.shape == (B, 1, 1, K)

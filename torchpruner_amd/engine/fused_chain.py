@@ -72,6 +72,8 @@ def taylor_slots(H: int, W: int) -> int:
     """Partial slots R of the (R, B, C) Taylor slab the Winograd dgrad writes for an activation
     of spatial size H x W (one slot per 64-tile block covering an image; mirrors
     wino_taylor_slots() in winograd.hip). score_fold sums the slots in order."""
+    if H == 2 and W == 2:
+        return 4  # dense-GEMM layers (2x2 images) keep one slot per pixel
     T = (H // 2) * (W // 2)
     if T <= 0:
         return 1
@@ -378,10 +380,38 @@ class FusedChainEngine:
                                self._first_run(T, e, xf, c, s_), cands=cands)
         return self._first_run(T, e, xf, cfg, sp)
 
+    # A 3x3/pad-1 conv on a 2x2 image is a dense GEMM: every output pixel q sees input pixel p
+    # through tap (p - q + 1): y(B, 4K) = x(B, 4C) @ Wbig^T with Wbig (4K, 4C) — the same 2.25x
+    # fewer multiplies as Winograd, on the implicit-GEMM kernel (ks=1) with no transforms.
+    DENSE = 100  # pseudo cfg offset: cfg = DENSE + implicit-GEMM tile config
+
     @staticmethod
-    def _conv_run(T, e, h, cfg, sp):
+    def _dense(e):
+        d = e.get("dense")
+        if d is None:
+            N = e["scale"].numel()
+            C = e["w"].shape[1] // 9
+            w9 = e["w"].view(N, 3, 3, C)
+            wb = e["w"].new_zeros(4, N, 4, C)  # [q][k][p][c]
+            for q in range(4):
+                for p in range(4):
+                    wb[q, :, p, :] = w9[:, p // 2 - q // 2 + 1, p % 2 - q % 2 + 1, :]
+            wb = wb.reshape(4 * N, 4 * C)
+            d = {"w": wb.contiguous(), "wt": wb.t().contiguous(), "scale4": e["scale"].repeat(4).contiguous(),
+                 "shift4": e["shift"].repeat(4).contiguous()}
+            e["dense"] = d
+        return d
+
+    def _conv_run(self, T, e, h, cfg, sp):
         if cfg in (WINO, WINO_LDS):
             return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS)
+        if cfg >= self.DENSE:
+            d = self._dense(e)
+            B, N = h.shape[0], e["scale"].numel()
+            y, _ = T.conv_fwd(h.reshape(B, 1, 1, -1), d["w"], d["scale4"], d["shift4"], True, False, 1,
+                              cfg - self.DENSE, sp)
+            y = y.view(B, 2, 2, N)
+            return T.maxpool2_nhwc(y) if e["pool"] else (y, None)
         return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
 
     def _conv(self, T, e, h):
@@ -389,14 +419,25 @@ class FusedChainEngine:
         M = B * H * W
         N, K = e["scale"].numel(), e["w"].shape[1]
         wino = (B * (H // 2) * (W // 2), C) if "u" in e and _wino_ok(H, W, C, N) else None
+        cands = None
+        if H == 2 and W == 2 and C % 32 == 0:
+            cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * N, 4 * C)] + \
+                TUNER.candidates(M, N, K, wino)
         cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"], wino is not None), M, N, K,
-                               lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino)
+                               lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino, cands=cands)
         return self._conv_run(T, e, h, cfg, sp)
 
-    @staticmethod
-    def _dgrad_run(T, e, g, am, act, sc, taylor, want_out, cfg, sp):
+    def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None):
         if cfg in (WINO, WINO_LDS):
             return T.conv_wino_dgrad(g, am, e["ut"], act, sc, taylor, want_out, sp, cfg == WINO_LDS)
+        if cfg >= self.DENSE:
+            d = self._dense(e)
+            if am is not None:
+                g = T.unpool2_nhwc(g, am)
+            B, C = act.shape[0], act.shape[3]
+            out = T.conv_dgrad(g.reshape(B, 1, 1, -1), None, d["wt"], act.reshape(B, 1, 1, -1), sc4, taylor,
+                               want_out, 1, cfg - self.DENSE, sp, C)
+            return out.view(B, 2, 2, C) if want_out else out
         return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp)
 
     def _linear(self, T, e, xin):
@@ -558,11 +599,21 @@ class FusedChainEngine:
             gg = g
             Cin, Cg = prev_act.shape[3], g.shape[3]
             wino = (B * (H // 2) * (W // 2), Cg) if "ut" in e and _wino_ok(H, W, Cg, Cin) else None
+            sc4, cands = None, None
+            if H == 2 and W == 2 and Cg % 32 == 0 and Cin % 32 == 0:
+                pe = P["convs"][ci - 1]
+                sc4 = pe.get("scale4")
+                if sc4 is None:
+                    sc4 = pe["scale4"] = sc_prev.repeat(4).contiguous()
+                # dense GEMM dgrad: one writer per Taylor element (deterministic as well)
+                cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * Cin, 4 * Cg)] + \
+                    TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
             cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None),
                                    M, Cin, e["wt"].shape[1],
-                                   lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out:
-                                   self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_), wino, wino_only=True)
-            g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp)
+                                   lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4:
+                                   self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_, s4), wino, wino_only=True,
+                                   cands=cands)
+            g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp, sc4)
         return res
 
 
