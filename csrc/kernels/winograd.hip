@@ -42,6 +42,19 @@ __device__ f32x2 buf_load_f32x2(i32x4 rsrc, int voffset, int soffset, int aux) _
 __device__ unsigned short buf_load_u16(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i16");
 
 enum WEpi : int { W_FWD = 0, W_FWD_POOL = 1, W_BWD = 2, W_PARTIAL = 3 };
+
+// Division by a runtime-invariant divisor as mul-hi + add + shift (Granlund-Montgomery; valid
+// for 0 <= n < 2^31): the tile -> (image, row, col) decode is otherwise ~25 VALU per division.
+struct FastDiv {
+  unsigned d = 1, m = 1, l = 0;
+  FastDiv() = default;
+  explicit FastDiv(unsigned dv) : d(dv) {
+    l = 0;
+    while ((1ull << l) < dv) ++l;
+    m = (unsigned)(((1ull << 32) * ((1ull << l) - dv)) / dv + 1);
+  }
+  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> l); }
+};
 enum XMode : int { X_DIRECT = 0, X_UNPOOL = 1, X_STAGED = 2, X_STAGED_UNPOOL = 3 };
 
 constexpr int W_TK = 32;             // output channels per block
@@ -71,6 +84,7 @@ struct WinoArgs {
   // X_STAGED_UNPOOL: pooled region pitches; argmax image rounds and its byte offset
   int arounds, aoff;
   int tay_slots;            // W_BWD: partial slots R of the (R, B, K) taylor slab
+  FastDiv fd_timg, fd_w2, fd_ip, fd_rw;  // T_img = (H/2)(W/2), W/2, IP, RW
   int dbg;                  // experiment switches (TP_WINO_DBG): 1 no epilogue, 2 no restaging, 4 no transform
 };
 
@@ -235,8 +249,8 @@ phase2:
       tq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (pt >= p.P || k >= p.K) continue;
       const float4 y = *reinterpret_cast<const float4*>(ybr + ybuf_row(tl, q) * 16);
-      const int bb = pt / T_img, rr = pt - bb * T_img;
-      const int oh2 = rr / W2, ow2 = rr - oh2 * W2;
+      const int bb = p.fd_timg.div(pt), rr = pt - bb * T_img;
+      const int oh2 = p.fd_w2.div(rr), ow2 = rr - oh2 * W2;
       const int oh = 2 * oh2 + (q >> 1), ow = 2 * ow2 + (q & 1);
       const long long pix = ((long long)bb * p.H + oh) * p.W + ow;
       if constexpr (EPI == W_FWD) {
@@ -295,9 +309,9 @@ phase2:
         }
       }
       __syncthreads();
-      const int b_first = t0 / T_img;
+      const int b_first = p.fd_timg.div(t0);
       const int t_last = min(t0 + 64, p.P) - 1;
-      const int n_img = t_last / T_img - b_first + 1;
+      const int n_img = p.fd_timg.div(t_last) - b_first + 1;
       for (int t = tid; t < n_img * W_TK; t += blockDim.x) {
         const int bb = b_first + t / W_TK, kk = t % W_TK, kc = k0 + kk;
         if (bb >= p.B || kc >= p.K) continue;
@@ -346,9 +360,9 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   int b = 0, th = 0, tw = 0;
   const bool tok = pin < p.P;
   if (tok) {
-    b = pin / T_img;
+    b = p.fd_timg.div(pin);
     const int r = pin - b * T_img;
-    th = r / W2;
+    th = p.fd_w2.div(r);
     tw = r - th * W2;
   }
 
@@ -382,8 +396,8 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   } else if constexpr (XMODE == X_STAGED) {
     // block region: images b0 .. b0+n_img-1, input rows 2*th0-1 .. 2*th0+2R, cols -1 .. W
     const int t0 = blk_p * 64;
-    const int b0 = t0 / T_img;
-    const int th0 = (t0 - b0 * T_img) / W2;
+    const int b0 = p.fd_timg.div(t0);
+    const int th0 = p.fd_w2.div(t0 - b0 * T_img);
     const int RH = 2 * p.R + 2, RWc = p.W + 2;
     // lane's patch in region coordinates (clamped for tail lanes: results are discarded)
     const int im = tok ? b - b0 : 0, rr0 = tok ? 2 * (th - th0) : 0, cc0 = tok ? 2 * tw : 0;
@@ -400,8 +414,8 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       const int s = i * 256 + tid;
       const int L = xswz(s);
       const int pix = L >> 1, h = L & 1;
-      const int imr = pix / p.IP, rem = pix - imr * p.IP;
-      const int rr = rem / p.RW, cc = rem - rr * p.RW;
+      const int imr = p.fd_ip.div(pix), rem = pix - imr * p.IP;
+      const int rr = p.fd_rw.div(rem), cc = rem - rr * p.RW;
       const int bb = b0 + imr, ih = 2 * th0 - 1 + rr, iw = cc - 1;
       const bool ok = i < p.rounds && imr < p.n_img && rr < RH && cc < RWc && bb < p.B && ih >= 0 &&
                       ih < p.H && iw >= 0 && iw < p.W;
@@ -409,8 +423,8 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
     }
   } else {  // X_STAGED_UNPOOL: pooled rows th0-1 .. th0+R, pooled cols -1 .. W2
     const int t0 = blk_p * 64;
-    const int b0 = t0 / T_img;
-    const int th0 = (t0 - b0 * T_img) / W2;
+    const int b0 = p.fd_timg.div(t0);
+    const int th0 = p.fd_w2.div(t0 - b0 * T_img);
     const int PRH = p.R + 2, PRWc = W2 + 2;
     const int im = tok ? b - b0 : 0, pr0 = tok ? th - th0 : 0, pc0 = tok ? tw : 0;
     const int cell0 = im * p.IP + pr0 * p.RW + pc0;
@@ -429,8 +443,8 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       const int s = val ? i * 256 + tid : (i - p.rounds) * 256 + tid;
       const int L = val ? xswz(s) : s;
       const int cell = L >> 1, h = L & 1;
-      const int imr = cell / p.IP, rem = cell - imr * p.IP;
-      const int pr = rem / p.RW, pc = rem - pr * p.RW;
+      const int imr = p.fd_ip.div(cell), rem = cell - imr * p.IP;
+      const int pr = p.fd_rw.div(rem), pc = rem - pr * p.RW;
       const int bb = b0 + imr, ph = th0 - 1 + pr, pw = pc - 1;
       const bool ok = i < p.rounds + p.arounds && imr < p.n_img && pr < PRH && pc < PRWc && bb < p.B &&
                       ph >= 0 && ph < H2 && pw >= 0 && pw < W2;
@@ -509,8 +523,9 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       const int pt = t0 + tl;
       unsigned off = 0x80000000u;
       if (pt < p.P && k0 + 4 * c4 < p.K) {
-        const int bb = pt / T_img, rr = pt - bb * T_img;
-        const int oh = 2 * (rr / W2) + (q >> 1), ow = 2 * (rr % W2) + (q & 1);
+        const int bb = p.fd_timg.div(pt), rr = pt - bb * T_img;
+        const int r2 = p.fd_w2.div(rr);
+        const int oh = 2 * r2 + (q >> 1), ow = 2 * (rr - r2 * W2) + (q & 1);
         off = (unsigned)(((((long long)bb * p.H + oh) * p.W + ow) * p.K + k0 + 4 * c4) * 4);
       }
       act_src[i] = off;
@@ -772,6 +787,8 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.act = act;
   a.taylor = taylor;
   a.tay_slots = wino_taylor_slots(H, W);
+  a.fd_timg = FastDiv((unsigned)std::max(1, (H / 2) * (W / 2)));
+  a.fd_w2 = FastDiv((unsigned)std::max(1, W / 2));
   if (const char* d = getenv("TP_WINO_DBG")) a.dbg = atoi(d);
   int xmode = unpool ? X_UNPOOL : X_DIRECT;
   if (staged) {
@@ -785,6 +802,8 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
       a.rounds = gm.rounds;
       a.arounds = gm.arounds;
       a.aoff = gm.aoff;
+      a.fd_ip = FastDiv((unsigned)gm.IP);
+      a.fd_rw = FastDiv((unsigned)gm.RW);
     }
   }
   const int n_p = (a.P + 63) / 64, n_k = K / 32;
