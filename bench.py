@@ -54,9 +54,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--train-steps", type=int, default=int(os.environ.get("BENCH_TRAIN_STEPS", 300)),
                     help="untimed SGD steps on the synthetic task before scoring (0 = random init)")
-    ap.add_argument("--task-noise", type=float, default=4.0,
-                    help="per-pixel noise of the synthetic prototype task (4.0: the teacher is not saturated, "
-                         "so loss gradients are informative; see profiles/taylor_quality_sweep.txt)")
+    ap.add_argument("--task-noise", type=float, default=2.0, help="per-pixel noise of the synthetic prototype task")
+    ap.add_argument("--task-modes", type=int, default=8,
+                    help="prototypes per class: a mixture task that needs VGG16's capacity, so pruning half of "
+                         "a layer costs accuracy and scoring methods separate (profiles/taylor_quality_sweep.txt)")
     return ap.parse_args()
 
 
@@ -141,7 +142,8 @@ def main():
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
     model = prunable_vgg16().to(dev)
-    task = PrototypeTask((3, 32, 32), 10, noise=args.task_noise, seed=args.seed, device=dev)
+    task = PrototypeTask((3, 32, 32), 10, noise=args.task_noise, seed=args.seed, device=dev,
+                         modes_per_class=args.task_modes)
     t0 = time.perf_counter()
     train_teacher(model, task, args.train_steps, dev, args.seed)
     log(f"[bench] teacher: {args.train_steps} SGD steps in {time.perf_counter() - t0:.1f}s (untimed)")
@@ -173,7 +175,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (CIFAR-10-shaped prototype task; random-init VGG16-BN briefly trained, untimed)",
+        "data": "synthetic (CIFAR-10-shaped prototype-mixture task, 8 modes/class; random-init VGG16-BN "
+                "briefly trained, untimed)",
         "config": {
             "model": "VGG16-BN (CIFAR-10, reference classifier)",
             "global_batch": B * world,

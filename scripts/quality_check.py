@@ -19,16 +19,17 @@ from torchpruner_amd.parallel import dist as pdist  # noqa: E402
 steps = int(os.environ.get("TEACHER_STEPS", "150"))
 noise = float(os.environ.get("NOISE", "2.0"))
 tseed = int(os.environ.get("TSEED", "0"))
+modes = int(os.environ.get("MODES", "1"))
 pdist.init_distributed()
 dev = torch.device("cuda")
 torch.manual_seed(tseed)
 model = prunable_vgg16().to(dev)
-task = PrototypeTask((3, 32, 32), 10, noise=noise, seed=tseed, device=dev)
+task = PrototypeTask((3, 32, 32), 10, noise=noise, seed=tseed, device=dev, modes_per_class=modes)
 bench.train_teacher(model, task, steps, dev, tseed)
 convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
 xt, yt = task.sample(10 * 512, 2)
 xv, yv = task.sample(2000, 3)
-print(f"noise {noise} tseed {tseed} steps {steps}: top1 before", bench.top1(model, xv, yv), "train-set top1", bench.top1(model, xt[:2000], yt[:2000]))
+print(f"noise {noise} modes {modes} tseed {tseed} steps {steps}: top1 before", bench.top1(model, xv, yv), "train-set top1", bench.top1(model, xt[:2000], yt[:2000]))
 
 
 def scores(tag):

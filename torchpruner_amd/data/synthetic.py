@@ -140,23 +140,29 @@ class PrototypeTask:
     any dataset download (random-init networks predict one class for every input).
     """
 
-    def __init__(self, shape=(3, 32, 32), num_classes=10, noise=1.0, seed=0, device="cpu", low_res=8):
+    def __init__(self, shape=(3, 32, 32), num_classes=10, noise=1.0, seed=0, device="cpu", low_res=8,
+                 modes_per_class=1):
         g = torch.Generator(device="cpu").manual_seed(seed)
         c, h, w = shape
-        low = torch.randn(num_classes, c, low_res, low_res, generator=g)
+        n_proto = num_classes * modes_per_class
+        low = torch.randn(n_proto, c, low_res, low_res, generator=g)
         protos = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=False)
         protos = (protos - protos.mean((1, 2, 3), keepdim=True)) / protos.std((1, 2, 3), keepdim=True)
         self.protos = protos.to(device)
         self.noise = noise
         self.num_classes = num_classes
+        self.modes_per_class = modes_per_class
         self.shape = tuple(shape)
         self.device = torch.device(device)
 
     def sample(self, n: int, seed: int):
+        """``modes_per_class`` > 1 makes every class a mixture of several prototypes (a task that
+        needs more of the network's capacity, so pruning a layer actually costs accuracy)."""
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
-        y = torch.randint(0, self.num_classes, (n,), generator=g, device=self.device)
-        x = self.protos[y] + self.noise * torch.randn((n,) + self.shape, generator=g, device=self.device)
+        idx = torch.randint(0, self.num_classes * self.modes_per_class, (n,), generator=g, device=self.device)
+        y = idx // self.modes_per_class
+        x = self.protos[idx] + self.noise * torch.randn((n,) + self.shape, generator=g, device=self.device)
         return x, y
 
     def loader(self, n: int, batch_size: int, seed: int) -> "DeviceLoader":
