@@ -12,6 +12,13 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
                          int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
                          float* taylor, int HWo, int tay_group, float* ws, hipStream_t st);
+int tp_conv_gen_k(int ks, int Cin);
+hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                       int pad, int cfg, int splits, const float* scale, const float* shift, int relu,
+                       const float* res, float* apoz, float* out, float* ws, hipStream_t st);
+hipError_t tp_maxpool_nhwc(const float* x, float* y, int B, int H, int W, int C, int k, int s, int pad,
+                           hipStream_t st);
+hipError_t tp_avgpool_nhwc(const float* x, float* y, int B, int HW, int C, hipStream_t st);
 hipError_t tp_maxpool2_nhwc(const float* x, float* y, uint8_t* am, int B, int H, int W, int C, hipStream_t st);
 hipError_t tp_unpool2_nhwc(const float* g, const uint8_t* am, float* out, int B, int H, int W, int C, hipStream_t st);
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
@@ -20,7 +27,8 @@ int tp_wino_taylor_slots(int H, int W);
 hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C, int H, int W, int Cp, hipStream_t st);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
-                        float* out, uint8_t* out_argmax, const float* act, float* taylor, float* ws, hipStream_t st);
+                        float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
+                        hipStream_t st);
 }
 
 namespace {
@@ -175,7 +183,7 @@ void need_u(const at::Tensor& u, int64_t C, int64_t K) {
 std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::Tensor& u,
                                                  const c10::optional<at::Tensor>& scale,
                                                  const c10::optional<at::Tensor>& shift, bool relu, bool pool,
-                                                 int64_t splits, bool staged) {
+                                                 int64_t splits, bool staged, const c10::optional<at::Tensor>& apoz) {
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
   need_u(u, C, K);
@@ -194,10 +202,17 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
   const int64_t sp = wino_splits(splits, C);
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * H * W * K}, x.options());
+  float* ap = nullptr;
+  if (apoz.has_value() && apoz->defined()) {
+    TORCH_CHECK(!pool, "apoz counts are supported without pooling");
+    TORCH_CHECK(apoz->is_cuda() && apoz->scalar_type() == at::kFloat && apoz->is_contiguous() &&
+                    apoz->numel() == B * K, "apoz must be a contiguous float32 (B, K) tensor");
+    ap = apoz->data_ptr<float>();
+  }
   TP_CHECK_HIP(tp_conv_wino(x.data_ptr<float>(), nullptr, u.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)K,
                             0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, staged ? 1 : 0, sc, sh, relu ? 1 : 0,
                             out.data_ptr<float>(),
-                            pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr,
+                            pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap,
                             sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
   return {out, am};
 }
@@ -241,13 +256,83 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
   TP_CHECK_HIP(tp_conv_wino(g.data_ptr<float>(), unpool ? g_argmax->data_ptr<uint8_t>() : nullptr,
                             ut.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, unpool ? 1 : 0, EPI_BWD,
                             (int)sp, staged ? 1 : 0, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
-                            act.data_ptr<float>(), tay, sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                            act.data_ptr<float>(), tay, nullptr, sp > 1 ? ws.data_ptr<float>() : nullptr,
+                            cur_stream()));
   return out;
 }
 
 }  // namespace
 
 int64_t wino_taylor_slots(int64_t H, int64_t W) { return tp_wino_taylor_slots((int)H, (int)W); }
+
+// General strided conv forward (ResNet): x NHWC (B,H,W,Cin) with Cin % 32 == 0 (ks 1 or 3) or
+// Cin == 4 (ks 7, padded stem input); w (Cout, K) with K = conv_gen_k(ks, Cin), k = (kh,kw,ci).
+// Epilogue: out = relu?(acc*scale + shift + res); apoz (B, Cout) += count(out > 0).
+at::Tensor conv_gen(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& scale,
+                    const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& res,
+                    const c10::optional<at::Tensor>& apoz, int64_t ks, int64_t stride, int64_t pad, int64_t cfg,
+                    int64_t splits) {
+  need(x, "x", 4);
+  need(w, "w", 2);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
+  TORCH_CHECK((Cin % 32 == 0 && (ks == 1 || ks == 3)) || (Cin == 4 && ks == 7),
+              "conv_gen supports ks 1/3 with Cin % 32 == 0, or ks 7 with a 4-channel input");
+  TORCH_CHECK(w.size(1) == tp_conv_gen_k((int)ks, (int)Cin), "weight K mismatch");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
+  const int64_t Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const float* sc = opt_ptr(scale, Cout, "scale");
+  const float* sh = opt_ptr(shift, Cout, "shift");
+  const float* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    need(*res, "res", 4);
+    TORCH_CHECK(res->size(0) == B && res->size(1) == Ho && res->size(2) == Wo && res->size(3) == Cout,
+                "res must be (B, Ho, Wo, Cout)");
+    rp = res->data_ptr<float>();
+  }
+  float* ap = nullptr;
+  if (apoz.has_value() && apoz->defined()) {
+    TORCH_CHECK(apoz->is_cuda() && apoz->scalar_type() == at::kFloat && apoz->is_contiguous() &&
+                    apoz->numel() == B * Cout, "apoz must be a contiguous float32 (B, Cout) tensor");
+    ap = apoz->data_ptr<float>();
+  }
+  auto out = at::empty({B, Ho, Wo, Cout}, x.options());
+  const int64_t K = w.size(1), kt = K / 32;
+  int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, kt));
+  const int64_t per = (kt + sp - 1) / sp;
+  sp = (kt + per - 1) / per;
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * Ho * Wo * Cout}, x.options());
+  TP_CHECK_HIP(tp_conv_gen(x.data_ptr<float>(), w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin, (int)Cout,
+                           (int)ks, (int)stride, (int)pad, (int)cfg, (int)sp, sc, sh, relu ? 1 : 0, rp, ap,
+                           out.data_ptr<float>(), sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+  return out;
+}
+
+int64_t conv_gen_k(int64_t ks, int64_t Cin) { return tp_conv_gen_k((int)ks, (int)Cin); }
+
+// NHWC k x k / stride s / padding p max-pool (NaN-propagating, padded taps skipped)
+at::Tensor maxpool_nhwc(const at::Tensor& x, int64_t k, int64_t s, int64_t pad) {
+  need(x, "x", 4);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 4 == 0, "maxpool_nhwc needs C % 4 == 0");
+  const int64_t Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({B, Ho, Wo, C}, x.options());
+  TP_CHECK_HIP(tp_maxpool_nhwc(x.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)k,
+                               (int)s, (int)pad, cur_stream()));
+  return y;
+}
+
+// NHWC global average pool -> (B, C)
+at::Tensor avgpool_nhwc(const at::Tensor& x) {
+  need(x, "x", 4);
+  const int64_t B = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({B, C}, x.options());
+  TP_CHECK_HIP(tp_avgpool_nhwc(x.data_ptr<float>(), y.data_ptr<float>(), (int)B, (int)HW, (int)C, cur_stream()));
+  return y;
+}
 
 // NHWC 2x2/stride-2 max-pool (NaN-propagating) -> (pooled, argmax bytes)
 std::tuple<at::Tensor, at::Tensor> maxpool2_nhwc(const at::Tensor& x) {
@@ -290,6 +375,11 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
   m.def("maxpool2_nhwc(Tensor x) -> (Tensor, Tensor)");
+  m.def("maxpool_nhwc(Tensor x, int k, int s, int pad) -> Tensor");
+  m.def("avgpool_nhwc(Tensor x) -> Tensor");
+  m.def("conv_gen(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, Tensor? res, Tensor(a!)? apoz, "
+        "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
+  m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits) -> (Tensor, Tensor)");
@@ -297,7 +387,7 @@ void register_engine_ops_def(torch::Library& m) {
         "bool want_out, int ks, int cfg, int splits, int tay_group=0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
-        "bool staged=True) -> (Tensor, Tensor)");
+        "bool staged=True, Tensor(a!)? apoz=None) -> (Tensor, Tensor)");
   m.def("conv_wino_dgrad(Tensor g, Tensor? g_argmax, Tensor ut, Tensor act, Tensor? bn_scale, "
         "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True) -> Tensor");
 }
@@ -309,6 +399,9 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_wino_fwd", &conv_wino_fwd);
   m.impl("nchw_to_nhwc_pad", &nchw_to_nhwc_pad);
   m.impl("maxpool2_nhwc", &maxpool2_nhwc);
+  m.impl("maxpool_nhwc", &maxpool_nhwc);
+  m.impl("avgpool_nhwc", &avgpool_nhwc);
+  m.impl("conv_gen", &conv_gen);
   m.impl("unpool2_nhwc", &unpool2_nhwc);
   m.impl("conv_wino_dgrad", &conv_wino_dgrad);
 }

@@ -48,7 +48,11 @@ struct ConvArgs {
   uint8_t* out_argmax;      // POOL: [M/4][N]
   const float* act;         // EPI_BWD: activation [M][N] the grad refers to
   float* taylor;            // EPI_BWD: [B][N] fp32 per-sample sums (atomic), nullable
-  int HWo;                  // EPI_BWD: pixels per image at the grad's resolution
+  int HWo;                  // EPI_BWD/EPI_FWD apoz: pixels per image at the output's resolution
+  // GEN (general strided conv) geometry: output Ho x Wo, stride, zero padding
+  int Ho, Wo, stride, pad;
+  const float* res;         // EPI_FWD: residual [M][N] added before the ReLU (nullable)
+  float* apoz;              // EPI_FWD: [B][N] counts of positive outputs (exact integers), nullable
   int tay_group;            // EPI_BWD: >0 -> N = P pixel groups x tay_group channels (a dense-GEMM conv);
                             // Taylor of column n goes to slot n / tay_group of a (P, B, tay_group) slab
 };
@@ -98,7 +102,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI>
+// GEN = 0: stride-1 "same" convs (VGG path, precomputed tap masks); GEN = 1: general strided /
+// padded conv (ResNet), Cin % 32 == 0; GEN = 2: the same with a 4-channel (padded NHWC) input,
+// where one 32-wide K slice holds 8 taps x 4 channels (7x7 stems).
+template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI, int GEN = 0>
 __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, WM, WN) / 128) void conv_igemm(ConvArgs p) {
   using T = Tile<BM, BN, WM, WN>;
   constexpr int BK = T::BK, LDK = T::LDK;
@@ -136,6 +143,17 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     a_row[i] = id / (BK / 4);
     a_c4[i] = id % (BK / 4);
     const int m = m0 + a_row[i];
+    if constexpr (GEN != 0) {
+      // a_off = image base offset, a_oh/a_ow = top-left input pixel of the receptive field,
+      // a_mask = row valid
+      int b = 0, oh = 0, ow = 0;
+      if (m < p.M) pix_of(m, p.Ho, p.Wo, false, b, oh, ow);
+      a_mask[i] = m < p.M ? 1u : 0u;
+      a_oh[i] = oh * p.stride - p.pad;
+      a_ow[i] = ow * p.stride - p.pad;
+      a_off[i] = b * p.H * p.W * p.Cin;
+      continue;
+    }
     int b = 0, oh = 0, ow = 0;
     unsigned mask = 0;
     if (m < p.M) {
@@ -165,6 +183,24 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   float4 ra[T::A_CHUNKS], rb[T::B_CHUNKS];
 
   auto load_tile = [&](int kt) {
+    if constexpr (GEN != 0) {
+#pragma unroll
+      for (int i = 0; i < T::A_CHUNKS; ++i) {
+        int tap, c;
+        if constexpr (GEN == 2) {
+          tap = kt * 8 + a_c4[i];
+          c = 0;
+        } else {
+          tap = kt / cin_tiles;
+          c = (kt - tap * cin_tiles) * BK + a_c4[i] * 4;
+        }
+        const int ih = a_oh[i] + tap / KS, iw = a_ow[i] + tap % KS;
+        const bool ok = a_mask[i] && tap < KS * KS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const unsigned vo = ok ? (unsigned)(a_off[i] + (ih * p.W + iw) * p.Cin + c) * 4u : OOB;
+        const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
+        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+      }
+    } else {
     const int tap = kt / cin_tiles;
     const int c0 = (kt - tap * cin_tiles) * BK;
     const int dh = tap / KS - (KS - 1) / 2, dw = tap % KS - (KS - 1) / 2;
@@ -190,6 +226,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
         ra[i] = make_float4(g[0], g[1], g[2], g[3]);
       }
+    }
     }
 #pragma unroll
     for (int i = 0; i < T::B_CHUNKS; ++i) {
@@ -325,6 +362,8 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         }
         if (p.taylor && cur_b >= 0) atomicAdd(p.taylor + tay_index(p, cur_b, n), tsum);
       } else {
+        int cur_b = -1;
+        float cnt = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = mt + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -332,12 +371,25 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
             float v = acc[i][j][r];
             if constexpr (EPI == EPI_FWD) {
               v = v * sc + sh;
+              if (p.res) v += p.res[(long long)m * p.N + n];
               if (p.relu) v = nan_relu(v);
               p.out[(long long)m * p.N + n] = v;
+              if (p.apoz) {  // counts are exact integers: atomics are order-independent here
+                const int b = m / p.HWo;
+                if (b != cur_b) {
+                  if (cur_b >= 0 && cnt > 0.f) atomicAdd(p.apoz + (long long)cur_b * p.N + n, cnt);
+                  cur_b = b;
+                  cnt = 0.f;
+                }
+                cnt += v > 0.f ? 1.f : 0.f;
+              }
             } else {  // EPI_PARTIAL
               p.out[((long long)split * p.M + m) * p.N + n] = v;
             }
           }
+        }
+        if constexpr (EPI == EPI_FWD) {
+          if (p.apoz && cur_b >= 0 && cnt > 0.f) atomicAdd(p.apoz + (long long)cur_b * p.N + n, cnt);
         }
       }
     }
@@ -380,8 +432,10 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
       const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
       v = v * sc + sh;
+      if (p.res) v += p.res[o];
       if (p.relu) v = nan_relu(v);
       p.out[o] = v;
+      if (p.apoz && v > 0.f) atomicAdd(p.apoz + (o / p.N / p.HWo) * p.N + n, 1.f);
     }
   } else if (p.HWo > 64) {
     // EPI_BWD, large images: handled by conv_epilogue_bwd_img (block per image x 64 channels)
@@ -602,6 +656,10 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   a.taylor = taylor;
   a.HWo = HWo;
   a.tay_group = tay_group;
+  a.Ho = H;
+  a.Wo = W;
+  a.stride = 1;
+  a.pad = (ks - 1) / 2;
   if (splits == 1 || epi == EPI_PARTIAL) {
     ConvArgs b = a;
     if (epi == EPI_PARTIAL) b.out = ws ? ws : out;
@@ -631,7 +689,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
 extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
                                               const float* scale, const float* shift, int relu, float* out,
                                               uint8_t* out_argmax, const float* act, float* taylor,
-                                              hipStream_t st) {
+                                              float* apoz, hipStream_t st) {
   using namespace tp;
   ConvArgs a{};
   a.B = B;
@@ -646,6 +704,7 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
   a.out_argmax = out_argmax;
   a.act = act;
   a.taylor = taylor;
+  a.apoz = apoz;
   a.HWo = H * W;
   const long long MN = (long long)a.M * a.N;
   const long long work = epi == EPI_FWD_POOL ? MN / 4 : (epi == EPI_BWD && a.HWo <= 64 ? MN / a.HWo : MN);
@@ -701,5 +760,90 @@ extern "C" hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C
   const long long total = (long long)B * H * W * (Cp / 4);
   const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
   tp::nchw_to_nhwc_pad<<<grid, 256, 0, st>>>(x, y, B, C, H * W, Cp);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// General strided / padded conv (ResNet): KS in {1, 3} with Cin % 32 == 0, or KS = 7 on a
+// 4-channel padded input (stem). Forward epilogue: BN affine, optional residual add, optional
+// ReLU, optional APoZ counts of the output (exact integer counts per (image, channel)).
+// ---------------------------------------------------------------------------------------------
+namespace {
+template <int BM, int BN, int WM, int WN, int KS, int GEN, int EPI>
+hipError_t launch_gen(const tp::ConvArgs& a, int splits, hipStream_t st) {
+  const int m_tiles = (a.M + BM - 1) / BM, n_tiles = (a.N + BN - 1) / BN;
+  dim3 grid(m_tiles * n_tiles, splits);
+  tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN><<<grid, tp::Tile<BM, BN, WM, WN>::NT, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+template <int KS, int GEN, int EPI>
+hipError_t gen_cfg(int cfg, const tp::ConvArgs& a, int splits, hipStream_t st) {
+  switch (cfg) {
+    case 0: return launch_gen<128, 128, 64, 64, KS, GEN, EPI>(a, splits, st);
+    case 2: return launch_gen<64, 64, 32, 32, KS, GEN, EPI>(a, splits, st);
+    case 3: return launch_gen<128, 64, 64, 32, KS, GEN, EPI>(a, splits, st);
+    case 4: return launch_gen<128, 128, 64, 32, KS, GEN, EPI>(a, splits, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int EPI>
+hipError_t gen_dispatch(int ks, int gen, int cfg, const tp::ConvArgs& a, int splits, hipStream_t st) {
+  if (gen == 2 && ks == 7) return gen_cfg<7, 2, EPI>(cfg, a, splits, st);
+  if (gen == 1 && ks == 1) return gen_cfg<1, 1, EPI>(cfg, a, splits, st);
+  if (gen == 1 && ks == 3) return gen_cfg<3, 1, EPI>(cfg, a, splits, st);
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+extern "C" int tp_conv_gen_k(int ks, int Cin) {
+  return Cin == 4 ? (ks * ks * 4 + 31) / 32 * 32 : ks * ks * Cin;
+}
+
+extern "C" hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                  int stride, int pad, int cfg, int splits, const float* scale, const float* shift,
+                                  int relu, const float* res, float* apoz, float* out, float* ws, hipStream_t st) {
+  using namespace tp;
+  const int gen = Cin == 4 ? 2 : 1;
+  if (gen == 1 && Cin % 32 != 0) return hipErrorInvalidValue;
+  ConvArgs a{};
+  a.x = x;
+  a.w = w;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.N = Cout;
+  a.K = tp_conv_gen_k(ks, Cin);
+  a.Ho = (H + 2 * pad - ks) / stride + 1;
+  a.Wo = (W + 2 * pad - ks) / stride + 1;
+  a.stride = stride;
+  a.pad = pad;
+  a.M = B * a.Ho * a.Wo;
+  a.HWo = a.Ho * a.Wo;
+  a.x_elems = (long long)B * H * W * Cin;
+  if (a.x_elems * 4 >= (1ll << 31) || (long long)Cout * a.K * 4 >= (1ll << 31) ||
+      (long long)a.M * Cout * 4 >= (1ll << 31))
+    return hipErrorInvalidValue;
+  const int kt = a.K / 32;
+  splits = std::max(1, std::min(splits, kt));
+  a.k_tiles_per_split = (kt + splits - 1) / splits;
+  splits = (kt + a.k_tiles_per_split - 1) / a.k_tiles_per_split;
+  a.scale = scale;
+  a.shift = shift;
+  a.relu = relu;
+  a.res = res;
+  a.apoz = apoz;
+  a.out = out;
+  if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);
+  if (!ws) return hipErrorInvalidValue;
+  ConvArgs b = a;
+  b.out = ws;
+  hipError_t e = gen_dispatch<EPI_PARTIAL>(ks, gen, cfg, b, splits, st);
+  if (e != hipSuccess) return e;
+  const long long MN = (long long)a.M * a.N;
+  const unsigned grid = (unsigned)std::min<long long>(ceil_div(MN, 256), 4096);
+  conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
   return hipGetLastError();
 }

@@ -171,3 +171,64 @@ extern "C" hipError_t tp_unpool2_nhwc(const float* g, const uint8_t* am, float* 
   tp::unpool2_nhwc<<<grid, 256, 0, st>>>(g, am, out, B, H, W, C);
   return hipGetLastError();
 }
+
+// Generic NHWC max-pool (k x k, stride s, zero-free padding p: padded taps are skipped, as in
+// PyTorch) with NaN propagation, and global average pooling NHWC -> (B, C).
+namespace tp {
+__global__ __launch_bounds__(256) void maxpool_nhwc(const float* __restrict__ x, float* __restrict__ y, int B, int H,
+                                                    int W, int C, int k, int s, int pad, int Ho, int Wo) {
+  const long long total = (long long)B * Ho * Wo * (C / 4);
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % (C / 4));
+    const long long r = t / (C / 4);
+    const int ow = (int)(r % Wo), oh = (int)((r / Wo) % Ho);
+    const long long b = r / ((long long)Wo * Ho);
+    float4 best = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * s - pad + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * s - pad + kw;
+        if (iw < 0 || iw >= W) continue;
+        const float4 v = *reinterpret_cast<const float4*>(x + ((b * H + ih) * W + iw) * C + c4 * 4);
+        best.x = nan_max(best.x, v.x);
+        best.y = nan_max(best.y, v.y);
+        best.z = nan_max(best.z, v.z);
+        best.w = nan_max(best.w, v.w);
+      }
+    }
+    *reinterpret_cast<float4*>(y + r * C + c4 * 4) = best;
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool_nhwc(const float* __restrict__ x, float* __restrict__ y, int B, int HW,
+                                                    int C) {
+  const long long total = (long long)B * C;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    const long long b = t / C;
+    float s = 0.f;
+    for (int i = 0; i < HW; ++i) s += x[(b * HW + i) * C + c];
+    y[t] = s / (float)HW;
+  }
+}
+}  // namespace tp
+
+extern "C" hipError_t tp_maxpool_nhwc(const float* x, float* y, int B, int H, int W, int C, int k, int s, int pad,
+                                      hipStream_t st) {
+  if (C % 4 != 0) return hipErrorInvalidValue;
+  const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
+  const long long total = (long long)B * Ho * Wo * (C / 4);
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::maxpool_nhwc<<<grid, 256, 0, st>>>(x, y, B, H, W, C, k, s, pad, Ho, Wo);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_avgpool_nhwc(const float* x, float* y, int B, int HW, int C, hipStream_t st) {
+  const long long total = (long long)B * C;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::avgpool_nhwc<<<grid, 256, 0, st>>>(x, y, B, HW, C);
+  return hipGetLastError();
+}

@@ -85,6 +85,7 @@ struct WinoArgs {
   int arounds, aoff;
   int tay_slots;            // W_BWD: partial slots R of the (R, B, K) taylor slab
   FastDiv fd_timg, fd_w2, fd_ip, fd_rw;  // T_img = (H/2)(W/2), W/2, IP, RW
+  float* apoz;              // W_FWD: [B][K] counts of positive outputs (exact integers), nullable
   int dbg;                  // experiment switches (TP_WINO_DBG): 1 no epilogue, 2 no restaging, 4 no transform
 };
 
@@ -266,6 +267,9 @@ phase2:
           v.w = nan_relu(v.w);
         }
         *reinterpret_cast<float4*>(p.out + pix * p.K + k) = v;
+        if (p.apoz)
+          tq[i] = make_float4(v.x > 0.f ? 1.f : 0.f, v.y > 0.f ? 1.f : 0.f, v.z > 0.f ? 1.f : 0.f,
+                              v.w > 0.f ? 1.f : 0.f);
       } else if constexpr (EPI == W_PARTIAL) {
         const long long mrow = p.pooled_m ? (long long)pt * 4 + q : pix;
         *reinterpret_cast<float4*>(p.out + ((long long)blockIdx.y * p.B * p.H * p.W + mrow) * p.K + k) = y;
@@ -284,8 +288,10 @@ phase2:
         }
       }
     }
-    if constexpr (EPI == W_BWD) {
-      if (!p.taylor) return;
+    if constexpr (EPI == W_BWD || EPI == W_FWD) {
+      // per-(image, channel) sums of the per-item partials: W_BWD Taylor (fixed order, slot
+      // write), W_FWD APoZ counts (exact integers: atomics are order-free)
+      if (EPI == W_BWD ? !p.taylor : !p.apoz) return;
       // sum the 4 pixels of each tile: lanes tid ^ 8, ^ 16 hold q ^ 1, q ^ 2 (fixed order)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -318,8 +324,12 @@ phase2:
         const int lo = max(bb * T_img, t0) - t0, hi = min((bb + 1) * T_img - 1, t_last) - t0;
         float sum = 0.f;
         for (int tl = lo; tl <= hi; ++tl) sum += yb0[tl * W_TK + kk];
-        const int slot = blk_p - (bb * T_img) / 64;
-        if (slot < p.tay_slots) p.taylor[((long long)slot * p.B + bb) * p.K + kc] += sum;
+        if constexpr (EPI == W_FWD) {
+          if (sum > 0.f) atomicAdd(p.apoz + (long long)bb * p.K + kc, sum);
+        } else {
+          const int slot = blk_p - (bb * T_img) / 64;
+          if (slot < p.tay_slots) p.taylor[((long long)slot * p.B + bb) * p.K + kc] += sum;
+        }
       }
     }
   }
@@ -539,7 +549,8 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       if constexpr (XMODE == X_STAGED) {
 #pragma unroll
         for (int t = 0; t < 16; ++t)
-          d[t] = *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(xb) + poff[t]);
+          d[t] = (p.dbg & 64) ? f32x2{(float)t, 1.f}
+                              : *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(xb) + poff[t]);
       } else if constexpr (XMODE == X_STAGED_UNPOOL) {
         f32x2 cv[9];
         unsigned ca[9];
@@ -618,7 +629,8 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_s_setprio(0);
-    __syncthreads();  // drains this chunk's DMA for the next one and orders buffer reuse
+    if (p.dbg & 32) __builtin_amdgcn_s_waitcnt(0);
+    else __syncthreads();  // drains this chunk's DMA for the next one and orders buffer reuse
   };
 
   if (c_begin < c_end) {
@@ -740,7 +752,7 @@ static XGeom staged_geometry(int H, int W, bool pooled) {
 extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
                                               const float* scale, const float* shift, int relu, float* out,
                                               uint8_t* out_argmax, const float* act, float* taylor,
-                                              hipStream_t st);
+                                              float* apoz, hipStream_t st);
 
 extern "C" int tp_wino_taylor_slots(int H, int W) { return tp::wino_taylor_slots(H, W); }
 
@@ -759,7 +771,7 @@ extern "C" void tp_wino_geometry(int H, int W, int unpool, int* out9) {
 extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W,
                                    int C, int K, int unpool, int epi, int splits, int staged, const float* scale,
                                    const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
-                                   float* taylor, float* ws, hipStream_t st) {
+                                   float* taylor, float* apoz, float* ws, hipStream_t st) {
   using namespace tp;
   if ((H & 1) || (W & 1) || C % 8 != 0 || K % 32 != 0) return hipErrorInvalidValue;
   WinoArgs a{};
@@ -786,6 +798,8 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.out_argmax = out_argmax;
   a.act = act;
   a.taylor = taylor;
+  a.apoz = epi == W_FWD ? apoz : nullptr;
+  if (apoz && epi != W_FWD) return hipErrorInvalidValue;
   a.tay_slots = wino_taylor_slots(H, W);
   a.fd_timg = FastDiv((unsigned)std::max(1, (H / 2) * (W / 2)));
   a.fd_w2 = FastDiv((unsigned)std::max(1, W / 2));
@@ -831,5 +845,6 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
 #undef TP_W
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || splits == 1) return e;
-  return tp_conv_epilogue_slabs(ws, splits, B, H, W, K, epi, scale, shift, relu, out, out_argmax, act, taylor, st);
+  return tp_conv_epilogue_slabs(ws, splits, B, H, W, K, epi, scale, shift, relu, out, out_argmax, act, taylor,
+                                a.apoz, st);
 }

@@ -400,3 +400,24 @@ def test_dense_gemm_2x2_layer_matches_winograd(cuda, pool):
     torch.testing.assert_close(t_d.sum(0), t_w.sum(0), rtol=3e-4, atol=3e-4)
     y2, am2 = T.maxpool2_nhwc(y_w if not pool else y_w.new_ones(B, 2, 2, K))
     assert y2.shape == (B, 1, 1, K)
+
+
+@pytest.mark.parametrize("staged", [False, True])
+@pytest.mark.parametrize("splits", [1, 2])
+def test_wino_fwd_apoz_counts(cuda, staged, splits):
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import winograd_weights
+    T = ops.require()
+    g = torch.Generator().manual_seed(31)
+    B, H, W, C, K = 5, 14, 14, 64, 96
+    x = _rand(B, H, W, C, gen=g)
+    w = _rand(K, C, 3, 3, gen=g) * (2.0 / (9 * C)) ** 0.5
+    sc = _rand(K, gen=g).abs() + 0.5
+    sh = _rand(K, gen=g) * 0.1
+    ref, _ = _ref_fwd(x, w, sc, sh, True, False)
+    apoz = torch.zeros(B, K, device=cuda)
+    out, _ = T.conv_wino_fwd(x.to(cuda), winograd_weights(w.to(cuda)), sc.to(cuda), sh.to(cuda), True, False, splits,
+                             staged, apoz)
+    torch.testing.assert_close(out.cpu(), ref, rtol=3e-4, atol=3e-4)
+    cnt = (ref > 0).sum((1, 2)).float()
+    assert (apoz.cpu() - cnt).abs().max() <= 2

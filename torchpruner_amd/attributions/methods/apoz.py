@@ -4,8 +4,13 @@ Per sample and unit: count of positive outputs summed over the trailing (spatial
 convolutions this is a *count*, not a fraction, exactly like the reference (apoz.py:31-33).
 The count is produced on device by the HIP channel-reduction kernel and accumulated in fp64;
 the pass is forward-only and skips the loss the reference computes but never uses.
+For torchvision-layout ResNets the whole forward runs on the HIP kernels of the ResNet engine
+(engine/resnet_engine.py) with the counts fused into the conv epilogues.
 """
+import torch
+
 from ... import ops
+from ...engine.resnet_engine import maybe_resnet_engine
 from ..base import _AttributionMetric
 
 
@@ -21,8 +26,37 @@ class APoZAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            self._forward_capture_pass(eval_modules,
-                                       lambda k, out, i: accs[k].add(ops.channel_reduce(out, None, "apoz"), i))
+            eng = maybe_resnet_engine(self.model, eval_modules, self.device)
+            if eng is not None:
+                self._engine_pass(eng, eval_modules, accs)
+            else:
+                self._forward_capture_pass(eval_modules,
+                                           lambda k, out, i: accs[k].add(ops.channel_reduce(out, None, "apoz"), i))
         finally:
             self._end_run()
         return [self._finalize(a) for a in accs]
+
+    def _engine_pass(self, eng, eval_modules, accs):
+        uniq = list(dict.fromkeys(eval_modules))
+        stats = accs[0].mode == "stats"
+        arena = None
+        with torch.no_grad():
+            for i, x, _y in self._batches():
+                B = x.shape[0]
+                if arena is None or arena.shape[0] != B * sum(m.num_features for m in uniq) or not stats:
+                    arena = torch.zeros(B * sum(m.num_features for m in uniq), device=x.device)
+                else:
+                    arena.zero_()
+                bufs, off = {}, 0
+                for m in uniq:
+                    bufs[m] = arena[off:off + B * m.num_features].view(B, m.num_features)
+                    off += B * m.num_features
+                eng.forward(x, bufs)
+                if stats:  # one fold launch for every module's counts (fp64 column sums)
+                    sums = [accs[k].ensure_sum(m.num_features, x.device) for k, m in enumerate(eval_modules)]
+                    ops.score_fold_([bufs[m] for m in eval_modules], sums, False, 0)
+                    for a in accs:
+                        a.count += B
+                else:
+                    for k, m in enumerate(eval_modules):
+                        accs[k].add(bufs[m], i)

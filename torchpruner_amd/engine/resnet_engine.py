@@ -1,0 +1,239 @@
+"""Forward engine for ResNets (BasicBlock / Bottleneck, torchvision layout) on the HIP kernels.
+
+BASELINE config #3 scores every bottleneck conv of a ResNet-50 with APoZ: a forward-only pass
+whose per-(sample, channel) statistic is the count of positive outputs of each block's BN (the
+evaluation module ``find_best_module_for_attributions`` picks for conv1/conv2, reference
+graph.py:9-34, apoz.py:28-39). The generic path runs MIOpen convolutions plus one HIP channel
+reduction per module; this engine runs the whole network on our own kernels instead:
+
+  stem   NCHW -> NHWC pad to 4 channels, 7x7/2 implicit GEMM (8 taps x 4 channels per K
+         slice) with the eval-mode BN folded into the epilogue affine + ReLU; 3x3/2 max-pool
+  block  1x1 -> 3x3 (stride s) -> 1x1 implicit-GEMM convs (``tpamd.conv_gen``), BN folded, the
+         residual add (identity or the 1x1/s downsample conv) and the final ReLU fused into the
+         last conv's epilogue; APoZ counts of the block's bn1/bn2 outputs are produced by the
+         conv epilogues (exact integer counts, order independent -> deterministic)
+  head   global average pool + fc GEMM
+
+fp32 throughout (exact fp32 MFMA). Works for any input size / batch; weights are re-packed
+whenever a parameter changes (pruning, training).
+"""
+from __future__ import annotations
+
+import weakref
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, winograd_weights
+
+
+@dataclass
+class _Conv:
+    conv: nn.Conv2d
+    bn: Optional[nn.BatchNorm2d]
+
+
+@dataclass
+class _Block:
+    convs: list            # [_Conv] in order (2 for BasicBlock, 3 for Bottleneck)
+    downsample: Optional[_Conv]
+
+
+@dataclass
+class ResNetPlan:
+    stem: _Conv
+    maxpool: nn.MaxPool2d
+    blocks: list = field(default_factory=list)
+    fc: Optional[nn.Linear] = None
+
+
+def _is_resnet(model) -> bool:
+    return all(hasattr(model, a) for a in ("conv1", "bn1", "maxpool", "layer1", "layer2", "layer3", "layer4", "fc"))
+
+
+def build_resnet_plan(model: nn.Module):
+    """Lower a torchvision-layout ResNet, or return (None, reason)."""
+    if not _is_resnet(model):
+        return None, "not a torchvision-layout ResNet"
+    c1 = model.conv1
+    if c1.kernel_size != (7, 7) or c1.stride != (2, 2) or c1.padding != (3, 3) or c1.in_channels > 4 or c1.groups != 1:
+        return None, "unsupported stem"
+    mp = model.maxpool
+    if not isinstance(mp, nn.MaxPool2d) or mp.ceil_mode or mp.dilation not in (1, (1, 1)):
+        return None, "unsupported stem pool"
+    plan = ResNetPlan(_Conv(c1, model.bn1), mp, fc=model.fc)
+    for layer in (model.layer1, model.layer2, model.layer3, model.layer4):
+        for blk in layer:
+            names = ["conv1", "conv2", "conv3"] if hasattr(blk, "conv3") else ["conv1", "conv2"]
+            convs = []
+            for i, n in enumerate(names):
+                conv = getattr(blk, n)
+                bn = getattr(blk, "bn" + str(i + 1))
+                if conv.groups != 1 or conv.dilation != (1, 1) or conv.kernel_size[0] not in (1, 3) or \
+                        conv.padding[0] != conv.kernel_size[0] // 2 or conv.in_channels % 32 != 0:
+                    return None, f"unsupported conv {conv}"
+                convs.append(_Conv(conv, bn))
+            ds = None
+            if blk.downsample is not None:
+                d = blk.downsample
+                if not (isinstance(d, nn.Sequential) and len(d) == 2 and isinstance(d[0], nn.Conv2d)
+                        and isinstance(d[1], nn.BatchNorm2d) and d[0].kernel_size == (1, 1)):
+                    return None, "unsupported downsample"
+                ds = _Conv(d[0], d[1])
+            plan.blocks.append(_Block(convs, ds))
+    if any(c.conv.out_channels % 4 for b in plan.blocks for c in b.convs) or c1.out_channels % 4:
+        return None, "channel counts must be multiples of 4"
+    return plan, ""
+
+
+def _fold(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d]):
+    w = conv.weight.detach().float()
+    cout = w.shape[0]
+    bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=w.device)
+    if bn is None:
+        return torch.ones(cout, device=w.device), bias
+    inv = torch.rsqrt(bn.running_var.float() + bn.eps)
+    g = bn.weight.float() if bn.weight is not None else torch.ones_like(inv)
+    beta = bn.bias.float() if bn.bias is not None else torch.zeros_like(inv)
+    scale = g * inv
+    return scale.contiguous(), ((bias - bn.running_mean.float()) * scale + beta).contiguous()
+
+
+class ResNetEngine:
+    def __init__(self, model: nn.Module, plan: ResNetPlan):
+        self.plan = plan
+        self._key = None
+        self._packed = None
+
+    def _all_convs(self):
+        p = self.plan
+        out = [p.stem]
+        for b in p.blocks:
+            out += b.convs + ([b.downsample] if b.downsample is not None else [])
+        return out
+
+    def _params_key(self):
+        key = []
+        for c in self._all_convs():
+            for t in (c.conv.weight, c.conv.bias) + ((c.bn.weight, c.bn.bias, c.bn.running_mean, c.bn.running_var)
+                                                     if c.bn is not None else ()):
+                if t is not None:
+                    key.append((t.data_ptr(), t._version, tuple(t.shape)))
+        for t in (self.plan.fc.weight, self.plan.fc.bias):
+            if t is not None:
+                key.append((t.data_ptr(), t._version, tuple(t.shape)))
+        return tuple(key)
+
+    @torch.no_grad()
+    def _pack_conv(self, c: _Conv, stem=False):
+        w = c.conv.weight.detach().float()
+        if stem:  # pad Cin to 4, K = 49 taps x 4 channels padded to a multiple of 32
+            w = F.pad(w, (0, 0, 0, 0, 0, 4 - w.shape[1]))
+        wk = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+        k_pad = ops.require().conv_gen_k(c.conv.kernel_size[0], w.shape[1]) - wk.shape[1]
+        if k_pad:
+            wk = F.pad(wk, (0, k_pad))
+        scale, shift = _fold(c.conv, c.bn)
+        e = {"w": wk.contiguous(), "scale": scale, "shift": shift, "ks": c.conv.kernel_size[0],
+             "stride": c.conv.stride[0], "pad": c.conv.padding[0]}
+        if e["ks"] == 3 and e["stride"] == 1 and w.shape[1] % 8 == 0 and w.shape[0] % 32 == 0:
+            e["u"] = winograd_weights(w)  # stride-1 3x3: Winograd candidate
+        return e
+
+    def _pack(self):
+        key = self._params_key()
+        if key == self._key:
+            return self._packed
+        p = self.plan
+        blocks = []
+        for b in p.blocks:
+            blocks.append({"convs": [self._pack_conv(c) for c in b.convs],
+                           "ds": self._pack_conv(b.downsample) if b.downsample is not None else None})
+        fc_w = p.fc.weight.detach().float()
+        fc_b = p.fc.bias.detach().float() if p.fc.bias is not None else torch.zeros(fc_w.shape[0],
+                                                                                   device=fc_w.device)
+        self._packed = {"stem": self._pack_conv(p.stem, stem=True), "blocks": blocks,
+                        "fc_w": fc_w.contiguous(), "fc_b": fc_b.contiguous()}
+        self._key = key
+        return self._packed
+
+    @staticmethod
+    def _conv(T, e, h, relu, res=None, apoz=None):
+        B, H, W, C = h.shape
+        ks, s, pd = e["ks"], e["stride"], e["pad"]
+        Ho, Wo = (H + 2 * pd - ks) // s + 1, (W + 2 * pd - ks) // s + 1
+        M, N, K = B * Ho * Wo, e["scale"].numel(), e["w"].shape[1]
+        cands = TUNER.candidates(M, N, K)
+        cands = [c for c in cands if c[0] in (0, 2, 3, 4)]  # tile configs conv_gen instantiates
+        if "u" in e and res is None and H % 2 == 0 and W % 2 == 0:
+            sp0 = _wino_splits(B * (H // 2) * (W // 2), N, C)
+            cands = [(WINO_LDS, sp0), (WINO, sp0)] + ([(WINO_LDS, 1)] if sp0 > 1 else []) + cands
+        key = ("gen", tuple(h.shape), N, ks, s, res is not None)
+
+        def run(cfg, sp, hh=h, ap=None):
+            if cfg in (WINO, WINO_LDS):
+                return T.conv_wino_fwd(hh, e["u"], e["scale"], e["shift"], relu, False, sp, cfg == WINO_LDS, ap)[0]
+            return T.conv_gen(hh, e["w"], e["scale"], e["shift"], relu, res, ap, ks, s, pd, cfg, sp)
+
+        cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands)
+        return run(cfg, sp, h, apoz)
+
+    def forward(self, x: torch.Tensor, apoz: Optional[dict] = None):
+        """Logits of the network; ``apoz`` maps BN modules of the blocks (bn1 / bn2 / ...) to
+        zeroed (B, C) float tensors that receive the per-sample counts of positive outputs."""
+        T = ops.require()
+        P = self._pack()
+        apoz = apoz or {}
+        h = T.nchw_to_nhwc_pad(x.float().contiguous(), 4)
+        h = self._conv(T, P["stem"], h, True, apoz=apoz.get(self.plan.stem.bn))
+        mp = self.plan.maxpool
+        k = mp.kernel_size if isinstance(mp.kernel_size, int) else mp.kernel_size[0]
+        s = mp.stride if isinstance(mp.stride, int) else mp.stride[0]
+        pd = mp.padding if isinstance(mp.padding, int) else mp.padding[0]
+        h = T.maxpool_nhwc(h, k, s, pd)
+        for blk, e in zip(self.plan.blocks, P["blocks"]):
+            idn = h
+            if e["ds"] is not None:
+                idn = self._conv(T, e["ds"], h, False)
+            t = h
+            n = len(e["convs"])
+            for i, (c, ce) in enumerate(zip(blk.convs, e["convs"])):
+                last = i == n - 1
+                t = self._conv(T, ce, t, True, res=idn if last else None, apoz=apoz.get(c.bn))
+            h = t
+        feat = T.avgpool_nhwc(h)
+        return F.linear(feat, P["fc_w"], P["fc_b"])
+
+    def eval_modules(self):
+        """BN modules whose outputs the engine can count (block bn1/bn2/..., stem bn)."""
+        mods = [self.plan.stem.bn]
+        for b in self.plan.blocks:
+            mods += [c.bn for c in b.convs[:-1]]
+        return mods
+
+
+_ENGINES: "weakref.WeakKeyDictionary[nn.Module, ResNetEngine]" = weakref.WeakKeyDictionary()
+
+
+def maybe_resnet_engine(model, eval_modules, device):
+    """A ResNetEngine when every eval module is a BN the engine counts, else None."""
+    dev = torch.device(device) if not isinstance(device, torch.device) else device
+    if dev.type != "cuda" or ops.backend() == "torch" or not ops.available() or model.training:
+        return None
+    if any(p.dtype != torch.float32 for p in model.parameters()):
+        return None
+    plan, _ = build_resnet_plan(model)  # re-validated every run: pruning changes channel counts
+    if plan is None:
+        return None
+    eng = _ENGINES.get(model)
+    if eng is None or [c.conv for c in eng._all_convs()] != [c.conv for c in ResNetEngine(model, plan)._all_convs()]:
+        eng = ResNetEngine(model, plan)
+        _ENGINES[model] = eng
+    ok = set(map(id, eng.eval_modules()))
+    if not all(id(m) in ok for m in eval_modules):
+        return None
+    return eng
