@@ -279,6 +279,7 @@ at::Tensor conv_gen(const at::Tensor& x, const at::Tensor& w, const c10::optiona
               "conv_gen supports ks 1/3 with Cin % 32 == 0, or ks 7 with a 4-channel input");
   TORCH_CHECK(w.size(1) == tp_conv_gen_k((int)ks, (int)Cin), "weight K mismatch");
   TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
+  TORCH_CHECK(Cout % 4 == 0, "conv_gen needs Cout % 4 == 0");
   const int64_t Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   const float* sc = opt_ptr(scale, Cout, "scale");

@@ -19,6 +19,8 @@
 // r = 4g..4g+3 — the max-pool is four in-register max operations.
 #include "tp_common.h"
 
+#include <cstdlib>
+
 namespace tp {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -53,6 +55,7 @@ struct ConvArgs {
   int Ho, Wo, stride, pad;
   const float* res;         // EPI_FWD: residual [M][N] added before the ReLU (nullable)
   float* apoz;              // EPI_FWD: [B][N] counts of positive outputs (exact integers), nullable
+  int epi_lds;              // GEN: 1 -> two-phase LDS-transposed forward epilogue (TP_GEN_EPI=0 disables)
   int tay_group;            // EPI_BWD: >0 -> N = P pixel groups x tay_group channels (a dense-GEMM conv);
                             // Taylor of column n goes to slot n / tay_group of a (P, B, tay_group) slab
 };
@@ -297,6 +300,106 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
       __syncthreads();
       buf ^= 1;
     }
+  }
+
+  // ---- GEN forward / partial epilogue: transpose through LDS, float4 rows ---------------
+  // (memory-bound 1x1 convs: scalar per-lane stores + residual loads ran at ~2 TB/s)
+  if constexpr (GEN != 0 && (EPI == EPI_FWD || EPI == EPI_PARTIAL)) {
+   if (p.epi_lds) {
+    constexpr int LDT = BN + 4;
+    constexpr int CB_IMG = 8;  // images per block whose counts are reduced in LDS
+    static_assert(BM * LDT + CB_IMG * BN <= 2 * (BM + BN) * LDK, "output tile must fit in the staging LDS");
+    float* ts = smem;  // the main loop ended with a barrier
+    float* cb = smem + BM * LDT;  // APoZ counts [image in block][column]
+    const int b_first = m0 / p.HWo;
+    const bool cb_lds = EPI == EPI_FWD && p.apoz && (min(m0 + BM, p.M) - 1) / p.HWo - b_first < CB_IMG;
+    if (cb_lds)
+      for (int t = tid; t < CB_IMG * BN; t += T::NT) cb[t] = 0.f;
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          ts[(wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDT + wn0 + j * 32 + li] = acc[i][j][r];
+    __syncthreads();
+    constexpr int C4 = BN / 4;
+    static_assert(T::NT % C4 == 0, "thread -> column-quad mapping");
+    const int c4 = tid % C4;
+    const int n = n0 + c4 * 4;
+    const bool ncol_ok = n < p.N;
+    float4 sc4 = make_float4(1.f, 1.f, 1.f, 1.f), sh4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (EPI == EPI_FWD) {
+      if (ncol_ok && p.scale) sc4 = *reinterpret_cast<const float4*>(p.scale + n);
+      if (ncol_ok && p.shift) sh4 = *reinterpret_cast<const float4*>(p.shift + n);
+    }
+    int cur_b = -1;
+    float4 cnt = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int row = tid / C4; ncol_ok && row < BM; row += T::NT / C4) {
+      const int m = m0 + row;
+      if (m >= p.M) break;
+      float4 v = *reinterpret_cast<const float4*>(ts + row * LDT + c4 * 4);
+      if constexpr (EPI == EPI_PARTIAL) {
+        *reinterpret_cast<float4*>(p.out + ((long long)split * p.M + m) * p.N + n) = v;
+      } else {
+        const long long o = (long long)m * p.N + n;
+        v.x = v.x * sc4.x + sh4.x;
+        v.y = v.y * sc4.y + sh4.y;
+        v.z = v.z * sc4.z + sh4.z;
+        v.w = v.w * sc4.w + sh4.w;
+        if (p.res) {
+          const float4 rr = *reinterpret_cast<const float4*>(p.res + o);
+          v.x += rr.x;
+          v.y += rr.y;
+          v.z += rr.z;
+          v.w += rr.w;
+        }
+        if (p.relu) {
+          v.x = nan_relu(v.x);
+          v.y = nan_relu(v.y);
+          v.z = nan_relu(v.z);
+          v.w = nan_relu(v.w);
+        }
+        *reinterpret_cast<float4*>(p.out + o) = v;
+        if (p.apoz) {  // exact integer counts: atomics are order-free
+          const int b = m / p.HWo;
+          if (b != cur_b) {
+            if (cur_b >= 0) {
+              float* ap = cb_lds ? cb + (cur_b - b_first) * BN + c4 * 4 : p.apoz + (long long)cur_b * p.N + n;
+              if (cnt.x > 0.f) atomicAdd(ap, cnt.x);
+              if (cnt.y > 0.f) atomicAdd(ap + 1, cnt.y);
+              if (cnt.z > 0.f) atomicAdd(ap + 2, cnt.z);
+              if (cnt.w > 0.f) atomicAdd(ap + 3, cnt.w);
+            }
+            cur_b = b;
+            cnt = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          cnt.x += v.x > 0.f ? 1.f : 0.f;
+          cnt.y += v.y > 0.f ? 1.f : 0.f;
+          cnt.z += v.z > 0.f ? 1.f : 0.f;
+          cnt.w += v.w > 0.f ? 1.f : 0.f;
+        }
+      }
+    }
+    if constexpr (EPI == EPI_FWD) {
+      if (p.apoz && cur_b >= 0) {
+        float* ap = cb_lds ? cb + (cur_b - b_first) * BN + c4 * 4 : p.apoz + (long long)cur_b * p.N + n;
+        if (cnt.x > 0.f) atomicAdd(ap, cnt.x);
+        if (cnt.y > 0.f) atomicAdd(ap + 1, cnt.y);
+        if (cnt.z > 0.f) atomicAdd(ap + 2, cnt.z);
+        if (cnt.w > 0.f) atomicAdd(ap + 3, cnt.w);
+      }
+      if (cb_lds) {  // one global atomic per (image, column) of this block
+        __syncthreads();
+        const int n_img = (min(m0 + BM, p.M) - 1) / p.HWo - b_first + 1;
+        for (int t = tid; t < n_img * BN; t += T::NT) {
+          const int col = n0 + t % BN;
+          if (cb[t] > 0.f && col < p.N) atomicAdd(p.apoz + (long long)(b_first + t / BN) * p.N + col, cb[t]);
+        }
+      }
+    }
+    return;
+   }
   }
 
   // ---- epilogue --------------------------------------------------------------------------
@@ -806,7 +909,7 @@ extern "C" hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, 
                                   int relu, const float* res, float* apoz, float* out, float* ws, hipStream_t st) {
   using namespace tp;
   const int gen = Cin == 4 ? 2 : 1;
-  if (gen == 1 && Cin % 32 != 0) return hipErrorInvalidValue;
+  if ((gen == 1 && Cin % 32 != 0) || Cout % 4 != 0) return hipErrorInvalidValue;
   ConvArgs a{};
   a.x = x;
   a.w = w;
@@ -836,6 +939,8 @@ extern "C" hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, 
   a.res = res;
   a.apoz = apoz;
   a.out = out;
+  const char* ge = getenv("TP_GEN_EPI");
+  a.epi_lds = ge ? atoi(ge) : 1;
   if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);
   if (!ws) return hipErrorInvalidValue;
   ConvArgs b = a;
