@@ -57,12 +57,15 @@ class ScoreAccumulator:
         self.count = 0
         self.slabs: list[tuple[int, torch.Tensor]] = []
         self.dtype = None
+        self.width = None  # real unit count when the engine's slabs are channel-padded
 
-    def ensure_sum(self, C: int, device) -> torch.Tensor:
-        """The fp64 (C,) running sum (allocated on first use) for kernels that fold into it."""
+    def ensure_sum(self, C: int, device, width=None) -> torch.Tensor:
+        """The fp64 (C,) running sum (allocated on first use) for kernels that fold into it;
+        ``width`` < C marks the trailing C - width entries as engine padding (dropped on output)."""
         if self.sum is None:
             self.sum = torch.zeros(C, dtype=torch.float64, device=device)
             self.dtype = torch.float32
+            self.width = width
         return self.sum
 
     def add(self, v: torch.Tensor, batch_index: int):
@@ -97,7 +100,7 @@ class ScoreAccumulator:
                 res = total / max(count, 1.0)
             else:
                 res = total
-            return res.astype(out_dtype)
+            return res[:self.width].astype(out_dtype)
         rows = pdist.gather_ordered_rows(self.slabs, group)
         return self._to_numpy_rows(rows, aggregate, out_dtype)
 
@@ -106,7 +109,7 @@ class ScoreAccumulator:
         if self.mode == "stats":
             total = self.sum.cpu().numpy() if self.sum is not None else np.zeros(0)
             res = total / max(self.count, 1) if reduction == "mean" else total
-            return res.astype(out_dtype)
+            return res[:self.width].astype(out_dtype)
         slabs = sorted(self.slabs, key=lambda s: s[0])
         rows = torch.cat([t for _, t in slabs], 0) if slabs else torch.empty(0)
         return self._to_numpy_rows(rows, aggregate, out_dtype)

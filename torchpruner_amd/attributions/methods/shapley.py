@@ -174,18 +174,28 @@ class ShapleyAttributionMetric(_AttributionMetric):
             return None
         engine, (k,) = fused
 
+        n = engine.real_width(k)
+        padded_ranks = {}
+
         def prepare(x, y):
-            zk, _ = engine.forward(x, stop_after=k)  # engine layout (B, H, W, C)
+            zk, _ = engine.forward(x, stop_after=k)  # engine layout (B, H, W, C padded)
             B = zk.shape[0]
             z_cl = zk.permute(0, 3, 1, 2)  # (B, C, H, W) view, channels_last strides
             base = engine.loss_from(k, zk, y)
+            pad = zk.shape[3] - n
 
             def evaluate(rank_t, p_first, cnt):
+                if pad:  # padding channels rank after every real unit: never masked
+                    r = padded_ranks.get(id(rank_t))
+                    if r is None or r[0] is not rank_t:
+                        r = padded_ranks[id(rank_t)] = (rank_t, torch.cat([rank_t, torch.full(
+                            (pad,), n + 1, dtype=rank_t.dtype, device=rank_t.device)]))
+                    rank_t = r[1]
                 masked = ops.prefix_mask(z_cl, rank_t, p_first, cnt)  # (cnt*B, C, H, W) channels_last
                 loss = engine.loss_from(k, masked.permute(0, 2, 3, 1), y.repeat(cnt))
                 return loss.view(cnt, B)
 
-            return zk.shape[3], B, zk[0].numel(), base, evaluate
+            return n, B, zk[0].numel(), base, evaluate
 
         return prepare
 

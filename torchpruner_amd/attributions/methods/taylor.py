@@ -46,7 +46,8 @@ class TaylorAttributionMetric(_AttributionMetric):
                 if stats:
                     arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
                     engine.taylor(x, y, set(uniq), arena)
-                    sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device) for b in uniq]
+                    sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device, engine.real_width(b))
+                            for b in uniq]
                     ops.score_fold_([arena[b] for b in uniq], sums, not self.signed, 2)
                     for b in uniq:
                         accs[owner[b]].count += B
@@ -54,7 +55,7 @@ class TaylorAttributionMetric(_AttributionMetric):
                     res = engine.taylor(x, y, set(uniq))
                     ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), not self.signed, 1)
                     for b in uniq:
-                        accs[owner[b]].add(engine.per_sample(res[b]), i)
+                        accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
             accs = [accs[owner[b]] for b in blocks]
         else:
             self._grad_capture_pass(eval_modules,

@@ -118,6 +118,7 @@ class AttributionCheckpoint:
             if s.get("sum") is not None:
                 a.sum = s["sum"].to(dev)
             a.count = int(s["count"])
+            a.width = s.get("width")
             a.slabs = [(int(i), t.to(dev)) for i, t in s.get("slabs", [])]
             if s.get("dtype") == "float32":
                 a.dtype = torch.float32
@@ -135,6 +136,7 @@ class AttributionCheckpoint:
         st = {"key": self.key, "done": sorted(self.done), "accs": []}
         for a in accs:
             st["accs"].append({"sum": a.sum.cpu() if a.sum is not None else None, "count": a.count,
+                               "width": a.width,
                                "slabs": [(i, t.cpu()) for i, t in a.slabs],
                                "dtype": "float32" if a.dtype in (None, torch.float32) else "float64"})
         tmp = self.path + ".tmp"

@@ -181,6 +181,11 @@ class Autotuner:
 TUNER = Autotuner()
 
 
+def cpad(c: int, q: int = 32) -> int:
+    """Channel count rounded up to the MFMA K-slice / column-tile granule the kernels need."""
+    return -(-c // q) * q
+
+
 @dataclass
 class ConvBlock:
     conv: nn.Conv2d
@@ -188,12 +193,14 @@ class ConvBlock:
     relu: Optional[nn.Module]
     pool: Optional[nn.MaxPool2d]
     first: bool = False
+    width: int = 0  # padded output width carried by the engine's activations
 
 
 @dataclass
 class LinearBlock:
     linear: nn.Linear
     relu: Optional[nn.Module]
+    width: int = 0
 
 
 @dataclass
@@ -250,12 +257,16 @@ def build_plan(model: nn.Module):
                 return None, f"unsupported pool {pool}"
             i += 1
         first = len(plan.convs) == 0
-        if first and (conv.in_channels % 32 != 0):
-            if pool is not None or conv.out_channels not in (16, 32, 64):
-                return None, "first conv must be unpooled with 16/32/64 outputs"
-        elif conv.in_channels % 32 != 0:
-            return None, "conv input channels must be a multiple of 32"
-        plan.convs.append(ConvBlock(conv, bn, relu, pool, first=first and conv.in_channels % 32 != 0))
+        # pruned (odd) channel counts are carried zero-padded to a multiple of 32: padded
+        # filters have zero weights and a zero BN affine, so their outputs, gradients and
+        # scores are exactly 0 and never influence the real channels
+        width = cpad(conv.out_channels)
+        if first and conv.in_channels % 32 != 0:
+            if pool is not None or conv.out_channels > 64:
+                return None, "first conv must be unpooled with at most 64 outputs"
+            width = 16 if conv.out_channels <= 16 else width
+        plan.convs.append(ConvBlock(conv, bn, relu, pool, first=first and conv.in_channels % 32 != 0,
+                                    width=width))
     if not plan.convs:
         return None, "no conv stack"
     # flatten
@@ -274,13 +285,14 @@ def build_plan(model: nn.Module):
             if i < n and isinstance(stages[i], nn.ReLU):
                 relu = stages[i]
                 i += 1
-            plan.linears.append(LinearBlock(st, relu))
+            plan.linears.append(LinearBlock(st, relu, cpad(st.out_features)))
             continue
         return None, f"unsupported classifier stage {st}"
     if not plan.linears or any(b.relu is None for b in plan.linears[:-1]) or plan.linears[-1].relu is not None:
         return None, "classifier must be Linear(+ReLU) blocks ending in a plain Linear"
     if plan.linears[0].linear.in_features != plan.convs[-1].conv.out_channels:
         return None, "features must end at 1x1 spatial resolution"
+    plan.linears[-1].width = plan.linears[-1].linear.out_features  # logits stay unpadded
     return plan, ""
 
 
@@ -315,6 +327,7 @@ class FusedChainEngine:
         if key == self._key:
             return self._packed
         convs = []
+        cin_p = None  # padded width of the previous block's activation
         for b in self.plan.convs:
             w = b.conv.weight.detach().float()
             cout = w.shape[0]
@@ -328,6 +341,10 @@ class FusedChainEngine:
             else:
                 scale = torch.ones(cout, device=w.device)
                 shift = bias
+            wp = b.width - cout
+            w = F.pad(w, (0, 0, 0, 0, 0, (cin_p - w.shape[1]) if cin_p is not None else 0, 0, wp))
+            scale, shift = F.pad(scale, (0, wp)), F.pad(shift, (0, wp))
+            cin_p, cout = b.width, b.width
             entry = {"scale": scale.contiguous(), "shift": shift.contiguous(), "pool": b.pool is not None}
             if b.first:
                 entry["w_first"] = w.contiguous()
@@ -349,6 +366,9 @@ class FusedChainEngine:
             w = b.linear.weight.detach().float()
             n_out = w.shape[0]
             bias = b.linear.bias.detach().float() if b.linear.bias is not None else torch.zeros(n_out, device=w.device)
+            w = F.pad(w, (0, cin_p - w.shape[1], 0, b.width - n_out))
+            bias = F.pad(bias, (0, b.width - n_out))
+            cin_p = n_out = b.width
             pad = (-n_out) % 32
             wt = w.t()
             if pad:
@@ -540,8 +560,12 @@ class FusedChainEngine:
         return t[0] if t.dim() == 3 else t
 
     def _block_width(self, b):
-        blocks = self.plan.blocks
-        blk = blocks[b]
+        """Padded width of block b's output in engine layout (score slabs use it too)."""
+        return self.plan.blocks[b].width
+
+    def real_width(self, b):
+        """Number of real (unpadded) units of block b."""
+        blk = self.plan.blocks[b]
         return blk.conv.out_channels if isinstance(blk, ConvBlock) else blk.linear.out_features
 
     def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None):
@@ -657,7 +681,7 @@ def maybe_engine(model, eval_modules, criterion, device):
         return None
     eng = _ENGINES.get(model)
     if eng is None or len(eng.plan.blocks) != len(plan.blocks) or any(
-            a.conv is not b.conv if isinstance(a, ConvBlock) else a.linear is not b.linear
+            (a.conv is not b.conv if isinstance(a, ConvBlock) else a.linear is not b.linear) or a.width != b.width
             for a, b in zip(eng.plan.blocks, plan.blocks)):
         eng = FusedChainEngine(model, plan)
         _ENGINES[model] = eng

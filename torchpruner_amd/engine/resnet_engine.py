@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, winograd_weights
+from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, cpad, winograd_weights
 
 
 @dataclass
@@ -74,7 +74,7 @@ def build_resnet_plan(model: nn.Module):
                 conv = getattr(blk, n)
                 bn = getattr(blk, "bn" + str(i + 1))
                 if conv.groups != 1 or conv.dilation != (1, 1) or conv.kernel_size[0] not in (1, 3) or \
-                        conv.padding[0] != conv.kernel_size[0] // 2 or conv.in_channels % 32 != 0:
+                        conv.padding[0] != conv.kernel_size[0] // 2:
                     return None, f"unsupported conv {conv}"
                 convs.append(_Conv(conv, bn))
             ds = None
@@ -85,8 +85,6 @@ def build_resnet_plan(model: nn.Module):
                     return None, "unsupported downsample"
                 ds = _Conv(d[0], d[1])
             plan.blocks.append(_Block(convs, ds))
-    if any(c.conv.out_channels % 4 for b in plan.blocks for c in b.convs) or c1.out_channels % 4:
-        return None, "channel counts must be multiples of 4"
     return plan, ""
 
 
@@ -131,13 +129,17 @@ class ResNetEngine:
     @torch.no_grad()
     def _pack_conv(self, c: _Conv, stem=False):
         w = c.conv.weight.detach().float()
-        if stem:  # pad Cin to 4, K = 49 taps x 4 channels padded to a multiple of 32
-            w = F.pad(w, (0, 0, 0, 0, 0, 4 - w.shape[1]))
+        cout = w.shape[0]
+        # activations carry channels zero-padded to a multiple of 32 (pruned, odd widths):
+        # padded filters have zero weights and a zero affine -> exact zeros downstream
+        cin_p = 4 if stem else cpad(w.shape[1])
+        w = F.pad(w, (0, 0, 0, 0, 0, cin_p - w.shape[1], 0, cpad(cout) - cout))
         wk = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
         k_pad = ops.require().conv_gen_k(c.conv.kernel_size[0], w.shape[1]) - wk.shape[1]
         if k_pad:
             wk = F.pad(wk, (0, k_pad))
         scale, shift = _fold(c.conv, c.bn)
+        scale, shift = F.pad(scale, (0, cpad(cout) - cout)), F.pad(shift, (0, cpad(cout) - cout))
         e = {"w": wk.contiguous(), "scale": scale, "shift": shift, "ks": c.conv.kernel_size[0],
              "stride": c.conv.stride[0], "pad": c.conv.padding[0]}
         if e["ks"] == 3 and e["stride"] == 1 and w.shape[1] % 8 == 0 and w.shape[0] % 32 == 0:
@@ -154,6 +156,7 @@ class ResNetEngine:
             blocks.append({"convs": [self._pack_conv(c) for c in b.convs],
                            "ds": self._pack_conv(b.downsample) if b.downsample is not None else None})
         fc_w = p.fc.weight.detach().float()
+        fc_w = F.pad(fc_w, (0, cpad(fc_w.shape[1]) - fc_w.shape[1]))
         fc_b = p.fc.bias.detach().float() if p.fc.bias is not None else torch.zeros(fc_w.shape[0],
                                                                                    device=fc_w.device)
         self._packed = {"stem": self._pack_conv(p.stem, stem=True), "blocks": blocks,
@@ -187,7 +190,13 @@ class ResNetEngine:
         zeroed (B, C) float tensors that receive the per-sample counts of positive outputs."""
         T = ops.require()
         P = self._pack()
-        apoz = apoz or {}
+        apoz = dict(apoz or {})
+        padded = []  # (user buffer, padded scratch) for channel counts that are not multiples of 32
+        for m, buf in apoz.items():
+            if buf.shape[1] % 32:
+                tmp = buf.new_zeros(buf.shape[0], cpad(buf.shape[1]))
+                padded.append((buf, tmp))
+                apoz[m] = tmp
         h = T.nchw_to_nhwc_pad(x.float().contiguous(), 4)
         h = self._conv(T, P["stem"], h, True, apoz=apoz.get(self.plan.stem.bn))
         mp = self.plan.maxpool
@@ -206,6 +215,8 @@ class ResNetEngine:
                 t = self._conv(T, ce, t, True, res=idn if last else None, apoz=apoz.get(c.bn))
             h = t
         feat = T.avgpool_nhwc(h)
+        for buf, tmp in padded:
+            buf.add_(tmp[:, :buf.shape[1]])
         return F.linear(feat, P["fc_w"], P["fc_b"])
 
     def eval_modules(self):
