@@ -13,6 +13,10 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
                          float* taylor, int HWo, int tay_group, float* ws, hipStream_t st);
 int tp_conv_gen_k(int ks, int Cin);
+hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                        int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
+                        const float* shift, int relu, const float* res, int res_stride, const float* mask,
+                        float* apoz, float* out, float* ws, hipStream_t st);
 hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
                        int pad, int cfg, int splits, const float* scale, const float* shift, int relu,
                        const float* res, float* apoz, float* out, float* ws, hipStream_t st);
@@ -372,6 +376,58 @@ at::Tensor nchw_to_nhwc_pad(const at::Tensor& x, int64_t Cp) {
   return y;
 }
 
+// Data gradient of a ResNet conv for the backward engine: g (B, H, W, C = forward Cout) NHWC,
+// wt (N = forward Cin, ks*ks*C) with k = (kh, kw, co) and the BN scale folded into co.
+// transposed: output (B, Ho, Wo, N) gathers y pixel ((oh + pad - kh)/stride, ...) (strided
+// conv dgrad); otherwise a plain stride-1 conv of g (1x1, or 3x3 with flipped taps).
+// Epilogue: v (+ res, res_stride-scattered) then out = mask > 0 ? v : 0 when mask is given.
+at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::optional<at::Tensor>& res,
+                        int64_t res_stride, const c10::optional<at::Tensor>& mask, int64_t ks, int64_t stride,
+                        int64_t pad, int64_t Ho, int64_t Wo, bool transposed, int64_t cfg, int64_t splits) {
+  need(g, "g", 4);
+  need(wt, "wt", 2);
+  const int64_t B = g.size(0), H = g.size(1), W = g.size(2), C = g.size(3), N = wt.size(0);
+  TORCH_CHECK(C % 32 == 0 && (ks == 1 || ks == 3), "conv_gen_bwd needs C % 32 == 0 and ks 1/3");
+  TORCH_CHECK(wt.size(1) == ks * ks * C, "wt must be (N, ks*ks*C)");
+  TORCH_CHECK(N % 4 == 0 && res_stride >= 1 && stride >= 1 && pad >= 0, "bad N/stride/pad");
+  if (!transposed) {
+    TORCH_CHECK(stride == 1, "non-transposed conv_gen_bwd is stride 1");
+    Ho = (H + 2 * pad - ks) + 1;
+    Wo = (W + 2 * pad - ks) + 1;
+  } else {
+    TORCH_CHECK((Ho + 2 * pad - ks) / stride + 1 == H && (Wo + 2 * pad - ks) / stride + 1 == W,
+                "Ho/Wo inconsistent with the forward conv geometry");
+  }
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  const float* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    need(*res, "res", 4);
+    const int64_t Hr = (Ho + res_stride - 1) / res_stride, Wr = (Wo + res_stride - 1) / res_stride;
+    TORCH_CHECK(res->size(0) == B && res->size(1) == Hr && res->size(2) == Wr && res->size(3) == N,
+                "res must be (B, ceil(Ho/s), ceil(Wo/s), N)");
+    rp = res->data_ptr<float>();
+  }
+  const float* mp = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    need(*mask, "mask", 4);
+    TORCH_CHECK(mask->size(0) == B && mask->size(1) == Ho && mask->size(2) == Wo && mask->size(3) == N,
+                "mask must be (B, Ho, Wo, N)");
+    mp = mask->data_ptr<float>();
+  }
+  auto out = at::empty({B, Ho, Wo, N}, g.options());
+  const int64_t kt = wt.size(1) / 32;
+  int64_t sp = transposed ? 1 : std::max<int64_t>(1, std::min<int64_t>(splits, kt));
+  const int64_t per = (kt + sp - 1) / sp;
+  sp = (kt + per - 1) / per;
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * Ho * Wo * N}, g.options());
+  TP_CHECK_HIP(tp_conv_gen2(g.data_ptr<float>(), wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)N,
+                            (int)ks, (int)stride, (int)pad, transposed ? 1 : 0, (int)Ho, (int)Wo, (int)cfg, (int)sp,
+                            nullptr, nullptr, 0, rp, (int)res_stride, mp, nullptr, out.data_ptr<float>(),
+                            sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+  return out;
+}
+
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
@@ -381,6 +437,8 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_gen(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, Tensor? res, Tensor(a!)? apoz, "
         "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
+  m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
+        "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits) -> (Tensor, Tensor)");
@@ -403,6 +461,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("maxpool_nhwc", &maxpool_nhwc);
   m.impl("avgpool_nhwc", &avgpool_nhwc);
   m.impl("conv_gen", &conv_gen);
+  m.impl("conv_gen_bwd", &conv_gen_bwd);
   m.impl("unpool2_nhwc", &unpool2_nhwc);
   m.impl("conv_wino_dgrad", &conv_wino_dgrad);
 }

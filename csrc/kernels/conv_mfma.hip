@@ -58,7 +58,29 @@ struct ConvArgs {
   int epi_lds;              // GEN: 1 -> two-phase LDS-transposed forward epilogue (TP_GEN_EPI=0 disables)
   int tay_group;            // EPI_BWD: >0 -> N = P pixel groups x tay_group channels (a dense-GEMM conv);
                             // Taylor of column n goes to slot n / tay_group of a (P, B, tay_group) slab
+  // GEN dgrad epilogue (ResNet backward engine)
+  const float* mask;        // [M][N] activation: out = mask > 0 ? v : 0 (ReLU backward), nullable
+  int res_stride;           // res is (B, ceil(Ho/s), ceil(Wo/s), N) added at pixels with oh, ow % s == 0
+                            // (gradient of a strided 1x1 downsample conv scattered back), 1 = dense
+  int parity;               // GEN 3: rows ordered (b, oh%2, ow%2, oh/2, ow/2) so a tile sees few taps
 };
+
+// GEN 3 output row m -> (image, oh, ow); parity order groups the four stride-2 phases
+__device__ __forceinline__ void gen3_pix(const ConvArgs& p, int m, int& b, int& oh, int& ow) {
+  const int HW = p.Ho * p.Wo;
+  b = m / HW;
+  const int r = m - b * HW;
+  if (p.parity) {
+    const int W2 = p.Wo >> 1, Q = (p.Ho >> 1) * W2;
+    const int cls = r / Q, q = r - cls * Q;
+    const int qy = q / W2;
+    oh = qy * 2 + (cls >> 1);
+    ow = (q - qy * W2) * 2 + (cls & 1);
+  } else {
+    oh = r / p.Wo;
+    ow = r - oh * p.Wo;
+  }
+}
 
 // Taylor slab index of (image b, GEMM column n)
 __device__ __forceinline__ long long tay_index(const ConvArgs& p, long long b, int n) {
@@ -105,9 +127,27 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Residual quad at output pixel ``pix`` (linear NHWC pixel index), columns n..n+3; res_stride
+// > 1 reads a strided-conv gradient that lives at the even-phase pixels only.
+__device__ __forceinline__ float4 res_quad(const ConvArgs& p, long long pix, int n) {
+  if (p.res_stride <= 1) return *reinterpret_cast<const float4*>(p.res + pix * p.N + n);
+  const int s = p.res_stride;
+  const long long HW = (long long)p.Ho * p.Wo;
+  const long long b = pix / HW;
+  const int r = (int)(pix - b * HW);
+  const int oh = r / p.Wo, ow = r - oh * p.Wo;
+  if (oh % s || ow % s) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const int Hr = (p.Ho + s - 1) / s, Wr = (p.Wo + s - 1) / s;
+  return *reinterpret_cast<const float4*>(p.res + ((b * Hr + oh / s) * Wr + ow / s) * p.N + n);
+}
+
 // GEN = 0: stride-1 "same" convs (VGG path, precomputed tap masks); GEN = 1: general strided /
 // padded conv (ResNet), Cin % 32 == 0; GEN = 2: the same with a 4-channel (padded NHWC) input,
-// where one 32-wide K slice holds 8 taps x 4 channels (7x7 stems).
+// where one 32-wide K slice holds 8 taps x 4 channels (7x7 stems); GEN = 3: transposed strided
+// conv = data gradient of a strided conv. x is dL/dy (B, H, W, Cin = forward Cout) and output
+// pixel (oh, ow) gathers y pixel ((oh + pad - kh) / s, (ow + pad - kw) / s) through tap (kh, kw)
+// when the division is exact; w[n = forward ci][k = (kh, kw, co)]. With parity row order a
+// tile only iterates the taps its stride phases use (1/4 of the 3x3 taps on average).
 template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI, int GEN = 0>
 __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, WM, WN) / 128) void conv_igemm(ConvArgs p) {
   using T = Tile<BM, BN, WM, WN>;
@@ -124,10 +164,30 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   const int n0 = (tile % n_tiles) * BN;
   if (m0 >= m_tiles * BM) return;
   const int split = blockIdx.y;
-  const int kt_total = p.K / BK;
-  const int kt_begin = split * p.k_tiles_per_split;
-  const int kt_end = min(kt_total, kt_begin + p.k_tiles_per_split);
   const int cin_tiles = p.Cin / BK;
+  unsigned tmask = (1u << (KS * KS)) - 1u;  // GEN 3: taps any row of this tile can use
+  if constexpr (GEN == 3) {
+    if (p.parity) {
+      const int HW = p.Ho * p.Wo, Q = HW >> 2;
+      const int ml = min(m0 + BM, p.M) - 1;
+      const int b0 = m0 / HW, b1 = ml / HW;
+      const int c0 = (m0 - b0 * HW) / Q, c1 = (ml - b1 * HW) / Q;
+      unsigned cls = 0;
+      for (int c = 0; c < 4; ++c) {
+        const bool in = b1 > b0 + 1 || (b1 == b0 ? (c >= c0 && c <= c1) : (c >= c0 || c <= c1));
+        cls |= in ? 1u << c : 0u;
+      }
+      tmask = 0;
+      for (int c = 0; c < 4; ++c) {
+        if (!((cls >> c) & 1u)) continue;
+        for (int t = 0; t < KS * KS; ++t)
+          if ((((c >> 1) + p.pad - t / KS) & 1) == 0 && (((c & 1) + p.pad - t % KS) & 1) == 0) tmask |= 1u << t;
+      }
+    }
+  }
+  const int kt_total = GEN == 3 ? __builtin_popcount(tmask) * cin_tiles : p.K / BK;
+  const int kt_begin = GEN == 3 ? 0 : split * p.k_tiles_per_split;
+  const int kt_end = GEN == 3 ? kt_total : min(kt_total, kt_begin + p.k_tiles_per_split);
 
   // ---- per-thread A rows: loop-invariant offsets + a bitmask of in-bounds taps ----------
   // Loads go through buffer descriptors: an out-of-range offset returns zeros in hardware,
@@ -146,7 +206,15 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     a_row[i] = id / (BK / 4);
     a_c4[i] = id % (BK / 4);
     const int m = m0 + a_row[i];
-    if constexpr (GEN != 0) {
+    if constexpr (GEN == 3) {
+      int b = 0, oh = 0, ow = 0;
+      if (m < p.M) gen3_pix(p, m, b, oh, ow);
+      a_mask[i] = m < p.M ? 1u : 0u;
+      a_oh[i] = oh + p.pad;
+      a_ow[i] = ow + p.pad;
+      a_off[i] = b * p.H * p.W * p.Cin;
+      continue;
+    } else if constexpr (GEN != 0) {
       // a_off = image base offset, a_oh/a_ow = top-left input pixel of the receptive field,
       // a_mask = row valid
       int b = 0, oh = 0, ow = 0;
@@ -186,7 +254,31 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   float4 ra[T::A_CHUNKS], rb[T::B_CHUNKS];
 
   auto load_tile = [&](int kt) {
-    if constexpr (GEN != 0) {
+    int kb = kt;  // K slice of the weight operand
+    if constexpr (GEN == 3) {
+      const int ti = kt / cin_tiles, cs = kt - ti * cin_tiles;
+      int tap = 0;
+      for (int t = 0, left = ti; t < KS * KS; ++t) {  // ti-th set bit of the tile's tap mask
+        if ((tmask >> t) & 1u) {
+          if (left == 0) {
+            tap = t;
+            break;
+          }
+          --left;
+        }
+      }
+      kb = tap * cin_tiles + cs;
+      const int kh = tap / KS, kw = tap % KS, s = p.stride;
+#pragma unroll
+      for (int i = 0; i < T::A_CHUNKS; ++i) {
+        const int th = a_oh[i] - kh, tw = a_ow[i] - kw;
+        const int yh = th / s, yw = tw / s;
+        const bool ok = a_mask[i] && th >= 0 && tw >= 0 && yh * s == th && yw * s == tw && yh < p.H && yw < p.W;
+        const unsigned vo = ok ? (unsigned)(a_off[i] + (yh * p.W + yw) * p.Cin + cs * BK + a_c4[i] * 4) * 4u : OOB;
+        const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
+        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+      }
+    } else if constexpr (GEN != 0) {
 #pragma unroll
       for (int i = 0; i < T::A_CHUNKS; ++i) {
         int tap, c;
@@ -233,7 +325,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     }
 #pragma unroll
     for (int i = 0; i < T::B_CHUNKS; ++i) {
-      const unsigned vo = b_off[i] >= 0 ? (unsigned)(b_off[i] + kt * BK * 4) : OOB;
+      const unsigned vo = b_off[i] >= 0 ? (unsigned)(b_off[i] + kb * BK * 4) : OOB;
       const f32x4 g = buf_load_f32x4(wr, (int)vo, 0, 0);
       rb[i] = make_float4(g[0], g[1], g[2], g[3]);
     }
@@ -342,17 +434,30 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
       if constexpr (EPI == EPI_PARTIAL) {
         *reinterpret_cast<float4*>(p.out + ((long long)split * p.M + m) * p.N + n) = v;
       } else {
-        const long long o = (long long)m * p.N + n;
+        long long pix = m;
+        if constexpr (GEN == 3) {
+          int b, oh, ow;
+          gen3_pix(p, m, b, oh, ow);
+          pix = ((long long)b * p.Ho + oh) * p.Wo + ow;
+        }
+        const long long o = pix * p.N + n;
         v.x = v.x * sc4.x + sh4.x;
         v.y = v.y * sc4.y + sh4.y;
         v.z = v.z * sc4.z + sh4.z;
         v.w = v.w * sc4.w + sh4.w;
         if (p.res) {
-          const float4 rr = *reinterpret_cast<const float4*>(p.res + o);
+          const float4 rr = res_quad(p, pix, n);
           v.x += rr.x;
           v.y += rr.y;
           v.z += rr.z;
           v.w += rr.w;
+        }
+        if (p.mask) {  // ReLU backward by the forward activation
+          const float4 a = *reinterpret_cast<const float4*>(p.mask + o);
+          v.x = a.x > 0.f ? v.x : 0.f;
+          v.y = a.y > 0.f ? v.y : 0.f;
+          v.z = a.z > 0.f ? v.z : 0.f;
+          v.w = a.w > 0.f ? v.w : 0.f;
         }
         if (p.relu) {
           v.x = nan_relu(v.x);
@@ -535,7 +640,15 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
       const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
       v = v * sc + sh;
-      if (p.res) v += p.res[o];
+      if (p.res) {
+        if (p.res_stride > 1) {
+          const float4 rq = res_quad(p, o / p.N, n & ~3);
+          v += (&rq.x)[n & 3];
+        } else {
+          v += p.res[o];
+        }
+      }
+      if (p.mask && !(p.mask[o] > 0.f)) v = 0.f;
       if (p.relu) v = nan_relu(v);
       p.out[o] = v;
       if (p.apoz && v > 0.f) atomicAdd(p.apoz + (o / p.N / p.HWo) * p.N + n, 1.f);
@@ -893,6 +1006,10 @@ hipError_t gen_cfg(int cfg, const tp::ConvArgs& a, int splits, hipStream_t st) {
 
 template <int EPI>
 hipError_t gen_dispatch(int ks, int gen, int cfg, const tp::ConvArgs& a, int splits, hipStream_t st) {
+  if constexpr (EPI == tp::EPI_FWD) {
+    if (gen == 3 && ks == 1) return gen_cfg<1, 3, EPI>(cfg, a, 1, st);
+    if (gen == 3 && ks == 3) return gen_cfg<3, 3, EPI>(cfg, a, 1, st);
+  }
   if (gen == 2 && ks == 7) return gen_cfg<7, 2, EPI>(cfg, a, splits, st);
   if (gen == 1 && ks == 1) return gen_cfg<1, 1, EPI>(cfg, a, splits, st);
   if (gen == 1 && ks == 3) return gen_cfg<3, 1, EPI>(cfg, a, splits, st);
@@ -904,12 +1021,31 @@ extern "C" int tp_conv_gen_k(int ks, int Cin) {
   return Cin == 4 ? (ks * ks * 4 + 31) / 32 * 32 : ks * ks * Cin;
 }
 
+extern "C" hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   hipStream_t st);
+
 extern "C" hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
                                   int stride, int pad, int cfg, int splits, const float* scale, const float* shift,
                                   int relu, const float* res, float* apoz, float* out, float* ws, hipStream_t st) {
+  return tp_conv_gen2(x, w, B, H, W, Cin, Cout, ks, stride, pad, 0, 0, 0, cfg, splits, scale, shift, relu, res, 1,
+                      nullptr, apoz, out, ws, st);
+}
+
+// Full entry: ``transposed`` = data gradient of a strided conv (GEN 3) producing Ho_t x Wo_t
+// (the forward conv's input size); ``mask`` = ReLU-backward activation; ``res_stride``: see
+// ConvArgs. Forward convs pass transposed = 0 (Ho_t/Wo_t ignored), mask = null, res_stride = 1.
+extern "C" hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   hipStream_t st) {
   using namespace tp;
-  const int gen = Cin == 4 ? 2 : 1;
-  if ((gen == 1 && Cin % 32 != 0) || Cout % 4 != 0) return hipErrorInvalidValue;
+  const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
+  if ((gen != 2 && Cin % 32 != 0) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
+  if (gen == 3 && (ks != 1 && ks != 3)) return hipErrorInvalidValue;
   ConvArgs a{};
   a.x = x;
   a.w = w;
@@ -919,8 +1055,10 @@ extern "C" hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, 
   a.Cin = Cin;
   a.N = Cout;
   a.K = tp_conv_gen_k(ks, Cin);
-  a.Ho = (H + 2 * pad - ks) / stride + 1;
-  a.Wo = (W + 2 * pad - ks) / stride + 1;
+  a.Ho = gen == 3 ? Ho_t : (H + 2 * pad - ks) / stride + 1;
+  a.Wo = gen == 3 ? Wo_t : (W + 2 * pad - ks) / stride + 1;
+  a.parity = gen == 3 && stride == 2 && a.Ho % 2 == 0 && a.Wo % 2 == 0;
+  if (gen == 3) splits = 1;
   a.stride = stride;
   a.pad = pad;
   a.M = B * a.Ho * a.Wo;
@@ -937,10 +1075,13 @@ extern "C" hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, 
   a.shift = shift;
   a.relu = relu;
   a.res = res;
+  a.res_stride = res_stride;
+  a.mask = mask;
   a.apoz = apoz;
   a.out = out;
   const char* ge = getenv("TP_GEN_EPI");
   a.epi_lds = ge ? atoi(ge) : 1;
+  if (gen == 3 || mask || res_stride > 1) a.epi_lds = 1;  // only the LDS epilogue implements these
   if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);
   if (!ws) return hipErrorInvalidValue;
   ConvArgs b = a;

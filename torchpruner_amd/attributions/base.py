@@ -342,6 +342,39 @@ class _AttributionMetric(ABC):
                 h.remove()
             self.restore_deterministic()
 
+    def _resnet_grad_engine(self, eval_modules):
+        """The ResNet engine when it can produce gradient scores for ``eval_modules`` (eval-mode
+        torchvision-layout ResNet, block BNs, mean cross-entropy criterion), else None."""
+        from ..engine.fused_chain import criterion_is_cross_entropy
+        from ..engine.resnet_engine import maybe_resnet_engine
+        eng = maybe_resnet_engine(self.model, eval_modules, self.device, grad=True)
+        if eng is None or not criterion_is_cross_entropy(self.criterion, self.device):
+            return None
+        return eng
+
+    def _resnet_grad_pass(self, eng, eval_modules, accs, mode):
+        """Per batch: one engine forward + input-gradient backward scores every module; the
+        (B, C_padded) slabs are folded into fp64 accumulators (16 layers per launch)."""
+        uniq = list(dict.fromkeys(eval_modules))
+        first = {}
+        for k, m in enumerate(eval_modules):
+            first.setdefault(m, k)
+        stats = accs[0].mode == "stats"
+        with torch.no_grad():
+            for i, x, y in self._batches():
+                res = eng.grad_scores(x, y, set(uniq), mode)
+                if stats:
+                    slabs = [res[m] for m in uniq]
+                    sums = [accs[first[m]].ensure_sum(res[m].shape[1], x.device, m.num_features) for m in uniq]
+                    for j in range(0, len(slabs), 16):
+                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], False, 0)
+                    for m in uniq:
+                        accs[first[m]].count += x.shape[0]
+                else:
+                    for m in uniq:
+                        accs[first[m]].add(res[m][:, :m.num_features].contiguous(), i)
+        return [accs[first[m]] for m in eval_modules]
+
     def _forward_capture_pass(self, eval_modules, on_out):
         """No-grad forward pass calling ``on_out(k, output, batch_index)`` per module."""
         state = {}

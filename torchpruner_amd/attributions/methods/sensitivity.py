@@ -19,8 +19,12 @@ class SensitivityAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            self._grad_capture_pass(eval_modules,
-                                    lambda k, a, g, i: accs[k].add(ops.channel_reduce(None, g, "sensitivity"), i))
+            rn = self._resnet_grad_engine(eval_modules)
+            if rn is not None:  # ResNets: forward + input-grad backward on the HIP engine
+                accs = self._resnet_grad_pass(rn, eval_modules, accs, "sensitivity")
+            else:
+                self._grad_capture_pass(eval_modules,
+                                        lambda k, a, g, i: accs[k].add(ops.channel_reduce(None, g, "sensitivity"), i))
         finally:
             self._end_run()
         return [self._finalize(a) for a in accs]

@@ -57,6 +57,8 @@ class TaylorAttributionMetric(_AttributionMetric):
                     for b in uniq:
                         accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
             accs = [accs[owner[b]] for b in blocks]
+        elif (rn := self._resnet_grad_engine(eval_modules)) is not None:
+            accs = self._resnet_grad_pass(rn, eval_modules, accs, mode)
         else:
             self._grad_capture_pass(eval_modules,
                                     lambda k, a, g, i: accs[k].add(ops.channel_reduce(a, g, mode), i))

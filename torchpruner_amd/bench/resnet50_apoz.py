@@ -18,7 +18,8 @@ import time
 import torch
 import torch.nn.functional as F
 
-from torchpruner_amd import APoZAttributionMetric, get_resnet_pruning_graph
+from torchpruner_amd import (APoZAttributionMetric, SensitivityAttributionMetric, TaylorAttributionMetric,
+                             get_resnet_pruning_graph)
 from torchpruner_amd.data import StreamLoader
 from torchpruner_amd.models import resnet50
 from torchpruner_amd.parallel import dist as pdist
@@ -30,7 +31,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--channels-last", type=int, default=1)
+    ap.add_argument("--metric", default="apoz", choices=["apoz", "taylor", "sensitivity"])
     args = ap.parse_args()
+    M = {"apoz": APoZAttributionMetric, "taylor": TaylorAttributionMetric,
+         "sensitivity": SensitivityAttributionMetric}[args.metric]
     ctx = pdist.init_distributed()
     dev, world = ctx.device, ctx.world_size
     torch.manual_seed(0)
@@ -42,8 +46,8 @@ def main():
                         channels_last=bool(args.channels_last))
     data = StreamLoader(args.steps * world, args.batch, (3, 224, 224), 1000, dev, seed=2,
                         channels_last=bool(args.channels_last))
-    APoZAttributionMetric(model, warm, F.cross_entropy, dev).run_many(modules, find_best_evaluation_module=True)
-    metric = APoZAttributionMetric(model, data, F.cross_entropy, dev)
+    M(model, warm, F.cross_entropy, dev).run_many(modules, find_best_evaluation_module=True)
+    metric = M(model, data, F.cross_entropy, dev)
     pdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -56,7 +60,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     if ctx.rank == 0:
-        print(json.dumps({"metric": "APoZ attribution images/sec (whole node), ResNet-50 224x224",
+        print(json.dumps({"metric": f"{M.__name__} attribution images/sec (whole node), ResNet-50 224x224",
                           "value": round(args.steps * args.batch * world / dt, 1), "unit": "images/s",
                           "n_gpus": world, "per_gpu_batch": args.batch, "steps": args.steps,
                           "modules_scored": len(modules), "dtype": "fp32", "data": "synthetic",

@@ -185,9 +185,11 @@ class ResNetEngine:
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands)
         return run(cfg, sp, h, apoz)
 
-    def forward(self, x: torch.Tensor, apoz: Optional[dict] = None):
+    def forward(self, x: torch.Tensor, apoz: Optional[dict] = None, save: bool = False):
         """Logits of the network; ``apoz`` maps BN modules of the blocks (bn1 / bn2 / ...) to
-        zeroed (B, C) float tensors that receive the per-sample counts of positive outputs."""
+        zeroed (B, C) float tensors that receive the per-sample counts of positive outputs.
+        ``save=True`` returns (logits, saved) with, per block, (input, internal post-ReLU
+        activations, output) in engine layout (NHWC, channel-padded) for :meth:`grad_scores`."""
         T = ops.require()
         P = self._pack()
         apoz = dict(apoz or {})
@@ -204,20 +206,120 @@ class ResNetEngine:
         s = mp.stride if isinstance(mp.stride, int) else mp.stride[0]
         pd = mp.padding if isinstance(mp.padding, int) else mp.padding[0]
         h = T.maxpool_nhwc(h, k, s, pd)
+        saved = []
         for blk, e in zip(self.plan.blocks, P["blocks"]):
             idn = h
             if e["ds"] is not None:
                 idn = self._conv(T, e["ds"], h, False)
             t = h
             n = len(e["convs"])
+            inner = []
             for i, (c, ce) in enumerate(zip(blk.convs, e["convs"])):
                 last = i == n - 1
                 t = self._conv(T, ce, t, True, res=idn if last else None, apoz=apoz.get(c.bn))
+                if not last:
+                    inner.append(t)
+            if save:
+                saved.append((h, inner, t))
             h = t
         feat = T.avgpool_nhwc(h)
         for buf, tmp in padded:
             buf.add_(tmp[:, :buf.shape[1]])
-        return F.linear(feat, P["fc_w"], P["fc_b"])
+        logits = F.linear(feat, P["fc_w"], P["fc_b"])
+        return (logits, saved) if save else logits
+
+    # ------------------------------------------------------------------ backward (Taylor, Sensitivity)
+    @staticmethod
+    @torch.no_grad()
+    def _bwd_operands(e):
+        """dgrad operands of a packed conv, cached in its entry: the BN scale of the conv's
+        output is folded into the weights' output channels (the gradient leaving a masked
+        epilogue is dL/d(BN output); the next GEMM consumes dL/d(conv output) = that x scale)."""
+        if "wt" in e:
+            return e
+        ks = e["ks"]
+        co = e["scale"].numel()
+        ci = e["w"].shape[1] // (ks * ks)
+        w4 = e["w"].view(co, ks, ks, ci) * e["scale"].view(co, 1, 1, 1)  # (co, kh, kw, ci)
+        if ks == 1:
+            e["wt"] = w4.view(co, ci).t().contiguous()
+        elif e["stride"] == 1:  # stride-1 3x3 dgrad = conv of g with flipped taps
+            e["wt"] = w4.flip(1, 2).permute(3, 1, 2, 0).reshape(ci, ks * ks * co).contiguous()
+            e["ut"] = winograd_weights(w4.permute(0, 3, 1, 2).flip(2, 3).transpose(0, 1))
+        else:  # strided: transposed gather kernel, natural tap order
+            e["wt"] = w4.permute(3, 1, 2, 0).reshape(ci, ks * ks * co).contiguous()
+        return e
+
+    def _dgrad(self, T, e, g, mask, res=None, res_stride=1, low_res=False):
+        """dL/d(input) of conv ``e`` from g = dL/d(conv output) (BN scale folded in), plus
+        ``res``, masked by ``mask`` (the input's post-ReLU activation). ``low_res``: a strided
+        1x1 conv's gradient at the output resolution (scattered by the consumer's res_stride)."""
+        e = self._bwd_operands(e)
+        B, H, W, C = g.shape
+        ks, s = e["ks"], e["stride"]
+        N = e["wt"].shape[0]
+        transposed = s > 1 and not low_res
+        Ho, Wo = (mask.shape[1], mask.shape[2]) if transposed else (H, W)
+        M, K = B * Ho * Wo, e["wt"].shape[1]
+        pad = e["pad"] if (transposed or ks == 3) else 0
+        if transposed:
+            cands = [(c, 1) for c in (0, 3, 4, 2)]
+        else:
+            cands = [c for c in TUNER.candidates(M, N, K) if c[0] in (0, 2, 3, 4)]
+        wino_ok = "ut" in e and res is None and mask is not None and H % 2 == 0 and W % 2 == 0
+        if wino_ok:
+            sp0 = _wino_splits(B * (H // 2) * (W // 2), N, C)
+            cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
+        key = ("rbwd", tuple(g.shape), N, ks, s, transposed, res is not None, res_stride, mask is not None)
+
+        def run(cfg, sp, gg=g, rr=res, mm=mask):
+            if cfg in (WINO, WINO_LDS):
+                return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, None, True, sp, cfg == WINO_LDS)
+            return T.conv_gen_bwd(gg, e["wt"], rr, res_stride, mm, ks, s if transposed else 1, pad, Ho, Wo,
+                                  transposed, cfg, sp)
+
+        cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands)
+        return run(cfg, sp)
+
+    def grad_scores(self, x: torch.Tensor, y: torch.Tensor, want, mode: str):
+        """One engine forward + input-gradient-only backward of the mean cross-entropy; returns
+        {BN module: (B, C_padded) per-sample ``ops.channel_reduce`` score} for the block BNs in
+        ``want`` (evaluation modules of conv1/conv2 of each block). No weight gradients, no
+        autograd graph; the backward stops at the earliest block holding a wanted BN."""
+        T = ops.require()
+        P = self._pack()
+        logits, saved = self.forward(x, save=True)
+        B = logits.shape[0]
+        _, g_log = ops.cross_entropy(logits, y, 1.0 / B, True)
+        g_feat = g_log @ P["fc_w"]  # (B, C_last padded)
+        y_last = saved[-1][2]
+        HW = y_last.shape[1] * y_last.shape[2]
+        # avg-pool backward + final ReLU of the last block: dL/d(pre-ReLU residual sum)
+        g_s = torch.where(y_last > 0, (g_feat / HW)[:, None, None, :], torch.zeros((), device=x.device)).contiguous()
+        blocks = self.plan.blocks
+        first = min((bi for bi, b in enumerate(blocks) if any(c.bn in want for c in b.convs[:-1])), default=None)
+        out = {}
+        if first is None:
+            return out
+        for bi in range(len(blocks) - 1, first - 1, -1):
+            blk, e = blocks[bi], P["blocks"][bi]
+            x_in, inner, _ = saved[bi]
+            g = g_s
+            for ci in range(len(blk.convs) - 1, 0, -1):
+                a_prev = inner[ci - 1]
+                g = self._dgrad(T, e["convs"][ci], g, a_prev)  # dL/d(bn_{ci} output), ReLU-masked
+                bn = blk.convs[ci - 1].bn
+                if bn in want:
+                    out[bn] = ops.channel_reduce(a_prev.permute(0, 3, 1, 2), g.permute(0, 3, 1, 2), mode)
+            if bi == first:
+                break
+            if e["ds"] is not None:
+                g_res = self._dgrad(T, e["ds"], g_s, None, low_res=True)
+                rs = e["ds"]["stride"]
+            else:
+                g_res, rs = g_s, 1
+            g_s = self._dgrad(T, e["convs"][0], g, x_in, res=g_res, res_stride=rs)
+        return out
 
     def eval_modules(self):
         """BN modules whose outputs the engine can count (block bn1/bn2/..., stem bn)."""
@@ -230,8 +332,9 @@ class ResNetEngine:
 _ENGINES: "weakref.WeakKeyDictionary[nn.Module, ResNetEngine]" = weakref.WeakKeyDictionary()
 
 
-def maybe_resnet_engine(model, eval_modules, device):
-    """A ResNetEngine when every eval module is a BN the engine counts, else None."""
+def maybe_resnet_engine(model, eval_modules, device, grad=False):
+    """A ResNetEngine when every eval module is a BN the engine counts (``grad``: scores by
+    :meth:`ResNetEngine.grad_scores`, block BNs only), else None."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda" or ops.backend() == "torch" or not ops.available() or model.training:
         return None
@@ -244,7 +347,7 @@ def maybe_resnet_engine(model, eval_modules, device):
     if eng is None or [c.conv for c in eng._all_convs()] != [c.conv for c in ResNetEngine(model, plan)._all_convs()]:
         eng = ResNetEngine(model, plan)
         _ENGINES[model] = eng
-    ok = set(map(id, eng.eval_modules()))
+    ok = set(map(id, eng.eval_modules()[1:] if grad else eng.eval_modules()))
     if not all(id(m) in ok for m in eval_modules):
         return None
     return eng
