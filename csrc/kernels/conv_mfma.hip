@@ -62,21 +62,25 @@ struct ConvArgs {
   const float* mask;        // [M][N] activation: out = mask > 0 ? v : 0 (ReLU backward), nullable
   int res_stride;           // res is (B, ceil(Ho/s), ceil(Wo/s), N) added at pixels with oh, ow % s == 0
                             // (gradient of a strided 1x1 downsample conv scattered back), 1 = dense
-  int parity;               // GEN 3: rows ordered (b, oh%2, ow%2, oh/2, ow/2) so a tile sees few taps
+  int parity;               // GEN 3: rows ordered (oh%2, ow%2, b, oh/2, ow/2) so a tile sees few taps
 };
 
-// GEN 3 output row m -> (image, oh, ow); parity order groups the four stride-2 phases
+// GEN 3 output row m -> (image, oh, ow). Parity order makes each stride-2 phase class one
+// contiguous range of B*Ho*Wo/4 rows: all but the (at most 3) boundary tiles see ONE class and
+// iterate exactly the taps it uses (1, 2, 2 or 4 of the 9 for a 3x3/s2 dgrad).
 __device__ __forceinline__ void gen3_pix(const ConvArgs& p, int m, int& b, int& oh, int& ow) {
-  const int HW = p.Ho * p.Wo;
-  b = m / HW;
-  const int r = m - b * HW;
   if (p.parity) {
-    const int W2 = p.Wo >> 1, Q = (p.Ho >> 1) * W2;
-    const int cls = r / Q, q = r - cls * Q;
+    const int W2 = p.Wo >> 1, Q = (p.Ho >> 1) * W2, BQ = p.B * Q;
+    const int cls = m / BQ, r = m - cls * BQ;
+    b = r / Q;
+    const int q = r - b * Q;
     const int qy = q / W2;
     oh = qy * 2 + (cls >> 1);
     ow = (q - qy * W2) * 2 + (cls & 1);
   } else {
+    const int HW = p.Ho * p.Wo;
+    b = m / HW;
+    const int r = m - b * HW;
     oh = r / p.Wo;
     ow = r - oh * p.Wo;
   }
@@ -168,18 +172,10 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   unsigned tmask = (1u << (KS * KS)) - 1u;  // GEN 3: taps any row of this tile can use
   if constexpr (GEN == 3) {
     if (p.parity) {
-      const int HW = p.Ho * p.Wo, Q = HW >> 2;
-      const int ml = min(m0 + BM, p.M) - 1;
-      const int b0 = m0 / HW, b1 = ml / HW;
-      const int c0 = (m0 - b0 * HW) / Q, c1 = (ml - b1 * HW) / Q;
-      unsigned cls = 0;
-      for (int c = 0; c < 4; ++c) {
-        const bool in = b1 > b0 + 1 || (b1 == b0 ? (c >= c0 && c <= c1) : (c >= c0 || c <= c1));
-        cls |= in ? 1u << c : 0u;
-      }
+      const int BQ = p.B * (p.Ho >> 1) * (p.Wo >> 1);
+      const int c0 = m0 / BQ, c1 = (min(m0 + BM, p.M) - 1) / BQ;
       tmask = 0;
-      for (int c = 0; c < 4; ++c) {
-        if (!((cls >> c) & 1u)) continue;
+      for (int c = c0; c <= c1; ++c) {
         for (int t = 0; t < KS * KS; ++t)
           if ((((c >> 1) + p.pad - t / KS) & 1) == 0 && (((c & 1) + p.pad - t % KS) & 1) == 0) tmask |= 1u << t;
       }
@@ -997,9 +993,12 @@ template <int KS, int GEN, int EPI>
 hipError_t gen_cfg(int cfg, const tp::ConvArgs& a, int splits, hipStream_t st) {
   switch (cfg) {
     case 0: return launch_gen<128, 128, 64, 64, KS, GEN, EPI>(a, splits, st);
+    case 1: return launch_gen<256, 64, 64, 64, KS, GEN, EPI>(a, splits, st);
     case 2: return launch_gen<64, 64, 32, 32, KS, GEN, EPI>(a, splits, st);
     case 3: return launch_gen<128, 64, 64, 32, KS, GEN, EPI>(a, splits, st);
     case 4: return launch_gen<128, 128, 64, 32, KS, GEN, EPI>(a, splits, st);
+    case 5: return launch_gen<256, 64, 64, 32, KS, GEN, EPI>(a, splits, st);
+    case 6: return launch_gen<128, 64, 32, 32, KS, GEN, EPI>(a, splits, st);
   }
   return hipErrorInvalidValue;
 }

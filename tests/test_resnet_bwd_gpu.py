@@ -19,7 +19,7 @@ def _dgrad_ref(g, wf, in_hw, stride, pad):
 @pytest.mark.parametrize("ks,stride,C,N,in_hw", [(3, 2, 64, 32, (16, 16)), (3, 2, 32, 64, (15, 13)),
                                                  (1, 2, 64, 32, (14, 14)), (1, 2, 32, 32, (9, 7)),
                                                  (3, 1, 32, 64, (10, 12))])
-@pytest.mark.parametrize("cfg", [0, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("with_mask", [False, True])
 def test_conv_gen_bwd_transposed(cuda, ks, stride, C, N, in_hw, cfg, with_mask):
     from torchpruner_amd import ops

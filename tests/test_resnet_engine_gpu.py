@@ -20,7 +20,7 @@ def _ref(x_nhwc, w, scale, shift, stride, pad, relu, res=None):
 
 @pytest.mark.parametrize("ks,stride,cin,cout,hw", [(1, 1, 64, 96, 14), (1, 2, 64, 128, 14), (3, 1, 32, 64, 9),
                                                    (3, 2, 64, 64, 15), (7, 2, 4, 64, 38)])
-@pytest.mark.parametrize("cfg,splits", [(0, 1), (2, 3), (3, 1), (4, 2)])
+@pytest.mark.parametrize("cfg,splits", [(0, 1), (1, 2), (2, 3), (3, 1), (4, 2), (5, 1), (6, 1)])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_conv_gen(cuda, ks, stride, cin, cout, hw, cfg, splits, with_res):
     from torchpruner_amd import ops

@@ -171,7 +171,6 @@ class ResNetEngine:
         Ho, Wo = (H + 2 * pd - ks) // s + 1, (W + 2 * pd - ks) // s + 1
         M, N, K = B * Ho * Wo, e["scale"].numel(), e["w"].shape[1]
         cands = TUNER.candidates(M, N, K)
-        cands = [c for c in cands if c[0] in (0, 2, 3, 4)]  # tile configs conv_gen instantiates
         if "u" in e and res is None and H % 2 == 0 and W % 2 == 0:
             sp0 = _wino_splits(B * (H // 2) * (W // 2), N, C)
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + ([(WINO_LDS, 1)] if sp0 > 1 else []) + cands
@@ -263,9 +262,9 @@ class ResNetEngine:
         M, K = B * Ho * Wo, e["wt"].shape[1]
         pad = e["pad"] if (transposed or ks == 3) else 0
         if transposed:
-            cands = [(c, 1) for c in (0, 3, 4, 2)]
+            cands = [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
         else:
-            cands = [c for c in TUNER.candidates(M, N, K) if c[0] in (0, 2, 3, 4)]
+            cands = TUNER.candidates(M, N, K)
         wino_ok = "ut" in e and res is None and mask is not None and H % 2 == 0 and W % 2 == 0
         if wino_ok:
             sp0 = _wino_splits(B * (H // 2) * (W // 2), N, C)
