@@ -13,6 +13,8 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
                          float* taylor, int HWo, int tay_group, float* ws, hipStream_t st);
 int tp_conv_gen_k(int ks, int Cin);
+hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
+                         int ks, int stride, int pad, int Kpad, int cfg, int splits, hipStream_t st);
 hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
                         int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
                         const float* shift, int relu, const float* res, int res_stride, const float* mask,
@@ -428,6 +430,32 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
   return out;
 }
 
+// Weight gradient: g (B, Ho, Wo, Cout) and x (B, H, W, Cin) NHWC -> dW (Cout, Kpad) with column
+// k = (kh, kw, ci) (Kpad = ks*ks*Cin rounded up to 32; padded columns are zero).
+at::Tensor conv_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t ks, int64_t stride, int64_t pad, int64_t cfg,
+                      int64_t splits) {
+  need(g, "g", 4);
+  need(x, "x", 4);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = g.size(3);
+  TORCH_CHECK(Cin % 4 == 0 && Cout % 4 == 0, "conv_wgrad needs Cin % 4 == 0 and Cout % 4 == 0");
+  TORCH_CHECK(ks >= 1 && stride >= 1 && pad >= 0, "bad conv geometry");
+  const int64_t Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
+  TORCH_CHECK(g.size(0) == B && g.size(1) == Ho && g.size(2) == Wo, "g must be (B, Ho, Wo, Cout) of this conv");
+  const int64_t Kpad = (ks * ks * Cin + 31) / 32 * 32;
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  auto dw = at::empty({Cout, Kpad}, g.options());
+  const int64_t slices = (B * Ho * Wo + 31) / 32;
+  int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, slices));
+  const int64_t per = (slices + sp - 1) / sp;
+  sp = (slices + per - 1) / per;
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * Cout * Kpad}, g.options());
+  TP_CHECK_HIP(tp_conv_wgrad(g.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(),
+                             sp > 1 ? ws.data_ptr<float>() : nullptr, (int)B, (int)H, (int)W, (int)Cin, (int)Cout,
+                             (int)ks, (int)stride, (int)pad, (int)Kpad, (int)cfg, (int)sp, cur_stream()));
+  return dw;
+}
+
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
@@ -437,6 +465,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_gen(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, Tensor? res, Tensor(a!)? apoz, "
         "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
+  m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
@@ -462,6 +491,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("avgpool_nhwc", &avgpool_nhwc);
   m.impl("conv_gen", &conv_gen);
   m.impl("conv_gen_bwd", &conv_gen_bwd);
+  m.impl("conv_wgrad", &conv_wgrad);
   m.impl("unpool2_nhwc", &unpool2_nhwc);
   m.impl("conv_wino_dgrad", &conv_wino_dgrad);
 }

@@ -1,0 +1,233 @@
+// Weight gradient of a convolution on fp32 MFMA: the finetune half of the
+// prune -> finetune loop (BASELINE config #5), so pruned shapes never wait for a JIT'd library
+// kernel.
+//
+//   dW[co][k] = sum_p g[p][co] * x_im2col[p][k],   k = (kh*KS + kw)*Cin + ci,  p = (b, oh, ow)
+//
+// GEMM with M = Cout, N = K columns and the reduction over all B*Ho*Wo output pixels. Both
+// operands are pixel-major in memory (NHWC rows), so slices of 32 pixels are staged into LDS
+// exactly as they sit in HBM (float4 copies, no transposes): sA[p][co], sB[p][k]. An MFMA
+// 32x32x2 step takes the two pixel rows 2s, 2s+1: lane (li, lh) reads sA[2s+lh][col li] and
+// sB[2s+lh][col li] — ds_read_b32 with consecutive lanes on consecutive words, and row pitch
+// = 32 (mod 64) words so the two lane halves hit disjoint banks.
+//
+// The pixel range is split over grid.y (split-K): partial slabs [split][Cout][Kpad] are summed
+// in split order by wgrad_combine (deterministic, no atomics).
+#include "tp_common.h"
+
+namespace tp {
+
+struct WgradArgs {
+  const float* g;  // (B, Ho, Wo, Cout) NHWC
+  const float* x;  // (B, H, W, Cin) NHWC
+  float* out;      // [splits][Cout][Kpad]
+  int B, H, W, Cin, Ho, Wo, Cout, ks, stride, pad;
+  int Kc;    // ks*ks*Cin valid columns
+  int Kpad;  // columns of the output (multiple of 32)
+  int P;     // B*Ho*Wo
+  int slices_per_split;
+  long long g_elems, x_elems;
+};
+
+template <int BM, int BN, int WM, int WN>
+struct WTile {
+  static constexpr int NW = (BM / WM) * (BN / WN);
+  static constexpr int NT = 64 * NW;
+  static constexpr int LDA = BM + 32, LDB = BN + 32;  // row pitch == 32 (mod 64) words
+  static constexpr int STAGE = 32 * (LDA + LDB);
+  static constexpr int A_CH = 32 * BM / 4 / NT;
+  static constexpr int B_CH = 32 * BN / 4 / NT;
+  static constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert(A_CH >= 1 && B_CH >= 1 && (NT % (BM / 4)) == 0 && (NT % (BN / 4)) == 0, "tile/thread mapping");
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradArgs p) {
+  using T = WTile<BM, BN, WM, WN>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k_tiles = (p.Kpad + BN - 1) / BN;
+  const int co0 = (blockIdx.x / k_tiles) * BM, k0 = (blockIdx.x % k_tiles) * BN;
+  const int s_begin = blockIdx.y * p.slices_per_split;
+  const int s_end = min((p.P + 31) / 32, s_begin + p.slices_per_split);
+  constexpr unsigned OOB = 0x80000000u;
+  const i32x4 gr = make_rsrc(p.g, (unsigned)(p.g_elems * 4));
+  const i32x4 xr = make_rsrc(p.x, (unsigned)(p.x_elems * 4));
+
+  // per-thread column decode of the im2col operand (fixed for the whole pixel loop)
+  const int b_c4 = tid % (BN / 4), b_r0 = tid / (BN / 4);
+  const int kcol = k0 + 4 * b_c4;
+  const int tap = kcol / p.Cin, ci = kcol - tap * p.Cin;
+  const int kh = tap / p.ks, kw = tap - kh * p.ks;
+  const bool col_ok = kcol < p.Kc;
+  const int a_c4 = tid % (BM / 4), a_r0 = tid / (BM / 4);
+  const bool co_ok = co0 + 4 * a_c4 < p.Cout;
+  const int HWo = p.Ho * p.Wo;
+
+  float4 ra[T::A_CH], rb[T::B_CH];
+  auto load = [&](int sl) {
+    const int p0 = sl * 32;
+#pragma unroll
+    for (int i = 0; i < T::A_CH; ++i) {
+      const int pix = p0 + a_r0 + i * (T::NT / (BM / 4));
+      const bool ok = co_ok && pix < p.P;
+      const unsigned vo = ok ? (unsigned)(pix * p.Cout + co0 + 4 * a_c4) * 4u : OOB;
+      const f32x4 v = buf_load_f32x4(gr, (int)vo, 0, 0);
+      ra[i] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_CH; ++i) {
+      const int pix = p0 + b_r0 + i * (T::NT / (BN / 4));
+      bool ok = col_ok && pix < p.P;
+      int off = 0;
+      if (ok) {
+        const int b = pix / HWo, r = pix - b * HWo;
+        const int oh = r / p.Wo, ow = r - oh * p.Wo;
+        const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+        ok = ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        off = ((b * p.H + ih) * p.W + iw) * p.Cin + ci;
+      }
+      const f32x4 v = buf_load_f32x4(xr, (int)(ok ? (unsigned)off * 4u : OOB), 0, 0);
+      rb[i] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store = [&](int buf) {
+    float* sA = smem + buf * T::STAGE;
+    float* sB = sA + 32 * T::LDA;
+#pragma unroll
+    for (int i = 0; i < T::A_CH; ++i)
+      *reinterpret_cast<float4*>(sA + (a_r0 + i * (T::NT / (BM / 4))) * T::LDA + 4 * a_c4) = ra[i];
+#pragma unroll
+    for (int i = 0; i < T::B_CH; ++i)
+      *reinterpret_cast<float4*>(sB + (b_r0 + i * (T::NT / (BN / 4))) * T::LDB + 4 * b_c4) = rb[i];
+  };
+
+  f32x16 acc[T::TM][T::TN];
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int wm0 = (wave / (BN / WN)) * WM, wn0 = (wave % (BN / WN)) * WN;
+  const int li = lane & 31, lh = lane >> 5;
+
+  if (s_begin < s_end) {
+    load(s_begin);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int sl = s_begin; sl < s_end; ++sl) {
+      const bool more = sl + 1 < s_end;
+      if (more) load(sl + 1);
+      const float* sA = smem + buf * T::STAGE + lh * T::LDA + wm0 + li;
+      const float* sB = smem + buf * T::STAGE + 32 * T::LDA + lh * T::LDB + wn0 + li;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        float af[T::TM], bf[T::TN];
+#pragma unroll
+        for (int i = 0; i < T::TM; ++i) af[i] = sA[(2 * s) * T::LDA + i * 32];
+#pragma unroll
+        for (int j = 0; j < T::TN; ++j) bf[j] = sB[(2 * s) * T::LDB + j * 32];
+#pragma unroll
+        for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < T::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (more) store(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  float* out = p.out + (long long)blockIdx.y * p.Cout * p.Kpad;
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j) {
+      const int k = k0 + wn0 + j * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (co < p.Cout && k < p.Kpad) out[(long long)co * p.Kpad + k] = acc[i][j][r];
+      }
+    }
+}
+
+// dW = sum of the split slabs in split order (float4 per thread); columns >= Kc are zero.
+__global__ __launch_bounds__(256) void wgrad_combine(const float* __restrict__ slabs, float* __restrict__ dw,
+                                                     int splits, long long n4) {
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += (long long)gridDim.x * blockDim.x) {
+    float4 s = reinterpret_cast<const float4*>(slabs)[t];
+    for (int q = 1; q < splits; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(slabs)[q * n4 + t];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    reinterpret_cast<float4*>(dw)[t] = s;
+  }
+}
+
+}  // namespace tp
+
+namespace {
+template <int BM, int BN, int WM, int WN>
+hipError_t launch_wgrad(const tp::WgradArgs& a, int splits, hipStream_t st) {
+  const int tiles = ((a.Cout + BM - 1) / BM) * ((a.Kpad + BN - 1) / BN);
+  tp::conv_wgrad<BM, BN, WM, WN><<<dim3(tiles, splits), tp::WTile<BM, BN, WM, WN>::NT, 0, st>>>(a);
+  return hipGetLastError();
+}
+}  // namespace
+
+// Tile configs: 0 = 128x128 (4 waves of 64x64), 1 = 64x64 (4 waves of 32x32), 2 = 128x64
+// (4 waves of 64x32). ``ws`` holds splits*Cout*Kpad floats (may alias dw when splits == 1).
+// x (B, H, W, Cin) NHWC with Cin % 4 == 0; g (B, Ho, Wo, Cout) NHWC with Cout % 4 == 0;
+// dw (Cout, Kpad), Kpad % 32 == 0 and >= ks*ks*Cin.
+extern "C" hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,
+                                    int Cin, int Cout, int ks, int stride, int pad, int Kpad, int cfg, int splits,
+                                    hipStream_t st) {
+  using namespace tp;
+  if (Cin % 4 || Cout % 4 || Kpad % 32 || Kpad < ks * ks * Cin || splits < 1) return hipErrorInvalidValue;
+  WgradArgs a{};
+  a.g = g;
+  a.x = x;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.Cout = Cout;
+  a.ks = ks;
+  a.stride = stride;
+  a.pad = pad;
+  a.Ho = (H + 2 * pad - ks) / stride + 1;
+  a.Wo = (W + 2 * pad - ks) / stride + 1;
+  a.Kc = ks * ks * Cin;
+  a.Kpad = Kpad;
+  a.P = B * a.Ho * a.Wo;
+  a.g_elems = (long long)a.P * Cout;
+  a.x_elems = (long long)B * H * W * Cin;
+  if (a.g_elems * 4 >= (1ll << 31) || a.x_elems * 4 >= (1ll << 31)) return hipErrorInvalidValue;
+  const int slices = (a.P + 31) / 32;
+  splits = std::min(splits, slices);
+  a.slices_per_split = (slices + splits - 1) / splits;
+  splits = (slices + a.slices_per_split - 1) / a.slices_per_split;
+  a.out = splits > 1 ? ws : dw;
+  if (splits > 1 && !ws) return hipErrorInvalidValue;
+  hipError_t e;
+  switch (cfg) {
+    case 0: e = launch_wgrad<128, 128, 64, 64>(a, splits, st); break;
+    case 1: e = launch_wgrad<64, 64, 32, 32>(a, splits, st); break;
+    case 2: e = launch_wgrad<128, 64, 64, 32>(a, splits, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  if (e != hipSuccess || splits == 1) return e;
+  const long long n4 = (long long)Cout * Kpad / 4;
+  const unsigned grid = (unsigned)std::min<long long>(ceil_div(n4, 256), 4096);
+  wgrad_combine<<<grid, 256, 0, st>>>(ws, dw, splits, n4);
+  return hipGetLastError();
+}

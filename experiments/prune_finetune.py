@@ -41,19 +41,25 @@ def main():
     ap.add_argument("--score-batches", type=int, default=2)
     ap.add_argument("--metric", default="taylor", choices=["taylor", "apoz"])
     ap.add_argument("--res", type=int, default=224)
+    ap.add_argument("--convs", default="native", choices=["native", "library"],
+                    help="native: training convolutions on the precompiled HIP kernels (engine/train.py); "
+                         "library: MIOpen (JIT-compiles every new pruned shape)")
     args = ap.parse_args()
     ctx = pdist.init_distributed()
     dev, world = ctx.device, ctx.world_size
     torch.manual_seed(0)
     np.random.seed(0)
     model = resnet50().to(dev).to(memory_format=torch.channels_last)
+    if args.convs == "native":
+        from torchpruner_amd.engine.train import enable_native_convs
+        enable_native_convs(model)
     wrapper = PrunableDDP(model, device=dev)
     opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
     pruner = Pruner(model, (3, args.res, args.res), dev, optimizer=opt)
     shape = (3, args.res, args.res)
     log = {"params": [count_parameters(model)], "rounds": []}
     for r in range(args.rounds):
-        # warm-up steps absorb MIOpen's JIT compilation of kernels for the new pruned shapes
+        # warm-up steps absorb kernel selection for the new pruned shapes (MIOpen: JIT compilation)
         t0 = time.perf_counter()
         wu = StreamLoader(3 * world, args.batch, shape, 1000, dev, seed=50 + r, channels_last=True)
         train(wrapper, dev, F.cross_entropy, wu, opt, r, log_every=0)

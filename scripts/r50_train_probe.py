@@ -10,11 +10,14 @@ import torch.nn.functional as F  # noqa: E402
 from torchpruner_amd.models import resnet50  # noqa: E402
 
 B = int(os.environ.get("B", 128))
-fmts = os.environ.get("FMTS", "nchw,nhwc").split(",")
+fmts = os.environ.get("FMTS", "nchw,nhwc,native").split(",")
 for fmt in fmts:
     torch.manual_seed(0)
-    mf = torch.channels_last if fmt == "nhwc" else torch.contiguous_format
+    mf = torch.contiguous_format if fmt == "nchw" else torch.channels_last
     m = resnet50().cuda().to(memory_format=mf).train()
+    if fmt == "native":
+        from torchpruner_amd.engine.train import enable_native_convs
+        print(f"native convs: {len(enable_native_convs(m))}", flush=True)
     opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
     x = torch.randn(B, 3, 224, 224, device="cuda").contiguous(memory_format=mf)
     y = torch.randint(0, 1000, (B,), device="cuda")

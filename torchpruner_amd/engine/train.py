@@ -1,0 +1,181 @@
+"""Native convolutions for training: the finetune half of prune -> finetune (BASELINE config #5).
+
+The reference finetunes with cuDNN convolutions (experiments/utils/train.py:11-48). On ROCm the
+library path is MIOpen, which JIT-compiles and benchmarks kernels for every new convolution
+shape: after each pruning round every pruned layer has a new shape, and the first steps of the
+round pay 20-40 s of compilation (profiles/resnet50_prune_finetune_1gpu.log). Here the
+convolutions of a model run on the precompiled gfx950 kernels instead, through autograd:
+
+  forward   implicit-GEMM fp32 MFMA conv (``tpamd.conv_gen``), bias in the epilogue
+  dgrad     stride 1: the same kernel on flipped, transposed weights; strided: the transposed
+            gather kernel with parity-ordered rows (``tpamd.conv_gen_bwd``)
+  wgrad     pixel-split MFMA GEMM, deterministic split combine (``tpamd.conv_wgrad``, K3)
+
+BatchNorm, activations, pooling and the loss stay PyTorch ops (autograd composes them), so
+any model works; only ``nn.Conv2d`` modules the kernels support are switched. Pruned (odd)
+channel counts are zero-padded to the kernels' granule inside the op and sliced off again:
+the parameters, their gradients and the optimizer state keep the module's real shapes.
+Every kernel choice is timed once per shape (``TUNER``, like ``cudnn.benchmark``) — a few
+milliseconds instead of a JIT compile.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import types
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .fused_chain import _CU, TUNER, cpad
+
+
+def _geom(conv: nn.Conv2d):
+    return conv.kernel_size[0], conv.stride[0], conv.padding[0]
+
+
+def eligible(conv: nn.Module) -> bool:
+    """Whether ``conv`` runs on the native training kernels (square 1x1 / 3x3 kernels, or the
+    7x7 stem on <= 4 input channels; groups 1, no dilation, zero padding)."""
+    if not isinstance(conv, nn.Conv2d) or conv.groups != 1 or conv.dilation != (1, 1):
+        return False
+    if conv.padding_mode != "zeros" or isinstance(conv.padding, str):
+        return False
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    if k[0] != k[1] or s[0] != s[1] or p[0] != p[1]:
+        return False
+    return k[0] in (1, 3) or (k[0] == 7 and conv.in_channels <= 4)
+
+
+def _wgrad_splits(P, tiles):
+    slices = math.ceil(P / 32)
+    sp = 1
+    while tiles * sp < 2 * _CU and sp * 2 <= max(1, slices // 8):
+        sp *= 2
+    return sp
+
+
+class _NativeConv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, ks, stride, pad):
+        T = ops.require()
+        B, Cin, H, W = x.shape
+        Cout = weight.shape[0]
+        cin_p = 4 if ks == 7 else cpad(Cin)
+        cout_p = cpad(Cout)
+        xh = x.permute(0, 2, 3, 1)
+        if cin_p != Cin:
+            xh = F.pad(xh, (0, cin_p - Cin))
+        xh = xh.float().contiguous()
+        wp = F.pad(weight.detach().float(), (0, 0, 0, 0, 0, cin_p - Cin, 0, cout_p - Cout))
+        wk = wp.permute(0, 2, 3, 1).reshape(cout_p, -1)
+        kk = T.conv_gen_k(ks, cin_p)
+        if kk != wk.shape[1]:
+            wk = F.pad(wk, (0, kk - wk.shape[1]))
+        wk = wk.contiguous()
+        shift = F.pad(bias.detach().float(), (0, cout_p - Cout)).contiguous() if bias is not None else None
+        Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
+        M = B * Ho * Wo
+
+        def run(cfg, sp):
+            return T.conv_gen(xh, wk, None, shift, False, None, None, ks, stride, pad, cfg, sp)
+
+        cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run,
+                               cands=TUNER.candidates(M, cout_p, kk))
+        y = run(cfg, sp)
+        if cout_p != Cout:
+            y = y[..., :Cout].contiguous()
+        ctx.save_for_backward(xh, wp)
+        ctx.geom = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype,
+                    weight.is_contiguous(memory_format=torch.channels_last) and weight.dim() == 4)
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        T = ops.require()
+        xh, wp = ctx.saved_tensors
+        ks, stride, pad, Cin, Cout, H, W, has_bias, wdtype, w_cl = ctx.geom
+        cout_p, cin_p = wp.shape[0], wp.shape[1]
+        g = gy.permute(0, 2, 3, 1).float()
+        if cout_p != Cout:
+            g = F.pad(g, (0, cout_p - Cout))
+        g = g.contiguous()
+        B, Ho, Wo = g.shape[0], g.shape[1], g.shape[2]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if ks in (1, 3):
+                same = stride == 1 and pad == ks // 2
+                if same:
+                    wt = wp.flip(2, 3).permute(1, 2, 3, 0).reshape(cin_p, -1).contiguous()
+                else:
+                    wt = wp.permute(1, 2, 3, 0).reshape(cin_p, -1).contiguous()
+                M, K = B * H * W, wt.shape[1]
+
+                def run(cfg, sp):
+                    return T.conv_gen_bwd(g, wt, None, 1, None, ks, 1 if same else stride, pad, H, W, not same,
+                                          cfg, sp)
+
+                cands = TUNER.candidates(M, cin_p, K) if same else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
+                cfg, sp = TUNER.choose(("tdgrad", tuple(g.shape), cin_p, ks, stride, pad), M, cin_p, K, run,
+                                       cands=cands)
+                dxh = run(cfg, sp)[..., :Cin]
+                dx = dxh.permute(0, 3, 1, 2).to(gy.dtype)
+            else:  # 7x7 stem input gradient (rarely needed: the input is data)
+                dx = torch.nn.grad.conv2d_input((B, Cin, H, W), wp[:Cout, :Cin].to(gy.dtype), gy, stride, pad)
+        if ctx.needs_input_grad[1]:
+            kk = -(-ks * ks * cin_p // 32) * 32
+            P = B * Ho * Wo
+
+            def run_w(cfg, sp):
+                return T.conv_wgrad(g, xh, ks, stride, pad, cfg, sp)
+
+            cands = []
+            for cfg, (bm, bn) in ((0, (128, 128)), (2, (128, 64)), (1, (64, 64))):
+                sp = _wgrad_splits(P, math.ceil(cout_p / bm) * math.ceil(kk / bn))
+                cands += [(cfg, sp)] + ([(cfg, sp // 2)] if sp > 1 else [])
+            cfg, sp = TUNER.choose(("twgrad", tuple(g.shape), tuple(xh.shape), ks, stride, pad), cout_p, kk, P, run_w,
+                                   cands=cands)
+            dwk = run_w(cfg, sp)
+            dw = dwk[:Cout, :ks * ks * cin_p].view(Cout, ks, ks, cin_p)[..., :Cin].permute(0, 3, 1, 2)
+            dw = dw.contiguous(memory_format=torch.channels_last if w_cl else torch.contiguous_format).to(wdtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = gy.sum((0, 2, 3))
+        return dx, dw, db, None, None, None
+
+
+def _native_forward(self, x):
+    if not x.is_cuda or x.dtype != torch.float32 or self.weight.dtype != torch.float32:
+        return type(self).forward(self, x)
+    ks, s, p = _geom(self)
+    return _NativeConv2d.apply(x, self.weight, self.bias, ks, s, p)
+
+
+def enable_native_convs(model: nn.Module) -> list:
+    """Route every eligible ``nn.Conv2d`` of ``model`` through the native kernels (instance-level
+    ``forward`` override; pruning keeps working because weights are re-packed per call).
+    Returns the switched modules; undo with :func:`disable_native_convs`."""
+    if not ops.available() or ops.backend() == "torch":
+        return []
+    switched = []
+    for m in model.modules():
+        if eligible(m) and "forward" not in m.__dict__:
+            m.forward = types.MethodType(_native_forward, m)
+            switched.append(m)
+    return switched
+
+
+def disable_native_convs(modules) -> None:
+    for m in modules:
+        m.__dict__.pop("forward", None)
+
+
+@contextlib.contextmanager
+def native_convs(model: nn.Module, enable: bool = True):
+    """``with native_convs(model): loss.backward()`` — scoped :func:`enable_native_convs`."""
+    switched = enable_native_convs(model) if enable else []
+    try:
+        yield switched
+    finally:
+        disable_native_convs(switched)
