@@ -41,7 +41,8 @@ struct WTile {
   static_assert(A_CH >= 1 && B_CH >= 1 && (NT % (BM / 4)) == 0 && (NT % (BN / 4)) == 0, "tile/thread mapping");
 };
 
-template <int BM, int BN, int WM, int WN>
+// DIRECT: 1x1 / stride 1 / no padding — the im2col operand is x itself (no pixel decode).
+template <int BM, int BN, int WM, int WN, bool DIRECT>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradArgs p) {
   using T = WTile<BM, BN, WM, WN>;
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
@@ -79,8 +80,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradAr
     for (int i = 0; i < T::B_CH; ++i) {
       const int pix = p0 + b_r0 + i * (T::NT / (BN / 4));
       bool ok = col_ok && pix < p.P;
-      int off = 0;
-      if (ok) {
+      int off = pix * p.Cin + ci;
+      if (!DIRECT && ok) {
         const int b = pix / HWo, r = pix - b * HWo;
         const int oh = r / p.Wo, ow = r - oh * p.Wo;
         const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
@@ -179,7 +180,11 @@ namespace {
 template <int BM, int BN, int WM, int WN>
 hipError_t launch_wgrad(const tp::WgradArgs& a, int splits, hipStream_t st) {
   const int tiles = ((a.Cout + BM - 1) / BM) * ((a.Kpad + BN - 1) / BN);
-  tp::conv_wgrad<BM, BN, WM, WN><<<dim3(tiles, splits), tp::WTile<BM, BN, WM, WN>::NT, 0, st>>>(a);
+  const dim3 grid(tiles, splits);
+  if (a.ks == 1 && a.stride == 1 && a.pad == 0)
+    tp::conv_wgrad<BM, BN, WM, WN, true><<<grid, tp::WTile<BM, BN, WM, WN>::NT, 0, st>>>(a);
+  else
+    tp::conv_wgrad<BM, BN, WM, WN, false><<<grid, tp::WTile<BM, BN, WM, WN>::NT, 0, st>>>(a);
   return hipGetLastError();
 }
 }  // namespace

@@ -11,7 +11,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("ks,stride,Cin,Cout,hw", [(1, 1, 64, 96, (14, 14)), (1, 2, 32, 64, (15, 13)),
+@pytest.mark.parametrize("ks,stride,Cin,Cout,hw", [(1, 1, 64, 96, (14, 14)), (1, 1, 36, 40, (7, 9)), (1, 2, 32, 64, (15, 13)),
                                                    (3, 1, 36, 52, (10, 12)), (3, 2, 64, 32, (16, 16)),
                                                    (7, 2, 4, 64, (30, 30))])
 @pytest.mark.parametrize("cfg", [0, 1, 2])
