@@ -423,37 +423,57 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     }
     int cur_b = -1;
     float4 cnt = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int row = tid / C4; ncol_ok && row < BM; row += T::NT / C4) {
+    // rows are visited in passes of RSTEP; the residual / mask quads of PF passes are loaded
+    // together first (PF global loads in flight per thread instead of one round trip per row)
+    constexpr int RSTEP = T::NT / C4, RPT = BM / RSTEP, PF = RPT < 4 ? RPT : 4;
+    static_assert(BM % RSTEP == 0 && RPT % PF == 0, "epilogue row passes");
+    const int row0 = tid / C4;
+    for (int it0 = 0; it0 < RPT; it0 += PF) {
+      float4 rq[PF], mq[PF];
+      long long pq[PF];
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int m = m0 + row0 + (it0 + u) * RSTEP;
+        const bool ok = ncol_ok && m < p.M;
+        long long pix = m;
+        if constexpr (GEN == 3) {
+          if (ok) {
+            int b, oh, ow;
+            gen3_pix(p, m, b, oh, ow);
+            pix = ((long long)b * p.Ho + oh) * p.Wo + ow;
+          }
+        }
+        pq[u] = pix;
+        rq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        mq[u] = make_float4(1.f, 1.f, 1.f, 1.f);
+        if constexpr (EPI != EPI_PARTIAL) {
+          if (ok && p.res) rq[u] = res_quad(p, pix, n);
+          if (ok && p.mask) mq[u] = *reinterpret_cast<const float4*>(p.mask + pix * p.N + n);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+      const int row = row0 + (it0 + u) * RSTEP;
       const int m = m0 + row;
-      if (m >= p.M) break;
+      if (!ncol_ok || m >= p.M) continue;
       float4 v = *reinterpret_cast<const float4*>(ts + row * LDT + c4 * 4);
       if constexpr (EPI == EPI_PARTIAL) {
         *reinterpret_cast<float4*>(p.out + ((long long)split * p.M + m) * p.N + n) = v;
       } else {
-        long long pix = m;
-        if constexpr (GEN == 3) {
-          int b, oh, ow;
-          gen3_pix(p, m, b, oh, ow);
-          pix = ((long long)b * p.Ho + oh) * p.Wo + ow;
-        }
-        const long long o = pix * p.N + n;
+        const long long o = pq[u] * p.N + n;
         v.x = v.x * sc4.x + sh4.x;
         v.y = v.y * sc4.y + sh4.y;
         v.z = v.z * sc4.z + sh4.z;
         v.w = v.w * sc4.w + sh4.w;
-        if (p.res) {
-          const float4 rr = res_quad(p, pix, n);
-          v.x += rr.x;
-          v.y += rr.y;
-          v.z += rr.z;
-          v.w += rr.w;
-        }
+        v.x += rq[u].x;
+        v.y += rq[u].y;
+        v.z += rq[u].z;
+        v.w += rq[u].w;
         if (p.mask) {  // ReLU backward by the forward activation
-          const float4 a = *reinterpret_cast<const float4*>(p.mask + o);
-          v.x = a.x > 0.f ? v.x : 0.f;
-          v.y = a.y > 0.f ? v.y : 0.f;
-          v.z = a.z > 0.f ? v.z : 0.f;
-          v.w = a.w > 0.f ? v.w : 0.f;
+          v.x = mq[u].x > 0.f ? v.x : 0.f;
+          v.y = mq[u].y > 0.f ? v.y : 0.f;
+          v.z = mq[u].z > 0.f ? v.z : 0.f;
+          v.w = mq[u].w > 0.f ? v.w : 0.f;
         }
         if (p.relu) {
           v.x = nan_relu(v.x);
@@ -480,6 +500,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           cnt.z += v.z > 0.f ? 1.f : 0.f;
           cnt.w += v.w > 0.f ? 1.f : 0.f;
         }
+      }
       }
     }
     if constexpr (EPI == EPI_FWD) {
