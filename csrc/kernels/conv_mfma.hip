@@ -627,18 +627,17 @@ template <int EPI>
 __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __restrict__ slabs, int splits) {
   const long long MN = (long long)p.M * p.N;
   if constexpr (EPI == EPI_FWD_POOL) {
-    const long long total = MN / 4;
-    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
-      const int n = (int)(t % p.N);
-      const long long mp = t / p.N;
+    const unsigned total = (unsigned)(MN / 4), N = (unsigned)p.N;
+    for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+      const int n = (int)(t % N);
+      const unsigned mp = t / N;
       const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
       float best = 0.f;
       int arg = 0;
       for (int q = 0; q < 4; ++q) {
-        const long long o = (mp * 4 + q) * p.N + n;
+        const unsigned o = (mp * 4 + q) * N + n;
         float v = 0.f;
-        for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
+        for (int s = 0; s < splits; ++s) v += slabs[(size_t)s * MN + o];
         v = v * sc + sh;
         if (p.relu) v = nan_relu(v);
         if (q == 0 || v > best || (v != v && best == best)) {
@@ -650,25 +649,71 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       p.out_argmax[t] = (uint8_t)arg;
     }
   } else if constexpr (EPI == EPI_FWD) {
-    for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < MN;
-         o += (long long)gridDim.x * blockDim.x) {
-      const int n = (int)(o % p.N);
-      float v = 0.f;
-      for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
-      const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
-      v = v * sc + sh;
-      if (p.res) {
-        if (p.res_stride > 1) {
-          const float4 rq = res_quad(p, o / p.N, n & ~3);
-          v += (&rq.x)[n & 3];
-        } else {
-          v += p.res[o];
+    // 32-bit index math (host guarantees M*N < 2^31): 64-bit div/mod per element made this
+    // combine kernel ~5x slower than its memory traffic
+    const unsigned N = (unsigned)p.N;
+    if ((N & 3u) == 0) {  // float4 columns
+      const unsigned N4 = N >> 2, total = (unsigned)(MN >> 2);
+      const float4* S = reinterpret_cast<const float4*>(slabs);
+      for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const unsigned row = t / N4;
+        const int n = (int)(t - row * N4) * 4;
+        float4 v = S[t];
+        for (int q = 1; q < splits; ++q) {
+          const float4 w = S[(size_t)q * total + t];
+          v.x += w.x;
+          v.y += w.y;
+          v.z += w.z;
+          v.w += w.w;
+        }
+        const float4 sc = p.scale ? *reinterpret_cast<const float4*>(p.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float4 sh = p.shift ? *reinterpret_cast<const float4*>(p.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v.x = v.x * sc.x + sh.x;
+        v.y = v.y * sc.y + sh.y;
+        v.z = v.z * sc.z + sh.z;
+        v.w = v.w * sc.w + sh.w;
+        if (p.res) {
+          const float4 r = res_quad(p, row, n);
+          v.x += r.x;
+          v.y += r.y;
+          v.z += r.z;
+          v.w += r.w;
+        }
+        if (p.mask) {
+          const float4 a = *reinterpret_cast<const float4*>(p.mask + (size_t)t * 4);
+          v.x = a.x > 0.f ? v.x : 0.f;
+          v.y = a.y > 0.f ? v.y : 0.f;
+          v.z = a.z > 0.f ? v.z : 0.f;
+          v.w = a.w > 0.f ? v.w : 0.f;
+        }
+        if (p.relu) {
+          v.x = nan_relu(v.x);
+          v.y = nan_relu(v.y);
+          v.z = nan_relu(v.z);
+          v.w = nan_relu(v.w);
+        }
+        *reinterpret_cast<float4*>(p.out + (size_t)t * 4) = v;
+        if (p.apoz) {
+          float* ap = p.apoz + (size_t)(row / (unsigned)p.HWo) * N + n;
+          if (v.x > 0.f) atomicAdd(ap, 1.f);
+          if (v.y > 0.f) atomicAdd(ap + 1, 1.f);
+          if (v.z > 0.f) atomicAdd(ap + 2, 1.f);
+          if (v.w > 0.f) atomicAdd(ap + 3, 1.f);
         }
       }
-      if (p.mask && !(p.mask[o] > 0.f)) v = 0.f;
-      if (p.relu) v = nan_relu(v);
-      p.out[o] = v;
-      if (p.apoz && v > 0.f) atomicAdd(p.apoz + (o / p.N / p.HWo) * p.N + n, 1.f);
+    } else {  // ragged columns (e.g. a 10-way classifier): scalar, no res / mask / apoz users
+      const unsigned total = (unsigned)MN;
+      for (unsigned o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+        const unsigned n = o % N;
+        float v = 0.f;
+        for (int q = 0; q < splits; ++q) v += slabs[(size_t)q * total + o];
+        v = v * (p.scale ? p.scale[n] : 1.f) + (p.shift ? p.shift[n] : 0.f);
+        if (p.res) v += p.res[o];
+        if (p.mask && !(p.mask[o] > 0.f)) v = 0.f;
+        if (p.relu) v = nan_relu(v);
+        p.out[o] = v;
+        if (p.apoz && v > 0.f) atomicAdd(p.apoz + (size_t)(o / N / (unsigned)p.HWo) * N + n, 1.f);
+      }
     }
   } else if (p.HWo > 64) {
     // EPI_BWD, large images: handled by conv_epilogue_bwd_img (block per image x 64 channels)
@@ -875,7 +920,9 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   a.M = B * H * W;
   a.x_elems = unpool ? (long long)B * (H / 2) * (W / 2) * Cin : (long long)B * H * W * Cin;
   // buffer descriptors address 32-bit byte offsets
-  if (a.x_elems * 4 >= (1ll << 31) || (long long)Cout * a.K * 4 >= (1ll << 31)) return hipErrorInvalidValue;
+  if (a.x_elems * 4 >= (1ll << 31) || (long long)Cout * a.K * 4 >= (1ll << 31) ||
+      (long long)a.M * a.N >= (1ll << 31))
+    return hipErrorInvalidValue;
   const int kt = a.K / 32;
   splits = std::max(1, std::min(splits, kt));
   a.k_tiles_per_split = (kt + splits - 1) / splits;
@@ -930,6 +977,7 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
   a.W = W;
   a.N = K;
   a.M = B * H * W;
+  if ((long long)a.M * K >= (1ll << 31)) return hipErrorInvalidValue;
   a.scale = scale;
   a.shift = shift;
   a.relu = relu;
