@@ -11,8 +11,15 @@ extern "C" {
 hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w, int B, int H, int W, int Cin,
                          int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
-                         float* taylor, int HWo, int tay_group, float* ws, hipStream_t st);
+                         float* taylor, int HWo, int tay_group, float* ws, int tay_mode, hipStream_t st);
 int tp_conv_gen_k(int ks, int Cin);
+int tp_bn_groups(int P, int C);
+hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
+                           float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
+                           float* b, double* ws, hipStream_t st);
+hipError_t tp_bn_bwd_train(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
+                           const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a, float* k1,
+                           float* k2, double* ws, hipStream_t st);
 hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                          int ks, int stride, int pad, int Kpad, int cfg, int splits, hipStream_t st);
 hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
@@ -34,7 +41,7 @@ hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C, int H, in
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
-                        hipStream_t st);
+                        int tay_mode, hipStream_t st);
 }
 
 namespace {
@@ -101,7 +108,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
   TP_CHECK_HIP(tp_conv_igemm(x.data_ptr<float>(), nullptr, w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin,
                              (int)Cout, (int)ks, pool ? 1 : 0, 0, pool ? EPI_FWD_POOL : EPI_FWD, (int)cfg, (int)sp, sc,
                              sh, relu ? 1 : 0, out.data_ptr<float>(), pool ? am.data_ptr<uint8_t>() : nullptr, nullptr,
-                             nullptr, (int)(H * W), 0, sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                             nullptr, (int)(H * W), 0, sp > 1 ? ws.data_ptr<float>() : nullptr, 0, cur_stream()));
   return {out, am};
 }
 
@@ -114,7 +121,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
 at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_argmax, const at::Tensor& wt,
                       const at::Tensor& act, const c10::optional<at::Tensor>& bn_scale,
                       const c10::optional<at::Tensor>& taylor, bool want_out, int64_t ks, int64_t cfg,
-                      int64_t splits, int64_t tay_group) {
+                      int64_t splits, int64_t tay_group, int64_t tay_mode) {
   need(g, "g", 4);
   need(wt, "wt", 2);
   need(act, "act", 4);
@@ -150,7 +157,8 @@ at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_ar
                              wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, (int)ks, 0,
                              unpool ? 1 : 0, EPI_BWD, (int)cfg, (int)sp, sc, nullptr, 0,
                              want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(), tay,
-                             (int)(H * W), (int)tay_group, sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                             (int)(H * W), (int)tay_group, sp > 1 ? ws.data_ptr<float>() : nullptr, (int)tay_mode,
+                             cur_stream()));
   return out;
 }
 
@@ -219,7 +227,7 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
                             0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, staged ? 1 : 0, sc, sh, relu ? 1 : 0,
                             out.data_ptr<float>(),
                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap,
-                            sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                            sp > 1 ? ws.data_ptr<float>() : nullptr, 0, cur_stream()));
   return {out, am};
 }
 
@@ -227,7 +235,8 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
 // flipped/transposed kernel, (16, Cout, Cin).
 at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_argmax, const at::Tensor& ut,
                            const at::Tensor& act, const c10::optional<at::Tensor>& bn_scale,
-                           const c10::optional<at::Tensor>& taylor, bool want_out, int64_t splits, bool staged) {
+                           const c10::optional<at::Tensor>& taylor, bool want_out, int64_t splits, bool staged,
+                           int64_t tay_mode) {
   need(g, "g", 4);
   need(act, "act", 4);
   const bool unpool = g_argmax.has_value() && g_argmax->defined();
@@ -263,7 +272,7 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
                             ut.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, unpool ? 1 : 0, EPI_BWD,
                             (int)sp, staged ? 1 : 0, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
                             act.data_ptr<float>(), tay, nullptr, sp > 1 ? ws.data_ptr<float>() : nullptr,
-                            cur_stream()));
+                            (int)tay_mode, cur_stream()));
   return out;
 }
 
@@ -456,6 +465,63 @@ at::Tensor conv_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t ks, int6
   return dw;
 }
 
+// Training-mode BatchNorm over the last dim of an NHWC activation x (..., C), C % 4 == 0.
+// Updates running_mean / running_var in place (momentum, unbiased variance) when given.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+                                                             const c10::optional<at::Tensor>& beta,
+                                                             const c10::optional<at::Tensor>& running_mean,
+                                                             const c10::optional<at::Tensor>& running_var, double eps,
+                                                             double momentum) {
+  need(x, "x", -1);
+  const int64_t C = x.size(-1), P = x.numel() / std::max<int64_t>(C, 1);
+  TORCH_CHECK(C % 4 == 0 && P > 0, "bn_train_fwd needs C % 4 == 0 and a non-empty batch");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const float* ga = opt_ptr(gamma, C, "gamma");
+  const float* be = opt_ptr(beta, C, "beta");
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    need(*running_mean, "running_mean", 1);
+    need(*running_var, "running_var", 1);
+    TORCH_CHECK(running_mean->numel() == C && running_var->numel() == C, "running stats must have C elements");
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  auto y = at::empty_like(x);
+  auto stats = at::empty({4, C}, x.options());  // mean, invstd, a, b
+  auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
+  float* sp = stats.data_ptr<float>();
+  TP_CHECK_HIP(tp_bn_fwd_train(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
+                               (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(),
+                               cur_stream()));
+  return {y, stats[0], stats[1]};
+}
+
+// Backward of bn_train_fwd: (dx or undefined, dgamma, dbeta).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(const at::Tensor& g, const at::Tensor& x,
+                                                             const c10::optional<at::Tensor>& gamma,
+                                                             const at::Tensor& mean, const at::Tensor& invstd,
+                                                             bool want_dx) {
+  need(g, "g", -1);
+  need(x, "x", -1);
+  TORCH_CHECK(g.sizes() == x.sizes(), "g and x must have the same shape");
+  const int64_t C = x.size(-1), P = x.numel() / std::max<int64_t>(C, 1);
+  TORCH_CHECK(C % 4 == 0 && P > 0, "bn_train_bwd needs C % 4 == 0");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const float* ga = opt_ptr(gamma, C, "gamma");
+  const float* mp = opt_ptr(mean, C, "mean");
+  const float* ip = opt_ptr(invstd, C, "invstd");
+  auto coef = at::empty({5, C}, x.options());  // dgamma, dbeta, a, k1, k2
+  auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
+  at::Tensor dx;
+  if (want_dx) dx = at::empty_like(x);
+  float* cp = coef.data_ptr<float>();
+  TP_CHECK_HIP(tp_bn_bwd_train(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
+                               (int)P, (int)C, ga, mp, ip, cp, cp + C, cp + 2 * C, cp + 3 * C, cp + 4 * C,
+                               ws.data_ptr<double>(), cur_stream()));
+  return {dx, coef[0], coef[1]};
+}
+
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
@@ -465,6 +531,10 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_gen(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, Tensor? res, Tensor(a!)? apoz, "
         "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
+  m.def("bn_train_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+        "float eps, float momentum) -> (Tensor, Tensor, Tensor)");
+  m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx) "
+        "-> (Tensor, Tensor, Tensor)");
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
@@ -472,12 +542,12 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits) -> (Tensor, Tensor)");
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
-        "bool want_out, int ks, int cfg, int splits, int tay_group=0) -> Tensor");
+        "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
         "bool staged=True, Tensor(a!)? apoz=None) -> (Tensor, Tensor)");
   m.def("conv_wino_dgrad(Tensor g, Tensor? g_argmax, Tensor ut, Tensor act, Tensor? bn_scale, "
-        "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True) -> Tensor");
+        "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True, int tay_mode=0) -> Tensor");
 }
 
 void register_engine_ops_impl(torch::Library& m) {
@@ -492,6 +562,8 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_gen", &conv_gen);
   m.impl("conv_gen_bwd", &conv_gen_bwd);
   m.impl("conv_wgrad", &conv_wgrad);
+  m.impl("bn_train_fwd", &bn_train_fwd);
+  m.impl("bn_train_bwd", &bn_train_bwd);
   m.impl("unpool2_nhwc", &unpool2_nhwc);
   m.impl("conv_wino_dgrad", &conv_wino_dgrad);
 }

@@ -1,0 +1,238 @@
+// Training-mode BatchNorm2d on NHWC activations: batch statistics,
+// normalisation and the backward pass of the finetune loop, deterministic (fixed-order
+// two-level reductions, no atomics).
+//
+//   x: P rows (= B*H*W pixels) x C channels, C % 4 == 0
+//   stats   : partial[g][0|1][c] = sum / sum of squares over row group g  (pass 1)
+//             finalize: mean, biased var -> invstd, running-stat update  (pass 2, fp64)
+//   forward : y = x * a[c] + b[c],  a = gamma * invstd, b = beta - mean * a
+//   backward: partial sums of g and g * xhat (pass 1), finalize -> (sum_g, sum_gxhat),
+//             dx = a * (g - sum_g / P - xhat * sum_gxhat / P)
+//
+// A block owns a 64-wide column quad range (16 threads x float4) x 16 row lanes, and walks
+// rows_per_group rows; the 16 row lanes are folded in LDS in a fixed order.
+#include "tp_common.h"
+
+namespace tp {
+
+constexpr int BN_T = 256, BN_CQ = 16, BN_RL = BN_T / BN_CQ;  // 16 column quads x 16 row lanes
+
+// MODE 0: (sum x, sum x^2); MODE 1: (sum g, sum g * (x - mean) * invstd)
+template <int MODE>
+__global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, const float* __restrict__ g,
+                                                   const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                   double* __restrict__ part, int P, int C, int rows_per_group) {
+  __shared__ double red[2][BN_RL][BN_CQ * 4];
+  const int cq = threadIdx.x % BN_CQ, rl = threadIdx.x / BN_CQ;
+  const int c = (blockIdx.x * BN_CQ + cq) * 4;
+  const int r0 = blockIdx.y * rows_per_group, r1 = min(P, r0 + rows_per_group);
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+  if (c < C) {
+    float4 mu = s0, is = s0;
+    if (MODE == 1) {
+      mu = *reinterpret_cast<const float4*>(mean + c);
+      is = *reinterpret_cast<const float4*>(invstd + c);
+    }
+    // 4 independent rows per iteration: 4 (8 in backward) loads in flight per thread
+    constexpr int U = 4;
+    int r = r0 + rl;
+    for (; r + (U - 1) * BN_RL < r1; r += U * BN_RL) {
+      float4 v[U], d[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = *reinterpret_cast<const float4*>(x + (size_t)(r + u * BN_RL) * C + c);
+        if (MODE == 1) d[u] = *reinterpret_cast<const float4*>(g + (size_t)(r + u * BN_RL) * C + c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (MODE == 0) {
+          s0.x += v[u].x;
+          s0.y += v[u].y;
+          s0.z += v[u].z;
+          s0.w += v[u].w;
+          s1.x += v[u].x * v[u].x;
+          s1.y += v[u].y * v[u].y;
+          s1.z += v[u].z * v[u].z;
+          s1.w += v[u].w * v[u].w;
+        } else {
+          s0.x += d[u].x;
+          s0.y += d[u].y;
+          s0.z += d[u].z;
+          s0.w += d[u].w;
+          s1.x += d[u].x * (v[u].x - mu.x) * is.x;
+          s1.y += d[u].y * (v[u].y - mu.y) * is.y;
+          s1.z += d[u].z * (v[u].z - mu.z) * is.z;
+          s1.w += d[u].w * (v[u].w - mu.w) * is.w;
+        }
+      }
+    }
+    for (; r < r1; r += BN_RL) {
+      const float4 v = *reinterpret_cast<const float4*>(x + (size_t)r * C + c);
+      if (MODE == 0) {
+        s0.x += v.x;
+        s0.y += v.y;
+        s0.z += v.z;
+        s0.w += v.w;
+        s1.x += v.x * v.x;
+        s1.y += v.y * v.y;
+        s1.z += v.z * v.z;
+        s1.w += v.w * v.w;
+      } else {
+        const float4 d = *reinterpret_cast<const float4*>(g + (size_t)r * C + c);
+        s0.x += d.x;
+        s0.y += d.y;
+        s0.z += d.z;
+        s0.w += d.w;
+        s1.x += d.x * (v.x - mu.x) * is.x;
+        s1.y += d.y * (v.y - mu.y) * is.y;
+        s1.z += d.z * (v.z - mu.z) * is.z;
+        s1.w += d.w * (v.w - mu.w) * is.w;
+      }
+    }
+  }
+  red[0][rl][cq * 4 + 0] = s0.x;
+  red[0][rl][cq * 4 + 1] = s0.y;
+  red[0][rl][cq * 4 + 2] = s0.z;
+  red[0][rl][cq * 4 + 3] = s0.w;
+  red[1][rl][cq * 4 + 0] = s1.x;
+  red[1][rl][cq * 4 + 1] = s1.y;
+  red[1][rl][cq * 4 + 2] = s1.z;
+  red[1][rl][cq * 4 + 3] = s1.w;
+  __syncthreads();
+  if (threadIdx.x < 2 * BN_CQ * 4) {
+    const int which = threadIdx.x / (BN_CQ * 4), col = threadIdx.x % (BN_CQ * 4);
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < BN_RL; ++i) t += red[which][i][col];
+    const int cc = blockIdx.x * BN_CQ * 4 + col;
+    if (cc < C) part[((size_t)blockIdx.y * 2 + which) * C + cc] = t;
+  }
+}
+
+// Forward finalize: mean / invstd for the apply pass, running statistics (PyTorch semantics:
+// running_var takes the unbiased variance), and the affine folded into (a, b).
+__global__ __launch_bounds__(256) void bn_fwd_finalize(const double* __restrict__ part, int groups, int P, int C,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, float momentum, float* __restrict__ run_mean,
+                                                       float* __restrict__ run_var, float* __restrict__ mean,
+                                                       float* __restrict__ invstd, float* __restrict__ a,
+                                                       float* __restrict__ b) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int i = 0; i < groups; ++i) {
+    s += part[(size_t)(2 * i) * C + c];
+    q += part[(size_t)(2 * i + 1) * C + c];
+  }
+  const double m = s / P;
+  const double var = fmax(q / P - m * m, 0.0);
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)m;
+  invstd[c] = is;
+  if (run_mean) {
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)m;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(P > 1 ? var * P / (P - 1) : var);
+  }
+  const float ga = gamma ? gamma[c] : 1.f, be = beta ? beta[c] : 0.f;
+  a[c] = ga * is;
+  b[c] = be - (float)m * ga * is;
+}
+
+// Backward finalize: dgamma = sum(g * xhat), dbeta = sum(g), and the coefficients of
+// dx = a * g + k1 + k2 * x  (k1, k2 fold the mean-subtraction terms).
+__global__ __launch_bounds__(256) void bn_bwd_finalize(const double* __restrict__ part, int groups, int P, int C,
+                                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                                       float* __restrict__ dbeta, float* __restrict__ a,
+                                                       float* __restrict__ k1, float* __restrict__ k2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int i = 0; i < groups; ++i) {
+    sg += part[(size_t)(2 * i) * C + c];
+    sgx += part[(size_t)(2 * i + 1) * C + c];
+  }
+  if (dgamma) dgamma[c] = (float)sgx;
+  if (dbeta) dbeta[c] = (float)sg;
+  const double is = invstd[c], ga = gamma ? gamma[c] : 1.0;
+  const double ac = ga * is;
+  // dx = ac * (g - sg/P - xhat * sgx/P), xhat = (x - mean) * is
+  a[c] = (float)ac;
+  k2[c] = (float)(-ac * is * sgx / P);
+  k1[c] = (float)(-ac * sg / P - (-ac * is * sgx / P) * mean[c]);
+}
+
+// out = x * a[c] + (BWD ? g-term : b[c]) — forward: y = x*a + b; backward: dx = g*a + k1 + k2*x
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, const float* __restrict__ g,
+                                                const float* __restrict__ a, const float* __restrict__ b,
+                                                const float* __restrict__ k2, float* __restrict__ out, unsigned n4,
+                                                unsigned C4) {
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += gridDim.x * blockDim.x) {
+    const unsigned c = (t % C4) * 4;
+    const float4 v = reinterpret_cast<const float4*>(x)[t];
+    const float4 av = *reinterpret_cast<const float4*>(a + c);
+    const float4 bv = *reinterpret_cast<const float4*>(b + c);
+    float4 o;
+    if (BWD) {
+      const float4 d = reinterpret_cast<const float4*>(g)[t];
+      const float4 kv = *reinterpret_cast<const float4*>(k2 + c);
+      o.x = d.x * av.x + bv.x + kv.x * v.x;
+      o.y = d.y * av.y + bv.y + kv.y * v.y;
+      o.z = d.z * av.z + bv.z + kv.z * v.z;
+      o.w = d.w * av.w + bv.w + kv.w * v.w;
+    } else {
+      o.x = v.x * av.x + bv.x;
+      o.y = v.y * av.y + bv.y;
+      o.z = v.z * av.z + bv.z;
+      o.w = v.w * av.w + bv.w;
+    }
+    reinterpret_cast<float4*>(out)[t] = o;
+  }
+}
+
+inline int bn_groups(int P, int C) {
+  const int col_blocks = (C + BN_CQ * 4 - 1) / (BN_CQ * 4);
+  int groups = std::max(1, std::min(1024, 1024 / std::max(1, col_blocks)));
+  return std::min(groups, std::max(1, P / 64));
+}
+
+}  // namespace tp
+
+// Workspace: ws holds 2 * groups * C doubles (groups = tp_bn_groups(P, C)).
+extern "C" int tp_bn_groups(int P, int C) { return tp::bn_groups(P, C); }
+
+extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
+                                      float eps, float momentum, float* run_mean, float* run_var, float* mean,
+                                      float* invstd, float* a, float* b, double* ws, hipStream_t st) {
+  using namespace tp;
+  if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int groups = bn_groups(P, C);
+  const int rpg = (P + groups - 1) / groups;
+  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
+  bn_partial<0><<<grid, BN_T, 0, st>>>(x, nullptr, nullptr, nullptr, ws, P, C, rpg);
+  bn_fwd_finalize<<<(C + 255) / 256, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
+                                                    mean, invstd, a, b);
+  const unsigned n4 = (unsigned)((long long)P * C / 4);
+  bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(x, nullptr, a, b, nullptr, y,
+                                                                                          n4, (unsigned)(C / 4));
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_bn_bwd_train(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
+                                      const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
+                                      float* k1, float* k2, double* ws, hipStream_t st) {
+  using namespace tp;
+  if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int groups = bn_groups(P, C);
+  const int rpg = (P + groups - 1) / groups;
+  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
+  bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg);
+  bn_bwd_finalize<<<(C + 255) / 256, 256, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
+  if (dx) {
+    const unsigned n4 = (unsigned)((long long)P * C / 4);
+    bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(x, g, a, k1, k2, dx, n4,
+                                                                                         (unsigned)(C / 4));
+  }
+  return hipGetLastError();
+}

@@ -62,6 +62,7 @@ struct ConvArgs {
   const float* mask;        // [M][N] activation: out = mask > 0 ? v : 0 (ReLU backward), nullable
   int res_stride;           // res is (B, ceil(Ho/s), ceil(Wo/s), N) added at pixels with oh, ow % s == 0
                             // (gradient of a strided 1x1 downsample conv scattered back), 1 = dense
+  int tay_mode;             // EPI_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
   int parity;               // GEN 3: rows ordered (oh%2, ow%2, b, oh/2, ow/2) so a tile sees few taps
 };
 
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
                   cur_b = b;
                   tsum = 0.f;
                 }
-                tsum += -(gval * a);
+                tsum += p.tay_mode ? fabsf(gval) : -(gval * a);
               }
               if (p.out) p.out[o] = a > 0.f ? gval * sc : 0.f;
             }
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         float v = 0.f;
         for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
         const float a = p.act[o];
-        tsum += -(v * a);
+        tsum += p.tay_mode ? fabsf(v) : -(v * a);
         if (p.out) p.out[o] = a > 0.f ? v * sc : 0.f;
       }
       if (p.taylor) p.taylor[tay_index(p, b, n)] += tsum;
@@ -757,7 +758,7 @@ __global__ __launch_bounds__(1024) void conv_epilogue_bwd_img(ConvArgs p, const 
       float v = 0.f;
       for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
       const float a = p.act[o];
-      tsum += -(v * a);
+      tsum += p.tay_mode ? fabsf(v) : -(v * a);
       if (p.out) p.out[o] = a > 0.f ? v * sc : 0.f;
     }
   }
@@ -904,7 +905,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
                                     int Cin, int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits,
                                     const float* scale, const float* shift, int relu, float* out,
                                     uint8_t* out_argmax, const float* act, float* taylor, int HWo, int tay_group,
-                                    float* ws, hipStream_t st) {
+                                    float* ws, int tay_mode, hipStream_t st) {
   using namespace tp;
   if (Cin % 32 != 0) return hipErrorInvalidValue;
   ConvArgs a{};
@@ -936,6 +937,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   a.taylor = taylor;
   a.HWo = HWo;
   a.tay_group = tay_group;
+  a.tay_mode = tay_mode;
   a.Ho = H;
   a.Wo = W;
   a.stride = 1;
@@ -969,7 +971,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
 extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
                                               const float* scale, const float* shift, int relu, float* out,
                                               uint8_t* out_argmax, const float* act, float* taylor,
-                                              float* apoz, hipStream_t st) {
+                                              float* apoz, int tay_mode, hipStream_t st) {
   using namespace tp;
   ConvArgs a{};
   a.B = B;
@@ -985,6 +987,7 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
   a.out_argmax = out_argmax;
   a.act = act;
   a.taylor = taylor;
+  a.tay_mode = tay_mode;
   a.apoz = apoz;
   a.HWo = H * W;
   const long long MN = (long long)a.M * a.N;

@@ -87,6 +87,7 @@ struct WinoArgs {
   FastDiv fd_timg, fd_w2, fd_ip, fd_rw;  // T_img = (H/2)(W/2), W/2, IP, RW
   float* apoz;              // W_FWD: [B][K] counts of positive outputs (exact integers), nullable
   int dbg;                  // experiment switches (TP_WINO_DBG): 1 no epilogue, 2 no restaging, 4 no transform
+  int tay_mode;             // W_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
 };
 
 __device__ __forceinline__ int xcd_remap_w(int bid, int nwg) {
@@ -277,7 +278,8 @@ phase2:
         // act: prefetched into LDS by the last chunk's DMA (slot tid + 256 i), else global
         const float4 a = al0 ? *reinterpret_cast<const float4*>((i < 4 ? al0 : al1) + ((i & 3) * 256 + tid) * 4)
                              : *reinterpret_cast<const float4*>(p.act + pix * p.K + k);
-        tq[i] = make_float4(-(y.x * a.x), -(y.y * a.y), -(y.z * a.z), -(y.w * a.w));
+        tq[i] = p.tay_mode ? make_float4(fabsf(y.x), fabsf(y.y), fabsf(y.z), fabsf(y.w))
+                           : make_float4(-(y.x * a.x), -(y.y * a.y), -(y.z * a.z), -(y.w * a.w));
         if (p.out) {
           float4 v;
           v.x = a.x > 0.f ? y.x * sc4.x : 0.f;
@@ -752,7 +754,7 @@ static XGeom staged_geometry(int H, int W, bool pooled) {
 extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
                                               const float* scale, const float* shift, int relu, float* out,
                                               uint8_t* out_argmax, const float* act, float* taylor,
-                                              float* apoz, hipStream_t st);
+                                              float* apoz, int tay_mode, hipStream_t st);
 
 extern "C" int tp_wino_taylor_slots(int H, int W) { return tp::wino_taylor_slots(H, W); }
 
@@ -771,7 +773,7 @@ extern "C" void tp_wino_geometry(int H, int W, int unpool, int* out9) {
 extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W,
                                    int C, int K, int unpool, int epi, int splits, int staged, const float* scale,
                                    const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
-                                   float* taylor, float* apoz, float* ws, hipStream_t st) {
+                                   float* taylor, float* apoz, float* ws, int tay_mode, hipStream_t st) {
   using namespace tp;
   if ((H & 1) || (W & 1) || C % 8 != 0 || K % 32 != 0) return hipErrorInvalidValue;
   WinoArgs a{};
@@ -798,6 +800,7 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.out_argmax = out_argmax;
   a.act = act;
   a.taylor = taylor;
+  a.tay_mode = tay_mode;
   a.apoz = epi == W_FWD ? apoz : nullptr;
   if (apoz && epi != W_FWD) return hipErrorInvalidValue;
   a.tay_slots = wino_taylor_slots(H, W);
@@ -846,5 +849,5 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || splits == 1) return e;
   return tp_conv_epilogue_slabs(ws, splits, B, H, W, K, epi, scale, shift, relu, out, out_argmax, act, taylor,
-                                a.apoz, st);
+                                a.apoz, tay_mode, st);
 }

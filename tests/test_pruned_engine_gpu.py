@@ -156,3 +156,38 @@ def test_pruned_resnet_engine_apoz_matches_generic(cuda):
         np.testing.assert_allclose(a, b, atol=0.5)
     with torch.no_grad():
         torch.testing.assert_close(eng.forward(x), model(x), rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prune", [False, True])
+def test_vgg_engine_sensitivity_matches_fp64(cuda, prune):
+    """Sensitivity (sum |dL/da|) from the fused dgrad epilogues vs an fp64 oracle."""
+    from torchpruner_amd import SensitivityAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.models import prunable_vgg16
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(2)
+    model = prunable_vgg16().to(cuda).eval()
+    if prune:
+        _prune_vgg_odd(model, cuda, seed=2)
+    mods = [m for m in model.features if isinstance(m, torch.nn.Conv2d)] + [model.classifier[1], model.classifier[4]]
+    assert maybe_engine(model, [find_best_module_for_attributions(model, m) for m in mods], F.cross_entropy,
+                        cuda) is not None
+    x = torch.randn(32, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (32,), device=cuda)
+    m64 = copy.deepcopy(model).double().cpu()
+    mods64 = [m for m in m64.features if isinstance(m, torch.nn.Conv2d)] + [m64.classifier[1], m64.classifier[4]]
+    for red in ("mean", "none"):
+        got = SensitivityAttributionMetric(model, DeviceLoader(x, y, 16), F.cross_entropy, cuda,
+                                           reduction=red).run_many(mods, True)
+        os.environ["TORCHPRUNER_BACKEND"] = "torch"
+        try:
+            ref = SensitivityAttributionMetric(m64, DeviceLoader(x.double().cpu(), y.cpu(), 16), F.cross_entropy,
+                                               "cpu", reduction=red).run_many(mods64, True)
+        finally:
+            del os.environ["TORCHPRUNER_BACKEND"]
+        for m, a, r in zip(mods, got, ref):
+            assert a.shape == r.shape and a.shape[-1] == m.weight.shape[0]
+            err = np.abs(a - r).max() / (np.abs(r).max() + 1e-30)
+            assert err < (5e-3 if red == "mean" else 2e-2), (m, red, err)

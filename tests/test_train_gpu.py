@@ -77,3 +77,34 @@ def test_native_conv_training_matches_autograd(cuda, arch):
     # running statistics were updated identically (BN stays PyTorch)
     for (n1, b1), (_, b2) in zip(model.named_buffers(), ref_model.named_buffers()):
         torch.testing.assert_close(b1.float(), b2.float(), rtol=1e-4, atol=1e-5, msg=n1)
+
+
+@pytest.mark.parametrize("C,hw,B", [(64, (7, 9), 5), (36, (14, 14), 3), (2048, (2, 2), 4), (4, (33, 1), 2)])
+@pytest.mark.parametrize("affine", [True, False])
+def test_bn_train_kernels_match_fp64(cuda, C, hw, B, affine):
+    """Batch statistics, running-stat update, normalisation and backward vs fp64 F.batch_norm."""
+    from torchpruner_amd.engine.train import native_convs
+    torch.manual_seed(C + B)
+    bn = torch.nn.BatchNorm2d(C, affine=affine).to(cuda).train()
+    if affine:
+        bn.weight.data.uniform_(0.5, 1.5)
+        bn.bias.data.uniform_(-0.5, 0.5)
+    ref = copy.deepcopy(bn).double()
+    x = (torch.randn(B, C, *hw, device=cuda) * 3 + 1).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(B, C, *hw, device=cuda).contiguous(memory_format=torch.channels_last)
+    xr = x.detach().double().requires_grad_(True)
+    x = x.requires_grad_(True)
+    with native_convs(bn) as sw:
+        assert sw == [bn]
+        y = bn(x)
+    y.backward(gy)
+    yr = ref(xr)
+    yr.backward(gy.double())
+    torch.testing.assert_close(y.double(), yr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.double(), xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_mean.double(), ref.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.running_var.double(), ref.running_var, rtol=1e-5, atol=1e-5)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+    if affine:
+        torch.testing.assert_close(bn.weight.grad.double(), ref.weight.grad, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(bn.bias.grad.double(), ref.bias.grad, rtol=1e-4, atol=1e-3)

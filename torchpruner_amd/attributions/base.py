@@ -342,6 +342,31 @@ class _AttributionMetric(ABC):
                 h.remove()
             self.restore_deterministic()
 
+    def _fused_grad_pass(self, engine, blocks, accs, mode, take_abs):
+        """Gradient metrics on the fused VGG-chain engine: per batch ONE fused forward +
+        input-gradient backward writes every block's per-sample partials (``mode`` taylor /
+        sensitivity), and ONE fold launch turns all layers' sums into fp64 accumulators."""
+        owner = {}
+        for k, b in enumerate(blocks):
+            owner.setdefault(b, k)
+        uniq = sorted(owner)
+        stats = accs[0].mode == "stats"
+        for i, x, y in self._batches():
+            B = x.shape[0]
+            if stats:
+                arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
+                engine.taylor(x, y, set(uniq), arena, mode=mode)
+                sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device, engine.real_width(b)) for b in uniq]
+                ops.score_fold_([arena[b] for b in uniq], sums, take_abs, 2)
+                for b in uniq:
+                    accs[owner[b]].count += B
+            else:
+                res = engine.taylor(x, y, set(uniq), mode=mode)
+                ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), take_abs, 1)
+                for b in uniq:
+                    accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
+        return [accs[owner[b]] for b in blocks]
+
     def _resnet_grad_engine(self, eval_modules):
         """The ResNet engine when it can produce gradient scores for ``eval_modules`` (eval-mode
         torchvision-layout ResNet, block BNs, mean cross-entropy criterion), else None."""

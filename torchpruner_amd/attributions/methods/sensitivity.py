@@ -4,6 +4,7 @@ Per sample: sum over trailing dims of |grad_output|, gradient of the per-batch *
 (so scores scale with 1/batch_size, as in the reference).
 """
 from ... import ops
+from ...engine import maybe_engine
 from ..base import _AttributionMetric
 
 
@@ -19,8 +20,11 @@ class SensitivityAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            rn = self._resnet_grad_engine(eval_modules)
-            if rn is not None:  # ResNets: forward + input-grad backward on the HIP engine
+            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device)
+            rn = None if fused is not None else self._resnet_grad_engine(eval_modules)
+            if fused is not None:  # VGG-style chains: |dL/da| partials from the fused dgrad epilogues
+                accs = self._fused_grad_pass(*fused, accs, "sensitivity", False)
+            elif rn is not None:  # ResNets: forward + input-grad backward on the HIP engine
                 accs = self._resnet_grad_pass(rn, eval_modules, accs, "sensitivity")
             else:
                 self._grad_capture_pass(eval_modules,

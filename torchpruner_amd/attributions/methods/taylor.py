@@ -35,28 +35,7 @@ class TaylorAttributionMetric(_AttributionMetric):
         if fused is not None:
             # native path: one fused forward + input-grad backward scores every module, then
             # ONE fold launch turns all layers' per-sample sums into |.| and fp64 accumulators
-            engine, blocks = fused
-            owner = {}
-            for k, b in enumerate(blocks):
-                owner.setdefault(b, k)
-            uniq = sorted(owner)
-            stats = accs[0].mode == "stats"
-            for i, x, y in self._batches():
-                B = x.shape[0]
-                if stats:
-                    arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
-                    engine.taylor(x, y, set(uniq), arena)
-                    sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device, engine.real_width(b))
-                            for b in uniq]
-                    ops.score_fold_([arena[b] for b in uniq], sums, not self.signed, 2)
-                    for b in uniq:
-                        accs[owner[b]].count += B
-                else:
-                    res = engine.taylor(x, y, set(uniq))
-                    ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), not self.signed, 1)
-                    for b in uniq:
-                        accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
-            accs = [accs[owner[b]] for b in blocks]
+            accs = self._fused_grad_pass(*fused, accs, "taylor", not self.signed)
         elif (rn := self._resnet_grad_engine(eval_modules)) is not None:
             accs = self._resnet_grad_pass(rn, eval_modules, accs, mode)
         else:

@@ -447,18 +447,19 @@ class FusedChainEngine:
                                lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino, cands=cands)
         return self._conv_run(T, e, h, cfg, sp)
 
-    def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None):
+    def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0):
+        """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
         if cfg in (WINO, WINO_LDS):
-            return T.conv_wino_dgrad(g, am, e["ut"], act, sc, taylor, want_out, sp, cfg == WINO_LDS)
+            return T.conv_wino_dgrad(g, am, e["ut"], act, sc, taylor, want_out, sp, cfg == WINO_LDS, tay_mode=tm)
         if cfg >= self.DENSE:
             d = self._dense(e)
             if am is not None:
                 g = T.unpool2_nhwc(g, am)
             B, C = act.shape[0], act.shape[3]
             out = T.conv_dgrad(g.reshape(B, 1, 1, -1), None, d["wt"], act.reshape(B, 1, 1, -1), sc4, taylor,
-                               want_out, 1, cfg - self.DENSE, sp, C)
+                               want_out, 1, cfg - self.DENSE, sp, C, tay_mode=tm)
             return out.view(B, 2, 2, C) if want_out else out
-        return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp)
+        return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp, tay_mode=tm)
 
     def _linear(self, T, e, xin):
         B = xin.shape[0]
@@ -568,11 +569,13 @@ class FusedChainEngine:
         blk = self.plan.blocks[b]
         return blk.conv.out_channels if isinstance(blk, ConvBlock) else blk.linear.out_features
 
-    def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None):
+    def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None, mode="taylor"):
         """One fused forward+backward; returns {block index: per-sample signed Taylor sums
-        sum_hw -(dL/da * a)} for every requested block (conv blocks first, then linear blocks;
-        the final linear has none) as (R, B, C) partial slots for conv blocks (sum over R, or
-        fold with ops.score_fold_) and (B, C) for linear blocks. Deterministic: no atomics."""
+        sum_hw -(dL/da * a)} (``mode="sensitivity"``: sum_hw |dL/da|) for every requested block
+        (conv blocks first, then linear blocks; the final linear has none) as (R, B, C) partial
+        slots for conv blocks (sum over R, or fold with ops.score_fold_) and (B, C) for linear
+        blocks. Deterministic: no atomics."""
+        tm = 1 if mode == "sensitivity" else 0
         T = ops.require()
         P = self._pack()
         nconv, nlin = len(self.plan.convs), len(self.plan.linears)
@@ -605,7 +608,7 @@ class FusedChainEngine:
             cfg, sp = TUNER.choose(("lin_bwd", tuple(g.shape), tuple(act.shape)), B, act.shape[3], e["wt"].shape[1],
                                    lambda c, s_, e=e, gg=gg, act=act, bn=bn_scale: T.conv_dgrad(
                                        gg, None, e["wt"], act, bn, None, True, 1, c, s_))
-            g = T.conv_dgrad(g, None, e["wt"], act, bn_scale, taylor, True, 1, cfg, sp)
+            g = T.conv_dgrad(g, None, e["wt"], act, bn_scale, taylor, True, 1, cfg, sp, tay_mode=tm)
         # conv stack: g is dL/d(pre-activation of conv nconv-1) * bn_scale, at the
         # (pooled, if pooled) output resolution of that block
         for ci in range(nconv - 1, 0, -1):
@@ -637,7 +640,7 @@ class FusedChainEngine:
                                    lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4:
                                    self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_, s4), wino, wino_only=True,
                                    cands=cands)
-            g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp, sc4)
+            g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp, sc4, tm)
         return res
 
 

@@ -11,8 +11,9 @@ convolutions of a model run on the precompiled gfx950 kernels instead, through a
             gather kernel with parity-ordered rows (``tpamd.conv_gen_bwd``)
   wgrad     pixel-split MFMA GEMM, deterministic split combine (``tpamd.conv_wgrad``, K3)
 
-BatchNorm, activations, pooling and the loss stay PyTorch ops (autograd composes them), so
-any model works; only ``nn.Conv2d`` modules the kernels support are switched. Pruned (odd)
+Training-mode ``BatchNorm2d`` runs on deterministic NHWC batch-statistics / normalisation /
+backward kernels (K5, ``tpamd.bn_train_*``); activations, pooling and the loss stay PyTorch ops
+(autograd composes them), so any model works; only modules the kernels support are switched. Pruned (odd)
 channel counts are zero-padded to the kernels' granule inside the op and sliced off again:
 the parameters, their gradients and the optimizer state keep the module's real shapes.
 Every kernel choice is timed once per shape (``TUNER``, like ``cudnn.benchmark``) — a few
@@ -30,6 +31,16 @@ import torch.nn.functional as F
 
 from .. import ops
 from .fused_chain import _CU, TUNER, cpad
+
+
+def _as_nchw(t: torch.Tensor) -> torch.Tensor:
+    """(B, C, H, W) channels_last tensor on the storage of a contiguous NHWC ``t`` that is NOT an
+    autograd view of it: a custom Function's output may then be modified in place
+    (``ReLU(inplace=True)`` right after a BatchNorm)."""
+    B, H, W, C = t.shape
+    out = t.new_empty(0)
+    out.set_(t.untyped_storage(), t.storage_offset(), (B, C, H, W), (H * W * C, 1, W * C, C))
+    return out
 
 
 def _geom(conv: nn.Conv2d):
@@ -88,15 +99,14 @@ class _NativeConv2d(torch.autograd.Function):
         if cout_p != Cout:
             y = y[..., :Cout].contiguous()
         ctx.save_for_backward(xh, wp)
-        ctx.geom = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype,
-                    weight.is_contiguous(memory_format=torch.channels_last) and weight.dim() == 4)
-        return y.permute(0, 3, 1, 2)
+        ctx.geom = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride())
+        return _as_nchw(y)
 
     @staticmethod
     def backward(ctx, gy):
         T = ops.require()
         xh, wp = ctx.saved_tensors
-        ks, stride, pad, Cin, Cout, H, W, has_bias, wdtype, w_cl = ctx.geom
+        ks, stride, pad, Cin, Cout, H, W, has_bias, wdtype, w_strides = ctx.geom
         cout_p, cin_p = wp.shape[0], wp.shape[1]
         g = gy.permute(0, 2, 3, 1).float()
         if cout_p != Cout:
@@ -139,10 +149,56 @@ class _NativeConv2d(torch.autograd.Function):
                                    cands=cands)
             dwk = run_w(cfg, sp)
             dw = dwk[:Cout, :ks * ks * cin_p].view(Cout, ks, ks, cin_p)[..., :Cin].permute(0, 3, 1, 2)
-            dw = dw.contiguous(memory_format=torch.channels_last if w_cl else torch.contiguous_format).to(wdtype)
+            # the gradient takes the parameter's exact strides (DDP bucket views expect them)
+            dw = torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=wdtype, device=dwk.device).copy_(dw)
         if has_bias and ctx.needs_input_grad[2]:
             db = gy.sum((0, 2, 3))
         return dx, dw, db, None, None, None
+
+
+class _NativeBN2d(torch.autograd.Function):
+    """Training-mode BatchNorm2d on channels_last activations (K5): batch statistics and the
+    running-stat update, the normalisation, and the backward, on ``tpamd.bn_train_*``."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum):
+        T = ops.require()
+        xh = x.permute(0, 2, 3, 1)
+        if not xh.is_contiguous():
+            xh = xh.contiguous()
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        y, mean, invstd = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum))
+        ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd)
+        ctx.has_w, ctx.has_b = weight is not None, bias is not None
+        return _as_nchw(y)
+
+    @staticmethod
+    def backward(ctx, gy):
+        T = ops.require()
+        xh, w, mean, invstd = ctx.saved_tensors
+        g = gy.permute(0, 2, 3, 1).contiguous()
+        dx, dgamma, dbeta = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd, ctx.needs_input_grad[0])
+        return (dx.permute(0, 3, 1, 2) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
+                dbeta if ctx.has_b else None, None, None, None, None)
+
+
+def _native_bn_forward(self, x):
+    """BatchNorm2d.forward with the training branch on the native kernels (eval mode and any
+    input the kernels do not take — non-channels_last, C % 4 != 0 — use the module's own)."""
+    ok = (self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] % 4 == 0
+          and x.is_contiguous(memory_format=torch.channels_last) and x.numel() > 0
+          and (self.weight is None or self.weight.dtype == torch.float32))
+    if not ok:
+        return type(self).forward(self, x)
+    momentum = self.momentum
+    if self.track_running_stats and self.num_batches_tracked is not None:
+        self.num_batches_tracked.add_(1)
+        if momentum is None:  # cumulative moving average
+            momentum = 1.0 / float(self.num_batches_tracked)
+    rm = self.running_mean if self.track_running_stats else None
+    rv = self.running_var if self.track_running_stats else None
+    return _NativeBN2d.apply(x, self.weight, self.bias, rm, rv, self.eps, momentum if momentum is not None else 0.0)
 
 
 def _native_forward(self, x):
@@ -152,16 +208,22 @@ def _native_forward(self, x):
     return _NativeConv2d.apply(x, self.weight, self.bias, ks, s, p)
 
 
-def enable_native_convs(model: nn.Module) -> list:
-    """Route every eligible ``nn.Conv2d`` of ``model`` through the native kernels (instance-level
-    ``forward`` override; pruning keeps working because weights are re-packed per call).
-    Returns the switched modules; undo with :func:`disable_native_convs`."""
+def enable_native_convs(model: nn.Module, bn: bool = True) -> list:
+    """Route every eligible ``nn.Conv2d`` of ``model`` (and, with ``bn``, every ``BatchNorm2d`` in
+    training mode) through the native kernels (instance-level ``forward`` override; pruning keeps
+    working because weights are re-packed per call). Returns the switched modules; undo with
+    :func:`disable_native_convs`."""
     if not ops.available() or ops.backend() == "torch":
         return []
     switched = []
     for m in model.modules():
-        if eligible(m) and "forward" not in m.__dict__:
+        if "forward" in m.__dict__:
+            continue
+        if eligible(m):
             m.forward = types.MethodType(_native_forward, m)
+            switched.append(m)
+        elif bn and isinstance(m, nn.BatchNorm2d):
+            m.forward = types.MethodType(_native_bn_forward, m)
             switched.append(m)
     return switched
 
@@ -172,9 +234,9 @@ def disable_native_convs(modules) -> None:
 
 
 @contextlib.contextmanager
-def native_convs(model: nn.Module, enable: bool = True):
+def native_convs(model: nn.Module, enable: bool = True, bn: bool = True):
     """``with native_convs(model): loss.backward()`` — scoped :func:`enable_native_convs`."""
-    switched = enable_native_convs(model) if enable else []
+    switched = enable_native_convs(model, bn) if enable else []
     try:
         yield switched
     finally:
