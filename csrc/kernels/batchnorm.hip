@@ -109,6 +109,30 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
   }
 }
 
+// Sum of the row-group partials of 16 channels per block: 16 group lanes stride over the
+// groups (coalesced 16-channel rows), then a fixed-order LDS fold (deterministic).
+__device__ __forceinline__ void fold_groups(const double* __restrict__ part, int groups, int C, int c, int cl, int gl,
+                                            double& s, double& q) {
+  __shared__ double red[2][16][16];
+  s = 0.0;
+  q = 0.0;
+  if (c < C)
+    for (int i = gl; i < groups; i += 16) {
+      s += part[(size_t)(2 * i) * C + c];
+      q += part[(size_t)(2 * i + 1) * C + c];
+    }
+  red[0][gl][cl] = s;
+  red[1][gl][cl] = q;
+  __syncthreads();
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    s += red[0][i][cl];
+    q += red[1][i][cl];
+  }
+}
+
 // Forward finalize: mean / invstd for the apply pass, running statistics (PyTorch semantics:
 // running_var takes the unbiased variance), and the affine folded into (a, b).
 __global__ __launch_bounds__(256) void bn_fwd_finalize(const double* __restrict__ part, int groups, int P, int C,
@@ -117,13 +141,10 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize(const double* __restrict_
                                                        float* __restrict__ run_var, float* __restrict__ mean,
                                                        float* __restrict__ invstd, float* __restrict__ a,
                                                        float* __restrict__ b) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int i = 0; i < groups; ++i) {
-    s += part[(size_t)(2 * i) * C + c];
-    q += part[(size_t)(2 * i + 1) * C + c];
-  }
+  const int cl = threadIdx.x % 16, gl = threadIdx.x / 16, c = blockIdx.x * 16 + cl;
+  double s, q;
+  fold_groups(part, groups, C, c, cl, gl, s, q);
+  if (gl != 0 || c >= C) return;
   const double m = s / P;
   const double var = fmax(q / P - m * m, 0.0);
   const float is = (float)(1.0 / sqrt(var + (double)eps));
@@ -145,13 +166,10 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize(const double* __restrict_
                                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                        float* __restrict__ dbeta, float* __restrict__ a,
                                                        float* __restrict__ k1, float* __restrict__ k2) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sg = 0.0, sgx = 0.0;
-  for (int i = 0; i < groups; ++i) {
-    sg += part[(size_t)(2 * i) * C + c];
-    sgx += part[(size_t)(2 * i + 1) * C + c];
-  }
+  const int cl = threadIdx.x % 16, gl = threadIdx.x / 16, c = blockIdx.x * 16 + cl;
+  double sg, sgx;
+  fold_groups(part, groups, C, c, cl, gl, sg, sgx);
+  if (gl != 0 || c >= C) return;
   if (dgamma) dgamma[c] = (float)sgx;
   if (dbeta) dbeta[c] = (float)sg;
   const double is = invstd[c], ga = gamma ? gamma[c] : 1.0;
@@ -211,7 +229,7 @@ extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, co
   const int rpg = (P + groups - 1) / groups;
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<0><<<grid, BN_T, 0, st>>>(x, nullptr, nullptr, nullptr, ws, P, C, rpg);
-  bn_fwd_finalize<<<(C + 255) / 256, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
+  bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
                                                     mean, invstd, a, b);
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(x, nullptr, a, b, nullptr, y,
@@ -228,7 +246,7 @@ extern "C" hipError_t tp_bn_bwd_train(const float* g, const float* x, float* dx,
   const int rpg = (P + groups - 1) / groups;
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg);
-  bn_bwd_finalize<<<(C + 255) / 256, 256, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
+  bn_bwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
   if (dx) {
     const unsigned n4 = (unsigned)((long long)P * C / 4);
     bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(x, g, a, k1, k2, dx, n4,
