@@ -1,0 +1,85 @@
+// Host-side validation of the kernel launchers, built with AddressSanitizer + UBSan on the host
+// code (SURVEY.md §5 "race detection / sanitizers"; GPU sanitizers are not available on this
+// pool). Every launcher must reject shapes its kernels do not support BEFORE touching the GPU,
+// and the host-side geometry helpers (tile/slot/group counts, the Winograd LDS-region search)
+// must be memory-clean. Runs on a CPU-only machine: no kernel is launched.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+extern "C" {
+int tp_conv_gen_k(int ks, int Cin);
+int tp_wino_taylor_slots(int H, int W);
+int tp_wino_staged_ok(int H, int W, int unpool);
+void tp_wino_geometry(int H, int W, int unpool, int* out9);
+int tp_bn_groups(int P, int C);
+hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                        int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
+                        const float* shift, int relu, const float* res, int res_stride, const float* mask,
+                        float* apoz, float* out, float* ws, hipStream_t st);
+hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
+                         int ks, int stride, int pad, int Kpad, int cfg, int splits, hipStream_t st);
+hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
+                        int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
+                        float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
+                        int tay_mode, hipStream_t st);
+hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
+                           float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
+                           float* b, double* ws, hipStream_t st);
+}
+
+static int failures = 0;
+#define EXPECT(cond)                                                   \
+  do {                                                                 \
+    if (!(cond)) {                                                     \
+      std::fprintf(stderr, "%s:%d: EXPECT(%s) failed\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                      \
+    }                                                                  \
+  } while (0)
+
+int main() {
+  // geometry helpers
+  EXPECT(tp_conv_gen_k(3, 64) == 576);
+  EXPECT(tp_conv_gen_k(7, 4) == 224);
+  EXPECT(tp_wino_taylor_slots(2, 2) == 1);
+  EXPECT(tp_wino_taylor_slots(32, 32) == 4);
+  for (int h = 2; h <= 64; h += 2)
+    for (int w = 2; w <= 64; w += 2)
+      for (int up = 0; up < 2; ++up) {
+        int g[9];
+        tp_wino_geometry(h, w, up, g);
+        EXPECT(g[0] == tp_wino_staged_ok(h, w, up));
+        if (g[0]) EXPECT(g[1] >= 1 && g[3] > 0 && g[4] > 0);
+      }
+  for (int p = 1; p < 5000; p = p * 3 + 1)
+    for (int c = 4; c <= 2048; c *= 2) EXPECT(tp_bn_groups(p, c) >= 1);
+
+  // launchers reject unsupported shapes before any GPU work (null pointers are never touched)
+  float* n = nullptr;
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 48, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // Cin % 32
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 62, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // Cout % 4
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 5, 2, 2, 1, 16, 16, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // transposed 5x5
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 0, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // res_stride 0
+  EXPECT(tp_conv_gen2(n, n, 4096, 256, 256, 64, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // exceeds the 32-bit buffer-descriptor range
+  EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 6, 64, 3, 1, 1, 64, 0, 1, 0) == hipErrorInvalidValue);   // Cin % 4
+  EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 96, 0, 1, 0) == hipErrorInvalidValue);  // Kpad small
+  EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 576, 7, 1, 0) == hipErrorInvalidValue); // bad cfg
+  EXPECT(tp_conv_wino(n, nullptr, n, 2, 7, 8, 64, 64, 0, 0, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
+         hipErrorInvalidValue);  // odd H
+  EXPECT(tp_conv_wino(n, nullptr, n, 2, 8, 8, 12, 64, 0, 0, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
+         hipErrorInvalidValue);  // C % 8
+  EXPECT(tp_bn_fwd_train(n, n, 16, 6, n, n, 1e-5f, 0.1f, n, n, n, n, n, n, nullptr, 0) == hipErrorInvalidValue);
+
+  if (failures) {
+    std::fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  std::printf("launcher validation ok\n");
+  return 0;
+}

@@ -115,6 +115,37 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
     return OUT
 
 
+SANITIZE_SOURCES = ("conv_mfma", "conv_wgrad", "winograd", "batchnorm")
+
+
+def build_host_sanitizer(verbose: bool = False) -> Path:
+    """Build ``csrc/tests/launcher_validation.cpp`` against the kernel launchers with
+    AddressSanitizer + UBSan on the HOST code only (``-Xarch_host -fsanitize=...``; GPU
+    sanitizers are not available on this pool). The program checks, on a CPU-only machine,
+    that every launcher rejects unsupported shapes before touching the GPU and that the host
+    geometry helpers are memory-clean. Returns the executable path."""
+    out_dir = ROOT / "build" / "asan"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    headers = sorted((CSRC / "include").glob("*.h"))
+    san = ["-Xarch_host", "-fsanitize=address,undefined"]
+    jobs, objs = [], []
+    for name in SANITIZE_SOURCES:
+        src, obj = CSRC / "kernels" / f"{name}.hip", out_dir / f"{name}.o"
+        objs.append(obj)
+        if _needs_rebuild(src, obj, headers):
+            jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", f"-I{CSRC / 'include'}", *san,
+                         "-c", src, "-o", obj])
+    test_src, test_obj = CSRC / "tests" / "launcher_validation.cpp", out_dir / "launcher_validation.o"
+    if _needs_rebuild(test_src, test_obj, headers):
+        jobs.append([HIPCC, "-O1", "-g", "-std=c++17", *san, "-c", test_src, "-o", test_obj])
+    with ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 4)) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+    exe = out_dir / "launcher_validation"
+    if jobs or not exe.exists():
+        _run([HIPCC, f"--offload-arch={ARCH}", "-fsanitize=address,undefined", test_obj, *objs, "-o", exe], verbose)
+    return exe
+
+
 if __name__ == "__main__":
     build(verbose=True, force="--force" in sys.argv)
     print(OUT)

@@ -7,6 +7,9 @@ Policy (no silent fallbacks on a GPU box):
   the tests, and the path the CPU-only CI exercises).
 * ``TORCHPRUNER_BACKEND=torch`` forces the PyTorch path everywhere; it exists only so the
   benchmark can measure the reference-semantics eager baseline on the same GPU.
+* ``TORCHPRUNER_DEBUG_SYNC=1`` (debug mode, the analogue of ``AMD_SERIALIZE_KERNEL``): every
+  native op is followed by a device synchronisation, so an asynchronous kernel fault is
+  reported by the op that launched it (name and argument shapes) instead of a later one.
 """
 from __future__ import annotations
 
@@ -46,10 +49,33 @@ def available() -> bool:
     return load()
 
 
+class _SyncOps:
+    """``torch.ops.tpamd`` proxy for TORCHPRUNER_DEBUG_SYNC=1: synchronise after every op."""
+
+    def __init__(self, ns):
+        self._ns = ns
+
+    def __getattr__(self, name):
+        op = getattr(self._ns, name)
+
+        def call(*args, **kwargs):
+            out = op(*args, **kwargs)
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                shapes = [tuple(a.shape) if isinstance(a, torch.Tensor) else a for a in args]
+                raise RuntimeError(f"tpamd.{name}{shapes} faulted: {e}") from e
+            return out
+
+        return call
+
+
 def require():
     """Return ``torch.ops.tpamd`` or raise loudly (used on every GPU code path)."""
     if not load():
         raise RuntimeError(f"torchpruner_amd native extension unavailable: {_error!r}")
+    if os.environ.get("TORCHPRUNER_DEBUG_SYNC", "0") == "1":
+        return _SyncOps(torch.ops.tpamd)
     return torch.ops.tpamd
 
 
