@@ -1,0 +1,76 @@
+"""CPU checks of the engines' lowering decisions (no GPU needed): which models/modules the fused
+VGG chain, the ResNet engine and the native training path accept, and channel padding."""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from torchpruner_amd import Pruner, get_resnet_pruning_graph
+
+
+def test_cpad():
+    from torchpruner_amd.engine.fused_chain import cpad
+    assert [cpad(c) for c in (1, 31, 32, 33, 64, 100)] == [32, 32, 32, 64, 64, 128]
+    assert cpad(5, 4) == 8
+
+
+def test_resnet_plan_accepts_pruned_widths():
+    from torchpruner_amd.engine.resnet_engine import build_resnet_plan
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    torch.manual_seed(0)
+    model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=10, width=32).eval()
+    rng = np.random.RandomState(0)
+    pruner = Pruner(model, (3, 32, 32), "cpu")
+    for module, cascade in get_resnet_pruning_graph(model):
+        n = module.weight.shape[0]
+        pruner.prune_model(module, rng.choice(n, 7, replace=False), cascade)
+    plan, why = build_resnet_plan(model)
+    assert plan is not None, why
+    assert any(c.conv.out_channels % 32 for b in plan.blocks for c in b.convs)
+
+
+def test_resnet_plan_rejects_non_resnets():
+    from torchpruner_amd.engine.resnet_engine import build_resnet_plan
+    from torchpruner_amd.models import prunable_vgg16
+    plan, why = build_resnet_plan(prunable_vgg16())
+    assert plan is None and "ResNet" in why
+
+
+def test_native_training_eligibility():
+    from torchpruner_amd.engine.train import eligible
+    assert eligible(nn.Conv2d(16, 32, 3, padding=1))
+    assert eligible(nn.Conv2d(64, 128, 1, stride=2))
+    assert eligible(nn.Conv2d(3, 64, 7, stride=2, padding=3))
+    assert not eligible(nn.Conv2d(16, 32, 5, padding=2))          # 5x5: library conv
+    assert not eligible(nn.Conv2d(16, 32, 3, groups=2))           # grouped
+    assert not eligible(nn.Conv2d(16, 32, 3, dilation=2))         # dilated
+    assert not eligible(nn.Conv2d(16, 32, (1, 3)))                # non-square
+    assert not eligible(nn.Conv2d(16, 32, 3, padding="same"))     # string padding
+    assert not eligible(nn.Conv2d(16, 32, 3, padding=1, padding_mode="reflect"))
+    assert not eligible(nn.Linear(4, 4))
+
+
+def test_native_convs_is_a_noop_without_gpu_kernels(monkeypatch):
+    """On CPU (or with TORCHPRUNER_BACKEND=torch) nothing is switched and modules are untouched."""
+    from torchpruner_amd.engine.train import native_convs
+    monkeypatch.setenv("TORCHPRUNER_BACKEND", "torch")
+    model = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.BatchNorm2d(8), nn.ReLU())
+    with native_convs(model) as switched:
+        assert switched == []
+        y = model(torch.randn(2, 3, 8, 8))
+    assert y.shape == (2, 8, 8, 8)
+    assert all("forward" not in m.__dict__ for m in model.modules())
+
+
+def test_debug_sync_proxy_wraps_ops(monkeypatch):
+    from torchpruner_amd.ops import _native
+    monkeypatch.setenv("TORCHPRUNER_DEBUG_SYNC", "1")
+
+    class _NS:
+        @staticmethod
+        def add_one(x):
+            return x + 1
+
+    synced = []
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda: synced.append(1))
+    proxy = _native._SyncOps(_NS())
+    assert proxy.add_one(1) == 2 and synced == [1]
