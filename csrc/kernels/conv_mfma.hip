@@ -68,11 +68,13 @@ struct ConvArgs {
 
 // GEN 3 output row m -> (image, oh, ow). Parity order makes each stride-2 phase class one
 // contiguous range of B*Ho*Wo/4 rows: all but the (at most 3) boundary tiles see ONE class and
-// iterate exactly the taps it uses (1, 2, 2 or 4 of the 9 for a 3x3/s2 dgrad).
+// iterate exactly the taps it uses (1, 2, 2 or 4 of the 9 for a 3x3/s2 dgrad). Classes are laid
+// out heaviest first (longest-job-first dispatch: no tail of 4-tap tiles at the end).
 __device__ __forceinline__ void gen3_pix(const ConvArgs& p, int m, int& b, int& oh, int& ow) {
   if (p.parity) {
     const int W2 = p.Wo >> 1, Q = (p.Ho >> 1) * W2, BQ = p.B * Q;
-    const int cls = m / BQ, r = m - cls * BQ;
+    const int cq = m / BQ, r = m - cq * BQ;
+    const int cls = 3 - cq;  // heaviest phase (4 taps) first: its tiles are dispatched first
     b = r / Q;
     const int q = r - b * Q;
     const int qy = q / W2;
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   if constexpr (GEN == 3) {
     if (p.parity) {
       const int BQ = p.B * (p.Ho >> 1) * (p.Wo >> 1);
-      const int c0 = m0 / BQ, c1 = (min(m0 + BM, p.M) - 1) / BQ;
+      const int c0 = 3 - (min(m0 + BM, p.M) - 1) / BQ, c1 = 3 - m0 / BQ;
       tmask = 0;
       for (int c = c0; c <= c1; ++c) {
         for (int t = 0; t < KS * KS; ++t)
