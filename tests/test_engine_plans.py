@@ -74,3 +74,27 @@ def test_debug_sync_proxy_wraps_ops(monkeypatch):
     monkeypatch.setattr(torch.cuda, "synchronize", lambda: synced.append(1))
     proxy = _native._SyncOps(_NS())
     assert proxy.add_one(1) == 2 and synced == [1]
+
+
+def test_reference_module_paths_import():
+    """Code importing the reference's submodules (not just the packages) runs unchanged."""
+    import importlib
+    import torchpruner_amd as tp
+    paths = {
+        "torchpruner.attributions.attributions": ["_AttributionMetric", "SUPPORTED_OUT_PRUNING_MODULES"],
+        "torchpruner.attributions.methods.random": ["RandomAttributionMetric"],
+        "torchpruner.attributions.methods.weight_norm": ["WeightNormAttributionMetric"],
+        "torchpruner.attributions.methods.apoz": ["APoZAttributionMetric"],
+        "torchpruner.attributions.methods.sensitivity": ["SensitivityAttributionMetric"],
+        "torchpruner.attributions.methods.taylor": ["TaylorAttributionMetric"],
+        "torchpruner.attributions.methods.shapley_values": ["ShapleyAttributionMetric"],
+        "torchpruner.pruner.pruner": ["Pruner", "SUPPORTED_IN_PRUNING_MODULES"],
+        "torchpruner.pruner.opt_pruner": ["OptimizerPruner"],
+        "torchpruner.utils.graph": ["find_best_module_for_attributions", "get_vgg_pruning_graph", "ACTIVATIONS"],
+    }
+    for mod, names in paths.items():
+        m = importlib.import_module(mod)
+        for n in names:
+            obj = getattr(m, n)
+            if hasattr(tp, n):
+                assert obj is getattr(tp, n), (mod, n)
