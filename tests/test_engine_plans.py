@@ -98,3 +98,36 @@ def test_reference_module_paths_import():
             obj = getattr(m, n)
             if hasattr(tp, n):
                 assert obj is getattr(tp, n), (mod, n)
+
+
+def test_prefetch_cpu_passthrough():
+    from torchpruner_amd.data import prefetch_to_device
+    items = [(i, torch.full((2,), float(i))) for i in range(5)]
+    out = list(prefetch_to_device(items, "cpu"))
+    assert [o[0] for o in out] == list(range(5)) and all(o[1][0] == i for i, o in enumerate(out))
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_prefetch_host_loader_matches_device_loader(cuda):
+    """A CPU DataLoader (pinned + copied ahead on a side stream) gives the same scores as
+    device-resident batches, in the same order."""
+    import torch.nn.functional as F
+    from torch.utils.data import DataLoader, TensorDataset
+    from torchpruner_amd import TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader, prefetch_to_device
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(0)
+    model = prunable_vgg16().to(cuda).eval()
+    x, y = torch.randn(40, 3, 32, 32), torch.randint(0, 10, (40,))
+    convs = [m for m in model.features if isinstance(m, nn.Conv2d)][:4]
+    host = DataLoader(TensorDataset(x, y), batch_size=8, shuffle=False)
+    a = TaylorAttributionMetric(model, host, F.cross_entropy, cuda, reduction="none").run_many(convs, True)
+    b = TaylorAttributionMetric(model, DeviceLoader(x.to(cuda), y.to(cuda), 8), F.cross_entropy, cuda,
+                                reduction="none").run_many(convs, True)
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(u, v)
+    got = [int(t[1][0]) for t in prefetch_to_device(((i, torch.full((3,), i)) for i in range(7)), cuda, depth=3)]
+    assert got == list(range(7))

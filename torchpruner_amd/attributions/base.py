@@ -33,6 +33,7 @@ import torch.nn as nn
 from torch.nn.modules.conv import _ConvNd
 
 from .. import ops
+from ..data.prefetch import prefetch_to_device
 from ..parallel import dist as pdist
 from ..utils.graph import ACTIVATIONS, find_best_module_for_attributions
 
@@ -237,10 +238,11 @@ class _AttributionMetric(ABC):
         it = pdist.ShardedBatches(self.data_gen, rank, world) if self._sharding() else \
             ((i, x, y) for i, (x, y) in enumerate(self.data_gen))
         ck = self._ckpt
-        for i, x, y in it:
-            if ck is not None and i in ck.done:
-                continue  # processed before an interruption
-            yield i, _to(x, self.device), _to(y, self.device)
+        if ck is not None:
+            it = ((i, x, y) for i, x, y in it if i not in ck.done)  # processed before an interruption
+        # host batches are pinned and copied one batch ahead on a side stream (copy/compute overlap)
+        for i, x, y in prefetch_to_device(it, self.device):
+            yield i, x, y
             if ck is not None:  # the consumer finished batch i before asking for the next one
                 ck.step(self._run_accs, i)
 
