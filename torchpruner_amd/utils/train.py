@@ -12,6 +12,7 @@ from timeit import default_timer as timer
 
 import torch
 
+from ..data.prefetch import prefetch_to_device
 from ..parallel import dist as pdist
 
 logger = logging.getLogger("torchpruner")
@@ -31,10 +32,9 @@ def train(model, device, loss, train_loader, optimizer, epoch, log_every=20, sha
     cumulative_loss = 0.0
     start = timer()
     world, rank = pdist.get_world_size(), pdist.get_rank()
-    for batch_idx, (data, target) in enumerate(_batches(train_loader, rank, world, shard)):
+    for batch_idx, (data, target) in enumerate(prefetch_to_device(_batches(train_loader, rank, world, shard), device)):
         if max_steps is not None and batch_idx >= max_steps:
             break
-        data, target = data.to(device, non_blocking=True), target.to(device, non_blocking=True)
         optimizer.zero_grad(set_to_none=True)
         output = model(data)
         curr_loss = loss(output, target)
@@ -57,8 +57,7 @@ def test(model, device, loss, test_loader, verbose=1, shard=False):
     model.eval()
     cum = torch.zeros(3, dtype=torch.float64, device=device)  # loss*n, correct, n
     world, rank = pdist.get_world_size(), pdist.get_rank()
-    for data, target in _batches(test_loader, rank, world, shard):
-        data, target = data.to(device, non_blocking=True), target.to(device, non_blocking=True)
+    for data, target in prefetch_to_device(_batches(test_loader, rank, world, shard), device):
         output = model(data)
         cum[0] += loss(output, target).double() * len(target)
         cum[1] += (output.argmax(1) == target.view(-1)).sum()
