@@ -547,11 +547,12 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         for (int g = 0; g < 4; ++g) {
           const int m = mt + 8 * g + 4 * lh;  // first row of this pooling window
           float best = 0.f;
-          int arg = 0;
+          int arg = 0, cnt = 0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float v = acc[i][j][4 * g + q] * sc + sh;
             if (p.relu) v = nan_relu(v);
+            cnt += v > 0.f ? 1 : 0;
             if (q == 0 || v > best || (v != v && best == best)) {
               best = v;
               arg = q;
@@ -561,6 +562,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
             const long long o = (long long)(m >> 2) * p.N + n;
             p.out[o] = best;
             p.out_argmax[o] = (uint8_t)arg;
+            if (p.apoz && cnt) atomicAdd(p.apoz + (long long)(m / p.HWo) * p.N + n, (float)cnt);
           }
         }
       } else if constexpr (EPI == EPI_BWD) {
@@ -636,13 +638,14 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       const unsigned mp = t / N;
       const float sc = p.scale ? p.scale[n] : 1.f, sh = p.shift ? p.shift[n] : 0.f;
       float best = 0.f;
-      int arg = 0;
+      int arg = 0, cnt = 0;
       for (int q = 0; q < 4; ++q) {
         const unsigned o = (mp * 4 + q) * N + n;
         float v = 0.f;
         for (int s = 0; s < splits; ++s) v += slabs[(size_t)s * MN + o];
         v = v * sc + sh;
         if (p.relu) v = nan_relu(v);
+        cnt += v > 0.f ? 1 : 0;
         if (q == 0 || v > best || (v != v && best == best)) {
           best = v;
           arg = q;
@@ -650,6 +653,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
       }
       p.out[t] = best;
       p.out_argmax[t] = (uint8_t)arg;
+      if (p.apoz && cnt) atomicAdd(p.apoz + (size_t)(mp * 4 / (unsigned)p.HWo) * N + n, (float)cnt);
     }
   } else if constexpr (EPI == EPI_FWD) {
     // 32-bit index math (host guarantees M*N < 2^31): 64-bit div/mod per element made this
@@ -907,7 +911,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
                                     int Cin, int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits,
                                     const float* scale, const float* shift, int relu, float* out,
                                     uint8_t* out_argmax, const float* act, float* taylor, int HWo, int tay_group,
-                                    float* ws, int tay_mode, hipStream_t st) {
+                                    float* ws, int tay_mode, float* apoz, hipStream_t st) {
   using namespace tp;
   if (Cin % 32 != 0) return hipErrorInvalidValue;
   ConvArgs a{};
@@ -940,6 +944,7 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
   a.HWo = HWo;
   a.tay_group = tay_group;
   a.tay_mode = tay_mode;
+  a.apoz = apoz;
   a.Ho = H;
   a.Wo = W;
   a.stride = 1;

@@ -196,18 +196,20 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
       output_transform(m, y);
       if constexpr (EPI == W_FWD_POOL) {
         float best = 0.f;
-        int arg = 0;
+        int arg = 0, cnt = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float v = y[q] * sc + sh;
           if (p.relu) v = nan_relu(v);
+          cnt += v > 0.f ? 1 : 0;
           if (q == 0 || v > best || (v != v && best == best)) {
             best = v;
             arg = q;
           }
         }
         yb[pbuf_row(tl) * 16 + j] = best;
-        ab[pbuf_row(tl) * 32 + j + 16 * n] = (unsigned char)arg;
+        // argmax in bits 0-1; the window's count of positive pre-pool outputs (APoZ) in bits 2-4
+        ab[pbuf_row(tl) * 32 + j + 16 * n] = (unsigned char)(arg | (cnt << 2));
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q) yb[ybuf_row(tl, q) * 16 + j] = y[q];
@@ -231,7 +233,20 @@ phase2:
       const unsigned a4 = *reinterpret_cast<const unsigned*>(ab + pbuf_row(tl) * 32 + 4 * c4);
       const long long o = (long long)pt * p.K + k;
       *reinterpret_cast<float4*>(p.out + o) = v;
-      *reinterpret_cast<unsigned*>(p.out_argmax + o) = a4;
+      *reinterpret_cast<unsigned*>(p.out_argmax + o) = a4 & 0x03030303u;
+    }
+    if (p.apoz) {  // per-(image, channel) counts of positive pre-pool outputs (exact integers)
+      const int b_first = p.fd_timg.div(t0);
+      const int t_last = min(t0 + 64, p.P) - 1;
+      const int n_img = p.fd_timg.div(t_last) - b_first + 1;
+      for (int t = tid; t < n_img * W_TK; t += blockDim.x) {
+        const int bb = b_first + t / W_TK, kk = t % W_TK, kc = k0 + kk;
+        if (bb >= p.B || kc >= p.K) continue;
+        const int lo = max(bb * T_img, t0) - t0, hi = min((bb + 1) * T_img - 1, t_last) - t0;
+        int sum = 0;
+        for (int tl = lo; tl <= hi; ++tl) sum += ab[pbuf_row(tl) * 32 + kk] >> 2;
+        if (sum > 0) atomicAdd(p.apoz + (long long)bb * p.K + kc, (float)sum);
+      }
     }
     return;
   } else {
@@ -801,8 +816,8 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.act = act;
   a.taylor = taylor;
   a.tay_mode = tay_mode;
-  a.apoz = epi == W_FWD ? apoz : nullptr;
-  if (apoz && epi != W_FWD) return hipErrorInvalidValue;
+  a.apoz = (epi == W_FWD || epi == W_FWD_POOL) ? apoz : nullptr;
+  if (apoz && epi != W_FWD && epi != W_FWD_POOL) return hipErrorInvalidValue;
   a.tay_slots = wino_taylor_slots(H, W);
   a.fd_timg = FastDiv((unsigned)std::max(1, (H / 2) * (W / 2)));
   a.fd_w2 = FastDiv((unsigned)std::max(1, W / 2));

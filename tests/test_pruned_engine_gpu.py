@@ -191,3 +191,38 @@ def test_vgg_engine_sensitivity_matches_fp64(cuda, prune):
             assert a.shape == r.shape and a.shape[-1] == m.weight.shape[0]
             err = np.abs(a - r).max() / (np.abs(r).max() + 1e-30)
             assert err < (5e-3 if red == "mean" else 2e-2), (m, red, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prune", [False, True])
+def test_vgg_engine_apoz_matches_generic(cuda, prune):
+    """APoZ counts fused into the VGG engine's forward epilogues (pre-pool ReLU outputs; Winograd
+    / implicit-GEMM / dense-2x2 / classifier blocks) vs the generic hook path."""
+    from torchpruner_amd import APoZAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.models import prunable_vgg16
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(3)
+    model = prunable_vgg16().to(cuda).eval()
+    _bn_stats(model)
+    if prune:
+        _prune_vgg_odd(model, cuda, seed=3)
+    mods = [m for m in model.features if isinstance(m, torch.nn.Conv2d)] + [model.classifier[1], model.classifier[4]]
+    ev = [find_best_module_for_attributions(model, m) for m in mods]
+    assert maybe_engine(model, ev, torch.nn.functional.mse_loss, cuda, need_ce=False) is not None
+    x = torch.randn(24, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (24,), device=cuda)
+    for red in ("mean", "none"):
+        dl = DeviceLoader(x, y, 8)
+        got = APoZAttributionMetric(model, dl, F.cross_entropy, cuda, reduction=red).run_many(mods, True)
+        os.environ["TORCHPRUNER_BACKEND"] = "torch"
+        try:
+            ref = APoZAttributionMetric(model, dl, F.cross_entropy, cuda, reduction=red).run_many(mods, True)
+        finally:
+            del os.environ["TORCHPRUNER_BACKEND"]
+        for m, a, r in zip(mods, got, ref):
+            assert a.shape == r.shape and a.shape[-1] == m.weight.shape[0]
+            # exact counts; only outputs within rounding of 0 may flip between the two conv paths
+            tol = 0.05 * (r.max() + 1) if red == "mean" else 2.0
+            assert np.abs(a - r).max() <= tol, (m, red, np.abs(a - r).max())

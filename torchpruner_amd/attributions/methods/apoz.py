@@ -10,6 +10,7 @@ For torchvision-layout ResNets the whole forward runs on the HIP kernels of the 
 import torch
 
 from ... import ops
+from ...engine import maybe_engine
 from ...engine.resnet_engine import maybe_resnet_engine
 from ..base import _AttributionMetric
 
@@ -26,8 +27,11 @@ class APoZAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            eng = maybe_resnet_engine(self.model, eval_modules, self.device)
-            if eng is not None:
+            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=False)
+            eng = None if fused is not None else maybe_resnet_engine(self.model, eval_modules, self.device)
+            if fused is not None:
+                accs = self._chain_pass(*fused, accs)
+            elif eng is not None:
                 self._engine_pass(eng, eval_modules, accs)
             else:
                 self._forward_capture_pass(eval_modules,
@@ -35,6 +39,29 @@ class APoZAttributionMetric(_AttributionMetric):
         finally:
             self._end_run()
         return [self._finalize(a) for a in accs]
+
+    def _chain_pass(self, engine, blocks, accs):
+        """VGG-style chains: counts fused into the fused engine's forward epilogues (pre-pool
+        ReLU outputs), forward stopped at the deepest requested block."""
+        owner = {}
+        for k, b in enumerate(blocks):
+            owner.setdefault(b, k)
+        uniq = sorted(owner)
+        stats = accs[0].mode == "stats"
+        with torch.no_grad():
+            for i, x, _y in self._batches():
+                B = x.shape[0]
+                bufs = {b: torch.zeros(B, engine._block_width(b), device=x.device) for b in uniq}
+                engine.forward(x, stop_after=uniq[-1], apoz=bufs)
+                if stats:
+                    sums = [accs[owner[b]].ensure_sum(bufs[b].shape[1], x.device, engine.real_width(b)) for b in uniq]
+                    ops.score_fold_([bufs[b] for b in uniq], sums, False, 0)
+                    for b in uniq:
+                        accs[owner[b]].count += B
+                else:
+                    for b in uniq:
+                        accs[owner[b]].add(bufs[b][:, :engine.real_width(b)], i)
+        return [accs[owner[b]] for b in blocks]
 
     def _engine_pass(self, eng, eval_modules, accs):
         uniq = list(dict.fromkeys(eval_modules))

@@ -422,19 +422,22 @@ class FusedChainEngine:
             e["dense"] = d
         return d
 
-    def _conv_run(self, T, e, h, cfg, sp):
+    def _conv_run(self, T, e, h, cfg, sp, apoz=None):
+        """``apoz``: (B, N) buffer that receives the counts of positive (pre-pool) outputs."""
         if cfg in (WINO, WINO_LDS):
-            return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS)
+            return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS, apoz)
         if cfg >= self.DENSE:
             d = self._dense(e)
             B, N = h.shape[0], e["scale"].numel()
             y, _ = T.conv_fwd(h.reshape(B, 1, 1, -1), d["w"], d["scale4"], d["shift4"], True, False, 1,
                               cfg - self.DENSE, sp)
             y = y.view(B, 2, 2, N)
+            if apoz is not None:
+                apoz += ops.channel_reduce(y.permute(0, 3, 1, 2), None, "apoz")
             return T.maxpool2_nhwc(y) if e["pool"] else (y, None)
-        return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp)
+        return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp, apoz)
 
-    def _conv(self, T, e, h):
+    def _conv(self, T, e, h, apoz=None):
         B, H, W, C = h.shape
         M = B * H * W
         N, K = e["scale"].numel(), e["w"].shape[1]
@@ -445,7 +448,7 @@ class FusedChainEngine:
                 TUNER.candidates(M, N, K, wino)
         cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"], wino is not None), M, N, K,
                                lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino, cands=cands)
-        return self._conv_run(T, e, h, cfg, sp)
+        return self._conv_run(T, e, h, cfg, sp, apoz)
 
     def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0):
         """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
@@ -469,23 +472,28 @@ class FusedChainEngine:
         out, _ = T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp)
         return out
 
-    def forward(self, x: torch.Tensor, stop_after: Optional[int] = None):
+    def forward(self, x: torch.Tensor, stop_after: Optional[int] = None, apoz: Optional[dict] = None):
         """Forward pass; returns (logits, saved) where saved holds what backward needs.
         With ``stop_after=k`` returns (output of block k in engine layout, saved) instead:
-        NHWC (pooled when the block pools) for conv blocks, (B,1,1,N) for linear blocks."""
+        NHWC (pooled when the block pools) for conv blocks, (B,1,1,N) for linear blocks.
+        ``apoz`` maps block indices to zeroed (B, padded width) buffers that receive, per sample
+        and unit, the count of positive outputs of the block's ReLU (before pooling)."""
         T = ops.require()
         P = self._pack()
         B = x.shape[0]
+        apoz = apoz or {}
         acts = []  # per conv: (activation NHWC (pooled if pool), argmax or None)
         h = None
         for ci, (blk, e) in enumerate(zip(self.plan.convs, P["convs"])):
             if ci == 0 and blk.first:
                 h = self._first(T, e, x)
                 am = None
+                if ci in apoz:  # first block never pools: count on its output
+                    apoz[ci] += ops.channel_reduce(h.permute(0, 3, 1, 2), None, "apoz")
             else:
                 if ci == 0:
                     h = x.float().permute(0, 2, 3, 1).contiguous()
-                h, am = self._conv(T, e, h)
+                h, am = self._conv(T, e, h, apoz.get(ci))
             acts.append((h, am if e["pool"] else None))
             if stop_after == ci:
                 return h, {"acts": acts}
@@ -493,6 +501,8 @@ class FusedChainEngine:
         nconv = len(self.plan.convs)
         for li, e in enumerate(P["lins"]):
             lin_acts.append(self._linear(T, e, lin_acts[-1]))
+            if nconv + li in apoz:
+                apoz[nconv + li] += ops.channel_reduce(lin_acts[-1].permute(0, 3, 1, 2), None, "apoz")
             if stop_after == nconv + li:
                 return lin_acts[-1], {"acts": acts, "lin_acts": lin_acts}
         logits = lin_acts[-1].reshape(B, -1)
@@ -657,8 +667,9 @@ def criterion_is_cross_entropy(criterion, device) -> bool:
         return False
 
 
-def maybe_engine(model, eval_modules, criterion, device):
-    """Return (engine, block indices of eval_modules) when the fused path applies, else None."""
+def maybe_engine(model, eval_modules, criterion, device, need_ce=True):
+    """Return (engine, block indices of eval_modules) when the fused path applies, else None.
+    ``need_ce=False``: forward-only use (APoZ), any criterion."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda" or ops.backend() == "torch" or not ops.available():
         return None
@@ -680,7 +691,7 @@ def maybe_engine(model, eval_modules, criterion, device):
         if found is None:
             return None
         idx.append(found)
-    if not criterion_is_cross_entropy(criterion, dev):
+    if need_ce and not criterion_is_cross_entropy(criterion, dev):
         return None
     eng = _ENGINES.get(model)
     if eng is None or len(eng.plan.blocks) != len(plan.blocks) or any(
