@@ -131,3 +131,32 @@ def test_prefetch_host_loader_matches_device_loader(cuda):
         np.testing.assert_array_equal(u, v)
     got = [int(t[1][0]) for t in prefetch_to_device(((i, torch.full((3,), i)) for i in range(7)), cuda, depth=3)]
     assert got == list(range(7))
+
+
+class _TinyRes(nn.Module):
+    """Residual model without forward_partial: Shapley's slow (hook) path."""
+
+    def __init__(self):
+        super().__init__()
+        self.fc1 = nn.Linear(6, 8)
+        self.fc2 = nn.Linear(8, 6)
+        self.head = nn.Linear(6, 3)
+
+    def forward(self, x):
+        h = torch.relu(self.fc1(x))
+        return self.head(torch.relu(self.fc2(h) + x))
+
+
+def test_shapley_slow_path_batched_prefixes_on_residual_model():
+    import torch.nn.functional as F
+    from torchpruner_amd import ShapleyAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    torch.manual_seed(0)
+    model = _TinyRes().eval()
+    x, y = torch.randn(10, 6), torch.randint(0, 3, (10,))
+    out = []
+    for pb in (1, None):  # one prefix per forward vs K stacked prefixes per forward
+        np.random.seed(3)
+        out.append(ShapleyAttributionMetric(model, DeviceLoader(x, y, 5), F.cross_entropy, "cpu", sv_samples=3,
+                                            prefix_batch=pb).run(model.fc1))
+    np.testing.assert_allclose(out[0], out[1], rtol=1e-5, atol=1e-7)

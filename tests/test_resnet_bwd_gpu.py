@@ -171,3 +171,38 @@ def test_resnet_engine_grad_scores_deterministic(cuda):
             for _ in range(2)]
     for a, b in zip(*runs):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("prune", [False, True])
+def test_resnet_engine_shapley_matches_fp64(cuda, prune):
+    """Shapley prefix evaluations through the ResNet engine (masked block-internal activation,
+    rest of the block with its residual, remaining blocks) vs the forward_partial path in fp64."""
+    import copy
+    import os
+    import numpy as np
+    from torchpruner_amd import ShapleyAttributionMetric, get_resnet_pruning_graph
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import maybe_resnet_engine
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    model = _resnet("bottleneck", cuda, prune)
+    mods = [m for m, _ in get_resnet_pruning_graph(model)]
+    m64 = copy.deepcopy(model).double().cpu()
+    mods64 = [m for m, _ in get_resnet_pruning_graph(m64)]
+    x = torch.randn(6, 3, 64, 64, device=cuda)
+    y = torch.randint(0, 10, (6,), device=cuda)
+    for li in (0, 3, len(mods) - 1):
+        ev = find_best_module_for_attributions(model, mods[li])
+        assert maybe_resnet_engine(model, [ev], cuda, grad=True) is not None
+        res = []
+        for backend, mdl, mod, d, xx, yy in (("hip", model, mods[li], cuda, x, y),
+                                             ("torch", m64, mods64[li], "cpu", x.double().cpu(), y.cpu())):
+            os.environ["TORCHPRUNER_BACKEND"] = backend
+            try:
+                np.random.seed(7)
+                res.append(ShapleyAttributionMetric(mdl, DeviceLoader(xx, yy, 3), F.cross_entropy, d, sv_samples=2,
+                                                    reduction="none").run(mod, find_best_evaluation_module=True))
+            finally:
+                del os.environ["TORCHPRUNER_BACKEND"]
+        assert res[0].shape == res[1].shape == (6, mods[li].weight.shape[0])
+        scale = np.abs(res[1]).max() + 1e-12
+        assert np.abs(res[0] - res[1]).max() / scale < 2e-2, (li, np.abs(res[0] - res[1]).max(), scale)

@@ -54,7 +54,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
     def run(self, module, sv_samples=None, **kwargs):
         module = super().run(module, **kwargs)
         sv_samples = sv_samples if sv_samples is not None else self.samples
-        fused = self._fused_prepare(module)
+        fused = self._fused_prepare(module) or self._resnet_prepare(module)
         if fused is not None:
             return self._run_batches(module, sv_samples, fused)
         if hasattr(self.model, "forward_partial"):
@@ -175,27 +175,51 @@ class ShapleyAttributionMetric(_AttributionMetric):
         engine, (k,) = fused
 
         n = engine.real_width(k)
-        padded_ranks = {}
+        pad_rank = _RankPadder(n)
 
         def prepare(x, y):
             zk, _ = engine.forward(x, stop_after=k)  # engine layout (B, H, W, C padded)
             B = zk.shape[0]
             z_cl = zk.permute(0, 3, 1, 2)  # (B, C, H, W) view, channels_last strides
             base = engine.loss_from(k, zk, y)
-            pad = zk.shape[3] - n
 
             def evaluate(rank_t, p_first, cnt):
-                if pad:  # padding channels rank after every real unit: never masked
-                    r = padded_ranks.get(id(rank_t))
-                    if r is None or r[0] is not rank_t:
-                        r = padded_ranks[id(rank_t)] = (rank_t, torch.cat([rank_t, torch.full(
-                            (pad,), n + 1, dtype=rank_t.dtype, device=rank_t.device)]))
-                    rank_t = r[1]
-                masked = ops.prefix_mask(z_cl, rank_t, p_first, cnt)  # (cnt*B, C, H, W) channels_last
+                masked = ops.prefix_mask(z_cl, pad_rank(rank_t, zk.shape[3]), p_first, cnt)  # channels_last
                 loss = engine.loss_from(k, masked.permute(0, 2, 3, 1), y.repeat(cnt))
                 return loss.view(cnt, B)
 
             return n, B, zk[0].numel(), base, evaluate
+
+        return prepare
+
+    def _resnet_prepare(self, module):
+        """Prefix evaluation on the ResNet engine (block-internal BN evaluation modules, CE loss):
+        the masked activation and the block's residual operand are produced once per batch,
+        K prefix-masked copies are pushed through the rest of the block and the network in ONE
+        engine forward."""
+        from ...engine.fused_chain import criterion_is_cross_entropy
+        from ...engine.resnet_engine import maybe_resnet_engine
+        eng = maybe_resnet_engine(self.model, [module], self.device, grad=True)
+        if eng is None or not criterion_is_cross_entropy(self.criterion, self.device):
+            return None
+        bi, ci = eng.locate(module)
+        n = module.num_features
+        pad_rank = _RankPadder(n)
+
+        def prepare(x, y):
+            a, idn = eng.forward_to(x, bi, ci)
+            B = a.shape[0]
+            a_cl = a.permute(0, 3, 1, 2)
+            base, _ = ops.cross_entropy(eng.logits_from(bi, ci, a, idn), y, 1.0, False)
+
+            def evaluate(rank_t, p_first, cnt):
+                masked = ops.prefix_mask(a_cl, pad_rank(rank_t, a.shape[3]), p_first, cnt)
+                idn_k = idn.repeat(cnt, 1, 1, 1) if cnt > 1 else idn
+                loss, _ = ops.cross_entropy(eng.logits_from(bi, ci, masked.permute(0, 2, 3, 1), idn_k),
+                                            y.repeat(cnt), 1.0, False)
+                return loss.view(cnt, B)
+
+            return n, B, 2 * a[0].numel(), base, evaluate
 
         return prepare
 
@@ -222,14 +246,16 @@ class ShapleyAttributionMetric(_AttributionMetric):
 
     # ------------------------------------------------------------------ slow path
     def run_module(self, module, samples):
-        """Shapley sampling through full forward passes and a masking forward hook."""
+        """Shapley sampling through full forward passes and a masking forward hook. K prefixes
+        are evaluated by ONE forward of the input stacked K times; the hook masks copy k with
+        prefix p0 + k (stacking at the module instead would break residual / branching models)."""
         state = {"mode": "off"}
 
         def hook(_m, _inp, out):
             module._tp_prune_dim = out.shape[1]
             if state["mode"] == "off":
                 return None
-            return ops.prefix_mask(out.contiguous(), state["rank"], state["p0"], state["K"])
+            return _mask_stacked(out, state["rank"], state["p0"], state["K"])
 
         handle = module.register_forward_hook(hook)
         try:
@@ -248,7 +274,8 @@ class ShapleyAttributionMetric(_AttributionMetric):
                     self.set_deterministic()
                     try:
                         yy = y.repeat((cnt,) + (1,) * (y.dim() - 1))
-                        loss = self.criterion(self.model(x), yy, reduction="none")
+                        xx = x.repeat((cnt,) + (1,) * (x.dim() - 1)) if cnt > 1 else x
+                        loss = self.criterion(self.model(xx), yy, reduction="none")
                     finally:
                         state["mode"] = "off"
                         self.restore_deterministic()
@@ -270,6 +297,36 @@ class ShapleyAttributionMetric(_AttributionMetric):
             return output.index_fill_(1, torch.tensor(self.mask_indices, dtype=torch.long,
                                                       device=output.device), 0.0)
         return _hook
+
+
+def _mask_stacked(out, rank, p0, K):
+    """``out`` holds K stacked copies (K*B, C, ...): zero, in copy k, the channels of rank <
+    p0 + k (exact zeros, as index_fill_ in the reference)."""
+    C = out.shape[1]
+    ks = torch.arange(K, device=out.device).view(K, 1) + p0
+    keep = rank.to(out.device).view(1, C) >= ks  # (K, C)
+    o = out.reshape((K, -1) + tuple(out.shape[1:]))
+    keep = keep.view((K, 1, C) + (1,) * (out.dim() - 2))
+    return torch.where(keep, o, torch.zeros((), dtype=out.dtype, device=out.device)).reshape(out.shape)
+
+
+class _RankPadder:
+    """Rank vectors over ``n`` real units extended to the engine's channel-padded width: padding
+    channels rank after every real unit, so no prefix ever masks them (cached per rank vector)."""
+
+    def __init__(self, n):
+        self.n = n
+        self.cache = {}
+
+    def __call__(self, rank_t, width):
+        pad = width - self.n
+        if pad <= 0:
+            return rank_t
+        r = self.cache.get(id(rank_t))
+        if r is None or r[0] is not rank_t:
+            r = self.cache[id(rank_t)] = (rank_t, torch.cat([rank_t, torch.full(
+                (pad,), self.n + 1, dtype=rank_t.dtype, device=rank_t.device)]))
+        return r[1]
 
 
 def _to(t, device):

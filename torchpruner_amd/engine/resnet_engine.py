@@ -198,34 +198,80 @@ class ResNetEngine:
                 tmp = buf.new_zeros(buf.shape[0], cpad(buf.shape[1]))
                 padded.append((buf, tmp))
                 apoz[m] = tmp
+        h = self._stem(T, P, x, apoz)
+        saved = []
+        for blk, e in zip(self.plan.blocks, P["blocks"]):
+            h = self._block(T, blk, e, h, apoz, saved if save else None)
+        feat = T.avgpool_nhwc(h)
+        for buf, tmp in padded:
+            buf.add_(tmp[:, :buf.shape[1]])
+        logits = F.linear(feat, P["fc_w"], P["fc_b"])
+        return (logits, saved) if save else logits
+
+    def _stem(self, T, P, x, apoz):
         h = T.nchw_to_nhwc_pad(x.float().contiguous(), 4)
         h = self._conv(T, P["stem"], h, True, apoz=apoz.get(self.plan.stem.bn))
         mp = self.plan.maxpool
         k = mp.kernel_size if isinstance(mp.kernel_size, int) else mp.kernel_size[0]
         s = mp.stride if isinstance(mp.stride, int) else mp.stride[0]
         pd = mp.padding if isinstance(mp.padding, int) else mp.padding[0]
-        h = T.maxpool_nhwc(h, k, s, pd)
-        saved = []
-        for blk, e in zip(self.plan.blocks, P["blocks"]):
-            idn = h
-            if e["ds"] is not None:
-                idn = self._conv(T, e["ds"], h, False)
-            t = h
-            n = len(e["convs"])
-            inner = []
-            for i, (c, ce) in enumerate(zip(blk.convs, e["convs"])):
-                last = i == n - 1
-                t = self._conv(T, ce, t, True, res=idn if last else None, apoz=apoz.get(c.bn))
-                if not last:
-                    inner.append(t)
-            if save:
-                saved.append((h, inner, t))
-            h = t
-        feat = T.avgpool_nhwc(h)
-        for buf, tmp in padded:
-            buf.add_(tmp[:, :buf.shape[1]])
-        logits = F.linear(feat, P["fc_w"], P["fc_b"])
-        return (logits, saved) if save else logits
+        return T.maxpool_nhwc(h, k, s, pd)
+
+    def _block(self, T, blk, e, h, apoz=None, saved=None):
+        """One residual block: downsample / identity, convs with the residual add + ReLU fused
+        into the last conv's epilogue; appends (input, inner activations, output) to ``saved``."""
+        apoz = apoz or {}
+        idn = self._conv(T, e["ds"], h, False) if e["ds"] is not None else h
+        t = h
+        n = len(e["convs"])
+        inner = []
+        for i, (c, ce) in enumerate(zip(blk.convs, e["convs"])):
+            last = i == n - 1
+            t = self._conv(T, ce, t, True, res=idn if last else None, apoz=apoz.get(c.bn))
+            if not last:
+                inner.append(t)
+        if saved is not None:
+            saved.append((h, inner, t))
+        return t
+
+    # ------------------------------------------------------------------ partial forward (Shapley)
+    def locate(self, bn):
+        """(block, conv) index whose BN output ``bn`` is, for the block-internal BNs."""
+        for bi, blk in enumerate(self.plan.blocks):
+            for ci, c in enumerate(blk.convs[:-1]):
+                if c.bn is bn:
+                    return bi, ci
+        raise KeyError("not a block-internal BatchNorm of this ResNet")
+
+    def forward_to(self, x: torch.Tensor, bi: int, ci: int):
+        """(post-ReLU output of conv ``ci`` of block ``bi``, that block's residual operand), both
+        in engine layout: the state ``logits_from`` continues from. Masking a channel of the BN
+        output equals masking it after the ReLU (ReLU(0) = 0)."""
+        T = ops.require()
+        P = self._pack()
+        h = self._stem(T, P, x, {})
+        for b in range(bi):
+            h = self._block(T, self.plan.blocks[b], P["blocks"][b], h)
+        e = P["blocks"][bi]
+        idn = self._conv(T, e["ds"], h, False) if e["ds"] is not None else h
+        t = h
+        for i in range(ci + 1):
+            t = self._conv(T, e["convs"][i], t, True)
+        return t, idn
+
+    def logits_from(self, bi: int, ci: int, a: torch.Tensor, idn: torch.Tensor) -> torch.Tensor:
+        """Logits of the network continued from ``forward_to``'s state (``a`` possibly masked and
+        stacked K times along the batch, ``idn`` stacked the same way)."""
+        T = ops.require()
+        P = self._pack()
+        e = P["blocks"][bi]
+        n = len(e["convs"])
+        t = a
+        for i in range(ci + 1, n):
+            t = self._conv(T, e["convs"][i], t, True, res=idn if i == n - 1 else None)
+        for b in range(bi + 1, len(self.plan.blocks)):
+            t = self._block(T, self.plan.blocks[b], P["blocks"][b], t)
+        return F.linear(T.avgpool_nhwc(t), P["fc_w"], P["fc_b"])
 
     # ------------------------------------------------------------------ backward (Taylor, Sensitivity)
     @staticmethod
