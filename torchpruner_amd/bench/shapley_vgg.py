@@ -53,17 +53,27 @@ def main():
     ap.add_argument("--sv-samples", type=int, default=5)
     ap.add_argument("--reference", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--model", default="vgg16", choices=["vgg16", "resnet50"],
+                    help="resnet50: ImageNet-shaped input, prunable = conv1/conv2 of every bottleneck")
     args = ap.parse_args()
     ctx = pdist.init_distributed()
     dev = ctx.device
     torch.manual_seed(0)
     np.random.seed(0)
-    model = prunable_vgg16().to(dev).eval()
-    task = PrototypeTask((3, 32, 32), 10, noise=2.0, seed=0, device=dev)
-    x, y = task.sample(args.images, 1)
+    if args.model == "resnet50":
+        from torchpruner_amd import get_resnet_pruning_graph
+        from torchpruner_amd.models import resnet50
+        model = resnet50().to(dev).eval()
+        x = torch.randn(args.images, 3, 224, 224, device=dev)
+        y = torch.randint(0, 1000, (args.images,), device=dev)
+        prunable = [m for m, _ in get_resnet_pruning_graph(model)][::-1]  # input -> output order
+    else:
+        model = prunable_vgg16().to(dev).eval()
+        task = PrototypeTask((3, 32, 32), 10, noise=2.0, seed=0, device=dev)
+        x, y = task.sample(args.images, 1)
+        prunable = [m for m in model.features if isinstance(m, torch.nn.Conv2d)] + [model.classifier[1],
+                                                                                     model.classifier[4]]
     dl = DeviceLoader(x, y, args.batch)
-    prunable = [m for m in model.features if isinstance(m, torch.nn.Conv2d)] + [model.classifier[1],
-                                                                                 model.classifier[4]]
     metric = ShapleyAttributionMetric(model, dl, F.cross_entropy, dev, sv_samples=args.sv_samples)
     out = {"n_gpus": ctx.world_size, "images": args.images, "batch": args.batch, "sv_samples": args.sv_samples,
            "layers": []}
