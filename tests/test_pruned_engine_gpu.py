@@ -226,3 +226,41 @@ def test_vgg_engine_apoz_matches_generic(cuda, prune):
             # exact counts; only outputs within rounding of 0 may flip between the two conv paths
             tol = 0.05 * (r.max() + 1) if red == "mean" else 2.0
             assert np.abs(a - r).max() <= tol, (m, red, np.abs(a - r).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth,bn", [(11, True), (13, False), (19, True)])
+def test_vgg_variants_on_engine(cuda, depth, bn):
+    """Every VGG of the zoo (11-19 layers, with / without BN; VGG11 pools right after its
+    tiny-Cin first conv) lowers to the fused engine: Taylor vs the fp64 oracle, APoZ vs the
+    generic hook path."""
+    from torchpruner_amd import APoZAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.models.vgg import vgg_cifar
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(depth)
+    model = vgg_cifar(depth, batch_norm=bn).to(cuda).eval()
+    _bn_stats(model)
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    ev = [find_best_module_for_attributions(model, m) for m in convs]
+    assert maybe_engine(model, ev, F.cross_entropy, cuda) is not None
+    x = torch.randn(16, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (16,), device=cuda)
+    dl = DeviceLoader(x, y, 8)
+    got = TaylorAttributionMetric(model, dl, F.cross_entropy, cuda).run_many(convs, True)
+    apoz = APoZAttributionMetric(model, dl, F.cross_entropy, cuda).run_many(convs, True)
+    m64 = copy.deepcopy(model).double().cpu()
+    c64 = [m for m in m64.features if isinstance(m, torch.nn.Conv2d)]
+    os.environ["TORCHPRUNER_BACKEND"] = "torch"
+    try:
+        ref = TaylorAttributionMetric(m64, DeviceLoader(x.double().cpu(), y.cpu(), 8), F.cross_entropy,
+                                      "cpu").run_many(c64, True)
+        apoz_ref = APoZAttributionMetric(model, dl, F.cross_entropy, cuda).run_many(convs, True)
+    finally:
+        del os.environ["TORCHPRUNER_BACKEND"]
+    for m, a, r in zip(convs, got, ref):
+        assert a.shape == r.shape
+        assert np.abs(a - r).max() / (np.abs(r).max() + 1e-30) < 5e-3, m
+    for m, a, r in zip(convs, apoz, apoz_ref):
+        assert np.abs(a - r).max() <= 0.05 * (r.max() + 1), m

@@ -262,8 +262,8 @@ def build_plan(model: nn.Module):
         # scores are exactly 0 and never influence the real channels
         width = cpad(conv.out_channels)
         if first and conv.in_channels % 32 != 0:
-            if pool is not None or conv.out_channels > 64:
-                return None, "first conv must be unpooled with at most 64 outputs"
+            if conv.out_channels > 64:
+                return None, "first (tiny-Cin) conv must have at most 64 outputs"
             width = 16 if conv.out_channels <= 16 else width
         plan.convs.append(ConvBlock(conv, bn, relu, pool, first=first and conv.in_channels % 32 != 0,
                                     width=width))
@@ -382,23 +382,27 @@ class FusedChainEngine:
     # ------------------------------------------------------------------ execution
     FIRST_DIRECT = -10  # pseudo cfg: VALU direct first-layer kernel
 
-    def _first_run(self, T, e, xf, cfg, sp):
+    def _first_run(self, T, e, xf, cfg, sp, apoz=None):
+        """First (tiny-Cin) conv block -> (output, argmax or None): the block's 2x2 max-pool is
+        fused into the Winograd epilogue, or applied after the VALU direct conv."""
         if cfg == self.FIRST_DIRECT:
-            return T.conv_first(xf, e["w_first"], e["scale"], e["shift"], True)
+            h = T.conv_first(xf, e["w_first"], e["scale"], e["shift"], True)
+            if apoz is not None:
+                apoz += ops.channel_reduce(h.permute(0, 3, 1, 2), None, "apoz")
+            return T.maxpool2_nhwc(h) if e["pool"] else (h, None)
         xp = T.nchw_to_nhwc_pad(xf, 8)
-        out, _ = T.conv_wino_fwd(xp, e["u_first"], e["scale"], e["shift"], True, False, sp, cfg == WINO_LDS)
-        return out
+        return T.conv_wino_fwd(xp, e["u_first"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS, apoz)
 
-    def _first(self, T, e, x):
+    def _first(self, T, e, x, apoz=None):
         xf = x.float().contiguous()
         B, _, H, W = xf.shape
         N = e["scale"].numel()
         if "u_first" not in e or not _wino_ok(H, W, 8, N):
-            return T.conv_first(xf, e["w_first"], e["scale"], e["shift"], True)
+            return self._first_run(T, e, xf, self.FIRST_DIRECT, 1, apoz)
         cands = [(WINO_LDS, 1), (self.FIRST_DIRECT, 1), (WINO, 1)]
-        cfg, sp = TUNER.choose(("first", tuple(xf.shape), N), B * H * W, N, 27, lambda c, s_, e=e, xf=xf:
-                               self._first_run(T, e, xf, c, s_), cands=cands)
-        return self._first_run(T, e, xf, cfg, sp)
+        cfg, sp = TUNER.choose(("first", tuple(xf.shape), N, e["pool"]), B * H * W, N, 27,
+                               lambda c, s_, e=e, xf=xf: self._first_run(T, e, xf, c, s_), cands=cands)
+        return self._first_run(T, e, xf, cfg, sp, apoz)
 
     # A 3x3/pad-1 conv on a 2x2 image is a dense GEMM: every output pixel q sees input pixel p
     # through tap (p - q + 1): y(B, 4K) = x(B, 4C) @ Wbig^T with Wbig (4K, 4C) — the same 2.25x
@@ -486,10 +490,7 @@ class FusedChainEngine:
         h = None
         for ci, (blk, e) in enumerate(zip(self.plan.convs, P["convs"])):
             if ci == 0 and blk.first:
-                h = self._first(T, e, x)
-                am = None
-                if ci in apoz:  # first block never pools: count on its output
-                    apoz[ci] += ops.channel_reduce(h.permute(0, 3, 1, 2), None, "apoz")
+                h, am = self._first(T, e, x, apoz.get(ci))
             else:
                 if ci == 0:
                     h = x.float().permute(0, 2, 3, 1).contiguous()
