@@ -127,7 +127,7 @@ class _AttributionMetric(ABC):
     """Abstract base of every metric (reference attributions.py:15-25)."""
 
     def __init__(self, model, data_generator, criterion, device, reduction="mean", *, group=None,
-                 shard_data=None, checkpoint=None, checkpoint_every=50):
+                 shard_data=None, checkpoint=None, checkpoint_every=50, compute_dtype=None):
         assert reduction in ["mean", "none", "sum"] or callable(reduction), \
             'Reduction must be a string in ["mean", "none", "sum"] or a function'
         self.model = model
@@ -145,6 +145,12 @@ class _AttributionMetric(ABC):
         # ``checkpoint_every`` batches to ``checkpoint`` (a per-rank path in DP runs).
         self.checkpoint = checkpoint
         self.checkpoint_every = checkpoint_every
+        # dtype policy (new): None / float32 = exact fp32 (the reference's precision; the fused
+        # engines apply); bfloat16 / float16 = opt-in autocast of the model's forward passes on
+        # the generic path (scores are still reduced and accumulated in fp32/fp64)
+        assert compute_dtype in (None, torch.float32, torch.bfloat16, torch.float16), \
+            "compute_dtype must be None, torch.float32, torch.bfloat16 or torch.float16"
+        self.compute_dtype = compute_dtype
         self._ckpt = None
         self._run_accs = None
 
@@ -167,7 +173,9 @@ class _AttributionMetric(ABC):
         try:
             with torch.no_grad():
                 for _, x, y in self._batches():
-                    losses.append(self.criterion(self.model(x), y, reduction="none"))
+                    with self._autocast():
+                        out = self.model(x)
+                    losses.append(self.criterion(out.float(), y, reduction="none"))
         finally:
             self.restore_deterministic()
         return torch.cat(losses, 0) if losses else None
@@ -177,7 +185,9 @@ class _AttributionMetric(ABC):
         self.set_deterministic()
         try:
             for _, x, y in self._batches():
-                loss = self.criterion(self.model(x), y)
+                with self._autocast():
+                    out = self.model(x)
+                loss = self.criterion(out.float(), y)
                 loss.backward()
         finally:
             self.restore_deterministic()
@@ -187,9 +197,10 @@ class _AttributionMetric(ABC):
         self.set_deterministic()
         loss = None
         try:
-            y = self.model.forward_partial(x, to_module=to_module, from_module=from_module)
+            with self._autocast():
+                y = self.model.forward_partial(x, to_module=to_module, from_module=from_module)
             if y_true is not None and to_module is None:
-                loss = self.criterion(y, y_true, reduction="none")
+                loss = self.criterion(y.float(), y_true, reduction="none")
         finally:
             self.restore_deterministic()
         return y, loss
@@ -225,6 +236,19 @@ class _AttributionMetric(ABC):
         torch.backends.cudnn.benchmark = self.benchmark
 
     # ------------------------------------------------------------------ engine internals
+    def _reduced_precision(self) -> bool:
+        return self.compute_dtype in (torch.bfloat16, torch.float16)
+
+    def _engines_allowed(self) -> bool:
+        """The fused HIP engines compute in exact fp32; a reduced compute dtype uses the
+        generic (autocast) path instead."""
+        return not self._reduced_precision()
+
+    def _autocast(self):
+        if not self._reduced_precision():
+            return contextlib.nullcontext()
+        return torch.autocast(device_type=torch.device(self.device).type, dtype=self.compute_dtype)
+
     def _world(self):
         return pdist.get_world_size(self.group), pdist.get_rank(self.group)
 
@@ -337,7 +361,9 @@ class _AttributionMetric(ABC):
                 for i, x, y in self._batches():
                     state["idx"] = i
                     state["leafed"] = False
-                    loss = self.criterion(self.model(x), y)
+                    with self._autocast():
+                        out = self.model(x)
+                    loss = self.criterion(out.float(), y)
                     loss.backward()
         finally:
             for h in handles:
@@ -374,6 +400,8 @@ class _AttributionMetric(ABC):
         torchvision-layout ResNet, block BNs, mean cross-entropy criterion), else None."""
         from ..engine.fused_chain import criterion_is_cross_entropy
         from ..engine.resnet_engine import maybe_resnet_engine
+        if not self._engines_allowed():
+            return None
         eng = maybe_resnet_engine(self.model, eval_modules, self.device, grad=True)
         if eng is None or not criterion_is_cross_entropy(self.criterion, self.device):
             return None
@@ -417,7 +445,8 @@ class _AttributionMetric(ABC):
             with torch.no_grad():
                 for i, x, _y in self._batches():
                     state["idx"] = i
-                    self.model(x)
+                    with self._autocast():
+                        self.model(x)
         finally:
             for h in handles:
                 h.remove()

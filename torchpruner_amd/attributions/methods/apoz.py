@@ -27,8 +27,9 @@ class APoZAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=False)
-            eng = None if fused is not None else maybe_resnet_engine(self.model, eval_modules, self.device)
+            ok = self._engines_allowed()
+            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=False) if ok else None
+            eng = None if fused is not None or not ok else maybe_resnet_engine(self.model, eval_modules, self.device)
             if fused is not None:
                 accs = self._chain_pass(*fused, accs)
             elif eng is not None:

@@ -20,7 +20,7 @@ class SensitivityAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device)
+            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device) if self._engines_allowed() else None
             rn = None if fused is not None else self._resnet_grad_engine(eval_modules)
             if fused is not None:  # VGG-style chains: |dL/da| partials from the fused dgrad epilogues
                 accs = self._fused_grad_pass(*fused, accs, "sensitivity", False)

@@ -169,7 +169,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
         are stacked by one kernel and pushed through the remaining fused layers in ONE forward.
         Masking a post-ReLU activation commutes with the following 2x2 max-pool, so the
         engine masks its pooled output (4x less data) with identical results."""
-        fused = maybe_engine(self.model, [module], self.criterion, self.device)
+        fused = maybe_engine(self.model, [module], self.criterion, self.device) if self._engines_allowed() else None
         if fused is None:
             return None
         engine, (k,) = fused
@@ -199,7 +199,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
         engine forward."""
         from ...engine.fused_chain import criterion_is_cross_entropy
         from ...engine.resnet_engine import maybe_resnet_engine
-        eng = maybe_resnet_engine(self.model, [module], self.device, grad=True)
+        eng = maybe_resnet_engine(self.model, [module], self.device, grad=True) if self._engines_allowed() else None
         if eng is None or not criterion_is_cross_entropy(self.criterion, self.device):
             return None
         bi, ci = eng.locate(module)
@@ -263,7 +263,9 @@ class ShapleyAttributionMetric(_AttributionMetric):
                 self.set_deterministic()
                 try:
                     state["mode"] = "off"
-                    base = self.criterion(self.model(x), y, reduction="none")
+                    with self._autocast():
+                        out = self.model(x)
+                    base = self.criterion(out.float(), y, reduction="none")
                 finally:
                     self.restore_deterministic()
                 B = x.shape[0]
@@ -275,7 +277,9 @@ class ShapleyAttributionMetric(_AttributionMetric):
                     try:
                         yy = y.repeat((cnt,) + (1,) * (y.dim() - 1))
                         xx = x.repeat((cnt,) + (1,) * (x.dim() - 1)) if cnt > 1 else x
-                        loss = self.criterion(self.model(xx), yy, reduction="none")
+                        with self._autocast():
+                            out = self.model(xx)
+                        loss = self.criterion(out.float(), yy, reduction="none")
                     finally:
                         state["mode"] = "off"
                         self.restore_deterministic()

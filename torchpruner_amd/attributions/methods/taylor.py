@@ -31,7 +31,7 @@ class TaylorAttributionMetric(_AttributionMetric):
             self._end_run()
 
     def _run_loop(self, eval_modules, accs, mode):
-        fused = maybe_engine(self.model, eval_modules, self.criterion, self.device)
+        fused = maybe_engine(self.model, eval_modules, self.criterion, self.device) if self._engines_allowed() else None
         if fused is not None:
             # native path: one fused forward + input-grad backward scores every module, then
             # ONE fold launch turns all layers' per-sample sums into |.| and fp64 accumulators

@@ -54,7 +54,12 @@ def channel_reduce(act: torch.Tensor | None, grad: torch.Tensor | None, mode: st
             act = act.float().contiguous(memory_format=fmt)
             grad = grad.float().contiguous(memory_format=fmt)
         return require().channel_reduce(_f32(act), _f32(grad), m)
-    # PyTorch reference
+    # PyTorch reference (reduced-precision operands are reduced in fp32)
+    if act is not None and act.dtype in (torch.float16, torch.bfloat16):
+        act = act.float()
+    if grad is not None and grad.dtype in (torch.float16, torch.bfloat16):
+        grad = grad.float()
+    ref = act if act is not None else grad
     if mode in ("taylor", "taylor_signed"):
         v = -(grad * act)
     elif mode == "sensitivity":
