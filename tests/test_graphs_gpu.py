@@ -1,0 +1,66 @@
+"""HIP-graph replay of the fused engine's Taylor step (small, launch-bound batches).
+
+The graphed path must give bit-identical scores to the eager launches (the engine's kernels are
+deterministic), survive ragged last batches (own graph per shape), and notice re-packed weights
+(pruning / BN changes invalidate the captured graph)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+
+def _scores(model, x, y, B, env, **kw):
+    from torchpruner_amd import SensitivityAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    metric = SensitivityAttributionMetric if kw.pop("sensitivity", False) else TaylorAttributionMetric
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    old = os.environ.get("TORCHPRUNER_GRAPHS")
+    os.environ["TORCHPRUNER_GRAPHS"] = env
+    try:
+        return metric(model, DeviceLoader(x, y, B), F.cross_entropy, x.device, **kw).run_many(convs, True)
+    finally:
+        if old is None:
+            del os.environ["TORCHPRUNER_GRAPHS"]
+        else:
+            os.environ["TORCHPRUNER_GRAPHS"] = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sensitivity", [False, True])
+def test_graphed_taylor_bit_identical(cuda, sensitivity):
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.models import prunable_vgg16
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(0)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    eng, _ = maybe_engine(model, [find_best_module_for_attributions(model, c) for c in convs], F.cross_entropy, cuda)
+    x = torch.randn(150, 3, 32, 32, device=cuda)  # 4 batches of 40 -> last one ragged (30)
+    y = torch.randint(0, 10, (150,), device=cuda)
+    ref = _scores(model, x, y, 40, "0", sensitivity=sensitivity)
+    for _ in range(2):  # first run: eager + capture; second: pure replay
+        got = _scores(model, x, y, 40, "1", sensitivity=sensitivity)
+        for a, r in zip(got, ref):
+            np.testing.assert_array_equal(a, r)
+    assert any(k[0] != "seen" for k in eng._graphs), "no graph was captured"
+
+
+@pytest.mark.gpu
+def test_graph_invalidated_by_new_weights(cuda):
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(1)
+    model = prunable_vgg16().to(cuda).eval()
+    x = torch.randn(64, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (64,), device=cuda)
+    _scores(model, x, y, 32, "1")
+    _scores(model, x, y, 32, "1")  # graph captured and replayed
+    with torch.no_grad():  # in-place BN change: version bump -> re-pack -> new graph
+        bn = model.features[1]
+        bn.weight.mul_(1.5)
+        bn.running_mean.add_(0.1)
+    got = _scores(model, x, y, 32, "1")
+    ref = _scores(model, x, y, 32, "0")
+    for a, r in zip(got, ref):
+        np.testing.assert_array_equal(a, r)

@@ -383,7 +383,10 @@ class _AttributionMetric(ABC):
             B = x.shape[0]
             if stats:
                 arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
-                engine.taylor(x, y, set(uniq), arena, mode=mode)
+                if engine.graphs_enabled(B):  # small batches are launch-bound: replay a HIP graph
+                    engine.taylor_graphed(x, y, set(uniq), arena, mode=mode)
+                else:
+                    engine.taylor(x, y, set(uniq), arena, mode=mode)
                 sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device, engine.real_width(b)) for b in uniq]
                 ops.score_fold_([arena[b] for b in uniq], sums, take_abs, 2)
                 for b in uniq:

@@ -305,6 +305,7 @@ class FusedChainEngine:
         self._key = None
         self._packed = None
         self._arenas = {}
+        self._graphs = {}  # HIP graphs of taylor() per (shapes, blocks, mode)
         self.use_wino = os.environ.get("TORCHPRUNER_WINOGRAD", "1") != "0"
 
     # ------------------------------------------------------------------ weights
@@ -579,6 +580,50 @@ class FusedChainEngine:
         """Number of real (unpadded) units of block b."""
         blk = self.plan.blocks[b]
         return blk.conv.out_channels if isinstance(blk, ConvBlock) else blk.linear.out_features
+
+    # TORCHPRUNER_GRAPHS=1: replay HIP graphs for batches up to GRAPH_MAX_B; "all": any size.
+    # Off by default: measured on MI355X the step is GPU-bound down to B=8 (1.0 ms/step), so
+    # graphs gain nothing there (profiles/hip_graphs_taylor_step.txt); they help when the host
+    # cannot keep the launch queue ahead (contended CPUs).
+    GRAPH_MAX_B = 1024
+
+    def graphs_enabled(self, B: int) -> bool:
+        mode = os.environ.get("TORCHPRUNER_GRAPHS", "0")
+        return mode == "all" or (mode == "1" and B <= self.GRAPH_MAX_B)
+
+    def taylor_graphed(self, x: torch.Tensor, y: torch.Tensor, want: set, arena: dict, mode="taylor"):
+        """``taylor()`` replayed from a captured HIP graph: the ~40 launches of one fused
+        forward + input-gradient backward become one graph launch, which is what small,
+        launch-bound batches need. One graph per (input shapes, blocks, mode, score arena,
+        packed weights): the first call of a new key runs eagerly (it also autotunes the kernels
+        and builds the lazily packed operands), the second captures, later calls copy the batch
+        into the graph's static inputs and replay. Re-packed weights (pruning, training) or a
+        new arena invalidate the graph. ``arena`` must be zero before each call, as for
+        ``taylor()`` (ops.score_fold_ with after=2 leaves it so)."""
+        P = self._pack()
+        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device))
+        g = self._graphs.get(key)
+        if g is not None and (g["P"] is not P or g["arena"] is not arena):
+            g = None
+        if g is None:
+            seen = self._graphs.get(("seen",) + key)
+            if seen is None or seen[0] is not P or seen[1] is not arena:
+                self._graphs[("seen",) + key] = (P, arena)
+                return self.taylor(x, y, want, arena, mode)
+            sx, sy = x.clone(), y.clone()
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(x.device)
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            with torch.cuda.graph(graph, stream=side):
+                self.taylor(sx, sy, want, arena, mode)
+            torch.cuda.current_stream(x.device).wait_stream(side)
+            if len(self._graphs) > 32:  # bound the graphs' private memory pools
+                self._graphs.clear()
+            g = self._graphs[key] = {"graph": graph, "x": sx, "y": sy, "P": P, "arena": arena}
+        g["x"].copy_(x)
+        g["y"].copy_(y)
+        g["graph"].replay()
+        return {b: arena[b] for b in want}
 
     def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None, mode="taylor"):
         """One fused forward+backward; returns {block index: per-sample signed Taylor sums
