@@ -626,6 +626,12 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   }
 }
 
+// dgrad combines of images with at least this many pixels run one 1024-thread block per
+// (image, 64 channels) (conv_epilogue_bwd_img); below it one thread per (image, channel) walks
+// the pixels. At 64 pixels the thread-per-channel walk left B=100 batches with 50-100 blocks
+// of 64-deep serial load chains (67-101 us per combine, 22% of the step).
+constexpr int BWD_IMG_MIN_HW = 16;
+
 // Split-K combine + epilogue (deterministic order over the slabs), one thread per output
 // element (or per pooled element).
 template <int EPI>
@@ -722,8 +728,8 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         if (p.apoz && v > 0.f) atomicAdd(p.apoz + (size_t)(o / N / (unsigned)p.HWo) * N + n, 1.f);
       }
     }
-  } else if (p.HWo > 64) {
-    // EPI_BWD, large images: handled by conv_epilogue_bwd_img (block per image x 64 channels)
+  } else if (p.HWo >= BWD_IMG_MIN_HW) {
+    // EPI_BWD, images of >= 16 pixels: handled by conv_epilogue_bwd_img (block per image x 64 channels)
   } else {  // EPI_BWD, small images: one thread per (image, channel) walks the image's
             // pixels, so the Taylor sum is a plain deterministic += (no atomics)
     const long long BN = (long long)(p.M / p.HWo) * p.N;
@@ -962,11 +968,11 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
                          : dispatch_epi<1>(cfg, EPI_PARTIAL, pooled_m, unpool, b, splits, st);
   if (e != hipSuccess) return e;
   const long long MN = (long long)a.M * a.N;
-  const long long work = epi == EPI_FWD_POOL ? MN / 4 : (epi == EPI_BWD && a.HWo <= 64 ? MN / a.HWo : MN);
+  const long long work = epi == EPI_FWD_POOL ? MN / 4 : (epi == EPI_BWD && a.HWo < BWD_IMG_MIN_HW ? MN / a.HWo : MN);
   unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
   if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
   else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
-  else if (epi == EPI_BWD && a.HWo > 64)
+  else if (epi == EPI_BWD && a.HWo >= BWD_IMG_MIN_HW)
     conv_epilogue_bwd_img<<<dim3((unsigned)ceil_div(a.N, 64), (unsigned)(a.M / a.HWo)), 1024, 0, st>>>(a, ws, splits);
   else if (epi == EPI_BWD) conv_epilogue<EPI_BWD><<<grid, 256, 0, st>>>(a, ws, splits);
   else return hipErrorInvalidValue;
@@ -998,11 +1004,11 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
   a.apoz = apoz;
   a.HWo = H * W;
   const long long MN = (long long)a.M * a.N;
-  const long long work = epi == EPI_FWD_POOL ? MN / 4 : (epi == EPI_BWD && a.HWo <= 64 ? MN / a.HWo : MN);
+  const long long work = epi == EPI_FWD_POOL ? MN / 4 : (epi == EPI_BWD && a.HWo < BWD_IMG_MIN_HW ? MN / a.HWo : MN);
   unsigned grid = (unsigned)std::min<long long>(ceil_div(work, 256), 4096);
   if (epi == EPI_FWD_POOL) conv_epilogue<EPI_FWD_POOL><<<grid, 256, 0, st>>>(a, ws, splits);
   else if (epi == EPI_FWD) conv_epilogue<EPI_FWD><<<grid, 256, 0, st>>>(a, ws, splits);
-  else if (epi == EPI_BWD && a.HWo > 64)
+  else if (epi == EPI_BWD && a.HWo >= BWD_IMG_MIN_HW)
     conv_epilogue_bwd_img<<<dim3((unsigned)ceil_div(a.N, 64), (unsigned)(a.M / a.HWo)), 1024, 0, st>>>(a, ws, splits);
   else if (epi == EPI_BWD) conv_epilogue<EPI_BWD><<<grid, 256, 0, st>>>(a, ws, splits);
   else return hipErrorInvalidValue;
