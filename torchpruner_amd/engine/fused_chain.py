@@ -649,7 +649,7 @@ class FusedChainEngine:
         # classifier (dgrad of linear j produces the grad at its input = output of block j-1)
         e_last = P["lins"][-1]
         if e_last["pad"]:
-            g = torch.cat([g, torch.zeros(B, e_last["pad"], device=g.device)], 1)
+            g = F.pad(g, (0, e_last["pad"]))  # one kernel (zeros + cat was two)
         g = g.reshape(B, 1, 1, -1).contiguous()
         for j in range(nlin - 1, -1, -1):
             e = P["lins"][j]
