@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--train-steps", type=int, default=int(os.environ.get("BENCH_TRAIN_STEPS", 300)),
                     help="untimed SGD steps on the synthetic task before scoring (0 = random init)")
+    ap.add_argument("--finetune-steps", type=int, default=int(os.environ.get("BENCH_FINETUNE_STEPS", 100)),
+                    help="untimed SGD steps after the one-shot all-layer 50%% prune (Taylor and Random alike)")
     ap.add_argument("--task-noise", type=float, default=2.0, help="per-pixel noise of the synthetic prototype task")
     ap.add_argument("--task-modes", type=int, default=8,
                     help="prototypes per class: a mixture task that needs VGG16's capacity, so pruning half of "
@@ -119,6 +121,25 @@ def prune_half(model, scores_by_conv, dev):
             continue
         idx = np.argsort(s, kind="stable")[: len(s) // 2]
         pruner.prune_model(module, idx, cascading_modules=cascade)
+
+
+def finetune(model, task, steps, seed):
+    """Untimed: a short SGD finetune of a pruned model (the reference's train loop shape,
+    experiments/utils/train.py:11-48) on the native training convolutions, so the new pruned
+    shapes need no MIOpen JIT. Taylor- and Random-pruned models see the same batches."""
+    from torchpruner_amd.engine.train import native_convs
+    if steps <= 0:
+        return
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-4)
+    model.train()
+    with native_convs(model):
+        for i in range(steps):
+            x, y = task.sample(128, seed * 100_003 + 77_777 + i)
+            opt.zero_grad(set_to_none=True)
+            F.cross_entropy(model(x), y).backward()
+            opt.step()
+    model.eval()
+    model.zero_grad(set_to_none=True)
 
 
 def timed_run(metric, convs, world):
@@ -234,6 +255,15 @@ def main():
         result["top1_oneshot_all_layers_50pct_random"] = round(after_rnd, 4)
         log(f"[bench] top-1 before {before:.4f}; after one-shot 50% prune of ALL conv layers (no finetune): "
             f"Taylor {after:.4f}, Random {after_rnd:.4f}")
+        if args.finetune_steps > 0:
+            finetune(model, task, args.finetune_steps, args.seed)
+            finetune(rnd, task, args.finetune_steps, args.seed)
+            ft, ft_rnd = top1(model, xv, yv), top1(rnd, xv, yv)
+            result["finetune_steps"] = args.finetune_steps
+            result["top1_oneshot_50pct_finetuned_taylor"] = round(ft, 4)
+            result["top1_oneshot_50pct_finetuned_random"] = round(ft_rnd, 4)
+            log(f"[bench] after {args.finetune_steps} finetune SGD steps (B=128, untimed): "
+                f"Taylor {ft:.4f}, Random {ft_rnd:.4f}")
 
     if rank == 0:
         print(json.dumps(result), flush=True)
