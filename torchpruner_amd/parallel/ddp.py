@@ -72,8 +72,5 @@ def params_in_sync(model: nn.Module, group=None) -> bool:
         ref = t.clone()
         pdist.broadcast_tensor_(ref, 0, group)
         ok = ok and bool(torch.equal(ref, t))
-    flag = torch.tensor([1.0 if ok else 0.0], device=next(model.parameters()).device)
-    vals = [None] * pdist.get_world_size(group)
-    import torch.distributed as dist
-    dist.all_gather_object(vals, float(flag.item()), group=group)
-    return all(v == 1.0 for v in vals)
+    flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+    return pdist.all_max_float(float(flag.item()), group) == 0.0  # any rank out of sync -> 1

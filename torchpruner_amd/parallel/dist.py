@@ -24,6 +24,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .comm import Communicator
+
 
 @dataclass
 class DistContext:
@@ -38,11 +40,20 @@ def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+def _comm(group):
+    """The Communicator behind ``group`` (None for torch process groups / the default group)."""
+    return group if isinstance(group, Communicator) else None
+
+
 def get_rank(group=None) -> int:
+    if _comm(group):
+        return group.rank
     return dist.get_rank(group) if is_dist() else 0
 
 
 def get_world_size(group=None) -> int:
+    if _comm(group):
+        return group.world_size
     return dist.get_world_size(group) if is_dist() else 1
 
 
@@ -92,6 +103,8 @@ def all_reduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
     """In-place SUM all-reduce that works for either backend (moves if needed)."""
     if get_world_size(group) == 1:
         return t
+    if _comm(group):
+        return group.all_reduce_(t, "sum")
     dev = _comm_device(t, group)
     if dev == t.device:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
@@ -105,6 +118,8 @@ def all_reduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
 def broadcast_object(obj: Any, src: int = 0, group=None) -> Any:
     if get_world_size(group) == 1:
         return obj
+    if _comm(group):
+        return group.broadcast_object(obj, src)
     lst = [obj]
     dist.broadcast_object_list(lst, src=src, group=group)
     return lst[0]
@@ -113,6 +128,8 @@ def broadcast_object(obj: Any, src: int = 0, group=None) -> Any:
 def broadcast_tensor_(t: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
     if get_world_size(group) == 1:
         return t
+    if _comm(group):
+        return group.broadcast_(t, src)
     dev = _comm_device(t, group)
     tmp = t if dev == t.device else t.to(dev)
     dist.broadcast(tmp, src=src, group=group)
@@ -125,6 +142,8 @@ def all_max_int(v: int, group=None) -> int:
     """Max of a Python int over ranks (used to agree on shapes when a rank saw no data)."""
     if get_world_size(group) == 1:
         return int(v)
+    if _comm(group):
+        return max(group.all_gather_object(int(v)))
     vals = [None] * get_world_size(group)
     dist.all_gather_object(vals, int(v), group=group)
     return max(vals)
@@ -134,6 +153,8 @@ def all_max_float(x: float, group=None) -> float:
     """MAX of a Python float over ranks (any backend)."""
     if get_world_size(group) == 1:
         return float(x)
+    if _comm(group):
+        return float(group.all_reduce_(torch.tensor([float(x)], dtype=torch.float64), "max").item())
     t = torch.tensor([float(x)], dtype=torch.float64)
     dev = _comm_device(t, group)
     t = t.to(dev)
@@ -143,7 +164,7 @@ def all_max_float(x: float, group=None) -> float:
 
 def barrier(group=None):
     if get_world_size(group) > 1:
-        dist.barrier(group=group)
+        group.barrier() if _comm(group) else dist.barrier(group=group)
 
 
 def gather_ordered_rows(slabs: list[tuple[int, torch.Tensor]], group=None) -> torch.Tensor:
@@ -159,19 +180,25 @@ def gather_ordered_rows(slabs: list[tuple[int, torch.Tensor]], group=None) -> to
         return torch.cat([s[1] for s in local], 0) if local else torch.empty(0)
     meta = [(i, t.shape[0]) for i, t in local]
     ncols = local[0][1].shape[1] if local else 0
-    metas = [None] * world
-    dist.all_gather_object(metas, (meta, ncols), group=group)
+    if _comm(group):
+        metas = group.all_gather_object((meta, ncols))
+    else:
+        metas = [None] * world
+        dist.all_gather_object(metas, (meta, ncols), group=group)
     ncols = max(m[1] for m in metas)
     rows = [sum(n for _, n in m[0]) for m in metas]
     maxrows = max(rows) if rows else 0
     ref = local[0][1] if local else torch.empty(0, ncols, dtype=torch.float32)
-    dev = _comm_device(ref, group)
+    dev = ref.device if _comm(group) else _comm_device(ref, group)
     buf = torch.zeros(maxrows, ncols, dtype=ref.dtype, device=dev)
     if local:
         mine = torch.cat([t for _, t in local], 0).to(dev)
         buf[: mine.shape[0]] = mine
-    outs = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(outs, buf, group=group)
+    if _comm(group):
+        outs = group.all_gather(buf)
+    else:
+        outs = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(outs, buf, group=group)
     pieces = []
     for r in range(world):
         off = 0
