@@ -90,6 +90,14 @@ struct WinoArgs {
   int tay_mode;             // W_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
 };
 
+// Phase-attribution switches for profiling experiments only: they skip barriers / stores and
+// give wrong results, so they exist only in a -DTP_WINO_DEBUG build (compiled out otherwise).
+#ifdef TP_WINO_DEBUG
+#define WDBG(p, bit) ((p).dbg & (bit))
+#else
+#define WDBG(p, bit) (0)
+#endif
+
 __device__ __forceinline__ int xcd_remap_w(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8;
   const int xcd = bid % 8, idx = bid / 8;
@@ -175,7 +183,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
   unsigned char* ab = reinterpret_cast<unsigned char*>(yb0 + 2048);  // FWD_POOL argmax bytes [64][32]
 
   // ---- phase 1: transform, park in LDS --------------------------------------------------
-  if (p.dbg & 16) goto phase2;
+  if WDBG(p, 16) goto phase2;
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
     float* yb = n == 0 ? yb0 : yb1;
@@ -219,7 +227,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
   __syncthreads();
 phase2:
   // ---- phase 2: coalesced global traffic ------------------------------------------------
-  if (p.dbg & 8) return;
+  if WDBG(p, 8) return;
   const int c4 = tid & 7;  // 4-channel group: channels k0 + 4*c4 .. +3
   const int k = k0 + 4 * c4;
   const float* ybr = (c4 < 4 ? yb0 : yb1) + (c4 & 3) * 4;
@@ -566,7 +574,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       if constexpr (XMODE == X_STAGED) {
 #pragma unroll
         for (int t = 0; t < 16; ++t)
-          d[t] = (p.dbg & 64) ? f32x2{(float)t, 1.f}
+          d[t] = WDBG(p, 64) ? f32x2{(float)t, 1.f}
                               : *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(xb) + poff[t]);
       } else if constexpr (XMODE == X_STAGED_UNPOOL) {
         f32x2 cv[9];
@@ -599,14 +607,14 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
             d[r * 4 + q][1] = ((amr[cell] >> 8) & 0xffu) == want ? xin[cell][1] : 0.f;
           }
       }
-      if (p.dbg & 4) {
+      if WDBG(p, 4) {
 #pragma unroll
         for (int t = 0; t < 16; ++t) v[t] = d[t];
       } else {
         input_transform2(d, v);
       }
     }
-    if (more && !(p.dbg & 2)) {
+    if (more && !WDBG(p, 2)) {
       stage(c0 + W_CH, ud_next, xd_next);
       if constexpr (!STAGED) issue_x(c0 + W_CH);
     }
@@ -646,7 +654,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_s_setprio(0);
-    if (p.dbg & 32) __builtin_amdgcn_s_waitcnt(0);
+    if WDBG(p, 32) __builtin_amdgcn_s_waitcnt(0);
     else __syncthreads();  // drains this chunk's DMA for the next one and orders buffer reuse
   };
 
@@ -659,7 +667,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       if (c0 + W_CH < c_end) compute(c0 + W_CH, us1, xs1, us0, xs0, c0 + 2 * W_CH < c_end);
     }
   }
-  if (p.dbg & 1) {
+  if WDBG(p, 1) {
     float t = 0.f;
 #pragma unroll
     for (int x = 0; x < 16; ++x) t += acc[x][0][0] + acc[x][1][3];
@@ -821,7 +829,15 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.tay_slots = wino_taylor_slots(H, W);
   a.fd_timg = FastDiv((unsigned)std::max(1, (H / 2) * (W / 2)));
   a.fd_w2 = FastDiv((unsigned)std::max(1, W / 2));
-  if (const char* d = getenv("TP_WINO_DBG")) a.dbg = atoi(d);
+#ifdef TP_WINO_DEBUG
+  static const int dbg_bits = [] {
+    const char* d = getenv("TP_WINO_DBG");
+    const int v = d ? atoi(d) : 0;
+    if (v) fprintf(stderr, "[tpamd] WARNING: TP_WINO_DBG=%d: Winograd results are WRONG (phase-cost experiment)\n", v);
+    return v;
+  }();
+  a.dbg = dbg_bits;
+#endif
   int xmode = unpool ? X_UNPOOL : X_DIRECT;
   if (staged) {
     const XGeom gm = staged_geometry(H, W, unpool != 0);

@@ -1,3 +1,5 @@
+# Needs an experiment build: TORCHPRUNER_HIPFLAGS=-DTP_WINO_DEBUG python -m torchpruner_amd._build --force
+# (the switches are compiled out of normal builds).
 # Attribute Winograd bwd epilogue time: TP_WINO_DBG 8 = skip phase 2 (global traffic), 16 = skip
 # phase 1 (output transform + LDS park); heuristic kernel choice so every run launches the same configs
 set -o pipefail

@@ -217,3 +217,17 @@ def test_inplace_relu_eval_module(dev):
         np.testing.assert_allclose(a1, a2, rtol=1e-5, atol=1e-7)
     # parameters keep requires_grad and get no .grad side effect
     assert all(p.requires_grad for p in base.parameters())
+
+
+def test_last_path_reports_generic_with_reason():
+    """Path transparency: every run records (and logs) which path served it and why the native
+    engines were rejected."""
+    x, y, model = max_model(torch.device("cpu"))
+    m = TaylorAttributionMetric(model, loader(x, y), F.mse_loss, torch.device("cpu"))
+    m.run(model[0])
+    assert m.last_path["path"] == "generic"
+    assert m.last_path["modules"] == ["0"]
+    assert any("not a GPU" in r for r in m.last_path["reasons"])
+    s = ShapleyAttributionMetric(model, loader(x, y), F.mse_loss, torch.device("cpu"), sv_samples=1)
+    s.run(model[0])
+    assert s.last_path["path"] == "generic-hook"

@@ -131,3 +131,30 @@ def test_communicator_single_rank_is_identity():
     t = torch.arange(4.0)
     assert pdist.all_reduce_sum_(t, comm) is t and t.tolist() == [0.0, 1.0, 2.0, 3.0]
     assert get_world_size(comm) == 1 and get_rank(comm) == 0
+
+
+def test_loopback_mismatched_collectives_raise():
+    """A rank calling broadcast_ while another calls all_reduce_ must fail, not mix payloads."""
+    def body(comm):
+        t = torch.ones(3)
+        if comm.rank == 0:
+            comm.broadcast_(t, 0)
+        else:
+            comm.all_reduce_(t)
+
+    with pytest.raises(RuntimeError, match="mismatched collectives"):
+        run_loopback(2, body)
+
+
+def test_loopback_all_gather_outputs_are_private():
+    def body(comm):
+        outs = comm.all_gather(torch.full((2,), float(comm.rank)))
+        comm.barrier()
+        if comm.rank == 0:
+            for o in outs:
+                o.fill_(-1.0)  # must not reach rank 1's results
+        comm.barrier()
+        return [o.tolist() for o in outs]
+
+    res = run_loopback(2, body)
+    assert res[1] == [[0.0, 0.0], [1.0, 1.0]]

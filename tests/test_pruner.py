@@ -192,3 +192,17 @@ def test_grouped_conv_rejected(dev):
     p = Pruner(model, input_size=(4, 5, 5), device=d)
     with pytest.raises(NotImplementedError):
         p.prune_module(model[0], [0], "out")
+
+
+@pytest.mark.parametrize("dev", DEVICES)
+def test_out_of_range_indices_raise(dev):
+    """Reference parity (pruner.py:106-107 raises through numpy): an index >= the axis length is
+    an error, not silently dropped."""
+    d = _dev(dev)
+    _, model = simple_model(d)
+    pruner = Pruner(model, (3,), d)
+    with pytest.raises(IndexError):
+        pruner.prune_parameter(model[0], "weight", [0, 5], axis=0)
+    assert model[0].weight.shape == (2, 3)  # untouched
+    with pytest.raises(IndexError):
+        pruner.prune_model(model[0], [2], cascading_modules=[model[2]])

@@ -53,6 +53,8 @@ def _common_flags():
         "-munsafe-fp-atomics",
         f"-I{CSRC / 'include'}",
         "-Wno-unused-result",
+        # extra flags for experiment builds, e.g. -DTP_WINO_DEBUG (scripts/gpu_wino_epi_attr.sh)
+        *os.environ.get("TORCHPRUNER_HIPFLAGS", "").split(),
     ]
 
 

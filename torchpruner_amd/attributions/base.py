@@ -153,6 +153,9 @@ class _AttributionMetric(ABC):
         self.compute_dtype = compute_dtype
         self._ckpt = None
         self._run_accs = None
+        # path transparency (new): which execution path served the last run() and, when the
+        # generic hook path ran, why the native engines were rejected
+        self.last_path = None
 
     # ------------------------------------------------------------------ API parity
     @abstractmethod
@@ -236,6 +239,19 @@ class _AttributionMetric(ABC):
         torch.backends.cudnn.benchmark = self.benchmark
 
     # ------------------------------------------------------------------ engine internals
+    def _record_path(self, path: str, eval_modules, why=()):
+        """Remember and log (once per run, ``torchpruner`` logger) which path served it:
+        ``fused`` (VGG-chain engine), ``resnet`` (ResNet engine) or ``generic`` (PyTorch
+        modules + HIP reduction kernels), with the engines' rejection reasons."""
+        names = {id(m): n for n, m in self.model.named_modules()}
+        mods = [names.get(id(m), type(m).__name__) for m in eval_modules]
+        reasons = [r for r in dict.fromkeys(why or ())]
+        self.last_path = {"path": path, "modules": mods, "reasons": reasons}
+        msg = f"{type(self).__name__}: {path} path for {', '.join(mods)}"
+        if reasons:
+            msg += " (" + "; ".join(reasons) + ")"
+        logger.info(msg)
+
     def _reduced_precision(self) -> bool:
         return self.compute_dtype in (torch.bfloat16, torch.float16)
 
@@ -398,17 +414,26 @@ class _AttributionMetric(ABC):
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
         return [accs[owner[b]] for b in blocks]
 
-    def _resnet_grad_engine(self, eval_modules):
+    def _resnet_grad_engine(self, eval_modules, why=None):
         """The ResNet engine when it can produce gradient scores for ``eval_modules`` (eval-mode
         torchvision-layout ResNet, block BNs, mean cross-entropy criterion), else None."""
-        from ..engine.fused_chain import criterion_is_cross_entropy
+        from ..engine.fused_chain import _reject, criterion_is_cross_entropy
         from ..engine.resnet_engine import maybe_resnet_engine
         if not self._engines_allowed():
+            return _reject(why, f"compute_dtype={self.compute_dtype} runs the generic autocast path")
+        eng = maybe_resnet_engine(self.model, eval_modules, self.device, grad=True, why=why)
+        if eng is None:
             return None
-        eng = maybe_resnet_engine(self.model, eval_modules, self.device, grad=True)
-        if eng is None or not criterion_is_cross_entropy(self.criterion, self.device):
-            return None
+        if not criterion_is_cross_entropy(self.criterion, self.device):
+            return _reject(why, "resnet engine: criterion is not mean cross-entropy")
         return eng
+
+    def _fused_engine(self, eval_modules, why=None, need_ce=True):
+        """The fused VGG-chain engine (engine, block indices) for ``eval_modules``, else None."""
+        from ..engine.fused_chain import _reject, maybe_engine
+        if not self._engines_allowed():
+            return _reject(why, f"compute_dtype={self.compute_dtype} runs the generic autocast path")
+        return maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=need_ce, why=why)
 
     def _resnet_grad_pass(self, eng, eval_modules, accs, mode):
         """Per batch: one engine forward + input-gradient backward scores every module; the

@@ -10,7 +10,6 @@ For torchvision-layout ResNets the whole forward runs on the HIP kernels of the 
 import torch
 
 from ... import ops
-from ...engine import maybe_engine
 from ...engine.resnet_engine import maybe_resnet_engine
 from ..base import _AttributionMetric
 
@@ -27,9 +26,11 @@ class APoZAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            ok = self._engines_allowed()
-            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=False) if ok else None
-            eng = None if fused is not None or not ok else maybe_resnet_engine(self.model, eval_modules, self.device)
+            why = []
+            fused = self._fused_engine(eval_modules, why, need_ce=False)
+            eng = None if fused is not None or not self._engines_allowed() else \
+                maybe_resnet_engine(self.model, eval_modules, self.device, why=why)
+            self._record_path("fused" if fused else "resnet" if eng else "generic", eval_modules, why)
             if fused is not None:
                 accs = self._chain_pass(*fused, accs)
             elif eng is not None:

@@ -4,7 +4,6 @@ Per sample: sum over trailing dims of |grad_output|, gradient of the per-batch *
 (so scores scale with 1/batch_size, as in the reference).
 """
 from ... import ops
-from ...engine import maybe_engine
 from ..base import _AttributionMetric
 
 
@@ -20,8 +19,10 @@ class SensitivityAttributionMetric(_AttributionMetric):
         accs = [self._new_accumulator() for _ in eval_modules]
         self._begin_run(accs, eval_modules)
         try:
-            fused = maybe_engine(self.model, eval_modules, self.criterion, self.device) if self._engines_allowed() else None
-            rn = None if fused is not None else self._resnet_grad_engine(eval_modules)
+            why = []
+            fused = self._fused_engine(eval_modules, why)
+            rn = None if fused is not None else self._resnet_grad_engine(eval_modules, why)
+            self._record_path("fused" if fused else "resnet" if rn else "generic", eval_modules, why)
             if fused is not None:  # VGG-style chains: |dL/da| partials from the fused dgrad epilogues
                 accs = self._fused_grad_pass(*fused, accs, "sensitivity", False)
             elif rn is not None:  # ResNets: forward + input-grad backward on the HIP engine

@@ -29,7 +29,6 @@ from torch.nn.modules.batchnorm import _BatchNorm
 from torch.nn.modules.dropout import _DropoutNd
 
 from ... import ops
-from ...engine import maybe_engine
 from ...parallel import dist as pdist
 from ..base import _AttributionMetric
 
@@ -54,11 +53,19 @@ class ShapleyAttributionMetric(_AttributionMetric):
     def run(self, module, sv_samples=None, **kwargs):
         module = super().run(module, **kwargs)
         sv_samples = sv_samples if sv_samples is not None else self.samples
-        fused = self._fused_prepare(module) or self._resnet_prepare(module)
+        why = []
+        fused = self._fused_prepare(module, why)
+        path = "fused" if fused is not None else None
+        if fused is None:
+            fused = self._resnet_prepare(module, why)
+            path = "resnet" if fused is not None else None
         if fused is not None:
+            self._record_path(path, [module], why)
             return self._run_batches(module, sv_samples, fused)
         if hasattr(self.model, "forward_partial"):
+            self._record_path("generic-partial", [module], why)
             return self.run_module_with_partial(module, sv_samples)
+        self._record_path("generic-hook", [module], why)
         logger.warning("Consider adding a 'forward_partial' method to your model to speed-up Shapley values "
                        "computation")
         return self.run_module(module, sv_samples)
@@ -163,13 +170,13 @@ class ShapleyAttributionMetric(_AttributionMetric):
         return self.aggregate_over_samples(sv.cpu().numpy())
 
     # ------------------------------------------------------------------ native path
-    def _fused_prepare(self, module):
+    def _fused_prepare(self, module, why=None):
         """Prefix evaluation on the fused HIP engine (eval-mode VGG-style chains, CE loss):
         the evaluation module's activation is produced once per batch, K prefix-masked copies
         are stacked by one kernel and pushed through the remaining fused layers in ONE forward.
         Masking a post-ReLU activation commutes with the following 2x2 max-pool, so the
         engine masks its pooled output (4x less data) with identical results."""
-        fused = maybe_engine(self.model, [module], self.criterion, self.device) if self._engines_allowed() else None
+        fused = self._fused_engine([module], why)
         if fused is None:
             return None
         engine, (k,) = fused
@@ -192,15 +199,13 @@ class ShapleyAttributionMetric(_AttributionMetric):
 
         return prepare
 
-    def _resnet_prepare(self, module):
+    def _resnet_prepare(self, module, why=None):
         """Prefix evaluation on the ResNet engine (block-internal BN evaluation modules, CE loss):
         the masked activation and the block's residual operand are produced once per batch,
         K prefix-masked copies are pushed through the rest of the block and the network in ONE
         engine forward."""
-        from ...engine.fused_chain import criterion_is_cross_entropy
-        from ...engine.resnet_engine import maybe_resnet_engine
-        eng = maybe_resnet_engine(self.model, [module], self.device, grad=True) if self._engines_allowed() else None
-        if eng is None or not criterion_is_cross_entropy(self.criterion, self.device):
+        eng = self._resnet_grad_engine([module], why)
+        if eng is None:
             return None
         bi, ci = eng.locate(module)
         n = module.num_features

@@ -5,7 +5,6 @@ The activation and gradient are read once by one fused HIP reduction; the refere
 full activation clone per batch and leaks it on the module (taylor.py:35).
 """
 from ... import ops
-from ...engine import maybe_engine
 from ..base import _AttributionMetric
 
 
@@ -31,12 +30,15 @@ class TaylorAttributionMetric(_AttributionMetric):
             self._end_run()
 
     def _run_loop(self, eval_modules, accs, mode):
-        fused = maybe_engine(self.model, eval_modules, self.criterion, self.device) if self._engines_allowed() else None
+        why = []
+        fused = self._fused_engine(eval_modules, why)
+        rn = None if fused is not None else self._resnet_grad_engine(eval_modules, why)
+        self._record_path("fused" if fused else "resnet" if rn else "generic", eval_modules, why)
         if fused is not None:
             # native path: one fused forward + input-grad backward scores every module, then
             # ONE fold launch turns all layers' per-sample sums into |.| and fp64 accumulators
             accs = self._fused_grad_pass(*fused, accs, "taylor", not self.signed)
-        elif (rn := self._resnet_grad_engine(eval_modules)) is not None:
+        elif rn is not None:
             accs = self._resnet_grad_pass(rn, eval_modules, accs, mode)
         else:
             self._grad_capture_pass(eval_modules,

@@ -1,0 +1,148 @@
+"""Accuracy half of the headline metric: top-1 retained after REALLY pruning 50% of VGG16's
+conv filters, Taylor vs Random, reproducibly.
+
+Protocol (iterative, the shape of the reference's nbUNT loop, ``nbUNT:169-193``, with the
+finetune steps of BASELINE config #5 in between; ``experiments/utils/train.py:11-48``):
+
+1. teacher: random-init VGG16-BN trained on a synthetic CIFAR-shaped prototype-mixture task;
+2. for every conv of ``get_vgg_pruning_graph`` (last layer first, as the reference's loop):
+   score the conv's filters (Taylor on held-out attribution images, B=100 as nbVGG:193-196, or
+   random scores), ``Pruner.prune_model`` the lowest-scored half (real slicing + cascade into the
+   next conv / BN, SGD momentum state rewired), then ``ft_steps`` SGD steps;
+3. a final ``final_ft_steps`` SGD steps; report held-out top-1 of the pruned network.
+
+Reproducibility: training runs on the native convolutions / BN kernels (deterministic: no
+atomics), every kernel configuration is the untimed heuristic choice (``TUNER.fixed()``), and
+all randomness comes from seeded generators, so the same seed gives the same top-1 in every run.
+The reference-scale task the reference uses (CIFAR-10) is not available offline; the synthetic
+task is sized so the teacher is not saturated and pruning costs accuracy.
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import hashlib
+import json
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .. import Pruner, TaylorAttributionMetric, get_vgg_pruning_graph
+from ..data import DeviceLoader, PrototypeTask
+from ..engine.fused_chain import TUNER
+from ..engine.train import native_convs
+from ..models import prunable_vgg16
+
+DEFAULTS = dict(noise=3.0, modes=16, teacher_steps=400, ft_steps=10, final_ft_steps=40, score_imgs=1000,
+                val_imgs=4000, lr=0.05, ft_lr=0.01, batch=128)
+
+
+@torch.no_grad()
+def top1(model, x, y, batch=1000):
+    model.eval()
+    correct = 0
+    for s in range(0, x.shape[0], batch):
+        correct += int((model(x[s:s + batch]).argmax(1) == y[s:s + batch]).sum())
+    return correct / x.shape[0]
+
+
+def sgd_steps(model, task, steps, seed, lr, batch, optimizer=None, schedule=False):
+    """``steps`` SGD steps (reference optimizer settings, cifar10.py:95-99) on fresh task batches,
+    native convolutions + BN kernels, fixed kernel configs (bit-reproducible)."""
+    if steps <= 0:
+        return optimizer
+    opt = optimizer or torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=lr, total_steps=steps) if schedule else None
+    model.train()
+    with TUNER.fixed(), native_convs(model):
+        for i in range(steps):
+            x, y = task.sample(batch, seed * 100_003 + i)
+            opt.zero_grad(set_to_none=True)
+            F.cross_entropy(model(x), y).backward()
+            opt.step()
+            if sched is not None:
+                sched.step()
+    model.eval()
+    return opt
+
+
+def make_teacher(seed, device, cfg):
+    torch.manual_seed(seed)
+    model = prunable_vgg16().to(device)
+    task = PrototypeTask((3, 32, 32), 10, noise=cfg["noise"], seed=seed, device=device,
+                         modes_per_class=cfg["modes"])
+    torch.cuda.manual_seed(seed)  # dropout masks
+    sgd_steps(model, task, cfg["teacher_steps"], seed, cfg["lr"], cfg["batch"], schedule=True)
+    model.zero_grad(set_to_none=True)
+    return model, task
+
+
+def iterative_prune(model, task, method, seed, cfg, frac=0.5, log=None):
+    """Prune ``frac`` of every conv's filters layer by layer (``method``: "taylor" | "random"),
+    finetuning between layers; returns the pruned model (modified in place)."""
+    dev = next(model.parameters()).device
+    xs, ys = task.sample(cfg["score_imgs"], seed * 7 + 11)
+    rng = np.random.RandomState(seed)
+    opt = torch.optim.SGD(model.parameters(), lr=cfg["ft_lr"], momentum=0.9, weight_decay=5e-4)
+    pruner = Pruner(model, (3, 32, 32), dev, optimizer=opt)
+    graph = [(m, c) for m, c in get_vgg_pruning_graph(model) if isinstance(m, torch.nn.Conv2d)]
+    for li, (module, cascade) in enumerate(graph):
+        n = module.out_channels
+        if method == "taylor":
+            model.eval()
+            with TUNER.fixed():
+                s = TaylorAttributionMetric(model, DeviceLoader(xs, ys, 100), F.cross_entropy, dev,
+                                            shard_data=False).run(module, find_best_evaluation_module=True)
+        else:
+            s = rng.random_sample(n)
+        idx = np.argsort(s, kind="stable")[: int(n * frac)]
+        pruner.prune_model(module, idx, cascading_modules=cascade)
+        sgd_steps(model, task, cfg["ft_steps"], seed * 1000 + 500 + li, cfg["ft_lr"], cfg["batch"], optimizer=opt)
+        if log:
+            log(f"  [{method}] layer {li}: {n} -> {module.out_channels} filters")
+    sgd_steps(model, task, cfg["final_ft_steps"], seed * 1000 + 900, cfg["ft_lr"], cfg["batch"], optimizer=opt)
+    model.zero_grad(set_to_none=True)
+    return model
+
+
+def weights_digest(model) -> str:
+    h = hashlib.sha256()
+    for t in model.state_dict().values():
+        h.update(t.detach().cpu().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
+def run_protocol(seed=0, device="cuda", log=None, **overrides):
+    """Teacher + Taylor- and Random-pruned copies; returns a dict of top-1 figures."""
+    cfg = dict(DEFAULTS, **overrides)
+    t0 = time.perf_counter()
+    teacher, task = make_teacher(seed, device, cfg)
+    xv, yv = task.sample(cfg["val_imgs"], seed * 7 + 3)
+    before = top1(teacher, xv, yv)
+    out = {"seed": seed, "top1_before": before, "teacher_digest": weights_digest(teacher)}
+    for method in ("taylor", "random"):
+        m = iterative_prune(copy.deepcopy(teacher), task, method, seed, cfg, log=log)
+        out[f"top1_pruned_{method}"] = top1(m, xv, yv)
+        out[f"digest_{method}"] = weights_digest(m)
+        out["params_pruned"] = sum(p.numel() for p in m.parameters())
+    out["params_before"] = sum(p.numel() for p in teacher.parameters())
+    out["seconds"] = round(time.perf_counter() - t0, 1)
+    out["config"] = cfg
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2])
+    for k, v in DEFAULTS.items():
+        ap.add_argument("--" + k.replace("_", "-"), type=type(v), default=v)
+    args = ap.parse_args()
+    cfg = {k: getattr(args, k) for k in DEFAULTS}
+    for s in args.seeds:
+        print(json.dumps(run_protocol(s, "cuda", **cfg)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -26,6 +26,7 @@ summation order differ from cuDNN/MIOpen only at rounding level.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import weakref
@@ -128,6 +129,19 @@ class Autotuner:
     def __init__(self):
         self.cache = {}
         self.enabled = os.environ.get("TORCHPRUNER_AUTOTUNE", "1") != "0"
+
+    @contextlib.contextmanager
+    def fixed(self):
+        """Untimed heuristic kernel choices with a private cache: every run of the same shapes
+        picks the same configs, so results are bit-reproducible across processes (accuracy
+        protocols, teacher training). Timing-based choices can differ between runs on a busy
+        GPU, and different split-K / tile configs round differently."""
+        saved = (self.cache, self.enabled)
+        self.cache, self.enabled = {}, False
+        try:
+            yield self
+        finally:
+            self.cache, self.enabled = saved
 
     def candidates(self, M, N, K, wino=None, wino_only=False):
         """``wino``: (P tiles, C) when the Winograd kernel applies to this conv; ``wino_only``
@@ -713,19 +727,29 @@ def criterion_is_cross_entropy(criterion, device) -> bool:
         return False
 
 
-def maybe_engine(model, eval_modules, criterion, device, need_ce=True):
+def _reject(why, reason):
+    """Record why an engine did not apply (path transparency) and return None."""
+    if why is not None:
+        why.append(reason)
+    return None
+
+
+def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None):
     """Return (engine, block indices of eval_modules) when the fused path applies, else None.
-    ``need_ce=False``: forward-only use (APoZ), any criterion."""
+    ``need_ce=False``: forward-only use (APoZ), any criterion. ``why``: a list that receives the
+    rejection reason when the engine does not apply."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
-    if dev.type != "cuda" or ops.backend() == "torch" or not ops.available():
-        return None
+    if dev.type != "cuda":
+        return _reject(why, f"device {dev} is not a GPU")
+    if ops.backend() == "torch" or not ops.available():
+        return _reject(why, "native extension disabled (TORCHPRUNER_BACKEND=torch) or not built")
     if model.training:
-        return None
+        return _reject(why, "model is in training mode (engines fold eval-mode BatchNorm)")
     if any(p.dtype != torch.float32 for p in model.parameters()):
-        return None
-    plan, _reason = build_plan(model)
+        return _reject(why, "parameters are not float32")
+    plan, reason = build_plan(model)
     if plan is None:
-        return None
+        return _reject(why, f"fused chain: {reason}")
     idx = []
     blocks = plan.blocks
     for m in eval_modules:
@@ -735,10 +759,11 @@ def maybe_engine(model, eval_modules, criterion, device, need_ce=True):
                 found = k
                 break
         if found is None:
-            return None
+            return _reject(why, f"fused chain: evaluation module {type(m).__name__} is not a block activation "
+                                "(use find_best_evaluation_module=True)")
         idx.append(found)
     if need_ce and not criterion_is_cross_entropy(criterion, dev):
-        return None
+        return _reject(why, "criterion is not mean cross-entropy")
     eng = _ENGINES.get(model)
     if eng is None or len(eng.plan.blocks) != len(plan.blocks) or any(
             (a.conv is not b.conv if isinstance(a, ConvBlock) else a.linear is not b.linear) or a.width != b.width

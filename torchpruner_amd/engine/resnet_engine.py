@@ -377,22 +377,24 @@ class ResNetEngine:
 _ENGINES: "weakref.WeakKeyDictionary[nn.Module, ResNetEngine]" = weakref.WeakKeyDictionary()
 
 
-def maybe_resnet_engine(model, eval_modules, device, grad=False):
+def maybe_resnet_engine(model, eval_modules, device, grad=False, why=None):
     """A ResNetEngine when every eval module is a BN the engine counts (``grad``: scores by
-    :meth:`ResNetEngine.grad_scores`, block BNs only), else None."""
+    :meth:`ResNetEngine.grad_scores`, block BNs only), else None (``why`` receives the reason)."""
+    from .fused_chain import _reject
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda" or ops.backend() == "torch" or not ops.available() or model.training:
-        return None
+        return _reject(why, "resnet engine: needs an eval-mode model on a GPU with the native extension")
     if any(p.dtype != torch.float32 for p in model.parameters()):
-        return None
-    plan, _ = build_resnet_plan(model)  # re-validated every run: pruning changes channel counts
+        return _reject(why, "resnet engine: parameters are not float32")
+    plan, reason = build_resnet_plan(model)  # re-validated every run: pruning changes channel counts
     if plan is None:
-        return None
+        return _reject(why, f"resnet engine: {reason}")
     eng = _ENGINES.get(model)
     if eng is None or [c.conv for c in eng._all_convs()] != [c.conv for c in ResNetEngine(model, plan)._all_convs()]:
         eng = ResNetEngine(model, plan)
         _ENGINES[model] = eng
     ok = set(map(id, eng.eval_modules()[1:] if grad else eng.eval_modules()))
     if not all(id(m) in ok for m in eval_modules):
-        return None
+        return _reject(why, "resnet engine: evaluation modules must be block BatchNorms "
+                            "(use find_best_evaluation_module=True)")
     return eng

@@ -1,14 +1,20 @@
 """Pluggable collective backend.
 
-Every ``group=`` argument of the package (metrics, ``parallel.dist`` helpers, ``PrunableDDP``
-checks) accepts either a ``torch.distributed`` process group — the production path: RCCL over
-xGMI on GPUs, gloo on CPUs — or a :class:`Communicator`. The in-process
+The ``group=`` arguments of the attribution metrics, the ``Pruner`` index broadcast (R5) and
+the ``parallel.dist`` helpers accept either a ``torch.distributed`` process group — the
+production path: RCCL over xGMI on GPUs, gloo on CPUs — or a :class:`Communicator`.
+``PrunableDDP`` and ``utils.train.test`` take torch process groups only (DDP itself needs one). The in-process
 :class:`LoopbackCommunicator` runs N ranks as N threads of one process; the data-parallel
 attribution logic (batch sharding, the once-per-run score all-reduce, Shapley prefix sharding
 and permutation broadcast) can then be unit-tested without spawning processes or opening
 sockets. The reference has no distributed code at all.
 
 Reductions are summed in rank order on the host, so a loopback run is bit-reproducible.
+
+Limitation: loopback ranks are threads of ONE process, so they share process-global state —
+NumPy's global RNG (Shapley permutations are drawn on rank 0 only and broadcast, so this is
+safe there), the ``torch.backends.cudnn`` flags the metrics save/restore, torch's RNG. Tests are
+valid only while no rank's result depends on such state being private.
 """
 from __future__ import annotations
 
@@ -47,7 +53,9 @@ class Communicator:
 class LoopbackHub:
     """Rendezvous shared by the ``world_size`` threads of one loopback job."""
 
-    def __init__(self, world_size: int, timeout: float = 120.0):
+    def __init__(self, world_size: int, timeout: float | None = None):
+        """``timeout`` (seconds) bounds every wait of a collective; None (default) waits for as
+        long as the slowest rank computes between two collectives."""
         self.world_size = world_size
         self.slots: list = [None] * world_size
         self.barrier = threading.Barrier(world_size, timeout=timeout)
@@ -63,15 +71,24 @@ class LoopbackCommunicator(Communicator):
         self.rank = rank
         self.world_size = hub.world_size
 
-    def _exchange(self, value):
-        self.hub.slots[self.rank] = value
+    def _exchange(self, value, tag):
+        """Publish ``value``; every rank must call the same collective (``tag``: op name and,
+        for tensors, shape/dtype) — a mismatch raises on every rank instead of mixing payloads."""
+        self.hub.slots[self.rank] = (tag, value)
         self.hub.barrier.wait()
         out = list(self.hub.slots)
         self.hub.barrier.wait()  # nobody overwrites a slot before everyone has read it
-        return out
+        tags = [o[0] for o in out]
+        if any(t != tags[0] for t in tags):
+            raise RuntimeError(f"mismatched collectives across loopback ranks: {tags}")
+        return [o[1] for o in out]
+
+    @staticmethod
+    def _ttag(op, t):
+        return (op, tuple(t.shape), t.dtype)
 
     def all_reduce_(self, t, op="sum"):
-        vals = self._exchange(t.detach().to("cpu", copy=True))
+        vals = self._exchange(t.detach().to("cpu", copy=True), self._ttag("all_reduce_" + op, t))
         acc = vals[0].clone()
         for v in vals[1:]:  # fixed rank order: deterministic
             if op == "sum":
@@ -84,24 +101,27 @@ class LoopbackCommunicator(Communicator):
         return t
 
     def broadcast_(self, t, src=0):
-        vals = self._exchange(t.detach().to("cpu", copy=True) if self.rank == src else None)
+        vals = self._exchange(t.detach().to("cpu", copy=True) if self.rank == src else None,
+                              self._ttag(f"broadcast_{src}", t))
         t.copy_(vals[src].to(t.device))
         return t
 
     def all_gather(self, t):
-        return [v.to(t.device) for v in self._exchange(t.detach().to("cpu", copy=True))]
+        # every rank owns its outputs: an in-place edit on one rank never reaches another
+        return [v.to(t.device, copy=True) for v in self._exchange(t.detach().to("cpu", copy=True),
+                                                                   self._ttag("all_gather", t))]
 
     def all_gather_object(self, obj):
-        return [copy.deepcopy(v) for v in self._exchange(obj)]
+        return [copy.deepcopy(v) for v in self._exchange(obj, ("all_gather_object",))]
 
     def broadcast_object(self, obj, src=0):
-        return copy.deepcopy(self._exchange(obj if self.rank == src else None)[src])
+        return copy.deepcopy(self._exchange(obj if self.rank == src else None, ("broadcast_object", src))[src])
 
     def barrier(self):
-        self._exchange(None)
+        self._exchange(None, ("barrier",))
 
 
-def run_loopback(world_size: int, fn: Callable[..., Any], *args, timeout: float = 120.0) -> list:
+def run_loopback(world_size: int, fn: Callable[..., Any], *args, timeout: float | None = None) -> list:
     """Run ``fn(comm, *args)`` on ``world_size`` threads, one :class:`LoopbackCommunicator`
     each; returns the per-rank results. An exception on any rank aborts the rendezvous (the
     other ranks fail fast instead of waiting out the timeout) and is re-raised."""

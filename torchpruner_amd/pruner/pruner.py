@@ -132,7 +132,12 @@ class Pruner:
             n = param.data.shape[axis]
             if keep is None:
                 mask = np.ones(n, dtype=bool)
-                mask[indices[indices < n]] = False
+                if indices.size and (indices.max() >= n or indices.min() < -n):
+                    # the reference raises here too (numpy fancy assignment, pruner.py:106-107):
+                    # a bad score->index mapping must not silently mis-prune
+                    raise IndexError(f"pruning index out of range for {name} with {n} entries along axis {axis}: "
+                                     f"{indices[(indices >= n) | (indices < -n)].tolist()[:8]}")
+                mask[indices] = False
                 keep = torch.from_numpy(np.arange(n)[mask]).to(param.device)
             tensors.append(param.data)
             axes.append(axis)
