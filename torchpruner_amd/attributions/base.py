@@ -36,6 +36,7 @@ from .. import ops
 from ..data.prefetch import prefetch_to_device
 from ..parallel import dist as pdist
 from ..utils.graph import ACTIVATIONS, find_best_module_for_attributions
+from ..utils.profiling import range_pop, range_push, trace_range
 
 logger = logging.getLogger("torchpruner")
 
@@ -85,6 +86,10 @@ class ScoreAccumulator:
         """Reduce across ranks (if ``collective``) and apply ``reduction``; returns NumPy."""
         if not collective:
             return self._finalize_local(reduction, aggregate)
+        with trace_range("tp.collective"):
+            return self._finalize_collective(reduction, aggregate, group)
+
+    def _finalize_collective(self, reduction, aggregate, group):
         out_dtype = np.float32 if self.dtype in (None, torch.float32, torch.float16, torch.bfloat16) else np.float64
         if self.mode == "stats":
             n = self.sum.numel() if self.sum is not None else 0
@@ -293,6 +298,7 @@ class _AttributionMetric(ABC):
         """Attach (and restore) the resumable checkpoint of this run, if configured."""
         self._run_accs = accs
         self._ckpt = None
+        self._range = range_push(f"tp.run/{type(self).__name__}")
         if self.checkpoint:
             from ..checkpoint import AttributionCheckpoint
             names = {id(m): n for n, m in self.model.named_modules()}
@@ -308,6 +314,8 @@ class _AttributionMetric(ABC):
             self._ckpt.save(self._run_accs)
         self._ckpt = None
         self._run_accs = None
+        range_pop(getattr(self, "_range", False))
+        self._range = False
 
     def _finalize(self, acc: ScoreAccumulator):
         # not sharded: every rank already holds the full result, so no collective
@@ -399,12 +407,14 @@ class _AttributionMetric(ABC):
             B = x.shape[0]
             if stats:
                 arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
-                if engine.graphs_enabled(B):  # small batches are launch-bound: replay a HIP graph
-                    engine.taylor_graphed(x, y, set(uniq), arena, mode=mode)
-                else:
-                    engine.taylor(x, y, set(uniq), arena, mode=mode)
+                with trace_range("tp.forward_backward"):
+                    if engine.graphs_enabled(B):  # small batches are launch-bound: replay a HIP graph
+                        engine.taylor_graphed(x, y, set(uniq), arena, mode=mode)
+                    else:
+                        engine.taylor(x, y, set(uniq), arena, mode=mode)
                 sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device, engine.real_width(b)) for b in uniq]
-                ops.score_fold_([arena[b] for b in uniq], sums, take_abs, 2)
+                with trace_range("tp.fold"):
+                    ops.score_fold_([arena[b] for b in uniq], sums, take_abs, 2)
                 for b in uniq:
                     accs[owner[b]].count += B
             else:
@@ -445,7 +455,8 @@ class _AttributionMetric(ABC):
         stats = accs[0].mode == "stats"
         with torch.no_grad():
             for i, x, y in self._batches():
-                res = eng.grad_scores(x, y, set(uniq), mode)
+                with trace_range("tp.forward_backward"):
+                    res = eng.grad_scores(x, y, set(uniq), mode)
                 if stats:
                     slabs = [res[m] for m in uniq]
                     sums = [accs[first[m]].ensure_sum(res[m].shape[1], x.device, m.num_features) for m in uniq]

@@ -30,6 +30,7 @@ from torch.nn.modules.dropout import _DropoutNd
 
 from ... import ops
 from ...parallel import dist as pdist
+from ...utils.profiling import trace_range
 from ..base import _AttributionMetric
 
 logger = logging.getLogger("torchpruner")
@@ -152,8 +153,10 @@ class ShapleyAttributionMetric(_AttributionMetric):
                     slab = torch.zeros(B, n, dtype=torch.float64, device=base_loss.device)
                     slabs.append(slab)
                     sink = lambda L, pt, k0, slab=slab: ops.shapley_scatter(L, pt, slab, 0, k0, 1.0 / S)
-                for j, p_lo, p_hi in segs:
-                    self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi, base_loss, evaluate, K, S, sink)
+                with trace_range("tp.shapley.prefixes"):
+                    for j, p_lo, p_hi in segs:
+                        self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi, base_loss, evaluate, K, S,
+                                                     sink)
                 count += B
         world, _ = self._world()
         collective = world > 1 and self.shard_data is not False
@@ -161,7 +164,8 @@ class ShapleyAttributionMetric(_AttributionMetric):
             if sv_col is None:
                 return np.zeros(0)
             if collective:
-                pdist.all_reduce_sum_(sv_col, self.group)
+                with trace_range("tp.collective"):
+                    pdist.all_reduce_sum_(sv_col, self.group)
             total = sv_col.cpu().numpy()
             return total / max(count, 1) if self.reduction == "mean" else total
         sv = torch.cat(slabs, 0) if slabs else torch.zeros(0, 0, dtype=torch.float64)

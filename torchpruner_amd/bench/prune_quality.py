@@ -8,8 +8,10 @@ finetune steps of BASELINE config #5 in between; ``experiments/utils/train.py:11
 2. for every conv of ``get_vgg_pruning_graph`` (last layer first, as the reference's loop):
    score the conv's filters (Taylor on held-out attribution images, B=100 as nbVGG:193-196, or
    random scores), ``Pruner.prune_model`` the lowest-scored half (real slicing + cascade into the
-   next conv / BN, SGD momentum state rewired), then ``ft_steps`` SGD steps;
-3. a final ``final_ft_steps`` SGD steps; report held-out top-1 of the pruned network.
+   next conv / BN, SGD momentum state rewired), re-estimate the BatchNorm running statistics
+   (``recal_batches`` no-grad batches, ``utils.recalibrate_bn``: the next layer lost half its
+   input channels, so its BN statistics are stale), then ``ft_steps`` SGD steps;
+3. a final ``final_ft_steps`` SGD steps + BN recalibration; report held-out top-1.
 
 Reproducibility: training runs on the native convolutions / BN kernels (deterministic: no
 atomics), every kernel configuration is the untimed heuristic choice (``TUNER.fixed()``), and
@@ -34,9 +36,10 @@ from ..data import DeviceLoader, PrototypeTask
 from ..engine.fused_chain import TUNER
 from ..engine.train import native_convs
 from ..models import prunable_vgg16
+from ..utils.train import recalibrate_bn
 
 DEFAULTS = dict(noise=3.0, modes=16, teacher_steps=400, ft_steps=10, final_ft_steps=40, score_imgs=1000,
-                val_imgs=4000, lr=0.05, ft_lr=0.01, batch=128)
+                val_imgs=4000, lr=0.05, ft_lr=0.01, batch=128, recal_batches=8, frac=0.5, increments=1)
 
 
 @torch.no_grad()
@@ -68,6 +71,16 @@ def sgd_steps(model, task, steps, seed, lr, batch, optimizer=None, schedule=Fals
     return opt
 
 
+def recalibrate(model, task, seed, cfg):
+    """BN running statistics re-estimated on ``recal_batches`` fresh task batches (native BN
+    kernels, fixed configs: reproducible)."""
+    if cfg["recal_batches"] <= 0:
+        return
+    with TUNER.fixed(), native_convs(model):
+        recalibrate_bn(model, (task.sample(cfg["batch"], seed * 100_003 + 50_000 + i)[0]
+                               for i in range(cfg["recal_batches"])))
+
+
 def make_teacher(seed, device, cfg):
     torch.manual_seed(seed)
     model = prunable_vgg16().to(device)
@@ -79,7 +92,7 @@ def make_teacher(seed, device, cfg):
     return model, task
 
 
-def iterative_prune(model, task, method, seed, cfg, frac=0.5, log=None):
+def iterative_prune(model, task, method, seed, cfg, log=None):
     """Prune ``frac`` of every conv's filters layer by layer (``method``: "taylor" | "random"),
     finetuning between layers; returns the pruned model (modified in place)."""
     dev = next(model.parameters()).device
@@ -88,21 +101,31 @@ def iterative_prune(model, task, method, seed, cfg, frac=0.5, log=None):
     opt = torch.optim.SGD(model.parameters(), lr=cfg["ft_lr"], momentum=0.9, weight_decay=5e-4)
     pruner = Pruner(model, (3, 32, 32), dev, optimizer=opt)
     graph = [(m, c) for m, c in get_vgg_pruning_graph(model) if isinstance(m, torch.nn.Conv2d)]
+    inc = max(1, int(cfg["increments"]))
     for li, (module, cascade) in enumerate(graph):
         n = module.out_channels
-        if method == "taylor":
-            model.eval()
-            with TUNER.fixed():
-                s = TaylorAttributionMetric(model, DeviceLoader(xs, ys, 100), F.cross_entropy, dev,
-                                            shard_data=False).run(module, find_best_evaluation_module=True)
-        else:
-            s = rng.random_sample(n)
-        idx = np.argsort(s, kind="stable")[: int(n * frac)]
-        pruner.prune_model(module, idx, cascading_modules=cascade)
-        sgd_steps(model, task, cfg["ft_steps"], seed * 1000 + 500 + li, cfg["ft_lr"], cfg["batch"], optimizer=opt)
+        target = n - int(n * cfg["frac"])
+        for step in range(inc):  # prune in ``increments`` equal pieces, re-scoring the survivors
+            keep = n - (n - target) * (step + 1) // inc
+            cut = module.out_channels - keep
+            if cut <= 0:
+                continue
+            if method == "taylor":
+                model.eval()
+                with TUNER.fixed():
+                    s = TaylorAttributionMetric(model, DeviceLoader(xs, ys, 100), F.cross_entropy, dev,
+                                                shard_data=False).run(module, find_best_evaluation_module=True)
+            else:
+                s = rng.random_sample(module.out_channels)
+            pruner.prune_model(module, np.argsort(s, kind="stable")[:cut], cascading_modules=cascade)
+            recalibrate(model, task, seed * 1000 + li * 16 + step, cfg)
+            sgd_steps(model, task, cfg["ft_steps"], seed * 1000 + 500 + li * 16 + step, cfg["ft_lr"], cfg["batch"],
+                      optimizer=opt)
         if log:
             log(f"  [{method}] layer {li}: {n} -> {module.out_channels} filters")
     sgd_steps(model, task, cfg["final_ft_steps"], seed * 1000 + 900, cfg["ft_lr"], cfg["batch"], optimizer=opt)
+    if cfg["final_ft_steps"] > 0:
+        recalibrate(model, task, seed * 1000 + 999, cfg)
     model.zero_grad(set_to_none=True)
     return model
 

@@ -169,6 +169,41 @@ class PrototypeTask:
         x, y = self.sample(n, seed)
         return DeviceLoader(x, y, batch_size)
 
+    def stream(self, num_batches: int, batch_size: int, seed: int, channels_last: bool = False) -> "TaskStream":
+        """Batches regenerated on device from ``(seed, i)`` (nothing stored; shardable)."""
+        return TaskStream(self, num_batches, batch_size, seed, channels_last)
+
+
+class TaskStream:
+    """Deterministic on-device stream of :class:`PrototypeTask` batches; ``shard(rank, world)``
+    yields only this rank's whole batches (data-parallel training / attribution)."""
+
+    def __init__(self, task: PrototypeTask, num_batches: int, batch_size: int, seed: int, channels_last=False):
+        self.task = task
+        self.num_batches = num_batches
+        self.batch_size = batch_size
+        self.seed = seed
+        self.channels_last = channels_last
+        self.dataset = _Len(num_batches * batch_size)
+
+    def __len__(self):
+        return self.num_batches
+
+    def _batch(self, i):
+        x, y = self.task.sample(self.batch_size, self.seed * 1_000_003 + i)
+        if self.channels_last and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        return x, y
+
+    def __iter__(self):
+        for i in range(self.num_batches):
+            yield self._batch(i)
+
+    def shard(self, rank: int, world: int):
+        for i in range(rank, self.num_batches, world):
+            x, y = self._batch(i)
+            yield i, x, y
+
 
 def loaders(name: str, n_train: int, n_val: int, batch_size: int, val_batch_size: int, device="cpu", seed: int = 0,
             teacher=None):

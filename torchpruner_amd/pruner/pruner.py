@@ -30,6 +30,7 @@ from torch.nn.modules.conv import _ConvNd, _ConvTransposeNd
 from torch.nn.modules.dropout import _DropoutNd
 
 from .. import ops
+from ..utils.profiling import trace_range
 from ..parallel import dist as pdist
 from .opt_pruner import OptimizerPruner
 
@@ -58,6 +59,10 @@ class Pruner:
     # ------------------------------------------------------------------ public API
     def prune_model(self, module, indices, cascading_modules=None):
         """Prune output units ``indices`` of ``module`` and cascade into ``cascading_modules``."""
+        with trace_range("tp.prune"):
+            return self._prune_model(module, indices, cascading_modules)
+
+    def _prune_model(self, module, indices, cascading_modules=None):
         indices = self._sync(_as_index_array(indices))
         if cascading_modules is None:
             logger.warning("no cascading modules defined")

@@ -6,7 +6,7 @@ from .graph import (
     get_vgg_pruning_graph,
 )
 from .flops import count_parameters, count_flops
-from .train import test, train
+from .train import recalibrate_bn, test, train
 
 __all__ = [
     "ACTIVATIONS",
@@ -18,4 +18,5 @@ __all__ = [
     "count_flops",
     "train",
     "test",
+    "recalibrate_bn",
 ]

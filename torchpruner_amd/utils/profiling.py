@@ -15,8 +15,21 @@ import torch
 _ENABLED = os.environ.get("TORCHPRUNER_TRACE", "0") == "1"
 
 
+def set_tracing(enabled: bool) -> None:
+    """Turn the roctx ranges on/off at run time (default: ``TORCHPRUNER_TRACE=1``)."""
+    global _ENABLED
+    _ENABLED = bool(enabled)
+
+
+def tracing() -> bool:
+    return _ENABLED
+
+
 @contextlib.contextmanager
 def trace_range(name: str):
+    """A roctx range named ``name`` (rocprofv3 --marker-trace) while tracing is on. Ranges used
+    by the package: ``tp.run/<Metric>``, ``tp.forward``, ``tp.backward``, ``tp.fold``,
+    ``tp.collective``, ``tp.shapley.prefixes``, ``tp.prune``."""
     if not _ENABLED or not torch.cuda.is_available():
         yield
         return
@@ -24,6 +37,19 @@ def trace_range(name: str):
     try:
         yield
     finally:
+        torch.cuda.nvtx.range_pop()
+
+
+def range_push(name: str) -> bool:
+    """Open a roctx range when tracing (pair with :func:`range_pop` if it returned True)."""
+    if not _ENABLED or not torch.cuda.is_available():
+        return False
+    torch.cuda.nvtx.range_push(name)
+    return True
+
+
+def range_pop(opened: bool) -> None:
+    if opened:
         torch.cuda.nvtx.range_pop()
 
 

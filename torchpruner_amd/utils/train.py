@@ -52,6 +52,44 @@ def train(model, device, loss, train_loader, optimizer, epoch, log_every=20, sha
 
 
 @torch.no_grad()
+def recalibrate_bn(model, batches, max_batches=None) -> int:
+    """Re-estimate the BatchNorm running statistics of a (freshly pruned) model.
+
+    Pruning a layer's filters removes input channels of the next conv, so the running mean /
+    variance of the BN after it no longer describe its input and eval-mode accuracy collapses
+    until training re-adapts them (momentum 0.1: ~20 steps). This resets every BN's running
+    statistics and re-accumulates them as an exact cumulative average over ``batches`` (inputs,
+    or (x, y) pairs) in training mode, without gradients; other modules (Dropout) stay in eval
+    mode. Feed every data-parallel rank the same batches to keep replicas identical. Returns
+    the number of batches used."""
+    from torch.nn.modules.batchnorm import _BatchNorm
+    bns = [m for m in model.modules() if isinstance(m, _BatchNorm) and m.track_running_stats]
+    if not bns:
+        return 0
+    was = model.training
+    saved = [(m, m.momentum, m.training) for m in bns]
+    model.eval()
+    for m in bns:
+        m.reset_running_stats()
+        m.momentum = None  # cumulative moving average
+        m.train()
+    n = 0
+    try:
+        for b in batches:
+            if max_batches is not None and n >= max_batches:
+                break
+            x = b[0] if isinstance(b, (tuple, list)) else b
+            model(x)
+            n += 1
+    finally:
+        for m, mom, tr in saved:
+            m.momentum = mom
+            m.train(tr)
+        model.train(was)
+    return n
+
+
+@torch.no_grad()
 def test(model, device, loss, test_loader, verbose=1, shard=False):
     """Eval-mode average loss and accuracy (reference train.py:51-72)."""
     model.eval()
