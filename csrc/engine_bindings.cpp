@@ -12,7 +12,7 @@ hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w
                          int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
                          float* taylor, int HWo, int tay_group, float* ws, int tay_mode, float* apoz,
-                         hipStream_t st);
+                         float slope, hipStream_t st);
 int tp_conv_gen_k(int ks, int Cin);
 int tp_bn_groups(int P, int C);
 hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
@@ -84,7 +84,8 @@ int64_t splits_ws(int64_t splits, int64_t K) {
 std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w,
                                             const c10::optional<at::Tensor>& scale,
                                             const c10::optional<at::Tensor>& shift, bool relu, bool pool, int64_t ks,
-                                            int64_t cfg, int64_t splits, const c10::optional<at::Tensor>& apoz) {
+                                            int64_t cfg, int64_t splits, const c10::optional<at::Tensor>& apoz,
+                                            double slope) {
   need(x, "x", 4);
   need(w, "w", 2);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
@@ -115,7 +116,8 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
   TP_CHECK_HIP(tp_conv_igemm(x.data_ptr<float>(), nullptr, w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin,
                              (int)Cout, (int)ks, pool ? 1 : 0, 0, pool ? EPI_FWD_POOL : EPI_FWD, (int)cfg, (int)sp, sc,
                              sh, relu ? 1 : 0, out.data_ptr<float>(), pool ? am.data_ptr<uint8_t>() : nullptr, nullptr,
-                             nullptr, (int)(H * W), 0, sp > 1 ? ws.data_ptr<float>() : nullptr, 0, ap, cur_stream()));
+                             nullptr, (int)(H * W), 0, sp > 1 ? ws.data_ptr<float>() : nullptr, 0, ap, (float)slope,
+                             cur_stream()));
   return {out, am};
 }
 
@@ -128,7 +130,7 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
 at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_argmax, const at::Tensor& wt,
                       const at::Tensor& act, const c10::optional<at::Tensor>& bn_scale,
                       const c10::optional<at::Tensor>& taylor, bool want_out, int64_t ks, int64_t cfg,
-                      int64_t splits, int64_t tay_group, int64_t tay_mode) {
+                      int64_t splits, int64_t tay_group, int64_t tay_mode, double slope) {
   need(g, "g", 4);
   need(wt, "wt", 2);
   need(act, "act", 4);
@@ -165,7 +167,7 @@ at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_ar
                              unpool ? 1 : 0, EPI_BWD, (int)cfg, (int)sp, sc, nullptr, 0,
                              want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(), tay,
                              (int)(H * W), (int)tay_group, sp > 1 ? ws.data_ptr<float>() : nullptr, (int)tay_mode,
-                             nullptr, cur_stream()));
+                             nullptr, (float)slope, cur_stream()));
   return out;
 }
 
@@ -546,9 +548,9 @@ void register_engine_ops_def(torch::Library& m) {
         "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
-        "int splits, Tensor(a!)? apoz=None) -> (Tensor, Tensor)");
+        "int splits, Tensor(a!)? apoz=None, float slope=0.0) -> (Tensor, Tensor)");
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
-        "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0) -> Tensor");
+        "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0, float slope=0.0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
         "bool staged=True, Tensor(a!)? apoz=None) -> (Tensor, Tensor)");

@@ -65,6 +65,14 @@ __device__ __forceinline__ float nan_max(float a, float b) {
   return (a > b || a != a) ? a : b;
 }
 __device__ __forceinline__ float nan_relu(float x) { return (x > 0.f || x != x) ? x : 0.f; }
+// NaN-propagating ReLU (slope 0) / LeakyReLU (slope > 0): NaN passes through (pruner NaN probe)
+__device__ __forceinline__ float nan_act(float x, float slope) {
+  return (x > 0.f || x != x) ? x : (slope != 0.f ? x * slope : 0.f);
+}
+// backward of nan_act given its OUTPUT a (sign(a) == sign(x) for slope >= 0)
+__device__ __forceinline__ float act_grad(float a, float g, float slope) {
+  return a > 0.f ? g : (slope != 0.f ? g * slope : 0.f);
+}
 
 inline unsigned ceil_div(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 

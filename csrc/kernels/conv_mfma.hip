@@ -64,6 +64,8 @@ struct ConvArgs {
                             // (gradient of a strided 1x1 downsample conv scattered back), 1 = dense
   int tay_mode;             // EPI_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
   int parity;               // GEN 3: rows ordered (oh%2, ow%2, b, oh/2, ow/2) so a tile sees few taps
+  float slope;              // activation: 0 = ReLU, > 0 = LeakyReLU negative slope (fwd relu flag /
+                            // EPI_BWD mask of the consumer activation)
 };
 
 // GEN 3 output row m -> (image, oh, ow). Parity order makes each stride-2 phase class one
@@ -479,10 +481,10 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           v.w = mq[u].w > 0.f ? v.w : 0.f;
         }
         if (p.relu) {
-          v.x = nan_relu(v.x);
-          v.y = nan_relu(v.y);
-          v.z = nan_relu(v.z);
-          v.w = nan_relu(v.w);
+          v.x = nan_act(v.x, p.slope);
+          v.y = nan_act(v.y, p.slope);
+          v.z = nan_act(v.z, p.slope);
+          v.w = nan_act(v.w, p.slope);
         }
         *reinterpret_cast<float4*>(p.out + o) = v;
         if (p.apoz) {  // exact integer counts: atomics are order-free
@@ -551,7 +553,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float v = acc[i][j][4 * g + q] * sc + sh;
-            if (p.relu) v = nan_relu(v);
+            if (p.relu) v = nan_act(v, p.slope);
             cnt += v > 0.f ? 1 : 0;
             if (q == 0 || v > best || (v != v && best == best)) {
               best = v;
@@ -586,7 +588,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
                 }
                 tsum += p.tay_mode ? fabsf(gval) : -(gval * a);
               }
-              if (p.out) p.out[o] = a > 0.f ? gval * sc : 0.f;
+              if (p.out) p.out[o] = act_grad(a, gval * sc, p.slope);
             }
           }
         }
@@ -602,7 +604,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
             if constexpr (EPI == EPI_FWD) {
               v = v * sc + sh;
               if (p.res) v += p.res[(long long)m * p.N + n];
-              if (p.relu) v = nan_relu(v);
+              if (p.relu) v = nan_act(v, p.slope);
               p.out[(long long)m * p.N + n] = v;
               if (p.apoz) {  // counts are exact integers: atomics are order-independent here
                 const int b = m / p.HWo;
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         float v = 0.f;
         for (int s = 0; s < splits; ++s) v += slabs[(size_t)s * MN + o];
         v = v * sc + sh;
-        if (p.relu) v = nan_relu(v);
+        if (p.relu) v = nan_act(v, p.slope);
         cnt += v > 0.f ? 1 : 0;
         if (q == 0 || v > best || (v != v && best == best)) {
           best = v;
@@ -700,10 +702,10 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
           v.w = a.w > 0.f ? v.w : 0.f;
         }
         if (p.relu) {
-          v.x = nan_relu(v.x);
-          v.y = nan_relu(v.y);
-          v.z = nan_relu(v.z);
-          v.w = nan_relu(v.w);
+          v.x = nan_act(v.x, p.slope);
+          v.y = nan_act(v.y, p.slope);
+          v.z = nan_act(v.z, p.slope);
+          v.w = nan_act(v.w, p.slope);
         }
         *reinterpret_cast<float4*>(p.out + (size_t)t * 4) = v;
         if (p.apoz) {
@@ -723,7 +725,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         v = v * (p.scale ? p.scale[n] : 1.f) + (p.shift ? p.shift[n] : 0.f);
         if (p.res) v += p.res[o];
         if (p.mask && !(p.mask[o] > 0.f)) v = 0.f;
-        if (p.relu) v = nan_relu(v);
+        if (p.relu) v = nan_act(v, p.slope);
         p.out[o] = v;
         if (p.apoz && v > 0.f) atomicAdd(p.apoz + (size_t)(o / N / (unsigned)p.HWo) * N + n, 1.f);
       }
@@ -745,7 +747,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
         const float a = p.act[o];
         tsum += p.tay_mode ? fabsf(v) : -(v * a);
-        if (p.out) p.out[o] = a > 0.f ? v * sc : 0.f;
+        if (p.out) p.out[o] = act_grad(a, v * sc, p.slope);
       }
       if (p.taylor) p.taylor[tay_index(p, b, n)] += tsum;
     }
@@ -771,7 +773,7 @@ __global__ __launch_bounds__(1024) void conv_epilogue_bwd_img(ConvArgs p, const 
       for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
       const float a = p.act[o];
       tsum += p.tay_mode ? fabsf(v) : -(v * a);
-      if (p.out) p.out[o] = a > 0.f ? v * sc : 0.f;
+      if (p.out) p.out[o] = act_grad(a, v * sc, p.slope);
     }
   }
   red[pg][c] = tsum;
@@ -917,10 +919,11 @@ extern "C" hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, con
                                     int Cin, int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits,
                                     const float* scale, const float* shift, int relu, float* out,
                                     uint8_t* out_argmax, const float* act, float* taylor, int HWo, int tay_group,
-                                    float* ws, int tay_mode, float* apoz, hipStream_t st) {
+                                    float* ws, int tay_mode, float* apoz, float slope, hipStream_t st) {
   using namespace tp;
-  if (Cin % 32 != 0) return hipErrorInvalidValue;
+  if (Cin % 32 != 0 || !(slope >= 0.f)) return hipErrorInvalidValue;
   ConvArgs a{};
+  a.slope = slope;
   a.x = x;
   a.x_argmax = x_argmax;
   a.w = w;

@@ -103,8 +103,9 @@ def main():
           lambda m: m.run_many(convs, find_best_evaluation_module=True), "fused", "vgg_apoz", report)
 
     def sv(s):
+        # 2 batches: world 2 shards whole batches, world 3 splits the prefixes of every batch
         np.random.seed(7)  # rank 0's draw is broadcast (R3); single-rank runs draw the same
-        return ShapleyAttributionMetric(vgg, DeviceLoader(x[:48], y[:48], 16), ce, dev, sv_samples=2, shard_data=s)
+        return ShapleyAttributionMetric(vgg, DeviceLoader(x[:32], y[:32], 16), ce, dev, sv_samples=2, shard_data=s)
 
     # atol: the prefix losses are ~2.3 (ulp 2.4e-7 in fp32); a rank re-batches its boundary prefix
     # (a different stacked batch -> another GEMM config), which may move one loss by an ulp, so

@@ -158,3 +158,18 @@ def test_loopback_all_gather_outputs_are_private():
 
     res = run_loopback(2, body)
     assert res[1] == [[0.0, 0.0], [1.0, 1.0]]
+
+
+def test_shapley_work_split_modes():
+    """Shapley shards whole batches when every rank gets one (no replicated upstream forward),
+    else splits each batch's prefixes across ranks."""
+    model, x, y = _model_and_data()
+    dl = DeviceLoader(x, y, 4)  # 6 batches
+
+    def body(comm):
+        m = ShapleyAttributionMetric(model, dl, F.cross_entropy, torch.device("cpu"), group=comm)
+        return m._work_split()
+
+    assert run_loopback(3, body) == ["batches"] * 3
+    assert run_loopback(8, body) == ["prefixes"] * 8
+    assert ShapleyAttributionMetric(model, dl, F.cross_entropy, torch.device("cpu"))._work_split() is None

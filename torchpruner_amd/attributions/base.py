@@ -438,12 +438,13 @@ class _AttributionMetric(ABC):
             return _reject(why, "resnet engine: criterion is not mean cross-entropy")
         return eng
 
-    def _fused_engine(self, eval_modules, why=None, need_ce=True):
-        """The fused VGG-chain engine (engine, block indices) for ``eval_modules``, else None."""
+    def _fused_engine(self, eval_modules, why=None, need_ce=True, pre_act_ok=False):
+        """The fused chain engine (engine, block indices) for ``eval_modules``, else None."""
         from ..engine.fused_chain import _reject, maybe_engine
         if not self._engines_allowed():
             return _reject(why, f"compute_dtype={self.compute_dtype} runs the generic autocast path")
-        return maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=need_ce, why=why)
+        return maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=need_ce, why=why,
+                            pre_act_ok=pre_act_ok)
 
     def _resnet_grad_pass(self, eng, eval_modules, accs, mode):
         """Per batch: one engine forward + input-gradient backward scores every module; the

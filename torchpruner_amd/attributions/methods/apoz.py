@@ -27,7 +27,7 @@ class APoZAttributionMetric(_AttributionMetric):
         self._begin_run(accs, eval_modules)
         try:
             why = []
-            fused = self._fused_engine(eval_modules, why, need_ce=False)
+            fused = self._fused_engine(eval_modules, why, need_ce=False, pre_act_ok=True)
             eng = None if fused is not None or not self._engines_allowed() else \
                 maybe_resnet_engine(self.model, eval_modules, self.device, why=why)
             self._record_path("fused" if fused else "resnet" if eng else "generic", eval_modules, why)

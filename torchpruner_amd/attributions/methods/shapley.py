@@ -15,9 +15,12 @@ MI355X-native execution:
   on device (``ops.shapley_scatter`` / ``ops.shapley_column``). The reference runs one tiny
   forward plus one device->host copy per unit (S*n per batch, shapley_values.py:55-61).
   K is sized from an element budget so the batch fills the GPU (288 GB HBM).
-* **Work sharding across ranks.** The S*n prefix evaluations per batch are split into
-  contiguous ranges over ranks (one boundary evaluation per range), permutations are
-  broadcast from rank 0 (R3), and the accumulators are all-reduced once per ``run()`` (R4).
+* **Work sharding across ranks.** With at least ``world`` batches, whole batches go
+  round-robin to ranks and each rank runs its own upstream forward plus every prefix of its
+  batches (nothing is replicated); with fewer batches, every rank sees every batch and the
+  S*n prefix evaluations are split into contiguous ranges (one boundary evaluation per
+  range). Permutations are broadcast from rank 0 (R3); the accumulators are all-reduced
+  (stats) or gathered in global batch order (per-sample) once per ``run()`` (R4/R2).
 """
 from __future__ import annotations
 
@@ -88,10 +91,11 @@ class ShapleyAttributionMetric(_AttributionMetric):
             perms = pdist.broadcast_object(perms, 0, self.group)
         return perms
 
-    def _segments(self, S, n):
-        """This rank's share of the flattened (permutation j, prefix p in 1..n) work."""
+    def _segments(self, S, n, split):
+        """This rank's share of the flattened (permutation j, prefix p in 1..n) work (all of it
+        unless ``split``)."""
         world, rank = self._world()
-        if world > 1 and self.shard_data is not False:
+        if split:
             lo, hi = pdist.split_range(S * n, rank, world)
         else:
             lo, hi = 0, S * n
@@ -104,6 +108,21 @@ class ShapleyAttributionMetric(_AttributionMetric):
             segs.append((j, p_lo, p_hi))
             u += p_hi - p_lo + 1
         return segs
+
+    def _work_split(self):
+        """How ranks share the work: ``"batches"`` — whole batches round-robin, each rank runs
+        its own upstream forward and every prefix (scales for deep layers, where the upstream
+        forward dominates); ``"prefixes"`` — every rank sees every batch and evaluates a
+        contiguous range of the S*n prefixes (when there are fewer batches than ranks);
+        ``None`` — single rank / sharding disabled."""
+        world, _ = self._world()
+        if world == 1 or self.shard_data is False:
+            return None
+        try:
+            nb = len(self.data_gen)
+        except TypeError:
+            return "prefixes"
+        return "batches" if nb >= world else "prefixes"
 
     @staticmethod
     def _rank_of(perm, device):
@@ -128,22 +147,23 @@ class ShapleyAttributionMetric(_AttributionMetric):
     def _run_batches(self, module, S, prepare):
         """Shared driver. ``prepare(x, y)`` -> (n, B, per_sample, base_loss, evaluate)."""
         stats = self.reduction in ("mean", "sum")
+        split = self._work_split()
         sv_col = None
         slabs = []
         count = 0
         perms = None
         perm_ts = rank_ts = None
         segs = None
+        batches = self._batches() if split == "batches" else \
+            ((i, _to(x, self.device), _to(y, self.device)) for i, (x, y) in enumerate(self.data_gen))
         with torch.no_grad():
-            # every rank iterates every batch; the prefix work (not the data) is sharded
-            for bidx, (x, y) in enumerate(self.data_gen):
-                x, y = _to(x, self.device), _to(y, self.device)
+            for bidx, x, y in batches:
                 n, B, per_sample, base_loss, evaluate = prepare(x, y)
                 if perms is None:
-                    perms = self._permutations(n, S)
+                    perms = self._permutations(n, S)  # drawn on rank 0, broadcast (R3)
                     perm_ts = [torch.as_tensor(p, dtype=torch.int32).to(base_loss.device) for p in perms]
                     rank_ts = [self._rank_of(p, base_loss.device) for p in perms]
-                    segs = self._segments(S, n)
+                    segs = self._segments(S, n, split == "prefixes")
                 K = self._prefix_chunk(B, per_sample)
                 if stats:
                     if sv_col is None:
@@ -151,26 +171,38 @@ class ShapleyAttributionMetric(_AttributionMetric):
                     sink = lambda L, pt, k0: ops.shapley_column(L, pt, sv_col, k0, 1.0 / S)
                 else:
                     slab = torch.zeros(B, n, dtype=torch.float64, device=base_loss.device)
-                    slabs.append(slab)
+                    slabs.append((bidx, slab))
                     sink = lambda L, pt, k0, slab=slab: ops.shapley_scatter(L, pt, slab, 0, k0, 1.0 / S)
                 with trace_range("tp.shapley.prefixes"):
                     for j, p_lo, p_hi in segs:
                         self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi, base_loss, evaluate, K, S,
                                                      sink)
                 count += B
-        world, _ = self._world()
-        collective = world > 1 and self.shard_data is not False
         if stats:
+            if split is not None:
+                with trace_range("tp.collective"):
+                    # ranks agree on n even if one saw no batch; one (n + 1,) fp64 all-reduce (R4)
+                    n = pdist.all_max_int(sv_col.numel() if sv_col is not None else 0, self.group)
+                    buf = torch.zeros(n + 1, dtype=torch.float64, device=self.device)
+                    if sv_col is not None:
+                        buf[:n] = sv_col
+                    buf[n] = float(count) if split == "batches" else 0.0
+                    pdist.all_reduce_sum_(buf, self.group)
+                    sv_col = buf[:n]
+                    if split == "batches":
+                        count = float(buf[n].item())
             if sv_col is None:
                 return np.zeros(0)
-            if collective:
-                with trace_range("tp.collective"):
-                    pdist.all_reduce_sum_(sv_col, self.group)
             total = sv_col.cpu().numpy()
             return total / max(count, 1) if self.reduction == "mean" else total
-        sv = torch.cat(slabs, 0) if slabs else torch.zeros(0, 0, dtype=torch.float64)
-        if collective:
-            pdist.all_reduce_sum_(sv, self.group)
+        if split == "batches":
+            with trace_range("tp.collective"):
+                sv = pdist.gather_ordered_rows(slabs, self.group)  # global batch order (R2)
+        else:
+            sv = torch.cat([t for _, t in slabs], 0) if slabs else torch.zeros(0, 0, dtype=torch.float64)
+            if split == "prefixes":
+                with trace_range("tp.collective"):
+                    pdist.all_reduce_sum_(sv, self.group)
         return self.aggregate_over_samples(sv.cpu().numpy())
 
     # ------------------------------------------------------------------ native path
@@ -180,7 +212,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
         are stacked by one kernel and pushed through the remaining fused layers in ONE forward.
         Masking a post-ReLU activation commutes with the following 2x2 max-pool, so the
         engine masks its pooled output (4x less data) with identical results."""
-        fused = self._fused_engine([module], why)
+        fused = self._fused_engine([module], why, pre_act_ok=True)
         if fused is None:
             return None
         engine, (k,) = fused

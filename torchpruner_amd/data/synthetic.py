@@ -64,6 +64,42 @@ class DeviceLoader:
             yield i, x, y
 
 
+class ShardLoader:
+    """One data-parallel rank's batches of a global batched data set, materialised on device:
+    ``batches`` maps global batch index -> (x, y) for the indices this rank owns (round-robin,
+    ``i % world == rank``). ``shard(rank, world)`` yields exactly those (each rank holds 1/world
+    of the data instead of all of it); iterating it plainly is only valid when it owns all
+    batches (world 1)."""
+
+    def __init__(self, batches: dict, num_batches: int, batch_size: int):
+        self.batches = batches
+        self.num_batches = num_batches
+        self.batch_size = batch_size
+        self.dataset = _Len(num_batches * batch_size)
+
+    @classmethod
+    def build(cls, make_batch: Callable, num_batches: int, batch_size: int, rank: int = 0, world: int = 1):
+        """``make_batch(i)`` -> (x, y) of global batch ``i`` (e.g. seeded from i); only this rank's
+        batches are built."""
+        return cls({i: make_batch(i) for i in range(rank, num_batches, world)}, num_batches, batch_size)
+
+    def __len__(self):
+        return self.num_batches
+
+    def __iter__(self):
+        if len(self.batches) != self.num_batches:
+            raise RuntimeError("ShardLoader holds one rank's batches; iterate it through shard(rank, world)")
+        for i in range(self.num_batches):
+            yield self.batches[i]
+
+    def shard(self, rank: int, world: int):
+        for i in range(rank, self.num_batches, world):
+            if i not in self.batches:
+                raise RuntimeError(f"batch {i} belongs to rank {rank} of {world} but was not built here")
+            x, y = self.batches[i]
+            yield i, x, y
+
+
 class StreamLoader:
     """Deterministic on-device stream of ``num_batches`` random batches (nothing stored)."""
 

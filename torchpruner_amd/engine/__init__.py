@@ -1,7 +1,26 @@
 """Fused native execution engines (HIP kernels, no autograd) used by the attribution metrics
 when the model/criterion/device allow it; everything else runs the generic hook path."""
+from __future__ import annotations
+
+import torch
+
 from .fused_chain import FusedChainEngine, Plan, build_plan, criterion_is_cross_entropy, maybe_engine
 from .resnet_engine import ResNetEngine, build_resnet_plan, maybe_resnet_engine
 
 __all__ = ["FusedChainEngine", "Plan", "build_plan", "criterion_is_cross_entropy", "maybe_engine", "ResNetEngine",
-           "build_resnet_plan", "maybe_resnet_engine"]
+           "build_resnet_plan", "maybe_resnet_engine", "native_logits"]
+
+
+@torch.no_grad()
+def native_logits(model, x: torch.Tensor):
+    """Eval-mode logits of ``model`` on the native engines (fused chain: VGG-style CNNs and
+    MLPs; ResNet engine), or None when neither applies (training mode, CPU, other models)."""
+    if not isinstance(x, torch.Tensor) or not x.is_cuda or model.training:
+        return None
+    r = maybe_engine(model, [], None, x.device, need_ce=False)
+    if r is not None:
+        return r[0].forward(x)[0]
+    eng = maybe_resnet_engine(model, [], x.device)
+    if eng is not None:
+        return eng.forward(x)
+    return None

@@ -213,8 +213,21 @@ class ConvBlock:
 @dataclass
 class LinearBlock:
     linear: nn.Linear
-    relu: Optional[nn.Module]
+    relu: Optional[nn.Module]  # the block's activation: nn.ReLU or nn.LeakyReLU (slope >= 0)
     width: int = 0
+
+    @property
+    def slope(self) -> float:
+        return _act_slope(self.relu)
+
+
+def _act_slope(m) -> float:
+    """Negative-side slope of a block activation (0 for ReLU)."""
+    return float(m.negative_slope) if isinstance(m, nn.LeakyReLU) else 0.0
+
+
+def _is_block_act(m) -> bool:
+    return isinstance(m, nn.ReLU) or (isinstance(m, nn.LeakyReLU) and m.negative_slope >= 0)
 
 
 @dataclass
@@ -281,12 +294,10 @@ def build_plan(model: nn.Module):
             width = 16 if conv.out_channels <= 16 else width
         plan.convs.append(ConvBlock(conv, bn, relu, pool, first=first and conv.in_channels % 32 != 0,
                                     width=width))
-    if not plan.convs:
-        return None, "no conv stack"
-    # flatten
+    # flatten (a conv-less MLP may start with it or take flattened inputs)
     if i < n and (isinstance(stages[i], nn.Flatten) or getattr(stages[i], "__name__", "") == "_flatten"):
         i += 1
-    else:
+    elif plan.convs:
         return None, "expected flatten after the conv stack"
     while i < n:
         st = stages[i]
@@ -295,16 +306,16 @@ def build_plan(model: nn.Module):
             continue
         if isinstance(st, nn.Linear):
             i += 1
-            relu = None
-            if i < n and isinstance(stages[i], nn.ReLU):
-                relu = stages[i]
+            act = None
+            if i < n and _is_block_act(stages[i]):
+                act = stages[i]
                 i += 1
-            plan.linears.append(LinearBlock(st, relu, cpad(st.out_features)))
+            plan.linears.append(LinearBlock(st, act, cpad(st.out_features)))
             continue
         return None, f"unsupported classifier stage {st}"
     if not plan.linears or any(b.relu is None for b in plan.linears[:-1]) or plan.linears[-1].relu is not None:
-        return None, "classifier must be Linear(+ReLU) blocks ending in a plain Linear"
-    if plan.linears[0].linear.in_features != plan.convs[-1].conv.out_channels:
+        return None, "classifier must be Linear(+ReLU/LeakyReLU) blocks ending in a plain Linear"
+    if plan.convs and plan.linears[0].linear.in_features != plan.convs[-1].conv.out_channels:
         return None, "features must end at 1x1 spatial resolution"
     plan.linears[-1].width = plan.linears[-1].linear.out_features  # logits stay unpadded
     return plan, ""
@@ -377,6 +388,8 @@ class FusedChainEngine:
                     entry["ut"] = winograd_weights(w.flip(2, 3).transpose(0, 1))
             convs.append(entry)
         lins = []
+        if cin_p is None:  # conv-less MLP: input features zero-padded to the 32-wide K granule
+            cin_p = cpad(self.plan.linears[0].linear.in_features)
         for b in self.plan.linears:
             w = b.linear.weight.detach().float()
             n_out = w.shape[0]
@@ -389,7 +402,7 @@ class FusedChainEngine:
             if pad:
                 wt = torch.cat([wt, torch.zeros(wt.shape[0], pad, device=w.device)], 1)
             lins.append({"w": w.contiguous(), "bias": bias.contiguous(), "wt": wt.contiguous(), "pad": pad,
-                         "relu": b.relu is not None})
+                         "relu": b.relu is not None, "slope": b.slope})
         self._packed = {"convs": convs, "lins": lins}
         self._key = key
         return self._packed
@@ -487,9 +500,18 @@ class FusedChainEngine:
         B = xin.shape[0]
         cfg, sp = TUNER.choose(("lin", tuple(xin.shape), e["w"].shape[0]), B, e["w"].shape[0], e["w"].shape[1],
                                lambda c, s_, e=e, xin=xin: T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"],
-                                                                    False, 1, c, s_))
-        out, _ = T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp)
+                                                                    False, 1, c, s_, slope=e["slope"]))
+        out, _ = T.conv_fwd(xin, e["w"], None, e["bias"], e["relu"], False, 1, cfg, sp, slope=e["slope"])
         return out
+
+    def _mlp_input(self, x: torch.Tensor) -> torch.Tensor:
+        """Flattened fp32 input of a conv-less chain, zero-padded to the packed K: (B, 1, 1, Kp)."""
+        B = x.shape[0]
+        kp = self._pack()["lins"][0]["w"].shape[1]
+        h = x.reshape(B, -1).float()
+        if h.shape[1] != kp:
+            h = F.pad(h, (0, kp - h.shape[1]))
+        return h.contiguous().view(B, 1, 1, kp)
 
     def forward(self, x: torch.Tensor, stop_after: Optional[int] = None, apoz: Optional[dict] = None):
         """Forward pass; returns (logits, saved) where saved holds what backward needs.
@@ -513,7 +535,7 @@ class FusedChainEngine:
             acts.append((h, am if e["pool"] else None))
             if stop_after == ci:
                 return h, {"acts": acts}
-        lin_acts = [h.reshape(B, 1, 1, -1)]
+        lin_acts = [h.reshape(B, 1, 1, -1) if h is not None else self._mlp_input(x)]
         nconv = len(self.plan.convs)
         for li, e in enumerate(P["lins"]):
             lin_acts.append(self._linear(T, e, lin_acts[-1]))
@@ -673,12 +695,16 @@ class FusedChainEngine:
             if blk_index in want:
                 taylor = arena[blk_index]
                 res[blk_index] = taylor
-            bn_scale = P["convs"][-1]["scale"] if j == 0 else None
+            bn_scale = P["convs"][-1]["scale"] if j == 0 and nconv else None
+            slope = P["lins"][j - 1]["slope"] if j > 0 else 0.0  # activation whose output is `act`
+            want_out = j > 0 or nconv > 0  # the input of a conv-less chain needs no gradient
+            if not want_out and taylor is None:
+                break
             gg = g
             cfg, sp = TUNER.choose(("lin_bwd", tuple(g.shape), tuple(act.shape)), B, act.shape[3], e["wt"].shape[1],
-                                   lambda c, s_, e=e, gg=gg, act=act, bn=bn_scale: T.conv_dgrad(
-                                       gg, None, e["wt"], act, bn, None, True, 1, c, s_))
-            g = T.conv_dgrad(g, None, e["wt"], act, bn_scale, taylor, True, 1, cfg, sp, tay_mode=tm)
+                                   lambda c, s_, e=e, gg=gg, act=act, bn=bn_scale, sl=slope: T.conv_dgrad(
+                                       gg, None, e["wt"], act, bn, None, True, 1, c, s_, slope=sl))
+            g = T.conv_dgrad(g, None, e["wt"], act, bn_scale, taylor, want_out, 1, cfg, sp, tay_mode=tm, slope=slope)
         # conv stack: g is dL/d(pre-activation of conv nconv-1) * bn_scale, at the
         # (pooled, if pooled) output resolution of that block
         for ci in range(nconv - 1, 0, -1):
@@ -734,10 +760,12 @@ def _reject(why, reason):
     return None
 
 
-def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None):
+def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None, pre_act_ok=False):
     """Return (engine, block indices of eval_modules) when the fused path applies, else None.
     ``need_ce=False``: forward-only use (APoZ), any criterion. ``why``: a list that receives the
-    rejection reason when the engine does not apply."""
+    rejection reason when the engine does not apply. ``pre_act_ok``: a classifier block's Linear
+    may stand for its activation output (valid for sign counts (APoZ) and zero-masking
+    (Shapley): ReLU / LeakyReLU keep the sign and map 0 to 0; not for Taylor / Sensitivity)."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda":
         return _reject(why, f"device {dev} is not a GPU")
@@ -755,7 +783,7 @@ def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None)
     for m in eval_modules:
         found = None
         for k, b in enumerate(blocks[:-1]):
-            if b.relu is m:
+            if b.relu is m or (pre_act_ok and isinstance(b, LinearBlock) and b.linear is m):
                 found = k
                 break
         if found is None:

@@ -159,8 +159,11 @@ class ResNetEngine:
         fc_w = F.pad(fc_w, (0, cpad(fc_w.shape[1]) - fc_w.shape[1]))
         fc_b = p.fc.bias.detach().float() if p.fc.bias is not None else torch.zeros(fc_w.shape[0],
                                                                                    device=fc_w.device)
+        n_cls = fc_w.shape[0]
+        # fc backward operand for the MFMA GEMM: (C, classes padded to 32) with zero columns
+        fc_wt = F.pad(fc_w, (0, 0, 0, cpad(n_cls) - n_cls)).t().contiguous()
         self._packed = {"stem": self._pack_conv(p.stem, stem=True), "blocks": blocks,
-                        "fc_w": fc_w.contiguous(), "fc_b": fc_b.contiguous()}
+                        "fc_w": fc_w.contiguous(), "fc_b": fc_b.contiguous(), "fc_wt": fc_wt}
         self._key = key
         return self._packed
 
@@ -205,8 +208,34 @@ class ResNetEngine:
         feat = T.avgpool_nhwc(h)
         for buf, tmp in padded:
             buf.add_(tmp[:, :buf.shape[1]])
-        logits = F.linear(feat, P["fc_w"], P["fc_b"])
-        return (logits, saved) if save else logits
+        logits = self._fc(T, P, feat)
+        if save:
+            saved.append(feat)
+            return logits, saved
+        return logits
+
+    @staticmethod
+    def _fc(T, P, feat):
+        """Classifier GEMM on the MFMA kernel (ks=1 implicit GEMM, bias in the epilogue)."""
+        B, C = feat.shape
+        w = P["fc_w"]
+        x = feat.contiguous().view(B, 1, 1, C)
+        cfg, sp = TUNER.choose(("fc", B, C, w.shape[0]), B, w.shape[0], C,
+                               lambda c, s_: T.conv_fwd(x, w, None, P["fc_b"], False, False, 1, c, s_))
+        return T.conv_fwd(x, w, None, P["fc_b"], False, False, 1, cfg, sp)[0].view(B, -1)
+
+    @staticmethod
+    def _fc_bwd(T, P, g_log, feat):
+        """dL/dfeat = g_log @ fc_w on the MFMA kernel (classes zero-padded to 32; the epilogue's
+        ReLU mask by feat > 0 is exact here: feat is an average of ReLU outputs, and a zero
+        average means every pixel of that channel is 0, masked again downstream)."""
+        B, C = feat.shape
+        wt = P["fc_wt"]
+        g = F.pad(g_log, (0, wt.shape[1] - g_log.shape[1])).contiguous().view(B, 1, 1, -1)
+        a = feat.contiguous().view(B, 1, 1, C)
+        cfg, sp = TUNER.choose(("fc_bwd", B, C, wt.shape[1]), B, C, wt.shape[1],
+                               lambda c, s_: T.conv_dgrad(g, None, wt, a, None, None, True, 1, c, s_))
+        return T.conv_dgrad(g, None, wt, a, None, None, True, 1, cfg, sp).view(B, C)
 
     def _stem(self, T, P, x, apoz):
         h = T.nchw_to_nhwc_pad(x.float().contiguous(), 4)
@@ -271,7 +300,7 @@ class ResNetEngine:
             t = self._conv(T, e["convs"][i], t, True, res=idn if i == n - 1 else None)
         for b in range(bi + 1, len(self.plan.blocks)):
             t = self._block(T, self.plan.blocks[b], P["blocks"][b], t)
-        return F.linear(T.avgpool_nhwc(t), P["fc_w"], P["fc_b"])
+        return self._fc(T, P, T.avgpool_nhwc(t))
 
     # ------------------------------------------------------------------ backward (Taylor, Sensitivity)
     @staticmethod
@@ -334,9 +363,10 @@ class ResNetEngine:
         T = ops.require()
         P = self._pack()
         logits, saved = self.forward(x, save=True)
+        feat = saved.pop()
         B = logits.shape[0]
         _, g_log = ops.cross_entropy(logits, y, 1.0 / B, True)
-        g_feat = g_log @ P["fc_w"]  # (B, C_last padded)
+        g_feat = self._fc_bwd(T, P, g_log, feat)  # (B, C_last padded)
         y_last = saved[-1][2]
         HW = y_last.shape[1] * y_last.shape[2]
         # avg-pool backward + final ReLU of the last block: dL/d(pre-ReLU residual sum)

@@ -90,13 +90,17 @@ def recalibrate_bn(model, batches, max_batches=None) -> int:
 
 
 @torch.no_grad()
-def test(model, device, loss, test_loader, verbose=1, shard=False):
-    """Eval-mode average loss and accuracy (reference train.py:51-72)."""
+def test(model, device, loss, test_loader, verbose=1, shard=False, native=True):
+    """Eval-mode average loss and accuracy (reference train.py:51-72). ``native``: logits come
+    from the HIP engines when the model lowers to one (same fp32 semantics, no library GEMMs)."""
+    from ..engine import native_logits
     model.eval()
     cum = torch.zeros(3, dtype=torch.float64, device=device)  # loss*n, correct, n
     world, rank = pdist.get_world_size(), pdist.get_rank()
     for data, target in prefetch_to_device(_batches(test_loader, rank, world, shard), device):
-        output = model(data)
+        output = native_logits(model, data) if native else None
+        if output is None:
+            output = model(data)
         cum[0] += loss(output, target).double() * len(target)
         cum[1] += (output.argmax(1) == target.view(-1)).sum()
         cum[2] += len(target)
