@@ -43,6 +43,10 @@ hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
                         int tay_mode, hipStream_t st);
+hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, const float* neg_one, const float* Y0, int M, int Kc,
+                                int N, int B0, int relu, float slope, int cfg, float* out, hipStream_t st);
+hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* perm, int B, int C, int N, int p0,
+                                  int cnt, int Kc, float* T, float* Wsub, hipStream_t st);
 }
 
 namespace {
@@ -185,6 +189,46 @@ at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor
   TP_CHECK_HIP(tp_conv_first_direct(x.data_ptr<float>(), w.data_ptr<float>(), scale.data_ptr<float>(),
                                     shift.data_ptr<float>(), out.data_ptr<float>(), (int)B, (int)Cin, (int)H, (int)W,
                                     (int)Cout, relu ? 1 : 0, cur_stream()));
+  return out;
+}
+
+// Shapley prefix-delta operands: z (B, C) block output, W (N, C) next Linear, perm (n) int32
+// permutation; returns T (cnt*B, Kc) lower-triangular gathered activations and Wsub (N, Kc).
+std::tuple<at::Tensor, at::Tensor> prefix_tri_operands(const at::Tensor& z, const at::Tensor& w, const at::Tensor& perm,
+                                                       int64_t p0, int64_t cnt, int64_t Kc) {
+  need(z, "z", 2);
+  need(w, "w", 2);
+  TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.is_contiguous() && perm.dim() == 1,
+              "perm must be a contiguous int32 GPU vector");
+  const int64_t B = z.size(0), C = z.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == C, "w must be (N, C) with z's C");
+  TORCH_CHECK(cnt >= 1 && Kc >= cnt && Kc % 32 == 0, "need 1 <= cnt <= Kc, Kc % 32 == 0");
+  TORCH_CHECK(p0 >= 0 && p0 + cnt <= perm.numel() && perm.numel() <= C, "prefix range out of the permutation");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(z.device());
+  auto T = at::empty({cnt * B, Kc}, z.options());
+  auto Ws = at::empty({N, Kc}, z.options());
+  TP_CHECK_HIP(tp_prefix_tri_operands(z.data_ptr<float>(), w.data_ptr<float>(), perm.data_ptr<int>(), (int)B, (int)C,
+                                      (int)N, (int)p0, (int)cnt, (int)Kc, T.data_ptr<float>(), Ws.data_ptr<float>(),
+                                      cur_stream()));
+  return {T, Ws};
+}
+
+// out (M, N) = act(Y0[r % B0] - T @ Wsub^T) on the MFMA GEMM (prefix-delta Shapley evaluation).
+at::Tensor prefix_delta(const at::Tensor& T, const at::Tensor& wsub, const at::Tensor& neg_one, const at::Tensor& y0,
+                        bool relu, double slope, int64_t cfg) {
+  need(T, "T", 2);
+  need(wsub, "wsub", 2);
+  need(y0, "y0", 2);
+  const int64_t M = T.size(0), Kc = T.size(1), N = wsub.size(0), B0 = y0.size(0);
+  TORCH_CHECK(wsub.size(1) == Kc && y0.size(1) == N, "shape mismatch: T (M, Kc), wsub (N, Kc), y0 (B0, N)");
+  TORCH_CHECK(Kc % 32 == 0 && N % 4 == 0 && M % B0 == 0, "need Kc % 32 == 0, N % 4 == 0, M % B0 == 0");
+  TORCH_CHECK(cfg >= 0 && cfg <= 6, "bad tile config");
+  const float* no = opt_ptr(neg_one, N, "neg_one");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(T.device());
+  auto out = at::empty({M, N}, T.options());
+  TP_CHECK_HIP(tp_prefix_delta_gemm(T.data_ptr<float>(), wsub.data_ptr<float>(), no, y0.data_ptr<float>(), (int)M,
+                                    (int)Kc, (int)N, (int)B0, relu ? 1 : 0, (float)slope, (int)cfg,
+                                    out.data_ptr<float>(), cur_stream()));
   return out;
 }
 
@@ -552,6 +596,8 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
         "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0, float slope=0.0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
+  m.def("prefix_tri_operands(Tensor z, Tensor w, Tensor perm, int p0, int cnt, int Kc) -> (Tensor, Tensor)");
+  m.def("prefix_delta(Tensor T, Tensor wsub, Tensor neg_one, Tensor y0, bool relu, float slope, int cfg) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
         "bool staged=True, Tensor(a!)? apoz=None) -> (Tensor, Tensor)");
   m.def("conv_wino_dgrad(Tensor g, Tensor? g_argmax, Tensor ut, Tensor act, Tensor? bn_scale, "
@@ -562,6 +608,8 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_fwd", &conv_fwd);
   m.impl("conv_dgrad", &conv_dgrad);
   m.impl("conv_first", &conv_first);
+  m.impl("prefix_tri_operands", &prefix_tri_operands);
+  m.impl("prefix_delta", &prefix_delta);
   m.impl("conv_wino_fwd", &conv_wino_fwd);
   m.impl("nchw_to_nhwc_pad", &nchw_to_nhwc_pad);
   m.impl("maxpool2_nhwc", &maxpool2_nhwc);

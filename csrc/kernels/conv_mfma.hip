@@ -66,6 +66,8 @@ struct ConvArgs {
   int parity;               // GEN 3: rows ordered (oh%2, ow%2, b, oh/2, ow/2) so a tile sees few taps
   float slope;              // activation: 0 = ReLU, > 0 = LeakyReLU negative slope (fwd relu flag /
                             // EPI_BWD mask of the consumer activation)
+  int res_rows;             // > 0: residual row = output row % res_rows (one (res_rows, N) residual
+                            // broadcast over row blocks: Shapley prefix-delta GEMM)
 };
 
 // GEN 3 output row m -> (image, oh, ow). Parity order makes each stride-2 phase class one
@@ -139,6 +141,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // Residual quad at output pixel ``pix`` (linear NHWC pixel index), columns n..n+3; res_stride
 // > 1 reads a strided-conv gradient that lives at the even-phase pixels only.
 __device__ __forceinline__ float4 res_quad(const ConvArgs& p, long long pix, int n) {
+  if (p.res_rows > 0) pix %= p.res_rows;
   if (p.res_stride <= 1) return *reinterpret_cast<const float4*>(p.res + pix * p.N + n);
   const int s = p.res_stride;
   const long long HW = (long long)p.Ho * p.Wo;
@@ -603,7 +606,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
             float v = acc[i][j][r];
             if constexpr (EPI == EPI_FWD) {
               v = v * sc + sh;
-              if (p.res) v += p.res[(long long)m * p.N + n];
+              if (p.res) v += p.res[(long long)(p.res_rows > 0 ? m % p.res_rows : m) * p.N + n];
               if (p.relu) v = nan_act(v, p.slope);
               p.out[(long long)m * p.N + n] = v;
               if (p.apoz) {  // counts are exact integers: atomics are order-independent here
@@ -723,7 +726,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         float v = 0.f;
         for (int q = 0; q < splits; ++q) v += slabs[(size_t)q * total + o];
         v = v * (p.scale ? p.scale[n] : 1.f) + (p.shift ? p.shift[n] : 0.f);
-        if (p.res) v += p.res[o];
+        if (p.res) v += p.res[p.res_rows > 0 ? (long long)(o / N % (unsigned)p.res_rows) * N + n : (long long)o];
         if (p.mask && !(p.mask[o] > 0.f)) v = 0.f;
         if (p.relu) v = nan_act(v, p.slope);
         p.out[o] = v;
@@ -1119,6 +1122,41 @@ extern "C" hipError_t tp_conv_gen(const float* x, const float* w, int B, int H, 
                                   int relu, const float* res, float* apoz, float* out, float* ws, hipStream_t st) {
   return tp_conv_gen2(x, w, B, H, W, Cin, Cout, ks, stride, pad, 0, 0, 0, cfg, splits, scale, shift, relu, res, 1,
                       nullptr, apoz, out, ws, st);
+}
+
+// Shapley prefix-delta GEMM (see prefix_tri_operands in shapley.hip):
+//   out[r, n] = act(Y0[r % B0, n] - (T @ Wsub^T)[r, n]),  T (M, Kc), Wsub (N, Kc), Y0 (B0, N)
+// on the GEN 1x1 kernel: scale = -1 (a device vector), residual Y0 broadcast by res_rows = B0,
+// ReLU / LeakyReLU (slope) in the epilogue.
+extern "C" hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, const float* neg_one, const float* Y0,
+                                           int M, int Kc, int N, int B0, int relu, float slope, int cfg,
+                                           float* out, hipStream_t st) {
+  using namespace tp;
+  if (Kc % 32 != 0 || N % 4 != 0 || B0 <= 0 || M % B0 != 0 || !(slope >= 0.f)) return hipErrorInvalidValue;
+  ConvArgs a{};
+  a.x = T;
+  a.w = Wsub;
+  a.B = M;
+  a.H = a.W = a.Ho = a.Wo = 1;
+  a.HWo = 1;
+  a.Cin = Kc;
+  a.N = N;
+  a.K = Kc;
+  a.M = M;
+  a.stride = 1;
+  a.pad = 0;
+  a.x_elems = (long long)M * Kc;
+  if (a.x_elems * 4 >= (1ll << 31) || (long long)M * N * 4 >= (1ll << 31)) return hipErrorInvalidValue;
+  a.k_tiles_per_split = Kc / 32;
+  a.scale = neg_one;
+  a.relu = relu;
+  a.slope = slope;
+  a.res = Y0;
+  a.res_stride = 1;
+  a.res_rows = B0;
+  a.out = out;
+  a.epi_lds = 1;
+  return gen_dispatch<EPI_FWD>(1, 1, cfg, a, 1, st);
 }
 
 // Full entry: ``transposed`` = data gradient of a strided conv (GEN 3) producing Ho_t x Wo_t

@@ -51,6 +51,33 @@ __global__ __launch_bounds__(256) void prefix_mask1(const float* __restrict__ z,
   }
 }
 
+// Prefix-delta operands (exact alternative to materialising K masked copies when the next layer
+// is a Linear): for prefixes p0 .. p0+cnt-1 of permutation `perm`, copy j differs from the base
+// prefix p0 by the units perm[p0], .., perm[p0+j-1] being zeroed as well, so its next-layer
+// pre-activation is  Y0 - sum_{i<j} z[:, perm[p0+i]] W[:, perm[p0+i]]  = Y0 - (T @ Wsub^T)[j]:
+//   T[(j*B + b)*Kc + i] = (i < j) ? z[b*C + perm[p0+i]] : 0     (cnt*B rows, Kc >= cnt columns)
+//   Wsub[n*Kc + i]      = (i < cnt) ? W[n*C + perm[p0+i]] : 0   (N rows)
+// The K x (C-wide) GEMM of the masked copies becomes one (B x C) GEMM + one K x (Kc-wide) GEMM.
+__global__ __launch_bounds__(256) void prefix_tri_operands(const float* __restrict__ z, const float* __restrict__ W,
+                                                           const int* __restrict__ perm, int B, int C, int N,
+                                                           int p0, int cnt, int Kc, float* __restrict__ T,
+                                                           float* __restrict__ Wsub) {
+  const long long nt = (long long)cnt * B * Kc, nw = (long long)N * Kc;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < nt + nw;
+       t += (long long)gridDim.x * blockDim.x) {
+    if (t < nt) {
+      const int i = (int)(t % Kc);
+      const long long r = t / Kc;
+      const int b = (int)(r % B), j = (int)(r / B);
+      T[t] = i < j ? z[(long long)b * C + perm[p0 + i]] : 0.f;
+    } else {
+      const long long u = t - nt;
+      const int i = (int)(u % Kc), n = (int)(u / Kc);
+      Wsub[u] = i < cnt ? W[(long long)n * C + perm[p0 + i]] : 0.f;
+    }
+  }
+}
+
 // Per-sample form: sv[(row0+b)*n + perm[k0+k]] += (L[k+1][b] - L[k][b]) * scale.
 __global__ void shapley_scatter(const float* __restrict__ L, const int* __restrict__ perm,
                                 double* __restrict__ sv, int row0, int B, int n, int k0, int K,
@@ -143,5 +170,14 @@ extern "C" hipError_t tp_cross_entropy(const float* logits, const int64_t* targe
   if (B == 0) return hipSuccess;
   tp::cross_entropy_fb<<<tp::ceil_div((long long)B * 64, 256), 256, 0, st>>>(logits, target, loss, grad, B, NC,
                                                                             gscale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* perm, int B, int C, int N,
+                                             int p0, int cnt, int Kc, float* T, float* Wsub, hipStream_t st) {
+  if (cnt <= 0 || cnt > Kc || B <= 0 || N <= 0) return hipErrorInvalidValue;
+  const long long total = (long long)cnt * B * Kc + (long long)N * Kc;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 8192);
+  tp::prefix_tri_operands<<<grid, 256, 0, st>>>(z, W, perm, B, C, N, p0, cnt, Kc, T, Wsub);
   return hipGetLastError();
 }

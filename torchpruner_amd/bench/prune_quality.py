@@ -93,6 +93,7 @@ def make_teacher(seed, device, cfg):
                          modes_per_class=cfg["modes"])
     torch.cuda.manual_seed(seed)  # dropout masks
     sgd_steps(model, task, cfg["teacher_steps"], seed, cfg["lr"], cfg["batch"], schedule=True)
+    model.eval()
     model.zero_grad(set_to_none=True)
     return model, task
 
