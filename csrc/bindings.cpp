@@ -255,6 +255,35 @@ std::tuple<at::Tensor, at::Tensor> cross_entropy(const at::Tensor& logits_, cons
   return {loss, grad};
 }
 
+// Batch of a device-resident uint8 dataset: gather rows ``idx`` of src (N, C, H, W), optional
+// per-image (dy, dx, flip) augmentation ``aug`` (B, 3) int32 with zero padding ``pad``, then
+// ToTensor + Normalize -> fp32 (B, C, H, W).
+at::Tensor augment_u8(const at::Tensor& src, const at::Tensor& idx, const c10::optional<at::Tensor>& aug, int64_t pad,
+                      const at::Tensor& mean, const at::Tensor& inv_std) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.dim() == 4 && src.is_contiguous(),
+              "src must be a contiguous uint8 (N, C, H, W) GPU tensor");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(),
+              "idx must be a contiguous int64 GPU vector");
+  const int64_t B = idx.size(0), C = src.size(1), H = src.size(2), W = src.size(3);
+  const int* ap = nullptr;
+  if (aug.has_value() && aug->defined()) {
+    TORCH_CHECK(aug->is_cuda() && aug->scalar_type() == at::kInt && aug->is_contiguous() && aug->numel() == 3 * B,
+                "aug must be a contiguous int32 (B, 3) GPU tensor");
+    ap = aug->data_ptr<int>();
+  }
+  check_cuda_f32(mean, "mean");
+  check_cuda_f32(inv_std, "inv_std");
+  TORCH_CHECK(mean.numel() == C && inv_std.numel() == C && mean.is_contiguous() && inv_std.is_contiguous(),
+              "mean / inv_std must have C elements");
+  TORCH_CHECK(pad >= 0, "pad must be >= 0");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  auto out = at::empty({B, C, H, W}, src.options().dtype(at::kFloat));
+  TP_CHECK_HIP(tp_augment_u8(src.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(), ap, (int)B, (int)C, (int)H, (int)W,
+                             (int)pad, mean.data_ptr<float>(), inv_std.data_ptr<float>(), out.data_ptr<float>(),
+                             cur_stream()));
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tpamd, m) {
@@ -268,6 +297,7 @@ TORCH_LIBRARY(tpamd, m) {
   m.def("shapley_scatter(Tensor L, Tensor perm, Tensor(a!) sv, int row0, int k0, float scale) -> ()");
   m.def("shapley_column(Tensor L, Tensor perm, Tensor(a!) sv_col, int k0, float scale) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor target, float gscale, bool want_grad) -> (Tensor, Tensor)");
+  m.def("augment_u8(Tensor src, Tensor idx, Tensor? aug, int pad, Tensor mean, Tensor inv_std) -> Tensor");
   register_engine_ops_def(m);
 }
 
@@ -282,5 +312,6 @@ TORCH_LIBRARY_IMPL(tpamd, CUDA, m) {
   m.impl("shapley_scatter", &shapley_scatter);
   m.impl("shapley_column", &shapley_column);
   m.impl("cross_entropy", &cross_entropy);
+  m.impl("augment_u8", &augment_u8);
   register_engine_ops_impl(m);
 }

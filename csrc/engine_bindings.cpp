@@ -203,7 +203,8 @@ std::tuple<at::Tensor, at::Tensor> prefix_tri_operands(const at::Tensor& z, cons
   const int64_t B = z.size(0), C = z.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == C, "w must be (N, C) with z's C");
   TORCH_CHECK(cnt >= 1 && Kc >= cnt && Kc % 32 == 0, "need 1 <= cnt <= Kc, Kc % 32 == 0");
-  TORCH_CHECK(p0 >= 0 && p0 + cnt <= perm.numel() && perm.numel() <= C, "prefix range out of the permutation");
+  // prefixes p0 .. p0+cnt-1 read perm[p0 .. p0+cnt-2] (the last copy's extra units)
+  TORCH_CHECK(p0 >= 0 && p0 + cnt - 1 <= perm.numel() && perm.numel() <= C, "prefix range out of the permutation");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(z.device());
   auto T = at::empty({cnt * B, Kc}, z.options());
   auto Ws = at::empty({N, Kc}, z.options());

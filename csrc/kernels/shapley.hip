@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void prefix_mask1(const float* __restrict__ z,
 // prefix p0 by the units perm[p0], .., perm[p0+j-1] being zeroed as well, so its next-layer
 // pre-activation is  Y0 - sum_{i<j} z[:, perm[p0+i]] W[:, perm[p0+i]]  = Y0 - (T @ Wsub^T)[j]:
 //   T[(j*B + b)*Kc + i] = (i < j) ? z[b*C + perm[p0+i]] : 0     (cnt*B rows, Kc >= cnt columns)
-//   Wsub[n*Kc + i]      = (i < cnt) ? W[n*C + perm[p0+i]] : 0   (N rows)
+//   Wsub[n*Kc + i]      = (i < cnt - 1) ? W[n*C + perm[p0+i]] : 0   (N rows)
 // The K x (C-wide) GEMM of the masked copies becomes one (B x C) GEMM + one K x (Kc-wide) GEMM.
 __global__ __launch_bounds__(256) void prefix_tri_operands(const float* __restrict__ z, const float* __restrict__ W,
                                                            const int* __restrict__ perm, int B, int C, int N,
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void prefix_tri_operands(const float* __restri
     } else {
       const long long u = t - nt;
       const int i = (int)(u % Kc), n = (int)(u / Kc);
-      Wsub[u] = i < cnt ? W[(long long)n * C + perm[p0 + i]] : 0.f;
+      Wsub[u] = i < cnt - 1 ? W[(long long)n * C + perm[p0 + i]] : 0.f;  // column cnt-1 of T is 0
     }
   }
 }

@@ -115,3 +115,43 @@ def test_mlp_engine_logits_and_nan_propagation(cuda):
         h, _ = eng.forward(x, stop_after=0)
     h = h.reshape(16, -1)[:, :model.fc[1].out_features]
     assert torch.isnan(h[3]).all() and not torch.isnan(h[[0, 1, 2, 4]]).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["mlp_hidden", "mlp_last", "vgg_conv12", "vgg_fc1"])
+def test_shapley_prefix_delta_matches_masked_copies(cuda, where):
+    """The prefix-delta GEMM (no masked copies) equals the masked-copy evaluation and the fp64
+    generic path up to fp32 rounding, for every Linear-fed evaluation point."""
+    from torchpruner_amd import ShapleyAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models import prunable_vgg16
+    g = torch.Generator().manual_seed(7)
+    if where.startswith("mlp"):
+        model = _fcnet(odd=True).to(cuda)
+        x = torch.randn(20, 784, generator=g)
+        module = model.fc[1] if where == "mlp_hidden" else model.fc[3]
+    else:
+        torch.manual_seed(2)
+        model = prunable_vgg16().to(cuda).eval()
+        x = torch.randn(12, 3, 32, 32, generator=g)
+        module = model.features[40] if where == "vgg_conv12" else model.classifier[1]
+    y = torch.randint(0, 10, (x.shape[0],), generator=g)
+    res = {}
+    for mode, backend, dev in (("delta", "hip", cuda), ("copies", "hip", cuda), ("fp64", "torch", "cpu")):
+        mdl = model if mode != "fp64" else copy.deepcopy(model).double().cpu()
+        mod = module if mode != "fp64" else dict(mdl.named_modules())[
+            {id(m): n for n, m in model.named_modules()}[id(module)]]
+        xx = x.to(dev).double() if mode == "fp64" else x.to(dev)
+        os.environ["TORCHPRUNER_BACKEND"] = backend
+        os.environ["TORCHPRUNER_PREFIX_DELTA"] = "1" if mode == "delta" else "0"
+        try:
+            np.random.seed(3)
+            m = ShapleyAttributionMetric(mdl, DeviceLoader(xx, y.to(dev), 5), F.cross_entropy, dev, sv_samples=2,
+                                         prefix_batch=7)
+            res[mode] = m.run(mod, find_best_evaluation_module=True)
+        finally:
+            del os.environ["TORCHPRUNER_BACKEND"], os.environ["TORCHPRUNER_PREFIX_DELTA"]
+    err_delta = np.abs(res["delta"] - res["fp64"]).max()
+    err_copies = np.abs(res["copies"] - res["fp64"]).max()
+    assert res["delta"].shape == res["fp64"].shape
+    assert err_delta <= 3 * err_copies + 2e-6, (err_delta, err_copies)

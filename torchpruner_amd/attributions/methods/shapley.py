@@ -219,6 +219,16 @@ class ShapleyAttributionMetric(_AttributionMetric):
 
         n = engine.real_width(k)
         pad_rank = _RankPadder(n)
+        delta = engine.prefix_delta_ok(k)
+        perms = {}
+
+        def perm_of(rank_t):  # permutation from its rank vector (cached per rank vector)
+            hit = perms.get(id(rank_t))
+            if hit is None or hit[0] is not rank_t:
+                p = torch.empty_like(rank_t)
+                p[rank_t.long()] = torch.arange(rank_t.numel(), dtype=rank_t.dtype, device=rank_t.device)
+                hit = perms[id(rank_t)] = (rank_t, p)
+            return hit[1]
 
         def prepare(x, y):
             zk, _ = engine.forward(x, stop_after=k)  # engine layout (B, H, W, C padded)
@@ -227,6 +237,9 @@ class ShapleyAttributionMetric(_AttributionMetric):
             base = engine.loss_from(k, zk, y)
 
             def evaluate(rank_t, p_first, cnt):
+                if delta:  # next block is a Linear: prefix-delta GEMM (no masked copies)
+                    return engine.prefix_delta_loss(k, zk, perm_of(rank_t), pad_rank(rank_t, zk.shape[3]), p_first,
+                                                    cnt, y)
                 masked = ops.prefix_mask(z_cl, pad_rank(rank_t, zk.shape[3]), p_first, cnt)  # channels_last
                 loss = engine.loss_from(k, masked.permute(0, 2, 3, 1), y.repeat(cnt))
                 return loss.view(cnt, B)

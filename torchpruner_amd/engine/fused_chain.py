@@ -560,6 +560,64 @@ class FusedChainEngine:
             h = self._linear(T, P["lins"][li], h)
         return h.reshape(B, -1)
 
+    # ------------------------------------------------------------------ Shapley prefix deltas
+    def prefix_delta_ok(self, k: int) -> bool:
+        """Whether prefixes masked at block ``k``'s output can be evaluated by the prefix-delta GEMM:
+        the next block is a Linear fed by that output (classifier blocks, or the last conv block
+        at 1x1 resolution)."""
+        nconv = len(self.plan.convs)
+        return nconv - 1 <= k < len(self.plan.blocks) - 1 and os.environ.get("TORCHPRUNER_PREFIX_DELTA", "1") != "0"
+
+    def _lin4(self, j):
+        """Linear j's packed operands with rows padded to a multiple of 4 (the GEN epilogue's
+        float4 columns) and the -1 scale vector of the delta GEMM; cached in the packed entry."""
+        e = self._pack()["lins"][j]
+        if "w4" not in e:
+            n = e["w"].shape[0]
+            n4 = -(-n // 4) * 4
+            e["w4"] = F.pad(e["w"], (0, 0, 0, n4 - n)).contiguous()
+            e["b4"] = F.pad(e["bias"], (0, n4 - n)).contiguous()
+            e["neg1"] = torch.full((n4,), -1.0, device=e["w"].device)
+        return e
+
+    def prefix_delta_loss(self, k: int, zk: torch.Tensor, perm_t: torch.Tensor, rank_t: torch.Tensor, p0: int,
+                          cnt: int, y: torch.Tensor) -> torch.Tensor:
+        """Per-sample losses (cnt, B) of prefixes p0 .. p0+cnt-1 (units of rank < p0+j zeroed in
+        copy j) of block ``k``'s output ``zk``, without materialising the cnt masked copies:
+
+          Y_{p0+j} = Y_{p0} - sum_{i<j} z[:, perm[p0+i]] W[:, perm[p0+i]]^T
+                   = Y_{p0} - (T @ Wsub^T)[j]        (T lower-triangular, cnt x Kc per sample)
+
+        Y_{p0} is one (B x C) GEMM of the base-masked input; the deltas are one (cnt*B x Kc) GEMM
+        whose epilogue subtracts from the broadcast Y_{p0} and applies the next block's
+        activation — cnt*Kc/C of the FLOPs of the masked-copy GEMM, and no (cnt*B x C) copies.
+        ``rank_t`` covers the padded width (padding ranks after every real unit)."""
+        T = ops.require()
+        nconv = len(self.plan.convs)
+        j = k + 1 - nconv
+        e = self._lin4(j)
+        B = zk.shape[0]
+        z2 = zk.reshape(B, -1)
+        N4, C = e["w4"].shape
+        zm = T.prefix_mask(z2.reshape(B, C, 1, 1), rank_t, int(p0), 1).view(B, 1, 1, C)
+        cfg, sp = TUNER.choose(("pd0", B, C, N4), B, N4, C,
+                               lambda c, s_: T.conv_fwd(zm, e["w4"], None, e["b4"], False, False, 1, c, s_))
+        y0 = T.conv_fwd(zm, e["w4"], None, e["b4"], False, False, 1, cfg, sp)[0].view(B, N4)
+        kc = cpad(cnt)
+        tri, wsub = T.prefix_tri_operands(z2, e["w4"], perm_t, int(p0), int(cnt), kc)
+        cfg2, _ = TUNER.choose(("pd1", cnt * B, kc, N4), cnt * B, N4, kc,
+                               lambda c, s_: T.prefix_delta(tri, wsub, e["neg1"], y0, e["relu"], e["slope"], c),
+                               cands=[(c, 1) for c in (0, 3, 1, 4, 5, 6, 2)])
+        out = T.prefix_delta(tri, wsub, e["neg1"], y0, e["relu"], e["slope"], cfg2)  # (cnt*B, N4)
+        yy = y.repeat(cnt)
+        if j == len(self.plan.linears) - 1:  # the delta GEMM produced the logits
+            n = self.plan.linears[-1].linear.out_features
+            logits = out if n == N4 else out[:, :n].contiguous()
+            loss, _ = ops.cross_entropy(logits, yy, 1.0, False)
+        else:
+            loss = self.loss_from(k + 1, out.view(cnt * B, 1, 1, N4), yy)
+        return loss.view(cnt, B)
+
     def loss_from(self, k: int, h: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         """Per-sample cross-entropy of the network continued from block ``k``'s output."""
         loss, _ = ops.cross_entropy(self.forward_from(k, h), y, 1.0, False)
