@@ -343,8 +343,8 @@ at::Tensor conv_gen(const at::Tensor& x, const at::Tensor& w, const c10::optiona
   need(x, "x", 4);
   need(w, "w", 2);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
-  TORCH_CHECK((Cin % 32 == 0 && (ks == 1 || ks == 3)) || (Cin == 4 && ks == 7),
-              "conv_gen supports ks 1/3 with Cin % 32 == 0, or ks 7 with a 4-channel input");
+  TORCH_CHECK((Cin % 32 == 0 && (ks == 1 || ks == 3 || ks == 5)) || (Cin == 4 && (ks == 3 || ks == 5 || ks == 7)),
+              "conv_gen supports ks 1/3/5 with Cin % 32 == 0, or ks 3/5/7 with a 4-channel input");
   TORCH_CHECK(w.size(1) == tp_conv_gen_k((int)ks, (int)Cin), "weight K mismatch");
   TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
   TORCH_CHECK(Cout % 4 == 0, "conv_gen needs Cout % 4 == 0");
@@ -451,7 +451,8 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
   need(g, "g", 4);
   need(wt, "wt", 2);
   const int64_t B = g.size(0), H = g.size(1), W = g.size(2), C = g.size(3), N = wt.size(0);
-  TORCH_CHECK(C % 32 == 0 && (ks == 1 || ks == 3), "conv_gen_bwd needs C % 32 == 0 and ks 1/3");
+  TORCH_CHECK(C % 32 == 0 && (ks == 1 || ks == 3 || (ks == 5 && !transposed)),
+              "conv_gen_bwd needs C % 32 == 0 and ks 1/3 (5 for stride-1 convs)");
   TORCH_CHECK(wt.size(1) == ks * ks * C, "wt must be (N, ks*ks*C)");
   TORCH_CHECK(N % 4 == 0 && res_stride >= 1 && stride >= 1 && pad >= 0, "bad N/stride/pad");
   if (!transposed) {

@@ -154,8 +154,9 @@ __device__ __forceinline__ float4 res_quad(const ConvArgs& p, long long pix, int
 }
 
 // GEN = 0: stride-1 "same" convs (VGG path, precomputed tap masks); GEN = 1: general strided /
-// padded conv (ResNet), Cin % 32 == 0; GEN = 2: the same with a 4-channel (padded NHWC) input,
-// where one 32-wide K slice holds 8 taps x 4 channels (7x7 stems); GEN = 3: transposed strided
+// padded conv (ResNet; 1x1 / 3x3 / 5x5), Cin % 32 == 0; GEN = 2: the same with a 4-channel
+// (padded NHWC) input, where one 32-wide K slice holds 8 taps x 4 channels (7x7 stems, tiny-Cin
+// 3x3 / 5x5 first layers); GEN = 3: transposed strided
 // conv = data gradient of a strided conv. x is dL/dy (B, H, W, Cin = forward Cout) and output
 // pixel (oh, ow) gathers y pixel ((oh + pad - kh) / s, (ow + pad - kw) / s) through tap (kh, kw)
 // when the division is exact; w[n = forward ci][k = (kh, kw, co)]. With parity row order a
@@ -1101,8 +1102,11 @@ hipError_t gen_dispatch(int ks, int gen, int cfg, const tp::ConvArgs& a, int spl
     if (gen == 3 && ks == 3) return gen_cfg<3, 3, EPI>(cfg, a, 1, st);
   }
   if (gen == 2 && ks == 7) return gen_cfg<7, 2, EPI>(cfg, a, splits, st);
+  if (gen == 2 && ks == 5) return gen_cfg<5, 2, EPI>(cfg, a, splits, st);
+  if (gen == 2 && ks == 3) return gen_cfg<3, 2, EPI>(cfg, a, splits, st);
   if (gen == 1 && ks == 1) return gen_cfg<1, 1, EPI>(cfg, a, splits, st);
   if (gen == 1 && ks == 3) return gen_cfg<3, 1, EPI>(cfg, a, splits, st);
+  if (gen == 1 && ks == 5) return gen_cfg<5, 1, EPI>(cfg, a, splits, st);
   return hipErrorInvalidValue;
 }
 }  // namespace

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void augment_u8(const uint8_t* __restrict__ sr
     r_ /= H;
     const int c = (int)(r_ % C);
     const int b = (int)(r_ / C);
-    int dy = 0, dx = 0, flip = 0;
+    int dy = pad, dx = pad, flip = 0;  // no augmentation: the centred (identity) crop
     if (aug) {
       dy = aug[3 * b];
       dx = aug[3 * b + 1];

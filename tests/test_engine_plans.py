@@ -40,7 +40,11 @@ def test_native_training_eligibility():
     assert eligible(nn.Conv2d(16, 32, 3, padding=1))
     assert eligible(nn.Conv2d(64, 128, 1, stride=2))
     assert eligible(nn.Conv2d(3, 64, 7, stride=2, padding=3))
-    assert not eligible(nn.Conv2d(16, 32, 5, padding=2))          # 5x5: library conv
+    assert eligible(nn.Conv2d(16, 32, 5, padding=2))              # 5x5 (FMNIST conv1)
+    assert eligible(nn.Conv2d(1, 32, 5, padding=2))               # tiny-Cin packed taps
+    assert eligible(nn.Conv2d(32, 64, 3, padding=2))              # FMNIST conv2: pad 2
+    assert not eligible(nn.Conv2d(16, 32, 5, stride=2, padding=2))  # no strided 5x5 dgrad
+    assert not eligible(nn.Conv2d(16, 32, 3, padding=3))          # pad > ks - 1
     assert not eligible(nn.Conv2d(16, 32, 3, groups=2))           # grouped
     assert not eligible(nn.Conv2d(16, 32, 3, dilation=2))         # dilated
     assert not eligible(nn.Conv2d(16, 32, (1, 3)))                # non-square

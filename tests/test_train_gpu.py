@@ -108,3 +108,57 @@ def test_bn_train_kernels_match_fp64(cuda, C, hw, B, affine):
     if affine:
         torch.testing.assert_close(bn.weight.grad.double(), ref.weight.grad, rtol=1e-4, atol=1e-3)
         torch.testing.assert_close(bn.bias.grad.double(), ref.bias.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("ks,pad,cin,cout,stride", [(5, 2, 1, 32, 1), (3, 2, 32, 64, 1), (5, 2, 40, 24, 1),
+                                                    (3, 1, 3, 64, 1), (3, 0, 36, 32, 1), (5, 1, 4, 8, 1),
+                                                    (3, 1, 3, 16, 2)])
+def test_native_conv_geometries(cuda, ks, pad, cin, cout, stride):
+    """5x5 convs, tiny-Cin (packed 4-channel taps) 3x3 / 5x5 first layers and stride-1 paddings
+    other than ks // 2 (FMNIST: conv5x5 p2 on 1 channel, conv3x3 p2; reference
+    experiments/models/fmnist.py:12-21): forward, input and weight gradients vs fp64 autograd."""
+    from torchpruner_amd.engine.train import eligible, native_convs
+    torch.manual_seed(ks * 10 + pad + cin)
+    conv = torch.nn.Conv2d(cin, cout, ks, stride=stride, padding=pad).to(cuda)
+    assert eligible(conv)
+    x = torch.randn(3, cin, 14, 13, device=cuda, requires_grad=True)
+    with native_convs(conv):
+        y = conv(x)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    c64 = copy.deepcopy(conv).double()
+    x64 = x.detach().double().requires_grad_(True)
+    y64 = c64(x64)
+    (y64 * g.double()).sum().backward()
+    torch.testing.assert_close(y.double(), y64, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(conv.weight.grad.double(), c64.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(conv.bias.grad.double(), c64.bias.grad, rtol=1e-4, atol=1e-3)
+
+
+def test_fmnist_generic_attribution_on_native_convs(cuda):
+    """A model the fused engines do not lower (FMNIST conv net) runs the generic hook path with
+    its convolutions on the native kernels: Taylor / APoZ scores vs an fp64 CPU oracle."""
+    import os
+    from torchpruner_amd import APoZAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models import FMNISTConvNet
+    torch.manual_seed(0)
+    model = FMNISTConvNet().to(cuda).eval()
+    x = torch.randn(24, 1, 28, 28, device=cuda)
+    y = torch.randint(0, 10, (24,), device=cuda)
+    mods = [model.conv1, model.conv2, model.fc1]
+    m = TaylorAttributionMetric(model, DeviceLoader(x, y, 8), F.cross_entropy, cuda)
+    got = [m.run(mod) for mod in mods]
+    assert m.last_path["path"] == "generic" and m.last_path["native_convs"] == 2, m.last_path
+    m64 = copy.deepcopy(model).double().cpu()
+    os.environ["TORCHPRUNER_BACKEND"] = "torch"
+    try:
+        ref = [TaylorAttributionMetric(m64, DeviceLoader(x.double().cpu(), y.cpu(), 8), F.cross_entropy, "cpu").run(
+            mod) for mod in (m64.conv1, m64.conv2, m64.fc1)]
+    finally:
+        del os.environ["TORCHPRUNER_BACKEND"]
+    for a, e in zip(got, ref):
+        assert np.abs(a - e).max() / (np.abs(e).max() + 1e-30) < 1e-4
+    ap = APoZAttributionMetric(model, DeviceLoader(x, y, 8), F.cross_entropy, cuda).run(model.conv2)
+    assert ap.shape == (64,) and np.isfinite(ap).all()

@@ -179,7 +179,7 @@ class _AttributionMetric(ABC):
         self.set_deterministic()
         losses = []
         try:
-            with torch.no_grad():
+            with torch.no_grad(), self._native_ctx():
                 for _, x, y in self._batches():
                     with self._autocast():
                         out = self.model(x)
@@ -193,10 +193,10 @@ class _AttributionMetric(ABC):
         self.set_deterministic()
         try:
             for _, x, y in self._batches():
-                with self._autocast():
+                with self._autocast(), self._native_ctx():
                     out = self.model(x)
-                loss = self.criterion(out.float(), y)
-                loss.backward()
+                    loss = self.criterion(out.float(), y)
+                    loss.backward()
         finally:
             self.restore_deterministic()
 
@@ -205,7 +205,7 @@ class _AttributionMetric(ABC):
         self.set_deterministic()
         loss = None
         try:
-            with self._autocast():
+            with self._autocast(), self._native_ctx():
                 y = self.model.forward_partial(x, to_module=to_module, from_module=from_module)
             if y_true is not None and to_module is None:
                 loss = self.criterion(y.float(), y_true, reduction="none")
@@ -244,6 +244,15 @@ class _AttributionMetric(ABC):
         torch.backends.cudnn.benchmark = self.benchmark
 
     # ------------------------------------------------------------------ engine internals
+    def _native_ctx(self):
+        """Generic path on the native kernels: every eligible ``nn.Conv2d`` (and training-mode
+        BatchNorm) of the model runs the HIP implicit-GEMM kernels through autograd instead of
+        MIOpen (TORCHPRUNER_GENERIC_NATIVE=0 disables; reduced compute dtypes keep autocast)."""
+        from ..engine.train import native_convs
+        enable = (torch.device(self.device).type == "cuda" and not self._reduced_precision()
+                  and os.environ.get("TORCHPRUNER_GENERIC_NATIVE", "1") != "0" and ops.backend() != "torch")
+        return native_convs(self.model, enable=enable)
+
     def _record_path(self, path: str, eval_modules, why=()):
         """Remember and log (once per run, ``torchpruner`` logger) which path served it:
         ``fused`` (VGG-chain engine), ``resnet`` (ResNet engine) or ``generic`` (PyTorch
@@ -252,6 +261,10 @@ class _AttributionMetric(ABC):
         mods = [names.get(id(m), type(m).__name__) for m in eval_modules]
         reasons = [r for r in dict.fromkeys(why or ())]
         self.last_path = {"path": path, "modules": mods, "reasons": reasons}
+        if path.startswith("generic") and torch.device(self.device).type == "cuda":
+            from ..engine.train import eligible
+            self.last_path["native_convs"] = sum(eligible(m) for m in self.model.modules()) \
+                if os.environ.get("TORCHPRUNER_GENERIC_NATIVE", "1") != "0" and not self._reduced_precision() else 0
         msg = f"{type(self).__name__}: {path} path for {', '.join(mods)}"
         if reasons:
             msg += " (" + "; ".join(reasons) + ")"
@@ -381,7 +394,7 @@ class _AttributionMetric(ABC):
         handles = [m.register_forward_hook(make_hook(k, m)) for k, m in enumerate(eval_modules)]
         self.set_deterministic()
         try:
-            with self._frozen_params():
+            with self._frozen_params(), self._native_ctx():
                 for i, x, y in self._batches():
                     state["idx"] = i
                     state["leafed"] = False
@@ -482,7 +495,7 @@ class _AttributionMetric(ABC):
         handles = [m.register_forward_hook(make_hook(k)) for k, m in enumerate(eval_modules)]
         self.set_deterministic()
         try:
-            with torch.no_grad():
+            with torch.no_grad(), self._native_ctx():
                 for i, x, _y in self._batches():
                     state["idx"] = i
                     with self._autocast():

@@ -317,7 +317,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
                 self.set_deterministic()
                 try:
                     state["mode"] = "off"
-                    with self._autocast():
+                    with self._autocast(), self._native_ctx():
                         out = self.model(x)
                     base = self.criterion(out.float(), y, reduction="none")
                 finally:
@@ -331,7 +331,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
                     try:
                         yy = y.repeat((cnt,) + (1,) * (y.dim() - 1))
                         xx = x.repeat((cnt,) + (1,) * (x.dim() - 1)) if cnt > 1 else x
-                        with self._autocast():
+                        with self._autocast(), self._native_ctx():
                             out = self.model(xx)
                         loss = self.criterion(out.float(), yy, reduction="none")
                     finally:

@@ -1,4 +1,5 @@
-"""Native convolutions for training: the finetune half of prune -> finetune (BASELINE config #5).
+"""Native convolutions for training: the finetune half of prune -> finetune (BASELINE config #5),
+and the convolutions of the generic attribution path (any model with standard convs).
 
 The reference finetunes with cuDNN convolutions (experiments/utils/train.py:11-48). On ROCm the
 library path is MIOpen, which JIT-compiles and benchmarks kernels for every new convolution
@@ -48,16 +49,27 @@ def _geom(conv: nn.Conv2d):
 
 
 def eligible(conv: nn.Module) -> bool:
-    """Whether ``conv`` runs on the native training kernels (square 1x1 / 3x3 kernels, or the
-    7x7 stem on <= 4 input channels; groups 1, no dilation, zero padding)."""
+    """Whether ``conv`` runs on the native kernels: square 1x1 / 3x3 / 5x5 kernels (strided 5x5
+    excluded: no transposed 5x5 dgrad), any zero padding up to ks-1, or a 7x7 stem on <= 4 input
+    channels; groups 1, no dilation. Tiny-Cin (<= 4) 3x3 / 5x5 / 7x7 layers use the 4-channel
+    packed-tap kernel instead of padding the input to 32 channels."""
     if not isinstance(conv, nn.Conv2d) or conv.groups != 1 or conv.dilation != (1, 1):
         return False
     if conv.padding_mode != "zeros" or isinstance(conv.padding, str):
         return False
     k, s, p = conv.kernel_size, conv.stride, conv.padding
-    if k[0] != k[1] or s[0] != s[1] or p[0] != p[1]:
+    if k[0] != k[1] or s[0] != s[1] or p[0] != p[1] or p[0] > k[0] - 1:
         return False
-    return k[0] in (1, 3) or (k[0] == 7 and conv.in_channels <= 4)
+    if k[0] == 7:
+        return conv.in_channels <= 4
+    if k[0] == 5:
+        return s[0] == 1
+    return k[0] in (1, 3)
+
+
+def _cin_pad(ks: int, cin: int) -> int:
+    """Channel width the kernels see: 4 (packed taps) for tiny-Cin 3x3/5x5/7x7, else 32-granule."""
+    return 4 if (ks in (3, 5, 7) and cin <= 4) else cpad(cin)
 
 
 def _wgrad_splits(P, tiles):
@@ -74,7 +86,7 @@ class _NativeConv2d(torch.autograd.Function):
         T = ops.require()
         B, Cin, H, W = x.shape
         Cout = weight.shape[0]
-        cin_p = 4 if ks == 7 else cpad(Cin)
+        cin_p = _cin_pad(ks, Cin)
         cout_p = cpad(Cout)
         xh = x.permute(0, 2, 3, 1)
         if cin_p != Cin:
@@ -115,19 +127,20 @@ class _NativeConv2d(torch.autograd.Function):
         B, Ho, Wo = g.shape[0], g.shape[1], g.shape[2]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            if ks in (1, 3):
-                same = stride == 1 and pad == ks // 2
-                if same:
+            if ks != 7:
+                if stride == 1:  # dgrad = stride-1 conv of g with flipped taps, padding ks-1-pad
                     wt = wp.flip(2, 3).permute(1, 2, 3, 0).reshape(cin_p, -1).contiguous()
-                else:
+                    pad_b, transposed = ks - 1 - pad, False
+                else:  # strided 1x1 / 3x3: transposed gather kernel, natural tap order
                     wt = wp.permute(1, 2, 3, 0).reshape(cin_p, -1).contiguous()
+                    pad_b, transposed = pad, True
                 M, K = B * H * W, wt.shape[1]
 
                 def run(cfg, sp):
-                    return T.conv_gen_bwd(g, wt, None, 1, None, ks, 1 if same else stride, pad, H, W, not same,
-                                          cfg, sp)
+                    return T.conv_gen_bwd(g, wt, None, 1, None, ks, stride if transposed else 1, pad_b, H, W,
+                                          transposed, cfg, sp)
 
-                cands = TUNER.candidates(M, cin_p, K) if same else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
+                cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
                 cfg, sp = TUNER.choose(("tdgrad", tuple(g.shape), cin_p, ks, stride, pad), M, cin_p, K, run,
                                        cands=cands)
                 dxh = run(cfg, sp)[..., :Cin]
@@ -201,9 +214,21 @@ def _native_bn_forward(self, x):
     return _NativeBN2d.apply(x, self.weight, self.bias, rm, rv, self.eps, momentum if momentum is not None else 0.0)
 
 
+_MAX_BYTES = (1 << 31) - 1  # the kernels address operands through 32-bit buffer descriptors
+
+
+def _fits(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    ks, s, p = _geom(conv)
+    B, Cin, H, W = x.shape
+    Ho, Wo = (H + 2 * p - ks) // s + 1, (W + 2 * p - ks) // s + 1
+    cin_p, cout_p = _cin_pad(ks, Cin), cpad(conv.out_channels)
+    return B * H * W * cin_p * 4 <= _MAX_BYTES and B * Ho * Wo * cout_p * 4 <= _MAX_BYTES and Ho > 0 and Wo > 0
+
+
 def _native_forward(self, x):
-    if not x.is_cuda or x.dtype != torch.float32 or self.weight.dtype != torch.float32:
-        return type(self).forward(self, x)
+    if not x.is_cuda or x.dtype != torch.float32 or self.weight.dtype != torch.float32 or x.dim() != 4 \
+            or not _fits(self, x):
+        return type(self).forward(self, x)  # other dtypes / tensors beyond 2 GiB: the library path
     ks, s, p = _geom(self)
     return _NativeConv2d.apply(x, self.weight, self.bias, ks, s, p)
 
