@@ -284,6 +284,18 @@ at::Tensor augment_u8(const at::Tensor& src, const at::Tensor& idx, const c10::o
   return out;
 }
 
+// Inverted dropout with a counter-based Philox mask (forward and, with the same seed, backward).
+at::Tensor dropout(const at::Tensor& x_, int64_t seed, double p) {
+  check_cuda_f32(x_, "x");
+  auto x = x_.contiguous();
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty_like(x);
+  TP_CHECK_HIP(tp_dropout(x.data_ptr<float>(), y.data_ptr<float>(), x.numel(), (unsigned long long)seed, p,
+                          cur_stream()));
+  return y;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tpamd, m) {
@@ -298,6 +310,7 @@ TORCH_LIBRARY(tpamd, m) {
   m.def("shapley_column(Tensor L, Tensor perm, Tensor(a!) sv_col, int k0, float scale) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor target, float gscale, bool want_grad) -> (Tensor, Tensor)");
   m.def("augment_u8(Tensor src, Tensor idx, Tensor? aug, int pad, Tensor mean, Tensor inv_std) -> Tensor");
+  m.def("dropout(Tensor x, int seed, float p) -> Tensor");
   register_engine_ops_def(m);
 }
 
@@ -313,5 +326,6 @@ TORCH_LIBRARY_IMPL(tpamd, CUDA, m) {
   m.impl("shapley_column", &shapley_column);
   m.impl("cross_entropy", &cross_entropy);
   m.impl("augment_u8", &augment_u8);
+  m.impl("dropout", &dropout);
   register_engine_ops_impl(m);
 }

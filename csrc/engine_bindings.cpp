@@ -21,6 +21,12 @@ hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* 
 hipError_t tp_bn_bwd_train(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a, float* k1,
                            float* k2, double* ws, hipStream_t st);
+hipError_t tp_bn_fwd_train2(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
+                            float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
+                            float* b, double* ws, const float* res, int relu, hipStream_t st);
+hipError_t tp_bn_bwd_train2(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
+                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a, float* k1,
+                            float* k2, double* ws, const float* ym, float* dres, hipStream_t st);
 hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                          int ks, int stride, int pad, int Kpad, int cfg, int splits, hipStream_t st);
 hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
@@ -521,11 +527,14 @@ at::Tensor conv_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t ks, int6
 
 // Training-mode BatchNorm over the last dim of an NHWC activation x (..., C), C % 4 == 0.
 // Updates running_mean / running_var in place (momentum, unbiased variance) when given.
+// Training BN on (.., C) channels-last data; optional fused residual add and ReLU:
+// y = relu?(BN(x) + res?). Returns (y, mean, invstd).
 std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                                              const c10::optional<at::Tensor>& beta,
                                                              const c10::optional<at::Tensor>& running_mean,
                                                              const c10::optional<at::Tensor>& running_var, double eps,
-                                                             double momentum) {
+                                                             double momentum, const c10::optional<at::Tensor>& res,
+                                                             bool relu) {
   need(x, "x", -1);
   const int64_t C = x.size(-1), P = x.numel() / std::max<int64_t>(C, 1);
   TORCH_CHECK(C % 4 == 0 && P > 0, "bn_train_fwd needs C % 4 == 0 and a non-empty batch");
@@ -541,21 +550,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x,
     rm = running_mean->data_ptr<float>();
     rv = running_var->data_ptr<float>();
   }
+  const float* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    need(*res, "res", -1);
+    TORCH_CHECK(res->sizes() == x.sizes(), "res must have x's shape");
+    rp = res->data_ptr<float>();
+  }
   auto y = at::empty_like(x);
   auto stats = at::empty({4, C}, x.options());  // mean, invstd, a, b
   auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   float* sp = stats.data_ptr<float>();
-  TP_CHECK_HIP(tp_bn_fwd_train(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
-                               (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(),
-                               cur_stream()));
+  TP_CHECK_HIP(tp_bn_fwd_train2(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
+                                (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(), rp,
+                                relu ? 1 : 0, cur_stream()));
   return {y, stats[0], stats[1]};
 }
 
-// Backward of bn_train_fwd: (dx or undefined, dgamma, dbeta).
-std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(const at::Tensor& g, const at::Tensor& x,
-                                                             const c10::optional<at::Tensor>& gamma,
-                                                             const at::Tensor& mean, const at::Tensor& invstd,
-                                                             bool want_dx) {
+// Backward of bn_train_fwd: (dx or undefined, dgamma, dbeta, dres or undefined). ``ym``: the
+// forward output y when it was ReLU'd (the gradient is masked by y > 0 first); ``want_dres``:
+// also return that masked gradient (the residual branch's gradient).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
+    const at::Tensor& g, const at::Tensor& x, const c10::optional<at::Tensor>& gamma, const at::Tensor& mean,
+    const at::Tensor& invstd, bool want_dx, const c10::optional<at::Tensor>& ym, bool want_dres) {
   need(g, "g", -1);
   need(x, "x", -1);
   TORCH_CHECK(g.sizes() == x.sizes(), "g and x must have the same shape");
@@ -565,15 +581,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(const at::Tensor& g,
   const float* ga = opt_ptr(gamma, C, "gamma");
   const float* mp = opt_ptr(mean, C, "mean");
   const float* ip = opt_ptr(invstd, C, "invstd");
+  const float* yp = nullptr;
+  if (ym.has_value() && ym->defined()) {
+    need(*ym, "ym", -1);
+    TORCH_CHECK(ym->sizes() == x.sizes(), "ym must have x's shape");
+    yp = ym->data_ptr<float>();
+  }
   auto coef = at::empty({5, C}, x.options());  // dgamma, dbeta, a, k1, k2
   auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
-  at::Tensor dx;
+  at::Tensor dx, dres;
   if (want_dx) dx = at::empty_like(x);
+  if (want_dres) dres = at::empty_like(x);
   float* cp = coef.data_ptr<float>();
-  TP_CHECK_HIP(tp_bn_bwd_train(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
-                               (int)P, (int)C, ga, mp, ip, cp, cp + C, cp + 2 * C, cp + 3 * C, cp + 4 * C,
-                               ws.data_ptr<double>(), cur_stream()));
-  return {dx, coef[0], coef[1]};
+  TP_CHECK_HIP(tp_bn_bwd_train2(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
+                                (int)P, (int)C, ga, mp, ip, cp, cp + C, cp + 2 * C, cp + 3 * C, cp + 4 * C,
+                                ws.data_ptr<double>(), yp, want_dres ? dres.data_ptr<float>() : nullptr,
+                                cur_stream()));
+  return {dx, coef[0], coef[1], dres};
 }
 
 void register_engine_ops_def(torch::Library& m) {
@@ -586,9 +610,9 @@ void register_engine_ops_def(torch::Library& m) {
         "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
   m.def("bn_train_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float eps, float momentum) -> (Tensor, Tensor, Tensor)");
-  m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx) "
-        "-> (Tensor, Tensor, Tensor)");
+        "float eps, float momentum, Tensor? res=None, bool relu=False) -> (Tensor, Tensor, Tensor)");
+  m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx, Tensor? ym=None, "
+        "bool want_dres=False) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");

@@ -25,6 +25,8 @@ hipError_t tp_shapley_column(const float* L, const int* perm, double* sv_col, in
                              hipStream_t st);
 hipError_t tp_cross_entropy(const float* logits, const int64_t* target, float* loss, float* grad, int B, int NC,
                             float gscale, hipStream_t st);
+// train_ops.hip
+hipError_t tp_dropout(const float* x, float* y, long long n, unsigned long long seed, double p, hipStream_t st);
 // data_ops.hip
 hipError_t tp_augment_u8(const uint8_t* src, const int64_t* idx, const int* aug, int B, int C, int H, int W, int pad,
                          const float* mean, const float* inv_std, float* out, hipStream_t st);

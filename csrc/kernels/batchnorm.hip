@@ -18,10 +18,19 @@ namespace tp {
 constexpr int BN_T = 256, BN_CQ = 16, BN_RL = BN_T / BN_CQ;  // 16 column quads x 16 row lanes
 
 // MODE 0: (sum x, sum x^2); MODE 1: (sum g, sum g * (x - mean) * invstd)
+// ReLU backward through the block's output y (MODE 1, ym non-null): the gradient reaching the BN
+// is g where y > 0 and 0 elsewhere (NaN y -> 0, as the ATen threshold backward)
+__device__ __forceinline__ float4 relu_mask4(float4 d, const float* ym, size_t off) {
+  if (!ym) return d;
+  const float4 m = *reinterpret_cast<const float4*>(ym + off);
+  return make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f, m.w > 0.f ? d.w : 0.f);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, const float* __restrict__ g,
                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                   double* __restrict__ part, int P, int C, int rows_per_group) {
+                                                   double* __restrict__ part, int P, int C, int rows_per_group,
+                                                   const float* __restrict__ ym = nullptr) {
   __shared__ double red[2][BN_RL][BN_CQ * 4];
   const int cq = threadIdx.x % BN_CQ, rl = threadIdx.x / BN_CQ;
   const int c = (blockIdx.x * BN_CQ + cq) * 4;
@@ -41,7 +50,9 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         v[u] = *reinterpret_cast<const float4*>(x + (size_t)(r + u * BN_RL) * C + c);
-        if (MODE == 1) d[u] = *reinterpret_cast<const float4*>(g + (size_t)(r + u * BN_RL) * C + c);
+        if (MODE == 1)
+          d[u] = relu_mask4(*reinterpret_cast<const float4*>(g + (size_t)(r + u * BN_RL) * C + c), ym,
+                            (size_t)(r + u * BN_RL) * C + c);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -78,7 +89,7 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
         s1.z += v.z * v.z;
         s1.w += v.w * v.w;
       } else {
-        const float4 d = *reinterpret_cast<const float4*>(g + (size_t)r * C + c);
+        const float4 d = relu_mask4(*reinterpret_cast<const float4*>(g + (size_t)r * C + c), ym, (size_t)r * C + c);
         s0.x += d.x;
         s0.y += d.y;
         s0.z += d.z;
@@ -180,12 +191,15 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize(const double* __restrict_
   k1[c] = (float)(-ac * sg / P - (-ac * is * sgx / P) * mean[c]);
 }
 
-// out = x * a[c] + (BWD ? g-term : b[c]) — forward: y = x*a + b; backward: dx = g*a + k1 + k2*x
+// forward: y = act(x*a + b (+ res));  backward: dx = gm*a + k1 + k2*x with gm = g masked by the
+// ReLU output ym (when given), and dres = gm (the residual branch's gradient) when requested
 template <bool BWD>
 __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, const float* __restrict__ g,
                                                 const float* __restrict__ a, const float* __restrict__ b,
                                                 const float* __restrict__ k2, float* __restrict__ out, unsigned n4,
-                                                unsigned C4) {
+                                                unsigned C4, const float* __restrict__ res = nullptr, int relu = 0,
+                                                const float* __restrict__ ym = nullptr,
+                                                float* __restrict__ dres = nullptr) {
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += gridDim.x * blockDim.x) {
     const unsigned c = (t % C4) * 4;
     const float4 v = reinterpret_cast<const float4*>(x)[t];
@@ -193,7 +207,9 @@ __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, con
     const float4 bv = *reinterpret_cast<const float4*>(b + c);
     float4 o;
     if (BWD) {
-      const float4 d = reinterpret_cast<const float4*>(g)[t];
+      const float4 d = relu_mask4(reinterpret_cast<const float4*>(g)[t], ym, (size_t)t * 4);
+      if (dres) reinterpret_cast<float4*>(dres)[t] = d;
+      if (!out) continue;
       const float4 kv = *reinterpret_cast<const float4*>(k2 + c);
       o.x = d.x * av.x + bv.x + kv.x * v.x;
       o.y = d.y * av.y + bv.y + kv.y * v.y;
@@ -204,6 +220,19 @@ __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, con
       o.y = v.y * av.y + bv.y;
       o.z = v.z * av.z + bv.z;
       o.w = v.w * av.w + bv.w;
+      if (res) {
+        const float4 rv = reinterpret_cast<const float4*>(res)[t];
+        o.x += rv.x;
+        o.y += rv.y;
+        o.z += rv.z;
+        o.w += rv.w;
+      }
+      if (relu) {
+        o.x = nan_relu(o.x);
+        o.y = nan_relu(o.y);
+        o.z = nan_relu(o.z);
+        o.w = nan_relu(o.w);
+      }
     }
     reinterpret_cast<float4*>(out)[t] = o;
   }
@@ -220,9 +249,11 @@ inline int bn_groups(int P, int C) {
 // Workspace: ws holds 2 * groups * C doubles (groups = tp_bn_groups(P, C)).
 extern "C" int tp_bn_groups(int P, int C) { return tp::bn_groups(P, C); }
 
-extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
-                                      float eps, float momentum, float* run_mean, float* run_var, float* mean,
-                                      float* invstd, float* a, float* b, double* ws, hipStream_t st) {
+// Fused block tail: y = relu?(BN(x) + res?) (res: the residual branch, same shape as x).
+extern "C" hipError_t tp_bn_fwd_train2(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
+                                       float eps, float momentum, float* run_mean, float* run_var, float* mean,
+                                       float* invstd, float* a, float* b, double* ws, const float* res, int relu,
+                                       hipStream_t st) {
   using namespace tp;
   if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
   const int groups = bn_groups(P, C);
@@ -232,25 +263,41 @@ extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, co
   bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
                                                     mean, invstd, a, b);
   const unsigned n4 = (unsigned)((long long)P * C / 4);
-  bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(x, nullptr, a, b, nullptr, y,
-                                                                                          n4, (unsigned)(C / 4));
+  bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
+      x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
+                                      float eps, float momentum, float* run_mean, float* run_var, float* mean,
+                                      float* invstd, float* a, float* b, double* ws, hipStream_t st) {
+  return tp_bn_fwd_train2(x, y, P, C, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, a, b, ws, nullptr,
+                          0, st);
+}
+
+// Backward of the fused tail: ym = the block output y (ReLU mask; nullable), dres = gradient of
+// the residual input (nullable). dx nullable (dgamma / dbeta only).
+extern "C" hipError_t tp_bn_bwd_train2(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
+                                       const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
+                                       float* k1, float* k2, double* ws, const float* ym, float* dres,
+                                       hipStream_t st) {
+  using namespace tp;
+  if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int groups = bn_groups(P, C);
+  const int rpg = (P + groups - 1) / groups;
+  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
+  bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym);
+  bn_bwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
+  if (dx || dres) {
+    const unsigned n4 = (unsigned)((long long)P * C / 4);
+    bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
+        x, g, a, k1, k2, dx, n4, (unsigned)(C / 4), nullptr, 0, ym, dres);
+  }
   return hipGetLastError();
 }
 
 extern "C" hipError_t tp_bn_bwd_train(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
                                       const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
                                       float* k1, float* k2, double* ws, hipStream_t st) {
-  using namespace tp;
-  if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
-  const int groups = bn_groups(P, C);
-  const int rpg = (P + groups - 1) / groups;
-  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
-  bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg);
-  bn_bwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
-  if (dx) {
-    const unsigned n4 = (unsigned)((long long)P * C / 4);
-    bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(x, g, a, k1, k2, dx, n4,
-                                                                                         (unsigned)(C / 4));
-  }
-  return hipGetLastError();
+  return tp_bn_bwd_train2(g, x, dx, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2, ws, nullptr, nullptr, st);
 }

@@ -162,3 +162,59 @@ def test_fmnist_generic_attribution_on_native_convs(cuda):
         assert np.abs(a - e).max() / (np.abs(e).max() + 1e-30) < 1e-4
     ap = APoZAttributionMetric(model, DeviceLoader(x, y, 8), F.cross_entropy, cuda).run(model.conv2)
     assert ap.shape == (64,) and np.isfinite(ap).all()
+
+
+@pytest.mark.parametrize("relu,with_res", [(True, False), (True, True), (False, True), (False, False)])
+def test_fused_bn_act_matches_autograd(cuda, relu, with_res):
+    """relu?(BN_train(x) + res?) fused (one apply pass; backward masks by the saved output and
+    returns the residual gradient) vs PyTorch autograd in fp64: output, running statistics and
+    the gradients of x, gamma, beta, res."""
+    from torchpruner_amd.engine.train import bn_act
+    torch.manual_seed(3)
+    bn = torch.nn.BatchNorm2d(36).to(cuda).train()
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-0.3, 0.3)
+    bn64 = copy.deepcopy(bn).double()
+    x = torch.randn(4, 36, 9, 7, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    res = torch.randn(4, 36, 9, 7, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True) \
+        if with_res else None
+    y = bn_act(bn, x, res, relu)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    x64 = x.detach().double().requires_grad_(True)
+    r64 = res.detach().double().requires_grad_(True) if with_res else None
+    y64 = bn64(x64) + (r64 if with_res else 0)
+    if relu:
+        y64 = torch.relu(y64)
+    (y64 * g.double()).sum().backward()
+    torch.testing.assert_close(y.double(), y64, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_mean.double(), bn64.running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn.running_var.double(), bn64.running_var, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn.weight.grad.double(), bn64.weight.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.bias.grad.double(), bn64.bias.grad, rtol=1e-4, atol=1e-4)
+    if with_res:
+        torch.testing.assert_close(res.grad.double(), r64.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_native_dropout(cuda):
+    """Philox dropout: keep rate ~ 1-p, kept values scaled by 1/(1-p), backward uses the same mask,
+    reproducible under torch.manual_seed, NaN inputs stay NaN."""
+    from torchpruner_amd.engine.train import native_convs
+    drop = torch.nn.Dropout(0.3).train()
+    x = torch.randn(1000, 513, device=cuda, requires_grad=True)
+    with native_convs(drop):
+        torch.manual_seed(5)
+        y = drop(x)
+        torch.manual_seed(5)
+        y2 = drop(x)
+    assert torch.equal(y, y2)
+    kept = y != 0
+    rate = kept.float().mean().item()
+    assert abs(rate - 0.7) < 0.01
+    torch.testing.assert_close(y[kept], x[kept] / 0.7)
+    y.backward(torch.ones_like(y))
+    assert torch.equal(x.grad != 0, kept)
+    with native_convs(drop):
+        z = drop(torch.full((64,), float("nan"), device=cuda))
+    assert torch.isnan(z).all()

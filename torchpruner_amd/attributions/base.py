@@ -251,7 +251,7 @@ class _AttributionMetric(ABC):
         from ..engine.train import native_convs
         enable = (torch.device(self.device).type == "cuda" and not self._reduced_precision()
                   and os.environ.get("TORCHPRUNER_GENERIC_NATIVE", "1") != "0" and ops.backend() != "torch")
-        return native_convs(self.model, enable=enable)
+        return native_convs(self.model, enable=enable, fuse=False)  # hooks must see every module
 
     def _record_path(self, path: str, eval_modules, why=()):
         """Remember and log (once per run, ``torchpruner`` logger) which path served it:

@@ -13,7 +13,8 @@ convolutions of a model run on the precompiled gfx950 kernels instead, through a
   wgrad     pixel-split MFMA GEMM, deterministic split combine (``tpamd.conv_wgrad``, K3)
 
 Training-mode ``BatchNorm2d`` runs on deterministic NHWC batch-statistics / normalisation /
-backward kernels (K5, ``tpamd.bn_train_*``); activations, pooling and the loss stay PyTorch ops
+backward kernels (K5, ``tpamd.bn_train_*``), training-mode ``nn.Dropout`` on a counter-based
+Philox kernel (K7b, mask regenerated in the backward); activations, pooling and the loss stay PyTorch ops
 (autograd composes them), so any model works; only modules the kernels support are switched. Pruned (odd)
 channel counts are zero-padded to the kernels' granule inside the op and sliced off again:
 the parameters, their gradients and the optimizer state keep the module's real shapes.
@@ -191,9 +192,121 @@ class _NativeBN2d(torch.autograd.Function):
         T = ops.require()
         xh, w, mean, invstd = ctx.saved_tensors
         g = gy.permute(0, 2, 3, 1).contiguous()
-        dx, dgamma, dbeta = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd, ctx.needs_input_grad[0])
+        dx, dgamma, dbeta, _ = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
+                                              ctx.needs_input_grad[0])
         return (dx.permute(0, 3, 1, 2) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
                 dbeta if ctx.has_b else None, None, None, None, None)
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    """(B, H, W, C) contiguous view of a channels_last NCHW tensor (copies otherwise)."""
+    th = t.permute(0, 2, 3, 1)
+    return th if th.is_contiguous() else th.contiguous()
+
+
+class _NativeBNAct(torch.autograd.Function):
+    """Fused training-mode block tail ``relu?(BN(x) + res?)`` (BN statistics, normalisation,
+    residual add and ReLU in one apply pass). The backward masks the gradient by the saved output
+    (ReLU), returns it as the residual branch's gradient, and runs the BN backward on it: the
+    ATen ReLU / add / threshold-backward passes of the unfused block disappear."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu):
+        T = ops.require()
+        xh = _nhwc(x)
+        rh = _nhwc(res) if res is not None else None
+        w = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        y, mean, invstd = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
+                                         bool(relu))
+        ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd,
+                              y if relu else torch.empty(0, device=x.device))
+        ctx.has_w, ctx.has_b, ctx.relu, ctx.has_res = weight is not None, bias is not None, relu, res is not None
+        return _as_nchw(y)
+
+    @staticmethod
+    def backward(ctx, gy):
+        T = ops.require()
+        xh, w, mean, invstd, y = ctx.saved_tensors
+        g = _nhwc(gy)
+        want_res = ctx.has_res and ctx.needs_input_grad[7]
+        dx, dgamma, dbeta, dres = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
+                                                 ctx.needs_input_grad[0], y if ctx.relu else None, want_res)
+        return (_as_nchw(dx) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
+                dbeta if ctx.has_b else None, None, None, None, None, _as_nchw(dres) if want_res else None, None)
+
+
+def _bn_fusable(bn, x, res=None) -> bool:
+    return (isinstance(bn, nn.BatchNorm2d) and bn.training and x.is_cuda and x.dtype == torch.float32
+            and x.dim() == 4 and x.shape[1] % 4 == 0 and x.numel() > 0
+            and (bn.weight is None or bn.weight.dtype == torch.float32)
+            and (res is None or (res.shape == x.shape and res.dtype == x.dtype and res.is_cuda)))
+
+
+def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: bool = True) -> torch.Tensor:
+    """``relu?(bn(x) + res?)`` — fused on the native kernels in training mode, the module's own
+    ops otherwise (eval mode, unsupported inputs)."""
+    if not _bn_fusable(bn, x, res):
+        y = bn(x)
+        if res is not None:
+            y = y + res
+        return F.relu(y) if relu else y
+    momentum = bn.momentum
+    if bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+        if momentum is None:
+            momentum = 1.0 / float(bn.num_batches_tracked)
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    return _NativeBNAct.apply(x, bn.weight, bn.bias, rm, rv, bn.eps, momentum if momentum is not None else 0.0, res,
+                              relu)
+
+
+def _block_kind(m) -> str | None:
+    """torchvision-layout residual blocks whose training forward can use the fused tails."""
+    names = ("conv1", "bn1", "conv2", "bn2", "relu", "downsample")
+    if not all(hasattr(m, a) for a in names) or not isinstance(m.relu, nn.ReLU):
+        return None
+    if hasattr(m, "conv3"):
+        return "bottleneck" if isinstance(getattr(m, "bn3", None), nn.BatchNorm2d) else None
+    return "basic"
+
+
+def _native_block_forward(self, x):
+    """Bottleneck / BasicBlock training forward with fused BN(+residual)+ReLU tails."""
+    if not (self.training and x.is_cuda):
+        return type(self).forward(self, x)
+    identity = self.downsample(x) if self.downsample is not None else x
+    out = bn_act(self.bn1, self.conv1(x), relu=True)
+    if _block_kind(self) == "bottleneck":
+        out = bn_act(self.bn2, self.conv2(out), relu=True)
+        return bn_act(self.bn3, self.conv3(out), res=identity, relu=True)
+    return bn_act(self.bn2, self.conv2(out), res=identity, relu=True)
+
+
+def _native_sequential_forward(self, x):
+    """nn.Sequential training forward fusing every (BatchNorm2d, ReLU) pair (VGG features)."""
+    mods = list(self.children())
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.BatchNorm2d) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU) \
+                and _bn_fusable(m, x):
+            x = bn_act(m, x, relu=True)
+            i += 2
+            continue
+        x = m(x)
+        i += 1
+    return x
+
+
+def _native_resnet_forward(self, x):
+    """ResNet training forward with the stem's BN+ReLU fused (the blocks patch themselves)."""
+    if not (self.training and x.is_cuda):
+        return type(self).forward(self, x)
+    x = self.maxpool(bn_act(self.bn1, self.conv1(x), relu=True))
+    x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+    return self.fc(torch.flatten(self.avgpool(x), 1))
 
 
 def _native_bn_forward(self, x):
@@ -225,6 +338,34 @@ def _fits(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return B * H * W * cin_p * 4 <= _MAX_BYTES and B * Ho * Wo * cout_p * 4 <= _MAX_BYTES and Ho > 0 and Wo > 0
 
 
+class _NativeDropout(torch.autograd.Function):
+    """Training-mode inverted dropout on the Philox kernel (K7b): the mask is regenerated from
+    (seed, element index) in the backward, nothing is stored."""
+
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        ctx.p, ctx.seed = p, seed
+        return ops.require().dropout(x.contiguous(), seed, p)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.require().dropout(g.contiguous(), ctx.seed, ctx.p), None, None
+
+
+def _native_dropout_forward(self, x):
+    if not (self.training and self.p > 0 and x.is_cuda and x.dtype == torch.float32 and type(self) is nn.Dropout):
+        return type(self).forward(self, x)
+    if self.p >= 1:
+        return x * 0.0
+    # seed from torch's CPU generator: reproducible under torch.manual_seed, no device sync
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    y = _NativeDropout.apply(x, float(self.p), seed)
+    if self.inplace:
+        x.copy_(y)
+        return x
+    return y
+
+
 def _native_forward(self, x):
     if not x.is_cuda or x.dtype != torch.float32 or self.weight.dtype != torch.float32 or x.dim() != 4 \
             or not _fits(self, x):
@@ -233,19 +374,35 @@ def _native_forward(self, x):
     return _NativeConv2d.apply(x, self.weight, self.bias, ks, s, p)
 
 
-def enable_native_convs(model: nn.Module, bn: bool = True) -> list:
+def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True) -> list:
     """Route every eligible ``nn.Conv2d`` of ``model`` (and, with ``bn``, every ``BatchNorm2d`` in
     training mode) through the native kernels (instance-level ``forward`` override; pruning keeps
-    working because weights are re-packed per call). Returns the switched modules; undo with
+    working because weights are re-packed per call). With ``bn`` and ``fuse``, residual blocks,
+    ResNet stems and ``nn.Sequential`` containers also fuse their BN(+residual)+ReLU tails in
+    training mode — the fused BN / ReLU modules are then not called, so forward hooks on them do
+    not fire (attribution passes use ``fuse=False``). Returns the switched modules; undo with
     :func:`disable_native_convs`."""
     if not ops.available() or ops.backend() == "torch":
         return []
+    from .resnet_engine import _is_resnet
     switched = []
     for m in model.modules():
         if "forward" in m.__dict__:
             continue
-        if eligible(m):
+        if bn and fuse and _block_kind(m) is not None:
+            m.forward = types.MethodType(_native_block_forward, m)
+            switched.append(m)
+        elif bn and fuse and _is_resnet(m) and isinstance(m.relu, nn.ReLU) and isinstance(m.bn1, nn.BatchNorm2d):
+            m.forward = types.MethodType(_native_resnet_forward, m)
+            switched.append(m)
+        elif bn and fuse and type(m) is nn.Sequential:
+            m.forward = types.MethodType(_native_sequential_forward, m)
+            switched.append(m)
+        elif eligible(m):
             m.forward = types.MethodType(_native_forward, m)
+            switched.append(m)
+        elif type(m) is nn.Dropout:
+            m.forward = types.MethodType(_native_dropout_forward, m)
             switched.append(m)
         elif bn and isinstance(m, nn.BatchNorm2d):
             m.forward = types.MethodType(_native_bn_forward, m)
@@ -259,9 +416,9 @@ def disable_native_convs(modules) -> None:
 
 
 @contextlib.contextmanager
-def native_convs(model: nn.Module, enable: bool = True, bn: bool = True):
+def native_convs(model: nn.Module, enable: bool = True, bn: bool = True, fuse: bool = True):
     """``with native_convs(model): loss.backward()`` — scoped :func:`enable_native_convs`."""
-    switched = enable_native_convs(model, bn) if enable else []
+    switched = enable_native_convs(model, bn, fuse) if enable else []
     try:
         yield switched
     finally:
