@@ -59,6 +59,9 @@ def test_native_conv_training_matches_autograd(cuda, arch):
     else:
         model = prunable_vgg16().to(cuda)
         shape, graph = (3, 32, 32), get_vgg_pruning_graph
+        for m in model.modules():  # the native Philox dropout draws other masks than ATen's
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
     rng = np.random.RandomState(0)
     pruner = Pruner(model, shape, cuda)
     for module, cascade in graph(model):  # odd widths: channel padding inside the native convs
@@ -218,3 +221,24 @@ def test_native_dropout(cuda):
     with native_convs(drop):
         z = drop(torch.full((64,), float("nan"), device=cuda))
     assert torch.isnan(z).all()
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(64, 96, (16, 16)), (40, 32, (10, 14))])
+def test_native_conv_winograd_training(cuda, cin, cout, hw):
+    """Stride-1 3x3 training convs on the Winograd F(2x2,3x3) kernel (forward and data gradient;
+    TUNER.fixed() puts Winograd first) vs fp64 autograd."""
+    from torchpruner_amd.engine.fused_chain import TUNER
+    from torchpruner_amd.engine.train import native_convs
+    torch.manual_seed(cin)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1).to(cuda)
+    x = torch.randn(2, cin, *hw, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    with TUNER.fixed(), native_convs(conv):
+        y = conv(x)
+        g = torch.randn_like(y)
+        (y * g).sum().backward()
+    c64 = copy.deepcopy(conv).double()
+    x64 = x.detach().double().requires_grad_(True)
+    (c64(x64) * g.double()).sum().backward()
+    torch.testing.assert_close(y.double(), c64(x64), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(conv.weight.grad.double(), c64.weight.grad, rtol=1e-4, atol=1e-3)

@@ -32,7 +32,12 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import _CU, TUNER, cpad
+from .fused_chain import _CU, TUNER, WINO, WINO_LDS, _wino_splits, cpad, winograd_weights
+
+
+def _wino_ok(ks, stride, pad, H, W, cin, cout) -> bool:
+    """Winograd F(2x2,3x3) applies: 3x3, stride 1, 'same' padding, even H/W, the kernel's granules."""
+    return ks == 3 and stride == 1 and pad == 1 and H % 2 == 0 and W % 2 == 0 and cin % 8 == 0 and cout % 32 == 0
 
 
 def _as_nchw(t: torch.Tensor) -> torch.Tensor:
@@ -103,11 +108,21 @@ class _NativeConv2d(torch.autograd.Function):
         Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
         M = B * Ho * Wo
 
+        wino = _wino_ok(ks, stride, pad, H, W, cin_p, cout_p)
+        cache = {}
+
         def run(cfg, sp):
+            if cfg in (WINO, WINO_LDS):  # Winograd F(2x2,3x3): 2.25x fewer multiplies
+                if "u" not in cache:
+                    cache["u"] = winograd_weights(wp)
+                return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
             return T.conv_gen(xh, wk, None, shift, False, None, None, ks, stride, pad, cfg, sp)
 
-        cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run,
-                               cands=TUNER.candidates(M, cout_p, kk))
+        cands = TUNER.candidates(M, cout_p, kk)
+        if wino:
+            sp0 = _wino_splits(B * (H // 2) * (W // 2), cout_p, cin_p)
+            cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
+        cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
         y = run(cfg, sp)
         if cout_p != Cout:
             y = y[..., :Cout].contiguous()
@@ -137,11 +152,20 @@ class _NativeConv2d(torch.autograd.Function):
                     pad_b, transposed = pad, True
                 M, K = B * H * W, wt.shape[1]
 
+                wino = not transposed and _wino_ok(ks, 1, pad_b, Ho, Wo, cout_p, cin_p)
+                cache = {}
+
                 def run(cfg, sp):
+                    if cfg in (WINO, WINO_LDS):  # stride-1 3x3 dgrad = Winograd conv of g, flipped taps
+                        if "ut" not in cache:
+                            cache["ut"] = winograd_weights(wp.flip(2, 3).transpose(0, 1))
+                        return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
                     return T.conv_gen_bwd(g, wt, None, 1, None, ks, stride if transposed else 1, pad_b, H, W,
                                           transposed, cfg, sp)
 
                 cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
+                if wino:
+                    cands = [(WINO_LDS, _wino_splits(B * (H // 2) * (W // 2), cin_p, cout_p)), (WINO, 1)] + cands
                 cfg, sp = TUNER.choose(("tdgrad", tuple(g.shape), cin_p, ks, stride, pad), M, cin_p, K, run,
                                        cands=cands)
                 dxh = run(cfg, sp)[..., :Cin]
