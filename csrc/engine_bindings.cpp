@@ -49,6 +49,7 @@ hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
                         int tay_mode, hipStream_t st);
+hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st);
 hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, const float* neg_one, const float* Y0, int M, int Kc,
                                 int N, int B0, int relu, float slope, int cfg, float* out, hipStream_t st);
 hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* perm, int B, int C, int N, int p0,
@@ -196,6 +197,20 @@ at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor
                                     shift.data_ptr<float>(), out.data_ptr<float>(), (int)B, (int)Cin, (int)H, (int)W,
                                     (int)Cout, relu ? 1 : 0, cur_stream()));
   return out;
+}
+
+// Winograd U images of a 3x3 weight: w (K, C, 3, 3) -> (C/8, K/32, 4096); flip_t: the data-gradient
+// operand of the forward weight w (Cout = K', Cin = C', 3, 3) -> images of (C', K') with rotated taps.
+at::Tensor wino_weights(const at::Tensor& w, bool flip_t) {
+  need(w, "w", 4);
+  TORCH_CHECK(w.size(2) == 3 && w.size(3) == 3, "w must be (.., .., 3, 3)");
+  const int64_t K = flip_t ? w.size(1) : w.size(0), C = flip_t ? w.size(0) : w.size(1);
+  TORCH_CHECK(K % 32 == 0 && C % 8 == 0, "Winograd images need K % 32 == 0 and C % 8 == 0");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(w.device());
+  auto u = at::empty({C / 8, K / 32, 4096}, w.options());
+  TP_CHECK_HIP(tp_wino_weights(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
+                               cur_stream()));
+  return u;
 }
 
 // Shapley prefix-delta operands: z (B, C) block output, W (N, C) next Linear, perm (n) int32
@@ -622,6 +637,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
         "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0, float slope=0.0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
+  m.def("wino_weights(Tensor w, bool flip_t) -> Tensor");
   m.def("prefix_tri_operands(Tensor z, Tensor w, Tensor perm, int p0, int cnt, int Kc) -> (Tensor, Tensor)");
   m.def("prefix_delta(Tensor T, Tensor wsub, Tensor neg_one, Tensor y0, bool relu, float slope, int cfg) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
@@ -635,6 +651,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_dgrad", &conv_dgrad);
   m.impl("conv_first", &conv_first);
   m.impl("prefix_tri_operands", &prefix_tri_operands);
+  m.impl("wino_weights", &wino_weights);
   m.impl("prefix_delta", &prefix_delta);
   m.impl("conv_wino_fwd", &conv_wino_fwd);
   m.impl("nchw_to_nhwc_pad", &nchw_to_nhwc_pad);

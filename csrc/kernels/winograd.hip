@@ -678,6 +678,40 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Weight transform U = G g G^T written straight into the LDS images the kernels DMA (the
+// layout of fused_chain.winograd_weights): word ((xi*2 + e)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + n of
+// image (cb, kb) holds U[xi][c = 8cb + 2g + e][k = 32kb + j + 16n]. Computed in fp64, rounded once.
+// ``flip_t``: the data-gradient operand — w'[k][c] = w[c][k] with the taps rotated 180 degrees —
+// read from the forward weight directly (no flipped / transposed copy).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wino_weight_transform(const float* __restrict__ w, float* __restrict__ u,
+                                                             int K, int C, int flip_t) {
+  const long long total = (long long)(C / 8) * (K / 32) * W_UIMG;
+  const double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int word = (int)(t % W_UIMG);
+    const long long img = t / W_UIMG;
+    const int kb = (int)(img % (K / 32)), cb = (int)(img / (K / 32));
+    const int n = word & 1, gs = (word >> 1) & 3, j = (word >> 3) & 15, e = (word >> 7) & 1, xi = word >> 8;
+    const int g = gs ^ ((j >> 3) << 1);
+    const int c = 8 * cb + 2 * g + e, k = 32 * kb + j + 16 * n;
+    const int i = xi >> 2, jj = xi & 3;
+    // source (K, C, 3, 3): forward w[k][c]; flip_t: the forward weight is (C, K, 3, 3) -> w[c][k] rotated
+    const float* src = flip_t ? w + ((long long)c * K + k) * 9 : w + ((long long)k * C + c) * 9;
+    double acc = 0.0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int tap = flip_t ? (2 - a) * 3 + (2 - b) : a * 3 + b;
+        acc += G[i][a] * (double)src[tap] * G[jj][b];
+      }
+    u[t] = (float)acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // host: staged-region geometry (bank-conflict-minimising pitches) per (B, H, W)
 // ---------------------------------------------------------------------------------------
 struct XGeom {
@@ -780,6 +814,16 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
                                               float* apoz, int tay_mode, hipStream_t st);
 
 extern "C" int tp_wino_taylor_slots(int H, int W) { return tp::wino_taylor_slots(H, W); }
+
+// w: (K, C, 3, 3) (flip_t = 0) or the forward weight (C, K, 3, 3) of which the dgrad operand is
+// wanted (flip_t = 1); u: (C/8, K/32, 4096) images. K % 32 == 0, C % 8 == 0.
+extern "C" hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st) {
+  if (K % 32 || C % 8 || K <= 0 || C <= 0) return hipErrorInvalidValue;
+  const long long total = (long long)(C / 8) * (K / 32) * tp::W_UIMG;
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
+  tp::wino_weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t);
+  return hipGetLastError();
+}
 
 extern "C" int tp_wino_staged_ok(int H, int W, int unpool) {
   return tp::staged_geometry(H, W, unpool != 0).ok ? 1 : 0;

@@ -242,3 +242,17 @@ def test_native_conv_winograd_training(cuda, cin, cout, hw):
     torch.testing.assert_close(y.double(), c64(x64), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(conv.weight.grad.double(), c64.weight.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("K,C", [(64, 32), (96, 40)])
+def test_wino_weights_kernel(cuda, K, C):
+    """GPU Winograd weight transform == fused_chain.winograd_weights (forward and flipped-transposed
+    data-gradient operand)."""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import winograd_weights
+    T = ops.require()
+    w = torch.randn(K, C, 3, 3, device=cuda)
+    torch.testing.assert_close(T.wino_weights(w, False), winograd_weights(w), rtol=1e-6, atol=1e-7)
+    wt = torch.randn(C, K, 3, 3, device=cuda)  # forward weight of a conv with Cout=C, Cin=K
+    torch.testing.assert_close(T.wino_weights(wt, True), winograd_weights(wt.flip(2, 3).transpose(0, 1)),
+                               rtol=1e-6, atol=1e-7)

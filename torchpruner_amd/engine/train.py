@@ -32,7 +32,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import _CU, TUNER, WINO, WINO_LDS, _wino_splits, cpad, winograd_weights
+from .fused_chain import _CU, TUNER, WINO, WINO_LDS, _wino_splits, cpad
 
 
 def _wino_ok(ks, stride, pad, H, W, cin, cout) -> bool:
@@ -113,8 +113,8 @@ class _NativeConv2d(torch.autograd.Function):
 
         def run(cfg, sp):
             if cfg in (WINO, WINO_LDS):  # Winograd F(2x2,3x3): 2.25x fewer multiplies
-                if "u" not in cache:
-                    cache["u"] = winograd_weights(wp)
+                if "u" not in cache:  # one transform launch per step (weights change every step)
+                    cache["u"] = T.wino_weights(wp.contiguous(), False)
                 return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
             return T.conv_gen(xh, wk, None, shift, False, None, None, ks, stride, pad, cfg, sp)
 
@@ -158,7 +158,7 @@ class _NativeConv2d(torch.autograd.Function):
                 def run(cfg, sp):
                     if cfg in (WINO, WINO_LDS):  # stride-1 3x3 dgrad = Winograd conv of g, flipped taps
                         if "ut" not in cache:
-                            cache["ut"] = winograd_weights(wp.flip(2, 3).transpose(0, 1))
+                            cache["ut"] = T.wino_weights(wp.contiguous(), True)
                         return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
                     return T.conv_gen_bwd(g, wt, None, 1, None, ks, stride if transposed else 1, pad_b, H, W,
                                           transposed, cfg, sp)
