@@ -74,6 +74,19 @@ __device__ __forceinline__ float act_grad(float a, float g, float slope) {
   return a > 0.f ? g : (slope != 0.f ? g * slope : 0.f);
 }
 
+// Division by a runtime-invariant divisor as mul-hi + add + shift (Granlund-Montgomery; valid
+// for 0 <= n < 2^31): a 32-bit integer division is otherwise ~25 VALU instructions.
+struct FastDiv {
+  unsigned d = 1, m = 1, l = 0;
+  FastDiv() = default;
+  explicit FastDiv(unsigned dv) : d(dv) {
+    l = 0;
+    while ((1ull << l) < dv) ++l;
+    m = (unsigned)(((1ull << 32) * ((1ull << l) - dv)) / dv + 1);
+  }
+  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> l); }
+};
+
 inline unsigned ceil_div(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
 
 }  // namespace tp

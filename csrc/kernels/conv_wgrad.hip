@@ -27,6 +27,7 @@ struct WgradArgs {
   int P;     // B*Ho*Wo
   int slices_per_split;
   long long g_elems, x_elems;
+  FastDiv fd_hwo, fd_wo;  // pixel -> (image, oh, ow) decode without integer divisions
 };
 
 template <int BM, int BN, int WM, int WN>
@@ -82,8 +83,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradAr
       bool ok = col_ok && pix < p.P;
       int off = pix * p.Cin + ci;
       if (!DIRECT && ok) {
-        const int b = pix / HWo, r = pix - b * HWo;
-        const int oh = r / p.Wo, ow = r - oh * p.Wo;
+        const int b = p.fd_hwo.div(pix), r = pix - b * HWo;
+        const int oh = p.fd_wo.div(r), ow = r - oh * p.Wo;
         const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
         ok = ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
         off = ((b * p.H + ih) * p.W + iw) * p.Cin + ci;
@@ -214,6 +215,8 @@ extern "C" hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, f
   a.Kc = ks * ks * Cin;
   a.Kpad = Kpad;
   a.P = B * a.Ho * a.Wo;
+  a.fd_hwo = FastDiv((unsigned)std::max(1, a.Ho * a.Wo));
+  a.fd_wo = FastDiv((unsigned)std::max(1, a.Wo));
   a.g_elems = (long long)a.P * Cout;
   a.x_elems = (long long)B * H * W * Cin;
   if (a.g_elems * 4 >= (1ll << 31) || a.x_elems * 4 >= (1ll << 31)) return hipErrorInvalidValue;

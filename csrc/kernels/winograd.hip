@@ -43,18 +43,6 @@ __device__ unsigned short buf_load_u16(i32x4 rsrc, int voffset, int soffset, int
 
 enum WEpi : int { W_FWD = 0, W_FWD_POOL = 1, W_BWD = 2, W_PARTIAL = 3 };
 
-// Division by a runtime-invariant divisor as mul-hi + add + shift (Granlund-Montgomery; valid
-// for 0 <= n < 2^31): the tile -> (image, row, col) decode is otherwise ~25 VALU per division.
-struct FastDiv {
-  unsigned d = 1, m = 1, l = 0;
-  FastDiv() = default;
-  explicit FastDiv(unsigned dv) : d(dv) {
-    l = 0;
-    while ((1ull << l) < dv) ++l;
-    m = (unsigned)(((1ull << 32) * ((1ull << l) - dv)) / dv + 1);
-  }
-  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> l); }
-};
 enum XMode : int { X_DIRECT = 0, X_UNPOOL = 1, X_STAGED = 2, X_STAGED_UNPOOL = 3 };
 
 constexpr int W_TK = 32;             // output channels per block

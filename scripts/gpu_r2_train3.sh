@@ -7,6 +7,6 @@ tail -2 gpurun_out/train_tests.log
 FMTS=native N=10 timeout -k 10 300 python scripts/r50_train_probe.py > gpurun_out/train_probe.log 2>&1 || { tail -30 gpurun_out/train_probe.log; exit 1; }
 grep "img/s" gpurun_out/train_probe.log
 cd /tmp && export TMPDIR=/tmp
-FMTS=native N=5 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train3 -o run --output-format csv -- python3 $R/scripts/r50_train_probe.py > $R/gpurun_out/prof_train3.log 2>&1 || { tail -30 $R/gpurun_out/prof_train3.log; exit 1; }
+FMTS=native N=5 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train4 -o run --output-format csv -- python3 $R/scripts/r50_train_probe.py > $R/gpurun_out/prof_train4.log 2>&1 || { tail -30 $R/gpurun_out/prof_train4.log; exit 1; }
 cd $R
-python scripts/train_step_breakdown.py gpurun_out/prof_train3/run_kernel_trace.csv
+python scripts/train_step_breakdown.py gpurun_out/prof_train4/run_kernel_trace.csv

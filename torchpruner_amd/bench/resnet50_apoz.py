@@ -4,10 +4,12 @@ per-unit scores all-reduced over RCCL (one collective per run).
     python -m torchpruner_amd.bench.resnet50_apoz [--batch 256] [--steps 10]
     torchrun --nproc-per-node 8 -m torchpruner_amd.bench.resnet50_apoz ...
 
-One pass scores every prunable conv of every bottleneck (``run_many``: a single forward per
-batch with the APoZ count fused into one HIP channel reduction per evaluation module).
-Activations are channels_last (NHWC) so MIOpen's convolutions and the reduction kernel read
-contiguous channel vectors. fp32; synthetic data (batch i regenerated on device from a seed).
+One pass scores every prunable conv of every bottleneck (``run_many``): the whole network runs
+on the ResNet engine (engine/resnet_engine.py: implicit-GEMM / Winograd MFMA convs with the
+eval-mode BN folded in, residual + ReLU fused in the epilogues) and the APoZ counts of every
+evaluation BN come out of the conv epilogues; ``--metric taylor|sensitivity`` adds the engine's
+input-gradient-only backward. ``metric.last_path`` is asserted to be the engine. fp32; synthetic
+data (batch i regenerated on device from a seed).
 """
 from __future__ import annotations
 
@@ -55,6 +57,7 @@ def main():
     torch.cuda.synchronize()
     pdist.barrier()
     dt = time.perf_counter() - t0
+    assert metric.last_path["path"] == "resnet", metric.last_path
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -63,6 +66,7 @@ def main():
         print(json.dumps({"metric": f"{M.__name__} attribution images/sec (whole node), ResNet-50 224x224",
                           "value": round(args.steps * args.batch * world / dt, 1), "unit": "images/s",
                           "n_gpus": world, "per_gpu_batch": args.batch, "steps": args.steps,
+                          "path": metric.last_path["path"],
                           "modules_scored": len(modules), "dtype": "fp32", "data": "synthetic",
                           "units_total": int(sum(len(s) for s in scores))}), flush=True)
     if world > 1:
