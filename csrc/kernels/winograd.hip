@@ -43,7 +43,11 @@ __device__ unsigned short buf_load_u16(i32x4 rsrc, int voffset, int soffset, int
 
 enum WEpi : int { W_FWD = 0, W_FWD_POOL = 1, W_BWD = 2, W_PARTIAL = 3 };
 
-enum XMode : int { X_DIRECT = 0, X_UNPOOL = 1, X_STAGED = 2, X_STAGED_UNPOOL = 3 };
+// X_SPAN: X_STAGED for any W/2 (ResNet's 56/28/14): the block's 64 consecutive tiles span a few
+// tile rows of up to MAX_SEG images; each image segment's input rows (halos included) are
+// stacked in the staged LDS image, so every shape gets the halo-sharing LDS input path.
+enum XMode : int { X_DIRECT = 0, X_UNPOOL = 1, X_STAGED = 2, X_STAGED_UNPOOL = 3, X_SPAN = 4 };
+constexpr int MAX_SEG = 4;
 
 constexpr int W_TK = 32;             // output channels per block
 constexpr int W_CH = 8;              // input channels per chunk
@@ -67,7 +71,7 @@ struct WinoArgs {
   float* taylor;
   int pooled_m;             // W_PARTIAL: write the slab in pooled M order (b, th, tw, q)
   // X_STAGED region geometry: a block's 64 tiles = n_img images x R tile rows each
-  int n_img, R, RW, IP;     // RW: row pitch (pixels), IP: image pitch (pixels)
+  int n_img, R, RW, IP;     // RW: row pitch (pixels), IP: image pitch (pixels); X_SPAN uses RW only
   int rounds;               // 256-slot DMA rounds per staged image
   // X_STAGED_UNPOOL: pooled region pitches; argmax image rounds and its byte offset
   int arounds, aoff;
@@ -350,7 +354,8 @@ phase2:
 
 template <int EPI, int XMODE>
 __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
-  constexpr bool STAGED = XMODE == X_STAGED || XMODE == X_STAGED_UNPOOL, UNPOOL = XMODE == X_UNPOOL;
+  constexpr bool STAGED = XMODE == X_STAGED || XMODE == X_STAGED_UNPOOL || XMODE == X_SPAN;
+  constexpr bool UNPOOL = XMODE == X_UNPOOL;
   // separate objects per buffer so the compiler's LDS-DMA alias tracking can tell them apart
   __shared__ __attribute__((aligned(16))) float us0[W_UIMG];
   __shared__ __attribute__((aligned(16))) float us1[W_UIMG];
@@ -416,6 +421,59 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
         poff[r * 3 + q] = ((b * H2 + ph) * W2 + pq) * p.C;
         pmask |= (ok ? 1u : 0u) << (r * 3 + q);
       }
+  } else if constexpr (XMODE == X_SPAN) {
+    // segments: images b0 .. bL of the block's tiles; segment sg holds input rows
+    // 2*th_lo[sg]-1 .. 2*th_hi[sg]+2 of image b0+sg at region rows base[sg] ..
+    const int t0 = blk_p * 64, tl = min(t0 + 63, p.P - 1);
+    const int b0 = p.fd_timg.div(t0), bL = p.fd_timg.div(tl);
+    int th_lo[MAX_SEG], base[MAX_SEG + 1];
+    base[0] = 0;
+#pragma unroll
+    for (int sg = 0; sg < MAX_SEG; ++sg) {
+      const int bb = b0 + sg;
+      const bool live = bb <= bL;
+      const int lo = sg == 0 ? p.fd_w2.div(t0 - b0 * T_img) : 0;
+      const int hi = bb == bL ? p.fd_w2.div(tl - bL * T_img) : H2 - 1;
+      th_lo[sg] = lo;
+      base[sg + 1] = base[sg] + (live ? 2 * (hi - lo + 1) + 2 : 0);
+    }
+    const int sg_l = tok ? b - b0 : 0;
+    int bsel = 0, lsel = 0;
+#pragma unroll
+    for (int sg = 0; sg < MAX_SEG; ++sg)
+      if (sg == sg_l) {
+        bsel = base[sg];
+        lsel = th_lo[sg];
+      }
+    const int pix0 = tok ? (bsel + 2 * (th - lsel)) * p.RW + 2 * tw : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int L = 2 * (pix0 + r * p.RW + q) + (g >> 1);
+        poff[r * 4 + q] = xswz(L) * 16 + (g & 1) * 8;
+      }
+#pragma unroll
+    for (int i = 0; i < MAX_ROUNDS; ++i) {
+      const int s_ = i * 256 + tid;
+      const int L = xswz(s_);
+      const int pix = L >> 1, h = L & 1;
+      const int row = p.fd_rw.div(pix), col = pix - row * p.RW;
+      int sg = 0;
+#pragma unroll
+      for (int k = 1; k < MAX_SEG; ++k) sg += row >= base[k] ? 1 : 0;
+      int rb = 0, lo = 0;
+#pragma unroll
+      for (int k = 0; k < MAX_SEG; ++k)
+        if (k == sg) {
+          rb = base[k];
+          lo = th_lo[k];
+        }
+      const int bb = b0 + sg, ih = 2 * lo - 1 + (row - rb), iw = col - 1;
+      const bool ok = i < p.rounds && row < base[MAX_SEG] && col < p.W + 2 && bb <= bL && bb < p.B && ih >= 0 &&
+                      ih < p.H && iw >= 0 && iw < p.W;
+      xsrc[i] = ok ? (unsigned)((((bb * p.H + ih) * p.W + iw) * p.C) * 4 + h * 16) : OOB;
+    }
   } else if constexpr (XMODE == X_STAGED) {
     // block region: images b0 .. b0+n_img-1, input rows 2*th0-1 .. 2*th0+2R, cols -1 .. W
     const int t0 = blk_p * 64;
@@ -481,7 +539,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
     const unsigned ubase = (unsigned)(((c0 / W_CH) * n_k + kb) * W_UIMG) * 4u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ubase);
-    if constexpr (XMODE == X_STAGED) {
+    if constexpr (XMODE == X_STAGED || XMODE == X_SPAN) {
 #pragma unroll
       for (int i = 0; i < MAX_ROUNDS; ++i)
         if (i < p.rounds) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
@@ -559,7 +617,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
     f32x2 v[16];
     {
       f32x2 d[16];
-      if constexpr (XMODE == X_STAGED) {
+      if constexpr (XMODE == X_STAGED || XMODE == X_SPAN) {
 #pragma unroll
         for (int t = 0; t < 16; ++t)
           d[t] = WDBG(p, 64) ? f32x2{(float)t, 1.f}
@@ -790,6 +848,102 @@ static XGeom staged_geometry(int H, int W, bool pooled) {
   return gm;
 }
 
+// X_SPAN geometry: the worst-case stacked row count over all block start phases, a row pitch
+// chosen by the same bank simulation (block starting at tile 0), and the DMA rounds.
+struct SpanGeom {
+  bool ok = false;
+  int RW = 0, rounds = 0, rows = 0;
+};
+
+static void span_rows(int t0, int P, int T_img, int W2, int H2, int* base /* MAX_SEG+1 */, int* th_lo) {
+  const int tl = std::min(t0 + 63, P - 1);
+  const int b0 = t0 / T_img, bL = tl / T_img;
+  base[0] = 0;
+  for (int sg = 0; sg < MAX_SEG; ++sg) {
+    const int bb = b0 + sg;
+    const int lo = sg == 0 ? (t0 - b0 * T_img) / W2 : 0;
+    const int hi = bb == bL ? (tl - bL * T_img) / W2 : H2 - 1;
+    th_lo[sg] = lo;
+    base[sg + 1] = base[sg] + (bb <= bL ? 2 * (hi - lo + 1) + 2 : 0);
+  }
+}
+
+static int span_conflicts(int W2, int H2, int RW) {
+  const int T_img = W2 * H2, P = 64 * 4;
+  int base[MAX_SEG + 1], th_lo[MAX_SEG];
+  span_rows(0, P, T_img, W2, H2, base, th_lo);
+  int total = 0;
+  for (int wave = 0; wave < 4; ++wave)
+    for (int r = 0; r < 4; ++r)
+      for (int q = 0; q < 4; ++q)
+        for (int half = 0; half < 2; ++half) {
+          int words[64];
+          int n = 0;
+          for (int jj = 0; jj < 16; ++jj)
+            for (int gg = 2 * half; gg < 2 * half + 2; ++gg) {
+              const int t = wave * 16 + jj;
+              const int bb = t / T_img, rem = t % T_img, th = rem / W2, tw = rem % W2;
+              const int pix = (base[bb] + 2 * (th - th_lo[bb]) + r) * RW + 2 * tw + q;
+              const int w0 = xswz(2 * pix + (gg >> 1)) * 4 + (gg & 1) * 2;
+              words[n++] = w0;
+              words[n++] = w0 + 1;
+            }
+          for (int bank = 0; bank < 64; ++bank) {
+            int distinct[64];
+            int nd = 0;
+            for (int a = 0; a < n; ++a) {
+              if ((words[a] & 63) != bank) continue;
+              bool seen = false;
+              for (int z = 0; z < nd; ++z) seen |= distinct[z] == words[a];
+              if (!seen) distinct[nd++] = words[a];
+            }
+            if (nd > 1) total += nd - 1;
+          }
+        }
+  return total;
+}
+
+static SpanGeom span_geometry(int H, int W) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, SpanGeom> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({H, W});
+  if (it != cache.end()) return it->second;
+  SpanGeom gm;
+  const int H2 = H / 2, W2 = W / 2, T_img = H2 * W2;
+  if (T_img > 0) {
+    // worst case over the block start phases t0 mod T_img (P large enough that no block is cut)
+    int rows = 0, segs = 0;
+    bool fits = true;
+    for (int ph = 0; ph < T_img && fits; ++ph) {
+      int base[MAX_SEG + 1], th_lo[MAX_SEG];
+      const int t0 = ph;  // a block starting at phase ph of an image
+      const int span_imgs = (ph + 63) / T_img + 1;
+      if (span_imgs > MAX_SEG) fits = false;
+      span_rows(t0, t0 + 64 + 4 * T_img, T_img, W2, H2, base, th_lo);
+      rows = std::max(rows, base[MAX_SEG]);
+      segs = std::max(segs, span_imgs);
+    }
+    int best = -1;
+    for (int RW = W + 2; fits && RW < W + 18; ++RW) {
+      const int items = 2 * rows * RW;
+      const int rounds = (items + 255) / 256;
+      if (rounds * 256 * 16 > W_XS * 4) continue;
+      const int cost = span_conflicts(W2, H2, RW) * 4 + rounds;
+      if (best < 0 || cost < best) {
+        best = cost;
+        gm.ok = true;
+        gm.RW = RW;
+        gm.rounds = rounds;
+        gm.rows = rows;
+      }
+    }
+    (void)segs;
+  }
+  cache[{H, W}] = gm;
+  return gm;
+}
+
 }  // namespace tp
 
 // Winograd conv: same operand/epilogue contract as tp_conv_igemm (3x3, stride 1, pad 1),
@@ -871,7 +1025,16 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.dbg = dbg_bits;
 #endif
   int xmode = unpool ? X_UNPOOL : X_DIRECT;
-  if (staged) {
+  if (staged && !unpool && !staged_geometry(H, W, false).ok && getenv("TP_WINO_NOSPAN") == nullptr) {
+    const SpanGeom sg = span_geometry(H, W);
+    if (sg.ok) {
+      xmode = X_SPAN;
+      a.RW = sg.RW;
+      a.rounds = sg.rounds;
+      a.fd_rw = FastDiv((unsigned)sg.RW);
+    }
+  }
+  if (staged && xmode != X_SPAN) {
     const XGeom gm = staged_geometry(H, W, unpool != 0);
     if (gm.ok) {
       xmode = unpool ? X_STAGED_UNPOOL : X_STAGED;
@@ -898,6 +1061,7 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
 #define TP_W(E)                                                                                 \
   do {                                                                                          \
     if (xmode == X_STAGED) wino_f2x3<E, X_STAGED><<<grid, 256, 0, st>>>(a);                    \
+    else if (xmode == X_SPAN) wino_f2x3<E, X_SPAN><<<grid, 256, 0, st>>>(a);                   \
     else if (xmode == X_STAGED_UNPOOL) wino_f2x3<E, X_STAGED_UNPOOL><<<grid, 256, 0, st>>>(a);  \
     else if (xmode == X_UNPOOL) wino_f2x3<E, X_UNPOOL><<<grid, 256, 0, st>>>(a);               \
     else wino_f2x3<E, X_DIRECT><<<grid, 256, 0, st>>>(a);                                      \

@@ -262,6 +262,12 @@ WINO_SHAPES = [  # B, H, W, Cin, Cout (staged-region modes: rows for W/2 | 64, i
     (16, 2, 2, 512, 512),
     (2, 6, 10, 40, 96),
     (3, 18, 14, 64, 32),
+    # ResNet geometries (W/2 = 7, 14, 28 do not divide 64): row-span staged input (X_SPAN),
+    # blocks straddling 2-3 images
+    (3, 14, 14, 64, 64),
+    (2, 28, 28, 32, 64),
+    (2, 56, 56, 64, 32),
+    (5, 10, 6, 32, 32),
 ]
 
 
