@@ -256,3 +256,25 @@ def test_wino_weights_kernel(cuda, K, C):
     wt = torch.randn(C, K, 3, 3, device=cuda)  # forward weight of a conv with Cout=C, Cin=K
     torch.testing.assert_close(T.wino_weights(wt, True), winograd_weights(wt.flip(2, 3).transpose(0, 1)),
                                rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("B,cin,cout", [(7, 512, 10), (64, 784, 200), (3, 36, 40)])
+def test_native_linear_training(cuda, B, cin, cout):
+    """nn.Linear on the MFMA GEMM through native_convs: forward, input, weight and bias gradients
+    vs fp64 autograd (K4 fwd / dgrad / wgrad)."""
+    from torchpruner_amd.engine.train import native_convs
+    torch.manual_seed(B + cin)
+    lin = torch.nn.Linear(cin, cout).to(cuda)
+    x = torch.randn(B, cin, device=cuda, requires_grad=True)
+    with native_convs(lin):
+        y = lin(x)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    l64 = copy.deepcopy(lin).double()
+    x64 = x.detach().double().requires_grad_(True)
+    y64 = l64(x64)
+    (y64 * g.double()).sum().backward()
+    torch.testing.assert_close(y.double(), y64, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(lin.weight.grad.double(), l64.weight.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(lin.bias.grad.double(), l64.bias.grad, rtol=1e-4, atol=1e-4)

@@ -390,6 +390,18 @@ def _native_dropout_forward(self, x):
     return y
 
 
+def _native_linear_forward(self, x):
+    """nn.Linear on the MFMA GEMM (a 1x1 conv of the (B, 1, 1, in) input): forward, data gradient
+    and the weight gradient (pixel-split wgrad kernel) — the classifier of a finetuned model."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and self.weight.dtype == torch.float32
+            and x.shape[0] > 0 and x.shape[0] * max(cpad(self.in_features), cpad(self.out_features)) * 4 <= _MAX_BYTES):
+        return type(self).forward(self, x)
+    B = x.shape[0]
+    y = _NativeConv2d.apply(x.reshape(B, self.in_features, 1, 1), self.weight.view(self.out_features, self.in_features,
+                                                                                    1, 1), self.bias, 1, 1, 0)
+    return y.reshape(B, self.out_features)
+
+
 def _native_forward(self, x):
     if not x.is_cuda or x.dtype != torch.float32 or self.weight.dtype != torch.float32 or x.dim() != 4 \
             or not _fits(self, x):
@@ -427,6 +439,9 @@ def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True) ->
             switched.append(m)
         elif type(m) is nn.Dropout:
             m.forward = types.MethodType(_native_dropout_forward, m)
+            switched.append(m)
+        elif type(m) is nn.Linear:
+            m.forward = types.MethodType(_native_linear_forward, m)
             switched.append(m)
         elif bn and isinstance(m, nn.BatchNorm2d):
             m.forward = types.MethodType(_native_bn_forward, m)
