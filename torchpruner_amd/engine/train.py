@@ -397,7 +397,7 @@ def _native_linear_forward(self, x):
             and x.shape[0] > 0 and x.shape[0] * max(cpad(self.in_features), cpad(self.out_features)) * 4 <= _MAX_BYTES):
         return type(self).forward(self, x)
     B = x.shape[0]
-    y = _NativeConv2d.apply(x.reshape(B, self.in_features, 1, 1), self.weight.view(self.out_features, self.in_features,
+    y = _NativeConv2d.apply(x.reshape(B, self.in_features, 1, 1), self.weight.reshape(self.out_features, self.in_features,
                                                                                     1, 1), self.bias, 1, 1, 0)
     return y.reshape(B, self.out_features)
 
