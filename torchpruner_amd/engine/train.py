@@ -392,14 +392,17 @@ def _native_dropout_forward(self, x):
 
 def _native_linear_forward(self, x):
     """nn.Linear on the MFMA GEMM (a 1x1 conv of the (B, 1, 1, in) input): forward, data gradient
-    and the weight gradient (pixel-split wgrad kernel) — the classifier of a finetuned model."""
-    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and self.weight.dtype == torch.float32
-            and x.shape[0] > 0 and x.shape[0] * max(cpad(self.in_features), cpad(self.out_features)) * 4 <= _MAX_BYTES):
+    and the weight gradient (pixel-split wgrad kernel) — the classifier of a finetuned model. The
+    GEMM shape comes from the weight tensor itself (like F.linear), not from the module's
+    ``in_features``/``out_features`` attributes, which user code may leave stale."""
+    w = self.weight
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and w.dtype == torch.float32 and w.dim() == 2
+            and x.shape[0] > 0 and x.shape[1] == w.shape[1] and (self.bias is None or self.bias.shape == w.shape[:1])
+            and x.shape[0] * max(cpad(w.shape[0]), cpad(w.shape[1])) * 4 <= _MAX_BYTES):
         return type(self).forward(self, x)
-    B = x.shape[0]
-    y = _NativeConv2d.apply(x.reshape(B, self.in_features, 1, 1), self.weight.reshape(self.out_features, self.in_features,
-                                                                                    1, 1), self.bias, 1, 1, 0)
-    return y.reshape(B, self.out_features)
+    B, (n_out, n_in) = x.shape[0], w.shape
+    y = _NativeConv2d.apply(x.reshape(B, n_in, 1, 1), w.reshape(n_out, n_in, 1, 1), self.bias, 1, 1, 0)
+    return y.reshape(B, n_out)
 
 
 def _native_forward(self, x):
