@@ -21,7 +21,7 @@ Accuracy (untimed; ``bench/prune_quality.py``, rank 0): the teacher is pruned fo
 increments per layer with a few SGD steps between increments (Molchanov-style iterative
 pruning), Taylor scores vs Random scores under the same finetune budget.
 ``top1_retained_at_50pct`` = top-1 of the Taylor-pruned network / top-1 of the teacher, on held-out
-samples. Training uses the deterministic native kernels with fixed configs, so the same seed
+samples, averaged over ``--quality-seeds`` seeds (each seed its own teacher and task draw). Training uses the deterministic native kernels with fixed configs, so the same seed
 gives the same numbers in every run. ``top1_layerwise_mask_50pct_*``: the reference's
 layerwise-robustness protocol at one point (nbVGG:1233-1285: each layer alone, lowest half of
 its units zeroed after BN+ReLU; mean over layers).
@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--baseline-batches", type=int, default=2)
     ap.add_argument("--no-prune", action="store_true", help="skip the (untimed) accuracy protocol")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--quality-seeds", type=int, default=3,
+                    help="accuracy protocol over seeds seed..seed+K-1 (each its own teacher); top-1 figures "
+                         "are means over the seeds, per-seed values are listed")
     ap.add_argument("--teacher-steps", type=int, default=pq.DEFAULTS["teacher_steps"])
     return ap.parse_args()
 
@@ -185,24 +188,36 @@ def main():
         lw_t = layerwise_mask_top1(model, convs, scores, xv, yv)
         lw_r = float(np.mean([layerwise_mask_top1(model, convs, [rng.random_sample(c.out_channels) for c in convs],
                                                   xv, yv) for _ in range(3)]))
-        pruned = {}
+        runs = [{"seed": args.seed, "top1_before": before}]
         for method in ("taylor", "random"):
             m = pq.iterative_prune(copy.deepcopy(model), task, method, args.seed, cfg)
-            pruned[method] = pq.top1(m, xv, yv)
+            runs[0][f"top1_pruned_{method}"] = pq.top1(m, xv, yv)
             params = sum(p.numel() for p in m.parameters())
+        for s in range(args.seed + 1, args.seed + max(1, args.quality_seeds)):
+            runs.append(pq.run_protocol(s, dev, **cfg))  # its own teacher, task and held-out set
+        mean = {k: float(np.mean([r[k] for r in runs])) for k in ("top1_before", "top1_pruned_taylor",
+                                                                 "top1_pruned_random")}
+        ret = {m: float(np.mean([r[f"top1_pruned_{m}"] / max(r["top1_before"], 1e-9) for r in runs]))
+               for m in ("taylor", "random")}
+        pruned = {m: mean[f"top1_pruned_{m}"] for m in ("taylor", "random")}
+        before = mean["top1_before"]
         result.update({
-            "top1_retained_at_50pct": round(pruned["taylor"] / max(before, 1e-9), 4),
+            "top1_retained_at_50pct": round(ret["taylor"], 4),
             "top1_before": round(before, 4),
             "top1_pruned_50pct_taylor": round(pruned["taylor"], 4),
             "top1_pruned_50pct_random": round(pruned["random"], 4),
-            "top1_retained_at_50pct_random": round(pruned["random"] / max(before, 1e-9), 4),
+            "top1_retained_at_50pct_random": round(ret["random"], 4),
+            "quality_seeds": [r["seed"] for r in runs],
+            "top1_pruned_50pct_taylor_per_seed": [round(r["top1_pruned_taylor"], 4) for r in runs],
+            "top1_pruned_50pct_random_per_seed": [round(r["top1_pruned_random"], 4) for r in runs],
             "params_before_after": [sum(p.numel() for p in model.parameters()), params],
             "prune_protocol": {k: cfg[k] for k in ("frac", "increments", "ft_steps", "final_ft_steps", "recal_batches",
-                                                   "score_imgs", "val_imgs", "ft_lr")},
+                                                   "score_imgs", "val_imgs", "ft_lr", "noise")},
             "top1_layerwise_mask_50pct_taylor": round(lw_t, 4),
             "top1_layerwise_mask_50pct_random": round(lw_r, 4),
         })
-        log(f"[bench] top-1 before {before:.4f}; 50% of every conv pruned (iterative, "
+        log(f"[bench] seeds {result['quality_seeds']}: mean top-1 before {before:.4f}; 50% of every conv pruned "
+            f"(iterative, "
             f"{cfg['increments']} increments/layer, {cfg['ft_steps']} SGD steps each, +{cfg['final_ft_steps']}): "
             f"Taylor {pruned['taylor']:.4f}, Random {pruned['random']:.4f}; layerwise mask (nbVGG protocol): "
             f"Taylor {lw_t:.4f}, Random {lw_r:.4f} ({time.perf_counter() - t1:.1f}s untimed)")

@@ -50,6 +50,12 @@ hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
                         int tay_mode, hipStream_t st);
 hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st);
+hipError_t tp_wino_weights2(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
+hipError_t tp_pack_conv_weight(const float* w, float* out, int O, int I, int KS, int rows, int cols, int cpad, int mode,
+                               hipStream_t st);
+hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
+                          int ks, int stride, int pad, int Kpad, int cfg, int splits, float* fin, int fin_co,
+                          int fin_ci, const long long* fs, hipStream_t st);
 hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, const float* neg_one, const float* Y0, int M, int Kc,
                                 int N, int B0, int relu, float slope, int cfg, float* out, hipStream_t st);
 hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* perm, int B, int C, int N, int p0,
@@ -201,16 +207,33 @@ at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor
 
 // Winograd U images of a 3x3 weight: w (K, C, 3, 3) -> (C/8, K/32, 4096); flip_t: the data-gradient
 // operand of the forward weight w (Cout = K', Cin = C', 3, 3) -> images of (C', K') with rotated taps.
-at::Tensor wino_weights(const at::Tensor& w, bool flip_t) {
+at::Tensor wino_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C) {
   need(w, "w", 4);
   TORCH_CHECK(w.size(2) == 3 && w.size(3) == 3, "w must be (.., .., 3, 3)");
-  const int64_t K = flip_t ? w.size(1) : w.size(0), C = flip_t ? w.size(0) : w.size(1);
+  // K, C: the padded GEMM sizes (0 = the weight's own); the source may be narrower (zero padding)
+  if (K <= 0) K = flip_t ? w.size(1) : w.size(0);
+  if (C <= 0) C = flip_t ? w.size(0) : w.size(1);
   TORCH_CHECK(K % 32 == 0 && C % 8 == 0, "Winograd images need K % 32 == 0 and C % 8 == 0");
+  TORCH_CHECK(flip_t ? (w.size(0) <= C && w.size(1) <= K) : (w.size(0) <= K && w.size(1) <= C),
+              "weight wider than the padded GEMM");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(w.device());
   auto u = at::empty({C / 8, K / 32, 4096}, w.options());
-  TP_CHECK_HIP(tp_wino_weights(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
-                               cur_stream()));
+  TP_CHECK_HIP(tp_wino_weights2(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
+                                (int)w.size(0), (int)w.size(1), cur_stream()));
   return u;
+}
+
+// Conv weight (O, I, KS, KS) -> a zero-padded GEMM operand (rows, cols): mode 0 forward
+// [n][(kh, kw, ci)], 1 stride-1 dgrad [ci][(kh, kw, co)] with flipped taps, 2 strided dgrad
+// (natural taps); cpad = channel granule of the column index.
+at::Tensor pack_conv_weight(const at::Tensor& w, int64_t rows, int64_t cols, int64_t cpad, int64_t mode) {
+  need(w, "w", 4);
+  TORCH_CHECK(w.size(2) == w.size(3), "square kernels only");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(w.device());
+  auto out = at::empty({rows, cols}, w.options());
+  TP_CHECK_HIP(tp_pack_conv_weight(w.data_ptr<float>(), out.data_ptr<float>(), (int)w.size(0), (int)w.size(1),
+                                   (int)w.size(2), (int)rows, (int)cols, (int)cpad, (int)mode, cur_stream()));
+  return out;
 }
 
 // Shapley prefix-delta operands: z (B, C) block output, W (N, C) next Linear, perm (n) int32
@@ -516,8 +539,11 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
 
 // Weight gradient: g (B, Ho, Wo, Cout) and x (B, H, W, Cin) NHWC -> dW (Cout, Kpad) with column
 // k = (kh, kw, ci) (Kpad = ks*ks*Cin rounded up to 32; padded columns are zero).
+// ``out`` (optional): the parameter-shaped gradient (Cout_r, Cin_r, ks, ks), any strides, written
+// directly (real channels only); the (Cout, Kpad) GEMM result is then not materialised and an
+// empty tensor is returned.
 at::Tensor conv_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t ks, int64_t stride, int64_t pad, int64_t cfg,
-                      int64_t splits) {
+                      int64_t splits, const c10::optional<at::Tensor>& out) {
   need(g, "g", 4);
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = g.size(3);
@@ -527,17 +553,32 @@ at::Tensor conv_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t ks, int6
   TORCH_CHECK(g.size(0) == B && g.size(1) == Ho && g.size(2) == Wo, "g must be (B, Ho, Wo, Cout) of this conv");
   const int64_t Kpad = (ks * ks * Cin + 31) / 32 * 32;
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
-  auto dw = at::empty({Cout, Kpad}, g.options());
+  float* fin = nullptr;
+  long long fs[4] = {0, 0, 0, 0};
+  int fco = 0, fci = 0;
+  if (out.has_value()) {
+    const at::Tensor& o = *out;
+    TORCH_CHECK(o.is_cuda() && o.scalar_type() == at::kFloat && o.dim() == 4 && o.device() == g.device(),
+                "out must be a float32 (Cout, Cin, ks, ks) tensor on the device");
+    TORCH_CHECK(o.size(0) <= Cout && o.size(1) <= Cin && o.size(2) == ks && o.size(3) == ks && o.size(0) > 0 &&
+                    o.size(1) > 0, "out must be (Cout_r <= Cout, Cin_r <= Cin, ks, ks)");
+    fin = o.data_ptr<float>();
+    fco = (int)o.size(0);
+    fci = (int)o.size(1);
+    for (int i = 0; i < 4; ++i) fs[i] = o.stride(i);
+  }
+  at::Tensor dw = fin ? at::Tensor() : at::empty({Cout, Kpad}, g.options());
   const int64_t slices = (B * Ho * Wo + 31) / 32;
   int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, slices));
   const int64_t per = (slices + sp - 1) / sp;
   sp = (slices + per - 1) / per;
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * Cout * Kpad}, g.options());
-  TP_CHECK_HIP(tp_conv_wgrad(g.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(),
-                             sp > 1 ? ws.data_ptr<float>() : nullptr, (int)B, (int)H, (int)W, (int)Cin, (int)Cout,
-                             (int)ks, (int)stride, (int)pad, (int)Kpad, (int)cfg, (int)sp, cur_stream()));
-  return dw;
+  TP_CHECK_HIP(tp_conv_wgrad2(g.data_ptr<float>(), x.data_ptr<float>(), fin ? nullptr : dw.data_ptr<float>(),
+                              sp > 1 ? ws.data_ptr<float>() : nullptr, (int)B, (int)H, (int)W, (int)Cin, (int)Cout,
+                              (int)ks, (int)stride, (int)pad, (int)Kpad, (int)cfg, (int)sp, fin, fco, fci,
+                              fin ? fs : nullptr, cur_stream()));
+  return fin ? at::empty({0}, g.options()) : dw;  // with ``out`` the result is in ``out``
 }
 
 // Training-mode BatchNorm over the last dim of an NHWC activation x (..., C), C % 4 == 0.
@@ -628,7 +669,9 @@ void register_engine_ops_def(torch::Library& m) {
         "float eps, float momentum, Tensor? res=None, bool relu=False) -> (Tensor, Tensor, Tensor)");
   m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx, Tensor? ym=None, "
         "bool want_dres=False) -> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits) -> Tensor");
+  m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "
+        "-> Tensor");
+  m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
@@ -637,7 +680,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
         "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0, float slope=0.0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
-  m.def("wino_weights(Tensor w, bool flip_t) -> Tensor");
+  m.def("wino_weights(Tensor w, bool flip_t, int K=0, int C=0) -> Tensor");
   m.def("prefix_tri_operands(Tensor z, Tensor w, Tensor perm, int p0, int cnt, int Kc) -> (Tensor, Tensor)");
   m.def("prefix_delta(Tensor T, Tensor wsub, Tensor neg_one, Tensor y0, bool relu, float slope, int cfg) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "
@@ -661,6 +704,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_gen", &conv_gen);
   m.impl("conv_gen_bwd", &conv_gen_bwd);
   m.impl("conv_wgrad", &conv_wgrad);
+  m.impl("pack_conv_weight", &pack_conv_weight);
   m.impl("bn_train_fwd", &bn_train_fwd);
   m.impl("bn_train_bwd", &bn_train_bwd);
   m.impl("unpool2_nhwc", &unpool2_nhwc);

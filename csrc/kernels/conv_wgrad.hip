@@ -28,7 +28,21 @@ struct WgradArgs {
   int slices_per_split;
   long long g_elems, x_elems;
   FastDiv fd_hwo, fd_wo;  // pixel -> (image, oh, ow) decode without integer divisions
+  // optional final layout: the parameter gradient (fin_co, fin_ci, ks, ks) with element strides
+  // fs[4], written straight from the GEMM tile (no split) or the split combine
+  float* fin;
+  int fin_co, fin_ci;
+  long long fs[4];
 };
+
+// column k = (kh*ks + kw)*Cin + ci of the (Cout, Kpad) GEMM -> offset in the final layout, or -1
+__device__ __forceinline__ long long wgrad_fin_off(const WgradArgs& p, int co, int k) {
+  if (co >= p.fin_co || k >= p.Kc) return -1;
+  const int tap = k / p.Cin, ci = k - tap * p.Cin;
+  if (ci >= p.fin_ci) return -1;
+  const int kh = tap / p.ks, kw = tap - kh * p.ks;
+  return co * p.fs[0] + ci * p.fs[1] + kh * p.fs[2] + kw * p.fs[3];
+}
 
 template <int BM, int BN, int WM, int WN>
 struct WTile {
@@ -146,6 +160,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradAr
   }
 
   float* out = p.out + (long long)blockIdx.y * p.Cout * p.Kpad;
+  const bool fin = p.fin && gridDim.y == 1;
 #pragma unroll
   for (int i = 0; i < T::TM; ++i)
 #pragma unroll
@@ -154,9 +169,27 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradAr
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = co0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (co < p.Cout && k < p.Kpad) out[(long long)co * p.Kpad + k] = acc[i][j][r];
+        if (fin) {
+          const long long o = wgrad_fin_off(p, co, k);
+          if (o >= 0) p.fin[o] = acc[i][j][r];
+        } else if (co < p.Cout && k < p.Kpad) {
+          out[(long long)co * p.Kpad + k] = acc[i][j][r];
+        }
       }
     }
+}
+
+// split combine straight into the final layout (one thread per GEMM element, split order)
+__global__ __launch_bounds__(256) void wgrad_combine_fin(const float* __restrict__ slabs, WgradArgs p, int splits) {
+  const long long n = (long long)p.Cout * p.Kpad;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(t / p.Kpad), k = (int)(t - (long long)co * p.Kpad);
+    const long long o = wgrad_fin_off(p, co, k);
+    if (o < 0) continue;
+    float s = slabs[t];
+    for (int q = 1; q < splits; ++q) s += slabs[q * n + t];
+    p.fin[o] = s;
+  }
 }
 
 // dW = sum of the split slabs in split order (float4 per thread); columns >= Kc are zero.
@@ -194,12 +227,21 @@ hipError_t launch_wgrad(const tp::WgradArgs& a, int splits, hipStream_t st) {
 // (4 waves of 64x32). ``ws`` holds splits*Cout*Kpad floats (may alias dw when splits == 1).
 // x (B, H, W, Cin) NHWC with Cin % 4 == 0; g (B, Ho, Wo, Cout) NHWC with Cout % 4 == 0;
 // dw (Cout, Kpad), Kpad % 32 == 0 and >= ks*ks*Cin.
-extern "C" hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,
-                                    int Cin, int Cout, int ks, int stride, int pad, int Kpad, int cfg, int splits,
-                                    hipStream_t st) {
+// fin (nullable): also/instead write the parameter-layout gradient (fin_co <= Cout, fin_ci <= Cin,
+// ks, ks) with element strides fs[4]; dw is then not written (may be null).
+extern "C" hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,
+                                     int Cin, int Cout, int ks, int stride, int pad, int Kpad, int cfg, int splits,
+                                     float* fin, int fin_co, int fin_ci, const long long* fs, hipStream_t st) {
   using namespace tp;
   if (Cin % 4 || Cout % 4 || Kpad % 32 || Kpad < ks * ks * Cin || splits < 1) return hipErrorInvalidValue;
+  if (fin && (fin_co > Cout || fin_ci > Cin || fin_co <= 0 || fin_ci <= 0 || !fs)) return hipErrorInvalidValue;
+  if (!fin && !dw) return hipErrorInvalidValue;
   WgradArgs a{};
+  a.fin = fin;
+  a.fin_co = fin_co;
+  a.fin_ci = fin_ci;
+  if (fin)
+    for (int i = 0; i < 4; ++i) a.fs[i] = fs[i];
   a.g = g;
   a.x = x;
   a.B = B;
@@ -234,8 +276,20 @@ extern "C" hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, f
     default: return hipErrorInvalidValue;
   }
   if (e != hipSuccess || splits == 1) return e;
+  if (fin) {
+    const unsigned grid = (unsigned)std::min<long long>(ceil_div((long long)Cout * Kpad, 256), 4096);
+    wgrad_combine_fin<<<grid, 256, 0, st>>>(ws, a, splits);
+    return hipGetLastError();
+  }
   const long long n4 = (long long)Cout * Kpad / 4;
   const unsigned grid = (unsigned)std::min<long long>(ceil_div(n4, 256), 4096);
   wgrad_combine<<<grid, 256, 0, st>>>(ws, dw, splits, n4);
   return hipGetLastError();
+}
+
+extern "C" hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,
+                                    int Cin, int Cout, int ks, int stride, int pad, int Kpad, int cfg, int splits,
+                                    hipStream_t st) {
+  return tp_conv_wgrad2(g, x, dw, ws, B, H, W, Cin, Cout, ks, stride, pad, Kpad, cfg, splits, nullptr, 0, 0, nullptr,
+                        st);
 }

@@ -731,7 +731,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
 // read from the forward weight directly (no flipped / transposed copy).
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void wino_weight_transform(const float* __restrict__ w, float* __restrict__ u,
-                                                             int K, int C, int flip_t) {
+                                                             int K, int C, int flip_t, int S0, int S1) {
   const long long total = (long long)(C / 8) * (K / 32) * W_UIMG;
   const double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -743,16 +743,20 @@ __global__ __launch_bounds__(256) void wino_weight_transform(const float* __rest
     const int g = gs ^ ((j >> 3) << 1);
     const int c = 8 * cb + 2 * g + e, k = 32 * kb + j + 16 * n;
     const int i = xi >> 2, jj = xi & 3;
-    // source (K, C, 3, 3): forward w[k][c]; flip_t: the forward weight is (C, K, 3, 3) -> w[c][k] rotated
-    const float* src = flip_t ? w + ((long long)c * K + k) * 9 : w + ((long long)k * C + c) * 9;
+    // source (S0, S1, 3, 3), unpadded: forward w[k][c]; flip_t: the forward weight w[c][k] rotated.
+    // (k, c) outside the source are the zero padding of the kernels' channel granules.
+    const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
     double acc = 0.0;
+    if (r0 < S0 && r1 < S1) {
+      const float* src = w + ((long long)r0 * S1 + r1) * 9;
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
+      for (int a = 0; a < 3; ++a)
 #pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const int tap = flip_t ? (2 - a) * 3 + (2 - b) : a * 3 + b;
-        acc += G[i][a] * (double)src[tap] * G[jj][b];
-      }
+        for (int b = 0; b < 3; ++b) {
+          const int tap = flip_t ? (2 - a) * 3 + (2 - b) : a * 3 + b;
+          acc += G[i][a] * (double)src[tap] * G[jj][b];
+        }
+    }
     u[t] = (float)acc;
   }
 }
@@ -957,14 +961,22 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
 
 extern "C" int tp_wino_taylor_slots(int H, int W) { return tp::wino_taylor_slots(H, W); }
 
-// w: (K, C, 3, 3) (flip_t = 0) or the forward weight (C, K, 3, 3) of which the dgrad operand is
-// wanted (flip_t = 1); u: (C/8, K/32, 4096) images. K % 32 == 0, C % 8 == 0.
-extern "C" hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st) {
-  if (K % 32 || C % 8 || K <= 0 || C <= 0) return hipErrorInvalidValue;
+// w: (S0, S1, 3, 3) = the forward weight (Cout, Cin, 3, 3), possibly narrower than the padded
+// GEMM: flip_t = 0 -> U of (K = Cout_p, C = Cin_p); flip_t = 1 -> the dgrad operand, (K = Cin_p,
+// C = Cout_p) with rotated taps. u: (C/8, K/32, 4096) images. K % 32 == 0, C % 8 == 0.
+extern "C" hipError_t tp_wino_weights2(const float* w, float* u, int K, int C, int flip_t, int S0, int S1,
+                                       hipStream_t st) {
+  if (K % 32 || C % 8 || K <= 0 || C <= 0 || S0 <= 0 || S1 <= 0) return hipErrorInvalidValue;
+  if (flip_t ? (S0 > C || S1 > K) : (S0 > K || S1 > C)) return hipErrorInvalidValue;
   const long long total = (long long)(C / 8) * (K / 32) * tp::W_UIMG;
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
-  tp::wino_weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t);
+  tp::wino_weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1);
   return hipGetLastError();
+}
+
+// w padded to the GEMM: (K, C, 3, 3) (flip_t = 0) or (C, K, 3, 3) (flip_t = 1)
+extern "C" hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st) {
+  return tp_wino_weights2(w, u, K, C, flip_t, flip_t ? C : K, flip_t ? K : C, st);
 }
 
 extern "C" int tp_wino_staged_ok(int H, int W, int unpool) {

@@ -5,7 +5,8 @@ import sys
 rows = [json.loads(line) for line in sys.stdin if line.startswith("{")]
 if rows:
     c = rows[0]["config"]
-    print("config:", {k: c[k] for k in ("noise", "modes", "teacher_steps", "ft_steps", "final_ft_steps")})
+    print("config:", {k: c.get(k) for k in ("noise", "modes", "teacher_steps", "teacher_wd", "ft_steps",
+                                             "final_ft_steps", "score_imgs", "increments", "recal_batches")})
 gaps = []
 for r in rows:
     gap = r["top1_pruned_taylor"] - r["top1_pruned_random"]

@@ -98,25 +98,23 @@ class _NativeConv2d(torch.autograd.Function):
         if cin_p != Cin:
             xh = F.pad(xh, (0, cin_p - Cin))
         xh = xh.float().contiguous()
-        wp = F.pad(weight.detach().float(), (0, 0, 0, 0, 0, cin_p - Cin, 0, cout_p - Cout))
-        wk = wp.permute(0, 2, 3, 1).reshape(cout_p, -1)
+        w32 = weight.detach().float().contiguous()  # the parameter itself for fp32 weights: no copy
         kk = T.conv_gen_k(ks, cin_p)
-        if kk != wk.shape[1]:
-            wk = F.pad(wk, (0, kk - wk.shape[1]))
-        wk = wk.contiguous()
         shift = F.pad(bias.detach().float(), (0, cout_p - Cout)).contiguous() if bias is not None else None
         Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
         M = B * Ho * Wo
 
         wino = _wino_ok(ks, stride, pad, H, W, cin_p, cout_p)
-        cache = {}
+        cache = {}  # padded operands, built on first use by one HIP launch each (weights change every step)
 
         def run(cfg, sp):
             if cfg in (WINO, WINO_LDS):  # Winograd F(2x2,3x3): 2.25x fewer multiplies
-                if "u" not in cache:  # one transform launch per step (weights change every step)
-                    cache["u"] = T.wino_weights(wp.contiguous(), False)
+                if "u" not in cache:
+                    cache["u"] = T.wino_weights(w32, False, cout_p, cin_p)
                 return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
-            return T.conv_gen(xh, wk, None, shift, False, None, None, ks, stride, pad, cfg, sp)
+            if "wk" not in cache:  # [cout_p][(kh, kw, ci)] zero-padded GEMM operand
+                cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
+            return T.conv_gen(xh, cache["wk"], None, shift, False, None, None, ks, stride, pad, cfg, sp)
 
         cands = TUNER.candidates(M, cout_p, kk)
         if wino:
@@ -126,16 +124,15 @@ class _NativeConv2d(torch.autograd.Function):
         y = run(cfg, sp)
         if cout_p != Cout:
             y = y[..., :Cout].contiguous()
-        ctx.save_for_backward(xh, wp)
-        ctx.geom = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride())
+        ctx.save_for_backward(xh, w32)
+        ctx.geom = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride(), cin_p, cout_p)
         return _as_nchw(y)
 
     @staticmethod
     def backward(ctx, gy):
         T = ops.require()
-        xh, wp = ctx.saved_tensors
-        ks, stride, pad, Cin, Cout, H, W, has_bias, wdtype, w_strides = ctx.geom
-        cout_p, cin_p = wp.shape[0], wp.shape[1]
+        xh, w32 = ctx.saved_tensors
+        ks, stride, pad, Cin, Cout, H, W, has_bias, wdtype, w_strides, cin_p, cout_p = ctx.geom
         g = gy.permute(0, 2, 3, 1).float()
         if cout_p != Cout:
             g = F.pad(g, (0, cout_p - Cout))
@@ -144,23 +141,22 @@ class _NativeConv2d(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             if ks != 7:
-                if stride == 1:  # dgrad = stride-1 conv of g with flipped taps, padding ks-1-pad
-                    wt = wp.flip(2, 3).permute(1, 2, 3, 0).reshape(cin_p, -1).contiguous()
-                    pad_b, transposed = ks - 1 - pad, False
-                else:  # strided 1x1 / 3x3: transposed gather kernel, natural tap order
-                    wt = wp.permute(1, 2, 3, 0).reshape(cin_p, -1).contiguous()
-                    pad_b, transposed = pad, True
-                M, K = B * H * W, wt.shape[1]
-
+                # stride 1: dgrad = stride-1 conv of g with flipped taps, padding ks-1-pad;
+                # strided 1x1 / 3x3: transposed gather kernel, natural tap order
+                transposed = stride != 1
+                pad_b = pad if transposed else ks - 1 - pad
+                M, K = B * H * W, ks * ks * cout_p
                 wino = not transposed and _wino_ok(ks, 1, pad_b, Ho, Wo, cout_p, cin_p)
                 cache = {}
 
                 def run(cfg, sp):
                     if cfg in (WINO, WINO_LDS):  # stride-1 3x3 dgrad = Winograd conv of g, flipped taps
                         if "ut" not in cache:
-                            cache["ut"] = T.wino_weights(wp.contiguous(), True)
+                            cache["ut"] = T.wino_weights(w32, True, cin_p, cout_p)
                         return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
-                    return T.conv_gen_bwd(g, wt, None, 1, None, ks, stride if transposed else 1, pad_b, H, W,
+                    if "wt" not in cache:  # [ci][(kh, kw, co)], flipped for stride 1
+                        cache["wt"] = T.pack_conv_weight(w32, cin_p, K, cout_p, 2 if transposed else 1)
+                    return T.conv_gen_bwd(g, cache["wt"], None, 1, None, ks, stride if transposed else 1, pad_b, H, W,
                                           transposed, cfg, sp)
 
                 cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
@@ -171,13 +167,16 @@ class _NativeConv2d(torch.autograd.Function):
                 dxh = run(cfg, sp)[..., :Cin]
                 dx = dxh.permute(0, 3, 1, 2).to(gy.dtype)
             else:  # 7x7 stem input gradient (rarely needed: the input is data)
-                dx = torch.nn.grad.conv2d_input((B, Cin, H, W), wp[:Cout, :Cin].to(gy.dtype), gy, stride, pad)
+                dx = torch.nn.grad.conv2d_input((B, Cin, H, W), w32.to(gy.dtype), gy, stride, pad)
         if ctx.needs_input_grad[1]:
             kk = -(-ks * ks * cin_p // 32) * 32
             P = B * Ho * Wo
+            # the gradient takes the parameter's exact strides (DDP bucket views expect them), written
+            # by the wgrad kernel / its split combine straight from the GEMM (no re-layout copies)
+            dw32 = torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=torch.float32, device=g.device)
 
             def run_w(cfg, sp):
-                return T.conv_wgrad(g, xh, ks, stride, pad, cfg, sp)
+                return T.conv_wgrad(g, xh, ks, stride, pad, cfg, sp, dw32)
 
             cands = []
             for cfg, (bm, bn) in ((0, (128, 128)), (2, (128, 64)), (1, (64, 64))):
@@ -185,10 +184,9 @@ class _NativeConv2d(torch.autograd.Function):
                 cands += [(cfg, sp)] + ([(cfg, sp // 2)] if sp > 1 else [])
             cfg, sp = TUNER.choose(("twgrad", tuple(g.shape), tuple(xh.shape), ks, stride, pad), cout_p, kk, P, run_w,
                                    cands=cands)
-            dwk = run_w(cfg, sp)
-            dw = dwk[:Cout, :ks * ks * cin_p].view(Cout, ks, ks, cin_p)[..., :Cin].permute(0, 3, 1, 2)
-            # the gradient takes the parameter's exact strides (DDP bucket views expect them)
-            dw = torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=wdtype, device=dwk.device).copy_(dw)
+            run_w(cfg, sp)
+            dw = dw32 if wdtype == torch.float32 else \
+                torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=wdtype, device=g.device).copy_(dw32)
         if has_bias and ctx.needs_input_grad[2]:
             db = gy.sum((0, 2, 3))
         return dx, dw, db, None, None, None
