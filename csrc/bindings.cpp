@@ -296,6 +296,48 @@ at::Tensor dropout(const at::Tensor& x_, int64_t seed, double p) {
   return y;
 }
 
+// Training max-pool on NHWC (B, H, W, C), C % 4 == 0: (y, window-local argmax bytes); the
+// backward gathers (deterministic). avgpool_bwd: global average pool gradient (B, C) -> (B, H, W, C).
+std::tuple<at::Tensor, at::Tensor> maxpool_train_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad) {
+  check_cuda_f32(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.size(3) % 4 == 0, "x must be contiguous NHWC with C % 4 == 0");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(k >= 1 && k * k <= 255 && s >= 1 && pad >= 0 && 2 * pad <= k && Ho > 0 && Wo > 0, "bad pool geometry");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({B, Ho, Wo, C}, x.options());
+  auto am = at::empty({B, Ho, Wo, C}, x.options().dtype(at::kByte));
+  TP_CHECK_HIP(tp_maxpool_fwd_arg(x.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(), (int)B, (int)H,
+                                  (int)W, (int)C, (int)k, (int)s, (int)pad, cur_stream()));
+  return {y, am};
+}
+
+at::Tensor maxpool_train_bwd(const at::Tensor& g_, const at::Tensor& am, int64_t H, int64_t W, int64_t k, int64_t s,
+                             int64_t pad) {
+  check_cuda_f32(g_, "g");
+  auto g = g_.contiguous();
+  TORCH_CHECK(g.dim() == 4 && am.sizes() == g.sizes() && am.scalar_type() == at::kByte && am.is_contiguous() &&
+                  am.device() == g.device(), "am must be the forward's (B, Ho, Wo, C) uint8 argmax");
+  const int64_t B = g.size(0), C = g.size(3);
+  TORCH_CHECK(g.size(1) == (H + 2 * pad - k) / s + 1 && g.size(2) == (W + 2 * pad - k) / s + 1, "g shape mismatch");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  auto dx = at::empty({B, H, W, C}, g.options());
+  TP_CHECK_HIP(tp_maxpool_bwd(g.data_ptr<float>(), am.data_ptr<uint8_t>(), dx.data_ptr<float>(), (int)B, (int)H,
+                              (int)W, (int)C, (int)k, (int)s, (int)pad, cur_stream()));
+  return dx;
+}
+
+at::Tensor avgpool_bwd(const at::Tensor& g_, int64_t H, int64_t W) {
+  check_cuda_f32(g_, "g");
+  auto g = g_.contiguous();
+  TORCH_CHECK(g.dim() == 2 && g.size(1) % 4 == 0 && H > 0 && W > 0, "g must be (B, C) with C % 4 == 0");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  auto dx = at::empty({g.size(0), H, W, g.size(1)}, g.options());
+  TP_CHECK_HIP(tp_avgpool_bwd(g.data_ptr<float>(), dx.data_ptr<float>(), (int)g.size(0), (int)(H * W),
+                              (int)g.size(1), cur_stream()));
+  return dx;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tpamd, m) {
@@ -311,6 +353,9 @@ TORCH_LIBRARY(tpamd, m) {
   m.def("cross_entropy(Tensor logits, Tensor target, float gscale, bool want_grad) -> (Tensor, Tensor)");
   m.def("augment_u8(Tensor src, Tensor idx, Tensor? aug, int pad, Tensor mean, Tensor inv_std) -> Tensor");
   m.def("dropout(Tensor x, int seed, float p) -> Tensor");
+  m.def("maxpool_train_fwd(Tensor x, int k, int s, int pad) -> (Tensor, Tensor)");
+  m.def("maxpool_train_bwd(Tensor g, Tensor am, int H, int W, int k, int s, int pad) -> Tensor");
+  m.def("avgpool_bwd(Tensor g, int H, int W) -> Tensor");
   register_engine_ops_def(m);
 }
 
@@ -327,5 +372,8 @@ TORCH_LIBRARY_IMPL(tpamd, CUDA, m) {
   m.impl("cross_entropy", &cross_entropy);
   m.impl("augment_u8", &augment_u8);
   m.impl("dropout", &dropout);
+  m.impl("maxpool_train_fwd", &maxpool_train_fwd);
+  m.impl("maxpool_train_bwd", &maxpool_train_bwd);
+  m.impl("avgpool_bwd", &avgpool_bwd);
   register_engine_ops_impl(m);
 }

@@ -27,6 +27,11 @@ hipError_t tp_cross_entropy(const float* logits, const int64_t* target, float* l
                             float gscale, hipStream_t st);
 // train_ops.hip
 hipError_t tp_dropout(const float* x, float* y, long long n, unsigned long long seed, double p, hipStream_t st);
+hipError_t tp_maxpool_fwd_arg(const float* x, float* y, uint8_t* am, int B, int H, int W, int C, int k, int s, int pad,
+                              hipStream_t st);
+hipError_t tp_maxpool_bwd(const float* g, const uint8_t* am, float* dx, int B, int H, int W, int C, int k, int s,
+                          int pad, hipStream_t st);
+hipError_t tp_avgpool_bwd(const float* g, float* dx, int B, int HW, int C, hipStream_t st);
 // data_ops.hip
 hipError_t tp_augment_u8(const uint8_t* src, const int64_t* idx, const int* aug, int B, int C, int H, int W, int pad,
                          const float* mean, const float* inv_std, float* out, hipStream_t st);

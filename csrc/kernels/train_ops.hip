@@ -72,3 +72,125 @@ extern "C" hipError_t tp_dropout(const float* x, float* y, long long n, unsigned
   if (n % 4) tp::dropout_tail<<<1, 4, 0, st>>>(x, y, n, n4, seed, threshold, scale);
   return hipGetLastError();
 }
+
+// ---- max-pool (k x k, stride s, padding p) with a window-local argmax byte, and its backward
+// as a gather (each input pixel sums the gradients of the windows whose argmax it is, in a fixed
+// window order: deterministic, no atomics). Tie / NaN rule of PyTorch's max_pool2d: a later tap
+// wins only if it is greater or NaN; the index starts at the first in-image tap.
+namespace tp {
+
+__global__ __launch_bounds__(256) void maxpool_fwd_arg(const float* __restrict__ x, float* __restrict__ y,
+                                                       uint8_t* __restrict__ am, int B, int H, int W, int C, int k,
+                                                       int s, int pad, int Ho, int Wo) {
+  const long long total = (long long)B * Ho * Wo * (C / 4);
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % (C / 4));
+    const long long r = t / (C / 4);
+    const int ow = (int)(r % Wo), oh = (int)((r / Wo) % Ho);
+    const long long b = r / ((long long)Wo * Ho);
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int arg[4] = {-1, -1, -1, -1};
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * s - pad + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * s - pad + kw;
+        if (iw < 0 || iw >= W) continue;
+        const float4 v4 = *reinterpret_cast<const float4*>(x + ((b * H + ih) * W + iw) * C + c4 * 4);
+        const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (arg[q] < 0) arg[q] = kh * k + kw;  // initial index: the first in-image tap
+          if (v[q] > best[q] || v[q] != v[q]) {
+            best[q] = v[q];
+            arg[q] = kh * k + kw;
+          }
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(y + r * C + c4 * 4) = make_float4(best[0], best[1], best[2], best[3]);
+    const unsigned packed = (unsigned)(arg[0] & 0xff) | ((unsigned)(arg[1] & 0xff) << 8) |
+                            ((unsigned)(arg[2] & 0xff) << 16) | ((unsigned)(arg[3] & 0xff) << 24);
+    *reinterpret_cast<unsigned*>(am + r * C + c4 * 4) = packed;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_gather(const float* __restrict__ g, const uint8_t* __restrict__ am,
+                                                          float* __restrict__ dx, int B, int H, int W, int C, int k,
+                                                          int s, int pad, int Ho, int Wo) {
+  const long long total = (long long)B * H * W * (C / 4);
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % (C / 4));
+    const long long r = t / (C / 4);
+    const int iw = (int)(r % W), ih = (int)((r / W) % H);
+    const long long b = r / ((long long)W * H);
+    // windows oh with oh*s - pad <= ih <= oh*s - pad + k - 1
+    const int oh0 = max(0, (ih + pad - k + s) / s), oh1 = min(Ho - 1, (ih + pad) / s);
+    const int ow0 = max(0, (iw + pad - k + s) / s), ow1 = min(Wo - 1, (iw + pad) / s);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const int th = ih - (oh * s - pad);
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const unsigned want = (unsigned)(th * k + iw - (ow * s - pad));
+        const long long o = ((b * Ho + oh) * Wo + ow) * C + c4 * 4;
+        const unsigned a = *reinterpret_cast<const unsigned*>(am + o);
+        const float4 gv = *reinterpret_cast<const float4*>(g + o);
+        if ((a & 0xffu) == want) acc.x += gv.x;
+        if (((a >> 8) & 0xffu) == want) acc.y += gv.y;
+        if (((a >> 16) & 0xffu) == want) acc.z += gv.z;
+        if ((a >> 24) == want) acc.w += gv.w;
+      }
+    }
+    *reinterpret_cast<float4*>(dx + r * C + c4 * 4) = acc;
+  }
+}
+
+// global average pool backward: dx[b][p][c] = g[b][c] / HW
+__global__ __launch_bounds__(256) void avgpool_bwd(const float* __restrict__ g, float* __restrict__ dx, int B, int HW,
+                                                   int C) {
+  const long long total = (long long)B * HW * (C / 4);
+  const float inv = 1.f / (float)HW;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % (C / 4));
+    const long long b = t / ((long long)(C / 4) * HW);
+    const float4 v = *reinterpret_cast<const float4*>(g + b * C + c4 * 4);
+    reinterpret_cast<float4*>(dx)[t] = make_float4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
+  }
+}
+
+}  // namespace tp
+
+extern "C" hipError_t tp_maxpool_fwd_arg(const float* x, float* y, uint8_t* am, int B, int H, int W, int C, int k,
+                                         int s, int pad, hipStream_t st) {
+  if (C % 4 || k < 1 || k * k > 255 || s < 1 || pad < 0 || 2 * pad > k) return hipErrorInvalidValue;
+  const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
+  if (Ho <= 0 || Wo <= 0) return hipErrorInvalidValue;
+  const long long total = (long long)B * Ho * Wo * (C / 4);
+  if (total == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::maxpool_fwd_arg<<<grid, 256, 0, st>>>(x, y, am, B, H, W, C, k, s, pad, Ho, Wo);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_maxpool_bwd(const float* g, const uint8_t* am, float* dx, int B, int H, int W, int C, int k,
+                                     int s, int pad, hipStream_t st) {
+  if (C % 4 || k < 1 || k * k > 255 || s < 1 || pad < 0 || 2 * pad > k) return hipErrorInvalidValue;
+  const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
+  const long long total = (long long)B * H * W * (C / 4);
+  if (total == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::maxpool_bwd_gather<<<grid, 256, 0, st>>>(g, am, dx, B, H, W, C, k, s, pad, Ho, Wo);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t tp_avgpool_bwd(const float* g, float* dx, int B, int HW, int C, hipStream_t st) {
+  if (C % 4 || HW <= 0) return hipErrorInvalidValue;
+  const long long total = (long long)B * HW * (C / 4);
+  if (total == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+  tp::avgpool_bwd<<<grid, 256, 0, st>>>(g, dx, B, HW, C);
+  return hipGetLastError();
+}

@@ -278,3 +278,94 @@ def test_native_linear_training(cuda, B, cin, cout):
     torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(lin.weight.grad.double(), l64.weight.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(lin.bias.grad.double(), l64.bias.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("O,I,KS,cpad_i,cpad_o", [(64, 32, 3, 32, 64), (40, 36, 3, 64, 64), (64, 3, 7, 4, 64),
+                                                   (52, 20, 1, 32, 64), (30, 17, 5, 32, 32)])
+def test_pack_conv_weight(cuda, O, I, KS, cpad_i, cpad_o):
+    """Weight re-layout kernel == the padded / permuted / flipped torch expressions it replaces."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    w = torch.randn(O, I, KS, KS, device=cuda)
+    wp = F.pad(w, (0, 0, 0, 0, 0, cpad_i - I, 0, cpad_o - O))
+    kk = -(-KS * KS * cpad_i // 32) * 32
+    ref0 = F.pad(wp.permute(0, 2, 3, 1).reshape(cpad_o, -1), (0, kk - KS * KS * cpad_i))
+    assert torch.equal(T.pack_conv_weight(w, cpad_o, kk, cpad_i, 0), ref0)
+    ref1 = wp.flip(2, 3).permute(1, 2, 3, 0).reshape(cpad_i, -1)
+    assert torch.equal(T.pack_conv_weight(w, cpad_i, KS * KS * cpad_o, cpad_o, 1), ref1)
+    ref2 = wp.permute(1, 2, 3, 0).reshape(cpad_i, -1)
+    assert torch.equal(T.pack_conv_weight(w, cpad_i, KS * KS * cpad_o, cpad_o, 2), ref2)
+
+
+@pytest.mark.parametrize("O,I", [(40, 36), (64, 32)])
+def test_wino_weights_padded_source(cuda, O, I):
+    """Winograd images from an UNPADDED weight == images of the zero-padded weight."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    from torchpruner_amd.engine.fused_chain import cpad
+    op, ip = cpad(O), cpad(I)
+    w = torch.randn(O, I, 3, 3, device=cuda)
+    wp = F.pad(w, (0, 0, 0, 0, 0, ip - I, 0, op - O))
+    assert torch.equal(T.wino_weights(w, False, op, ip), T.wino_weights(wp, False))
+    assert torch.equal(T.wino_weights(w, True, ip, op), T.wino_weights(wp, True))
+
+
+@pytest.mark.parametrize("splits", [1, 5])
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_conv_wgrad_param_layout(cuda, splits, channels_last):
+    """conv_wgrad writing the parameter-shaped gradient (real channels, any strides) directly ==
+    the sliced / permuted GEMM result."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    g = torch.Generator().manual_seed(splits)
+    B, H, W, Cin_p, Cout_p, Cin, Cout, ks = 2, 10, 12, 64, 64, 50, 44, 3
+    x = torch.randn(B, H, W, Cin_p, generator=g).to(cuda)
+    x[..., Cin:] = 0
+    gy = torch.randn(B, H, W, Cout_p, generator=g).to(cuda)
+    gy[..., Cout:] = 0
+    dwk = T.conv_wgrad(gy, x, ks, 1, 1, 0, splits)
+    ref = dwk[:Cout, :ks * ks * Cin_p].view(Cout, ks, ks, Cin_p)[..., :Cin].permute(0, 3, 1, 2)
+    out = torch.full((Cout, Cin, ks, ks), float("nan"), device=cuda)
+    if channels_last:
+        out = out.contiguous(memory_format=torch.channels_last)
+    T.conv_wgrad(gy, x, ks, 1, 1, 0, splits, out)
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (2, 2, 0), (3, 1, 1), (5, 3, 2)])
+def test_native_maxpool_training(cuda, k, s, p):
+    """Native max-pool (argmax byte + gather backward) == ATen max_pool2d, incl. ReLU-zero ties and
+    NaN propagation (forward value and the gradient's routing)."""
+    from torchpruner_amd.engine.train import native_convs
+    torch.manual_seed(k * 10 + s)
+    x = F.relu(torch.randn(3, 8, 13, 11, device=cuda)).contiguous(memory_format=torch.channels_last)
+    x[0, 1, 4, 5] = float("nan")
+    mp = torch.nn.MaxPool2d(k, s, p)
+    xa = x.detach().clone().requires_grad_(True)
+    xb = x.detach().clone().requires_grad_(True)
+    with native_convs(mp):
+        assert "forward" in mp.__dict__
+        ya = mp(xa)
+    yb = F.max_pool2d(xb, k, s, p)
+    torch.testing.assert_close(ya, yb, equal_nan=True)
+    g = torch.randn_like(yb)
+    g[torch.isnan(yb)] = 0.0
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-6, atol=1e-6)
+
+
+def test_native_global_avgpool_training(cuda):
+    from torchpruner_amd.engine.train import native_convs
+    torch.manual_seed(3)
+    x = torch.randn(4, 64, 7, 7, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    gap = torch.nn.AdaptiveAvgPool2d((1, 1))
+    with native_convs(gap):
+        y = gap(x)
+    y2 = F.adaptive_avg_pool2d(x2, 1)
+    torch.testing.assert_close(y, y2, rtol=1e-5, atol=1e-6)
+    g = torch.randn_like(y2)
+    y.backward(g)
+    y2.backward(g)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-6, atol=1e-7)

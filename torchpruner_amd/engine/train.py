@@ -14,8 +14,10 @@ convolutions of a model run on the precompiled gfx950 kernels instead, through a
 
 Training-mode ``BatchNorm2d`` runs on deterministic NHWC batch-statistics / normalisation /
 backward kernels (K5, ``tpamd.bn_train_*``), training-mode ``nn.Dropout`` on a counter-based
-Philox kernel (K7b, mask regenerated in the backward); activations, pooling and the loss stay PyTorch ops
-(autograd composes them), so any model works; only modules the kernels support are switched. Pruned (odd)
+Philox kernel (K7b, mask regenerated in the backward), max-pool (argmax byte + gather backward)
+and global average pool on NHWC kernels, ``nn.Linear`` on the MFMA GEMM; the loss and the optimizer
+stay PyTorch ops (autograd composes everything), so any model works; only modules the kernels
+support are switched. Pruned (odd)
 channel counts are zero-padded to the kernels' granule inside the op and sliced off again:
 the parameters, their gradients and the optimizer state keep the module's real shapes.
 Every kernel choice is timed once per shape (``TUNER``, like ``cudnn.benchmark``) — a few
@@ -349,6 +351,65 @@ def _native_bn_forward(self, x):
     return _NativeBN2d.apply(x, self.weight, self.bias, rm, rv, self.eps, momentum if momentum is not None else 0.0)
 
 
+class _NativeMaxPool(torch.autograd.Function):
+    """Max-pool on NHWC with a window-local argmax byte; backward as a deterministic gather."""
+
+    @staticmethod
+    def forward(ctx, x, k, s, pad):
+        xh = _nhwc(x)
+        y, am = ops.require().maxpool_train_fwd(xh, k, s, pad)
+        ctx.save_for_backward(am)
+        ctx.geom = (xh.shape[1], xh.shape[2], k, s, pad)
+        return _as_nchw(y)
+
+    @staticmethod
+    def backward(ctx, gy):
+        am, = ctx.saved_tensors
+        H, W, k, s, pad = ctx.geom
+        return _as_nchw(ops.require().maxpool_train_bwd(_nhwc(gy), am, H, W, k, s, pad)), None, None, None
+
+
+class _NativeGlobalAvgPool(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) on NHWC: (B, C, 1, 1); backward broadcasts g / HW in one kernel."""
+
+    @staticmethod
+    def forward(ctx, x):
+        xh = _nhwc(x)
+        ctx.hw = (xh.shape[1], xh.shape[2])
+        return ops.require().avgpool_nhwc(xh).view(xh.shape[0], xh.shape[3], 1, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        H, W = ctx.hw
+        return _as_nchw(ops.require().avgpool_bwd(gy.reshape(gy.shape[0], gy.shape[1]), H, W))
+
+
+def _pair1(v) -> int | None:
+    v = (v, v) if isinstance(v, int) else tuple(v)
+    return v[0] if len(v) == 2 and v[0] == v[1] else None
+
+
+def _cl_f32(x) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] % 4 == 0 and x.numel() > 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _native_maxpool_forward(self, x):
+    k, s = _pair1(self.kernel_size), _pair1(self.stride if self.stride is not None else self.kernel_size)
+    p, d = _pair1(self.padding), _pair1(self.dilation)
+    if not (_cl_f32(x) and k is not None and s is not None and p is not None and d == 1 and not self.ceil_mode
+            and not self.return_indices and k * k <= 255 and 2 * p <= k
+            and (x.shape[2] + 2 * p - k) // s + 1 > 0 and (x.shape[3] + 2 * p - k) // s + 1 > 0):
+        return type(self).forward(self, x)
+    return _NativeMaxPool.apply(x, k, s, p)
+
+
+def _native_gap_forward(self, x):
+    if not (_cl_f32(x) and _pair1(self.output_size) == 1):
+        return type(self).forward(self, x)
+    return _NativeGlobalAvgPool.apply(x)
+
+
 _MAX_BYTES = (1 << 31) - 1  # the kernels address operands through 32-bit buffer descriptors
 
 
@@ -443,6 +504,12 @@ def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True) ->
             switched.append(m)
         elif type(m) is nn.Linear:
             m.forward = types.MethodType(_native_linear_forward, m)
+            switched.append(m)
+        elif type(m) is nn.MaxPool2d:
+            m.forward = types.MethodType(_native_maxpool_forward, m)
+            switched.append(m)
+        elif type(m) is nn.AdaptiveAvgPool2d:
+            m.forward = types.MethodType(_native_gap_forward, m)
             switched.append(m)
         elif bn and isinstance(m, nn.BatchNorm2d):
             m.forward = types.MethodType(_native_bn_forward, m)
