@@ -88,110 +88,202 @@ def _wgrad_splits(P, tiles):
     return sp
 
 
+def _conv_fwd(x, weight, bias, ks, stride, pad):
+    """Forward of one native conv: returns (y NHWC (B, Ho, Wo, Cout), saved (xh, w32), meta)."""
+    T = ops.require()
+    B, Cin, H, W = x.shape
+    Cout = weight.shape[0]
+    cin_p = _cin_pad(ks, Cin)
+    cout_p = cpad(Cout)
+    xh = x.permute(0, 2, 3, 1)
+    if cin_p != Cin:
+        xh = F.pad(xh, (0, cin_p - Cin))
+    xh = xh.float().contiguous()
+    w32 = weight.detach().float().contiguous()  # the parameter itself for fp32 weights: no copy
+    kk = T.conv_gen_k(ks, cin_p)
+    shift = F.pad(bias.detach().float(), (0, cout_p - Cout)).contiguous() if bias is not None else None
+    Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
+    M = B * Ho * Wo
+
+    wino = _wino_ok(ks, stride, pad, H, W, cin_p, cout_p)
+    cache = {}  # padded operands, built on first use by one HIP launch each (weights change every step)
+
+    def run(cfg, sp):
+        if cfg in (WINO, WINO_LDS):  # Winograd F(2x2,3x3): 2.25x fewer multiplies
+            if "u" not in cache:
+                cache["u"] = T.wino_weights(w32, False, cout_p, cin_p)
+            return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
+        if "wk" not in cache:  # [cout_p][(kh, kw, ci)] zero-padded GEMM operand
+            cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
+        return T.conv_gen(xh, cache["wk"], None, shift, False, None, None, ks, stride, pad, cfg, sp)
+
+    cands = TUNER.candidates(M, cout_p, kk)
+    if wino:
+        sp0 = _wino_splits(B * (H // 2) * (W // 2), cout_p, cin_p)
+        cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
+    cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
+    y = run(cfg, sp)
+    if cout_p != Cout:
+        y = y[..., :Cout].contiguous()
+    meta = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride(), cin_p, cout_p)
+    return y, (xh, w32), meta
+
+
+def _grad_nhwc(gy, meta):
+    """dL/dy (NCHW view) -> contiguous NHWC, zero-padded to the kernels' output-channel granule."""
+    Cout, cout_p = meta[4], meta[11]
+    g = gy.permute(0, 2, 3, 1).float()
+    if cout_p != Cout:
+        g = F.pad(g, (0, cout_p - Cout))
+    return g.contiguous()
+
+
+def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
+    """Input gradient (B, H, W, cin_p) NHWC of a native conv (ks != 7); ``res`` (optional, NHWC,
+    (B, ceil(H/res_stride), ceil(W/res_stride), cin_p)) is added in the GEMM epilogue at the pixels
+    with h, w % res_stride == 0 — the other branch's gradient of a tensor read twice (residual
+    blocks), without a separate add pass."""
+    T = ops.require()
+    ks, stride, pad, Cin, Cout, H, W, _, _, _, cin_p, cout_p = meta
+    B, Ho, Wo = g.shape[0], g.shape[1], g.shape[2]
+    # stride 1: dgrad = stride-1 conv of g with flipped taps, padding ks-1-pad;
+    # strided 1x1 / 3x3: transposed gather kernel, natural tap order
+    transposed = stride != 1
+    assert res is None or not transposed
+    pad_b = pad if transposed else ks - 1 - pad
+    M, K = B * H * W, ks * ks * cout_p
+    wino = res is None and not transposed and _wino_ok(ks, 1, pad_b, Ho, Wo, cout_p, cin_p)
+    cache = {}
+
+    def run(cfg, sp):
+        if cfg in (WINO, WINO_LDS):  # stride-1 3x3 dgrad = Winograd conv of g, flipped taps
+            if "ut" not in cache:
+                cache["ut"] = T.wino_weights(w32, True, cin_p, cout_p)
+            return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
+        if "wt" not in cache:  # [ci][(kh, kw, co)], flipped for stride 1
+            cache["wt"] = T.pack_conv_weight(w32, cin_p, K, cout_p, 2 if transposed else 1)
+        return T.conv_gen_bwd(g, cache["wt"], res, res_stride, None, ks, stride if transposed else 1, pad_b, H, W,
+                              transposed, cfg, sp)
+
+    cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
+    if wino:
+        cands = [(WINO_LDS, _wino_splits(B * (H // 2) * (W // 2), cin_p, cout_p)), (WINO, 1)] + cands
+    key = ("tdgrad", tuple(g.shape), cin_p, ks, stride, pad, res is not None and res_stride)
+    cfg, sp = TUNER.choose(key, M, cin_p, K, run, cands=cands)
+    return run(cfg, sp)
+
+
+def _conv_wgrad(g, xh, meta):
+    """Weight gradient in the parameter's exact shape / strides (DDP bucket views expect them),
+    written by the wgrad kernel / its split combine straight from the GEMM (no re-layout copies)."""
+    T = ops.require()
+    ks, stride, pad, Cin, Cout, _, _, _, wdtype, w_strides, cin_p, cout_p = meta
+    kk = -(-ks * ks * cin_p // 32) * 32
+    P = g.shape[0] * g.shape[1] * g.shape[2]
+    dw32 = torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=torch.float32, device=g.device)
+
+    def run_w(cfg, sp):
+        return T.conv_wgrad(g, xh, ks, stride, pad, cfg, sp, dw32)
+
+    cands = []
+    for cfg, (bm, bn) in ((0, (128, 128)), (2, (128, 64)), (1, (64, 64))):
+        sp = _wgrad_splits(P, math.ceil(cout_p / bm) * math.ceil(kk / bn))
+        cands += [(cfg, sp)] + ([(cfg, sp // 2)] if sp > 1 else [])
+    cfg, sp = TUNER.choose(("twgrad", tuple(g.shape), tuple(xh.shape), ks, stride, pad), cout_p, kk, P, run_w,
+                           cands=cands)
+    run_w(cfg, sp)
+    if wdtype == torch.float32:
+        return dw32
+    return torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=wdtype, device=g.device).copy_(dw32)
+
+
 class _NativeConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, ks, stride, pad):
-        T = ops.require()
-        B, Cin, H, W = x.shape
-        Cout = weight.shape[0]
-        cin_p = _cin_pad(ks, Cin)
-        cout_p = cpad(Cout)
-        xh = x.permute(0, 2, 3, 1)
-        if cin_p != Cin:
-            xh = F.pad(xh, (0, cin_p - Cin))
-        xh = xh.float().contiguous()
-        w32 = weight.detach().float().contiguous()  # the parameter itself for fp32 weights: no copy
-        kk = T.conv_gen_k(ks, cin_p)
-        shift = F.pad(bias.detach().float(), (0, cout_p - Cout)).contiguous() if bias is not None else None
-        Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
-        M = B * Ho * Wo
-
-        wino = _wino_ok(ks, stride, pad, H, W, cin_p, cout_p)
-        cache = {}  # padded operands, built on first use by one HIP launch each (weights change every step)
-
-        def run(cfg, sp):
-            if cfg in (WINO, WINO_LDS):  # Winograd F(2x2,3x3): 2.25x fewer multiplies
-                if "u" not in cache:
-                    cache["u"] = T.wino_weights(w32, False, cout_p, cin_p)
-                return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
-            if "wk" not in cache:  # [cout_p][(kh, kw, ci)] zero-padded GEMM operand
-                cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
-            return T.conv_gen(xh, cache["wk"], None, shift, False, None, None, ks, stride, pad, cfg, sp)
-
-        cands = TUNER.candidates(M, cout_p, kk)
-        if wino:
-            sp0 = _wino_splits(B * (H // 2) * (W // 2), cout_p, cin_p)
-            cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
-        cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
-        y = run(cfg, sp)
-        if cout_p != Cout:
-            y = y[..., :Cout].contiguous()
-        ctx.save_for_backward(xh, w32)
-        ctx.geom = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride(), cin_p, cout_p)
+        y, saved, ctx.meta = _conv_fwd(x, weight, bias, ks, stride, pad)
+        ctx.save_for_backward(*saved)
         return _as_nchw(y)
 
     @staticmethod
     def backward(ctx, gy):
-        T = ops.require()
         xh, w32 = ctx.saved_tensors
-        ks, stride, pad, Cin, Cout, H, W, has_bias, wdtype, w_strides, cin_p, cout_p = ctx.geom
-        g = gy.permute(0, 2, 3, 1).float()
-        if cout_p != Cout:
-            g = F.pad(g, (0, cout_p - Cout))
-        g = g.contiguous()
-        B, Ho, Wo = g.shape[0], g.shape[1], g.shape[2]
+        meta = ctx.meta
+        ks, stride, pad, Cin, _, H, W, has_bias = meta[:8]
+        g = _grad_nhwc(gy, meta)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             if ks != 7:
-                # stride 1: dgrad = stride-1 conv of g with flipped taps, padding ks-1-pad;
-                # strided 1x1 / 3x3: transposed gather kernel, natural tap order
-                transposed = stride != 1
-                pad_b = pad if transposed else ks - 1 - pad
-                M, K = B * H * W, ks * ks * cout_p
-                wino = not transposed and _wino_ok(ks, 1, pad_b, Ho, Wo, cout_p, cin_p)
-                cache = {}
-
-                def run(cfg, sp):
-                    if cfg in (WINO, WINO_LDS):  # stride-1 3x3 dgrad = Winograd conv of g, flipped taps
-                        if "ut" not in cache:
-                            cache["ut"] = T.wino_weights(w32, True, cin_p, cout_p)
-                        return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
-                    if "wt" not in cache:  # [ci][(kh, kw, co)], flipped for stride 1
-                        cache["wt"] = T.pack_conv_weight(w32, cin_p, K, cout_p, 2 if transposed else 1)
-                    return T.conv_gen_bwd(g, cache["wt"], None, 1, None, ks, stride if transposed else 1, pad_b, H, W,
-                                          transposed, cfg, sp)
-
-                cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
-                if wino:
-                    cands = [(WINO_LDS, _wino_splits(B * (H // 2) * (W // 2), cin_p, cout_p)), (WINO, 1)] + cands
-                cfg, sp = TUNER.choose(("tdgrad", tuple(g.shape), cin_p, ks, stride, pad), M, cin_p, K, run,
-                                       cands=cands)
-                dxh = run(cfg, sp)[..., :Cin]
-                dx = dxh.permute(0, 3, 1, 2).to(gy.dtype)
+                dx = _conv_dgrad(g, w32, meta)[..., :Cin].permute(0, 3, 1, 2).to(gy.dtype)
             else:  # 7x7 stem input gradient (rarely needed: the input is data)
-                dx = torch.nn.grad.conv2d_input((B, Cin, H, W), w32.to(gy.dtype), gy, stride, pad)
+                dx = torch.nn.grad.conv2d_input((g.shape[0], Cin, H, W), w32.to(gy.dtype), gy, stride, pad)
         if ctx.needs_input_grad[1]:
-            kk = -(-ks * ks * cin_p // 32) * 32
-            P = B * Ho * Wo
-            # the gradient takes the parameter's exact strides (DDP bucket views expect them), written
-            # by the wgrad kernel / its split combine straight from the GEMM (no re-layout copies)
-            dw32 = torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=torch.float32, device=g.device)
-
-            def run_w(cfg, sp):
-                return T.conv_wgrad(g, xh, ks, stride, pad, cfg, sp, dw32)
-
-            cands = []
-            for cfg, (bm, bn) in ((0, (128, 128)), (2, (128, 64)), (1, (64, 64))):
-                sp = _wgrad_splits(P, math.ceil(cout_p / bm) * math.ceil(kk / bn))
-                cands += [(cfg, sp)] + ([(cfg, sp // 2)] if sp > 1 else [])
-            cfg, sp = TUNER.choose(("twgrad", tuple(g.shape), tuple(xh.shape), ks, stride, pad), cout_p, kk, P, run_w,
-                                   cands=cands)
-            run_w(cfg, sp)
-            dw = dw32 if wdtype == torch.float32 else \
-                torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=wdtype, device=g.device).copy_(dw32)
+            dw = _conv_wgrad(g, xh, meta)
         if has_bias and ctx.needs_input_grad[2]:
             db = gy.sum((0, 2, 3))
         return dx, dw, db, None, None, None
+
+
+class _NativeBlockEntry(torch.autograd.Function):
+    """The two readers of a residual block's input x, as one autograd node: conv1 (1x1, stride 1)
+    and the identity branch — x itself, or the downsample conv (1x1, stride s). Returns
+    (conv1(x), identity-branch pre-BN). The backward sums the two input gradients inside conv1's
+    data-gradient GEMM epilogue (the identity gradient, or the downsample conv's gradient computed
+    at its low resolution and scattered to the stride-s pixels), so the separate autograd
+    accumulation pass over x (an add kernel per block) disappears."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, wd, bd, ds_stride):
+        y1, saved1, ctx.meta1 = _conv_fwd(x, w1, b1, 1, 1, 0)
+        ctx.has_ds = wd is not None
+        if ctx.has_ds:
+            yd, saved_d, ctx.meta_d = _conv_fwd(x, wd, bd, 1, ds_stride, 0)
+            ctx.save_for_backward(*saved1, saved_d[1])
+            return _as_nchw(y1), _as_nchw(yd)
+        ctx.save_for_backward(*saved1)
+        return _as_nchw(y1), x
+
+    @staticmethod
+    def backward(ctx, g1, gid):
+        if ctx.has_ds:
+            xh, w1, wd = ctx.saved_tensors
+        else:
+            xh, w1 = ctx.saved_tensors
+        m1 = ctx.meta1
+        Cin = m1[3]
+        dx = dw1 = db1 = dwd = dbd = None
+        g1h = _grad_nhwc(g1, m1) if g1 is not None else None
+        res, res_stride, gdh = None, 1, None
+        if gid is not None:
+            if ctx.has_ds:
+                md = ctx.meta_d
+                gdh = _grad_nhwc(gid, md)
+                if ctx.needs_input_grad[0]:
+                    # the strided 1x1 conv's input gradient lives on the stride-s pixels only: the
+                    # low-resolution 1x1 GEMM here (stride 1 on the (Ho, Wo) grid), scattered by
+                    # conv1's dgrad epilogue
+                    res = _conv_dgrad(gdh, wd, (1, 1, 0, md[3], md[4], gdh.shape[1], gdh.shape[2]) + md[7:])
+                    res_stride = md[1]
+            elif ctx.needs_input_grad[0]:
+                res = _nhwc(gid).float()
+                if m1[10] != Cin:
+                    res = F.pad(res, (0, m1[10] - Cin))
+                res = res.contiguous()
+        if ctx.needs_input_grad[0]:
+            if g1h is None:  # only the identity branch carries a gradient (rare): dgrad of zeros + res
+                B, H, W = xh.shape[0], xh.shape[1], xh.shape[2]
+                g1h = torch.zeros((B, H, W, m1[11]), dtype=torch.float32, device=xh.device)
+            dx = _conv_dgrad(g1h, w1, m1, res, res_stride)[..., :Cin].permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1] and g1 is not None:
+            dw1 = _conv_wgrad(g1h, xh, m1)
+        if m1[7] and ctx.needs_input_grad[2] and g1 is not None:
+            db1 = g1.sum((0, 2, 3))
+        if ctx.has_ds and gdh is not None:
+            md = ctx.meta_d
+            if ctx.needs_input_grad[3]:
+                dwd = _conv_wgrad(gdh, xh, md)
+            if md[7] and ctx.needs_input_grad[4]:
+                dbd = gid.sum((0, 2, 3))
+        return dx, dw1, db1, dwd, dbd, None
 
 
 class _NativeBN2d(torch.autograd.Function):
@@ -296,12 +388,40 @@ def _block_kind(m) -> str | None:
     return "basic"
 
 
+def _entry_convs(block, x):
+    """(conv1, downsample conv or None, downsample BN or None) when the block's input readers can
+    run as one :class:`_NativeBlockEntry` (1x1 stride-1 conv1; identity or a 1x1 conv + BN
+    downsample; fp32 NHWC input), else None."""
+    c1, ds = block.conv1, block.downsample
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and isinstance(c1, nn.Conv2d) and eligible(c1)
+            and _geom(c1) == (1, 1, 0) and c1.weight.dtype == torch.float32 and _fits(c1, x)):
+        return None
+    if ds is None:
+        return c1, None, None
+    if not (type(ds) is nn.Sequential and len(ds) == 2 and isinstance(ds[0], nn.Conv2d) and eligible(ds[0])
+            and ds[0].kernel_size == (1, 1) and ds[0].padding == (0, 0) and ds[0].weight.dtype == torch.float32
+            and isinstance(ds[1], nn.BatchNorm2d) and _fits(ds[0], x)):
+        return None
+    return c1, ds[0], ds[1]
+
+
 def _native_block_forward(self, x):
-    """Bottleneck / BasicBlock training forward with fused BN(+residual)+ReLU tails."""
+    """Bottleneck / BasicBlock training forward with fused BN(+residual)+ReLU tails; a
+    bottleneck's conv1 and identity branch share one autograd node (:class:`_NativeBlockEntry`),
+    whose backward adds the two input gradients inside conv1's dgrad epilogue."""
     if not (self.training and x.is_cuda):
         return type(self).forward(self, x)
-    identity = self.downsample(x) if self.downsample is not None else x
-    out = bn_act(self.bn1, self.conv1(x), relu=True)
+    entry = _entry_convs(self, x)
+    if entry is not None:
+        c1, dconv, dbn = entry
+        y1, idp = _NativeBlockEntry.apply(x, c1.weight, c1.bias, dconv.weight if dconv is not None else None,
+                                          dconv.bias if dconv is not None else None,
+                                          dconv.stride[0] if dconv is not None else 1)
+        identity = bn_act(dbn, idp, relu=False) if dbn is not None else idp
+        out = bn_act(self.bn1, y1, relu=True)
+    else:
+        identity = self.downsample(x) if self.downsample is not None else x
+        out = bn_act(self.bn1, self.conv1(x), relu=True)
     if _block_kind(self) == "bottleneck":
         out = bn_act(self.bn2, self.conv2(out), relu=True)
         return bn_act(self.bn3, self.conv3(out), res=identity, relu=True)
@@ -477,8 +597,9 @@ def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True) ->
     training mode) through the native kernels (instance-level ``forward`` override; pruning keeps
     working because weights are re-packed per call). With ``bn`` and ``fuse``, residual blocks,
     ResNet stems and ``nn.Sequential`` containers also fuse their BN(+residual)+ReLU tails in
-    training mode — the fused BN / ReLU modules are then not called, so forward hooks on them do
-    not fire (attribution passes use ``fuse=False``). Returns the switched modules; undo with
+    training mode — the fused BN / ReLU modules (and a bottleneck's conv1 / downsample conv, run by
+    the block's entry node) are then not called, so forward hooks on them do not fire (attribution
+    passes use ``fuse=False``). Returns the switched modules; undo with
     :func:`disable_native_convs`."""
     if not ops.available() or ops.backend() == "torch":
         return []
