@@ -91,6 +91,18 @@ def main():
             torch.cuda.synchronize()
             results.append((e0.elapsed_time(e1) / args.iters * 1e3, cfg, sp))
         us, cfg, sp = min(results)
+        blas = ""
+        if ks == 1 and s == 1:  # the same GEMM on hipBLASLt (torch.mm), no epilogue: a reference point
+            a2, b2 = x.view(M, cin_p), w.view(cout, cin_p)
+            torch.mm(a2, b2.t())
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                torch.mm(a2, b2.t())
+            e1.record()
+            torch.cuda.synchronize()
+            blas = f"  hipBLASLt mm {e0.elapsed_time(e1) / args.iters * 1e3:.1f} us"
         flop = 2.0 * M * cout * cin * ks * ks
         byts = 4.0 * (B * H * W * cin_p + cout * kk + M * cout * (2 if res is not None else 1))
         roof = max(flop / (PEAK_TF * 1e12), byts / (PEAK_TBS * 1e12)) * 1e6
@@ -98,7 +110,7 @@ def main():
         total_roof += roof * n
         name = {WINO: "wino", WINO_LDS: "wino_lds"}.get(cfg, f"igemm{cfg}") + f" sp{sp}"
         print(f"{cin:>5} {cout:>5} {ks:>2} {s:>2} {H:>4} {n:>2} {name:>24} {us:>8.1f} {flop / us / 1e6:>6.1f} "
-              f"{byts / us / 1e6:>6.2f} {100 * roof / us:>5.0f}%", flush=True)
+              f"{byts / us / 1e6:>6.2f} {100 * roof / us:>5.0f}%{blas}", flush=True)
     print(f"sum over the network (x count): {total_best / 1e3:.2f} ms, roofline {total_roof / 1e3:.2f} ms "
           f"({100 * total_roof / total_best:.0f}%)")
 
