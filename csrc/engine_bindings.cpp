@@ -53,6 +53,9 @@ hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, h
 hipError_t tp_wino_weights2(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
 hipError_t tp_pack_conv_weight(const float* w, float* out, int O, int I, int KS, int rows, int cols, int cpad, int mode,
                                hipStream_t st);
+long long tp_wino_wgrad_ws_elems(int B, int H, int W, int Cin, int Cout, int splits);
+hipError_t tp_wino_wgrad(const float* g, const float* x, float* ws, int B, int H, int W, int Cin, int Cout, int cfg,
+                         int splits, float* fin, int fin_co, int fin_ci, const long long* fs, hipStream_t st);
 hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                           int ks, int stride, int pad, int Kpad, int cfg, int splits, float* fin, int fin_co,
                           int fin_ci, const long long* fs, hipStream_t st);
@@ -581,6 +584,31 @@ at::Tensor conv_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t ks, int6
   return fin ? at::empty({0}, g.options()) : dw;  // with ``out`` the result is in ``out``
 }
 
+// Winograd F(2x2,3x3) weight gradient of a stride-1 pad-1 3x3 conv: g (B, H, W, Cout), x (B, H, W,
+// Cin) NHWC (H, W even, Cin % 32 == 0) -> ``out`` (Cout_r, Cin_r, 3, 3), any strides (real channels).
+void wino_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t cfg, int64_t splits, at::Tensor& out) {
+  need(g, "g", 4);
+  need(x, "x", 4);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = g.size(3);
+  TORCH_CHECK(g.size(0) == B && g.size(1) == H && g.size(2) == W, "g must be (B, H, W, Cout) of a same-size conv");
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && Cin % 32 == 0 && Cout % 4 == 0, "wino_wgrad needs even H/W, Cin % 32, Cout % 4");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 4 && out.size(2) == 3 &&
+                  out.size(3) == 3 && out.size(0) <= Cout && out.size(1) <= Cin && out.device() == g.device(),
+              "out must be a float32 (Cout_r, Cin_r, 3, 3) tensor on the device");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  const int64_t T = B * (H / 2) * (W / 2);
+  const int64_t slices = (T + 31) / 32;
+  int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, slices));
+  const int64_t per = (slices + sp - 1) / sp;
+  sp = (slices + per - 1) / per;
+  auto ws = at::empty({tp_wino_wgrad_ws_elems((int)B, (int)H, (int)W, (int)Cin, (int)Cout, (int)sp)}, g.options());
+  long long fs[4];
+  for (int i = 0; i < 4; ++i) fs[i] = out.stride(i);
+  TP_CHECK_HIP(tp_wino_wgrad(g.data_ptr<float>(), x.data_ptr<float>(), ws.data_ptr<float>(), (int)B, (int)H, (int)W,
+                             (int)Cin, (int)Cout, (int)cfg, (int)sp, out.data_ptr<float>(), (int)out.size(0),
+                             (int)out.size(1), fs, cur_stream()));
+}
+
 // Training-mode BatchNorm over the last dim of an NHWC activation x (..., C), C % 4 == 0.
 // Updates running_mean / running_var in place (momentum, unbiased variance) when given.
 // Training BN on (.., C) channels-last data; optional fused residual add and ReLU:
@@ -672,6 +700,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "
         "-> Tensor");
   m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");
+  m.def("wino_wgrad(Tensor g, Tensor x, int cfg, int splits, Tensor(a!) out) -> ()");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
@@ -705,6 +734,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_gen_bwd", &conv_gen_bwd);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("pack_conv_weight", &pack_conv_weight);
+  m.impl("wino_wgrad", &wino_wgrad);
   m.impl("bn_train_fwd", &bn_train_fwd);
   m.impl("bn_train_bwd", &bn_train_bwd);
   m.impl("unpool2_nhwc", &unpool2_nhwc);

@@ -33,6 +33,9 @@ struct WgradArgs {
   float* fin;
   int fin_co, fin_ci;
   long long fs[4];
+  // batched GEMMs (blockIdx.z): operand z at g + z*g_bstride, x + z*x_bstride, result [z][Cout][Kpad]
+  int batch;
+  long long g_bstride, x_bstride;
 };
 
 // column k = (kh*ks + kw)*Cin + ci of the (Cout, Kpad) GEMM -> offset in the final layout, or -1
@@ -67,8 +70,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradAr
   const int s_begin = blockIdx.y * p.slices_per_split;
   const int s_end = min((p.P + 31) / 32, s_begin + p.slices_per_split);
   constexpr unsigned OOB = 0x80000000u;
-  const i32x4 gr = make_rsrc(p.g, (unsigned)(p.g_elems * 4));
-  const i32x4 xr = make_rsrc(p.x, (unsigned)(p.x_elems * 4));
+  const int z = blockIdx.z;
+  const i32x4 gr = make_rsrc(p.g + z * p.g_bstride, (unsigned)(p.g_elems * 4));
+  const i32x4 xr = make_rsrc(p.x + z * p.x_bstride, (unsigned)(p.x_elems * 4));
 
   // per-thread column decode of the im2col operand (fixed for the whole pixel loop)
   const int b_c4 = tid % (BN / 4), b_r0 = tid / (BN / 4);
@@ -159,8 +163,8 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradAr
     }
   }
 
-  float* out = p.out + (long long)blockIdx.y * p.Cout * p.Kpad;
-  const bool fin = p.fin && gridDim.y == 1;
+  float* out = p.out + ((long long)blockIdx.y * p.batch + z) * p.Cout * p.Kpad;
+  const bool fin = p.fin && gridDim.y == 1 && gridDim.z == 1;
 #pragma unroll
   for (int i = 0; i < T::TM; ++i)
 #pragma unroll
@@ -214,7 +218,7 @@ namespace {
 template <int BM, int BN, int WM, int WN>
 hipError_t launch_wgrad(const tp::WgradArgs& a, int splits, hipStream_t st) {
   const int tiles = ((a.Cout + BM - 1) / BM) * ((a.Kpad + BN - 1) / BN);
-  const dim3 grid(tiles, splits);
+  const dim3 grid(tiles, splits, a.batch);
   if (a.ks == 1 && a.stride == 1 && a.pad == 0)
     tp::conv_wgrad<BM, BN, WM, WN, true><<<grid, tp::WTile<BM, BN, WM, WN>::NT, 0, st>>>(a);
   else
@@ -229,14 +233,21 @@ hipError_t launch_wgrad(const tp::WgradArgs& a, int splits, hipStream_t st) {
 // dw (Cout, Kpad), Kpad % 32 == 0 and >= ks*ks*Cin.
 // fin (nullable): also/instead write the parameter-layout gradient (fin_co <= Cout, fin_ci <= Cin,
 // ks, ks) with element strides fs[4]; dw is then not written (may be null).
-extern "C" hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,
+// batch > 1: ``batch`` independent GEMMs (operands g + z*g_bstride, x + z*x_bstride) -> dw
+// [batch][Cout][Kpad]; no ``fin`` (the Winograd weight gradient's 16 transform-point GEMMs).
+extern "C" hipError_t tp_conv_wgrad3(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,
                                      int Cin, int Cout, int ks, int stride, int pad, int Kpad, int cfg, int splits,
-                                     float* fin, int fin_co, int fin_ci, const long long* fs, hipStream_t st) {
+                                     float* fin, int fin_co, int fin_ci, const long long* fs, int batch,
+                                     long long g_bstride, long long x_bstride, hipStream_t st) {
   using namespace tp;
   if (Cin % 4 || Cout % 4 || Kpad % 32 || Kpad < ks * ks * Cin || splits < 1) return hipErrorInvalidValue;
+  if (batch < 1 || batch > 65535 || (batch > 1 && fin)) return hipErrorInvalidValue;
   if (fin && (fin_co > Cout || fin_ci > Cin || fin_co <= 0 || fin_ci <= 0 || !fs)) return hipErrorInvalidValue;
   if (!fin && !dw) return hipErrorInvalidValue;
   WgradArgs a{};
+  a.batch = batch;
+  a.g_bstride = g_bstride;
+  a.x_bstride = x_bstride;
   a.fin = fin;
   a.fin_co = fin_co;
   a.fin_ci = fin_ci;
@@ -281,10 +292,17 @@ extern "C" hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, 
     wgrad_combine_fin<<<grid, 256, 0, st>>>(ws, a, splits);
     return hipGetLastError();
   }
-  const long long n4 = (long long)Cout * Kpad / 4;
+  const long long n4 = (long long)batch * Cout * Kpad / 4;
   const unsigned grid = (unsigned)std::min<long long>(ceil_div(n4, 256), 4096);
   wgrad_combine<<<grid, 256, 0, st>>>(ws, dw, splits, n4);
   return hipGetLastError();
+}
+
+extern "C" hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,
+                                     int Cin, int Cout, int ks, int stride, int pad, int Kpad, int cfg, int splits,
+                                     float* fin, int fin_co, int fin_ci, const long long* fs, hipStream_t st) {
+  return tp_conv_wgrad3(g, x, dw, ws, B, H, W, Cin, Cout, ks, stride, pad, Kpad, cfg, splits, fin, fin_co, fin_ci, fs,
+                        1, 0, 0, st);
 }
 
 extern "C" hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W,

@@ -369,3 +369,22 @@ def test_native_global_avgpool_training(cuda):
     y.backward(g)
     y2.backward(g)
     torch.testing.assert_close(x.grad, x2.grad, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,cin_r,cout_r,splits", [(2, 8, 10, 32, 64, 32, 64, 1), (3, 6, 6, 64, 36, 50, 36, 4),
+                                                                (2, 14, 14, 128, 128, 128, 100, 7)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_wino_wgrad(cuda, B, H, W, Cin, Cout, cin_r, cout_r, splits, cfg):
+    """Winograd F(2x2,3x3) weight gradient == fp64 conv2d_weight (stride 1, pad 1), written into a
+    parameter-shaped tensor of the real channels."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    g = torch.Generator().manual_seed(B * 100 + Cin + cfg)
+    x = torch.randn(B, H, W, Cin, generator=g)
+    x[..., cin_r:] = 0
+    gy = torch.randn(B, H, W, Cout, generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (Cout, Cin, 3, 3),
+                                      gy.permute(0, 3, 1, 2).double(), stride=1, padding=1)[:cout_r, :cin_r]
+    out = torch.full((cout_r, cin_r, 3, 3), float("nan"), device=cuda)
+    T.wino_wgrad(gy.to(cuda), x.to(cuda), cfg, splits, out)
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-4, atol=2e-3)
