@@ -21,6 +21,12 @@ hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* 
 hipError_t tp_bn_bwd_train(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a, float* k1,
                            float* k2, double* ws, hipStream_t st);
+hipError_t tp_bn_fwd_train3(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
+                            float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
+                            float* b, double* ws, const float* res, int relu, uint8_t* mko, hipStream_t st);
+hipError_t tp_bn_bwd_train3(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
+                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a, float* k1,
+                            float* k2, double* ws, const float* ym, float* dres, const uint8_t* mk, hipStream_t st);
 hipError_t tp_bn_fwd_train2(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
                             float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
                             float* b, double* ws, const float* res, int relu, hipStream_t st);
@@ -613,7 +619,8 @@ void wino_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t cfg, int64_t s
 // Updates running_mean / running_var in place (momentum, unbiased variance) when given.
 // Training BN on (.., C) channels-last data; optional fused residual add and ReLU:
 // y = relu?(BN(x) + res?). Returns (y, mean, invstd).
-std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+// With ``relu`` also returns the ReLU bit mask (P*C/4 bytes; else an empty tensor) for bn_train_bwd.
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                                              const c10::optional<at::Tensor>& beta,
                                                              const c10::optional<at::Tensor>& running_mean,
                                                              const c10::optional<at::Tensor>& running_var, double eps,
@@ -641,13 +648,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x,
     rp = res->data_ptr<float>();
   }
   auto y = at::empty_like(x);
+  auto mk = at::empty({relu ? P * C / 4 : 0}, x.options().dtype(at::kByte));
   auto stats = at::empty({4, C}, x.options());  // mean, invstd, a, b
   auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   float* sp = stats.data_ptr<float>();
-  TP_CHECK_HIP(tp_bn_fwd_train2(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
+  TP_CHECK_HIP(tp_bn_fwd_train3(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
                                 (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(), rp,
-                                relu ? 1 : 0, cur_stream()));
-  return {y, stats[0], stats[1]};
+                                relu ? 1 : 0, relu ? mk.data_ptr<uint8_t>() : nullptr, cur_stream()));
+  return {y, stats[0], stats[1], mk};
 }
 
 // Backward of bn_train_fwd: (dx or undefined, dgamma, dbeta, dres or undefined). ``ym``: the
@@ -655,7 +663,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x,
 // also return that masked gradient (the residual branch's gradient).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
     const at::Tensor& g, const at::Tensor& x, const c10::optional<at::Tensor>& gamma, const at::Tensor& mean,
-    const at::Tensor& invstd, bool want_dx, const c10::optional<at::Tensor>& ym, bool want_dres) {
+    const at::Tensor& invstd, bool want_dx, const c10::optional<at::Tensor>& ym, bool want_dres,
+    const c10::optional<at::Tensor>& mask) {
   need(g, "g", -1);
   need(x, "x", -1);
   TORCH_CHECK(g.sizes() == x.sizes(), "g and x must have the same shape");
@@ -671,16 +680,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
     TORCH_CHECK(ym->sizes() == x.sizes(), "ym must have x's shape");
     yp = ym->data_ptr<float>();
   }
+  const uint8_t* mkp = nullptr;
+  if (mask.has_value() && mask->defined() && mask->numel() > 0) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == P * C / 4 && mask->device() == x.device(),
+                "mask must be bn_train_fwd's ReLU bit mask (P*C/4 uint8)");
+    mkp = mask->data_ptr<uint8_t>();
+  }
   auto coef = at::empty({5, C}, x.options());  // dgamma, dbeta, a, k1, k2
   auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   at::Tensor dx, dres;
   if (want_dx) dx = at::empty_like(x);
   if (want_dres) dres = at::empty_like(x);
   float* cp = coef.data_ptr<float>();
-  TP_CHECK_HIP(tp_bn_bwd_train2(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
+  TP_CHECK_HIP(tp_bn_bwd_train3(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
                                 (int)P, (int)C, ga, mp, ip, cp, cp + C, cp + 2 * C, cp + 3 * C, cp + 4 * C,
-                                ws.data_ptr<double>(), yp, want_dres ? dres.data_ptr<float>() : nullptr,
-                                cur_stream()));
+                                ws.data_ptr<double>(), mkp ? nullptr : yp, want_dres ? dres.data_ptr<float>() : nullptr,
+                                mkp, cur_stream()));
   return {dx, coef[0], coef[1], dres};
 }
 
@@ -694,9 +710,9 @@ void register_engine_ops_def(torch::Library& m) {
         "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
   m.def("bn_train_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float eps, float momentum, Tensor? res=None, bool relu=False) -> (Tensor, Tensor, Tensor)");
+        "float eps, float momentum, Tensor? res=None, bool relu=False) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx, Tensor? ym=None, "
-        "bool want_dres=False) -> (Tensor, Tensor, Tensor, Tensor)");
+        "bool want_dres=False, Tensor? mask=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "
         "-> Tensor");
   m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");

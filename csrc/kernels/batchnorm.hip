@@ -20,7 +20,13 @@ constexpr int BN_T = 256, BN_CQ = 16, BN_RL = BN_T / BN_CQ;  // 16 column quads 
 // MODE 0: (sum x, sum x^2); MODE 1: (sum g, sum g * (x - mean) * invstd)
 // ReLU backward through the block's output y (MODE 1, ym non-null): the gradient reaching the BN
 // is g where y > 0 and 0 elsewhere (NaN y -> 0, as the ATen threshold backward)
-__device__ __forceinline__ float4 relu_mask4(float4 d, const float* ym, size_t off) {
+// or, cheaper, by the forward's ReLU bit mask mk (one byte per 4 channels, bit q = y[c+q] > 0:
+// 1/16 of the bytes of reading y back)
+__device__ __forceinline__ float4 relu_mask4(float4 d, const float* ym, size_t off, const uint8_t* mk = nullptr) {
+  if (mk) {
+    const unsigned m = mk[off >> 2];
+    return make_float4((m & 1u) ? d.x : 0.f, (m & 2u) ? d.y : 0.f, (m & 4u) ? d.z : 0.f, (m & 8u) ? d.w : 0.f);
+  }
   if (!ym) return d;
   const float4 m = *reinterpret_cast<const float4*>(ym + off);
   return make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f, m.w > 0.f ? d.w : 0.f);
@@ -30,7 +36,8 @@ template <int MODE>
 __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, const float* __restrict__ g,
                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
                                                    double* __restrict__ part, int P, int C, int rows_per_group,
-                                                   const float* __restrict__ ym = nullptr) {
+                                                   const float* __restrict__ ym = nullptr,
+                                                   const uint8_t* __restrict__ mk = nullptr) {
   __shared__ double red[2][BN_RL][BN_CQ * 4];
   const int cq = threadIdx.x % BN_CQ, rl = threadIdx.x / BN_CQ;
   const int c = (blockIdx.x * BN_CQ + cq) * 4;
@@ -52,7 +59,7 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
         v[u] = *reinterpret_cast<const float4*>(x + (size_t)(r + u * BN_RL) * C + c);
         if (MODE == 1)
           d[u] = relu_mask4(*reinterpret_cast<const float4*>(g + (size_t)(r + u * BN_RL) * C + c), ym,
-                            (size_t)(r + u * BN_RL) * C + c);
+                            (size_t)(r + u * BN_RL) * C + c, mk);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -89,7 +96,8 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
         s1.z += v.z * v.z;
         s1.w += v.w * v.w;
       } else {
-        const float4 d = relu_mask4(*reinterpret_cast<const float4*>(g + (size_t)r * C + c), ym, (size_t)r * C + c);
+        const float4 d =
+            relu_mask4(*reinterpret_cast<const float4*>(g + (size_t)r * C + c), ym, (size_t)r * C + c, mk);
         s0.x += d.x;
         s0.y += d.y;
         s0.z += d.z;
@@ -127,11 +135,35 @@ __device__ __forceinline__ void fold_groups(const double* __restrict__ part, int
   __shared__ double red[2][16][16];
   s = 0.0;
   q = 0.0;
-  if (c < C)
-    for (int i = gl; i < groups; i += 16) {
-      s += part[(size_t)(2 * i) * C + c];
-      q += part[(size_t)(2 * i + 1) * C + c];
+  if (c < C) {
+    // 8 groups per lane in flight (independent partial sums, folded in a fixed order): the fold is
+    // L2-latency bound, one dependent load per iteration took ~10 us per call
+    constexpr int U = 8;
+    double ps[U], pq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ps[u] = pq[u] = 0.0;
+    int i = gl;
+    for (; i + 16 * (U - 1) < groups; i += 16 * U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ps[u] += part[(size_t)(2 * (i + 16 * u)) * C + c];
+        pq[u] += part[(size_t)(2 * (i + 16 * u) + 1) * C + c];
+      }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // the < U remaining groups of this lane (static register indexing)
+      const int j = i + 16 * u;
+      if (j < groups) {
+        ps[u] += part[(size_t)(2 * j) * C + c];
+        pq[u] += part[(size_t)(2 * j + 1) * C + c];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s += ps[u];
+      q += pq[u];
+    }
+  }
   red[0][gl][cl] = s;
   red[1][gl][cl] = q;
   __syncthreads();
@@ -199,7 +231,8 @@ __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, con
                                                 const float* __restrict__ k2, float* __restrict__ out, unsigned n4,
                                                 unsigned C4, const float* __restrict__ res = nullptr, int relu = 0,
                                                 const float* __restrict__ ym = nullptr,
-                                                float* __restrict__ dres = nullptr) {
+                                                float* __restrict__ dres = nullptr,
+                                                uint8_t* __restrict__ mk = nullptr) {
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += gridDim.x * blockDim.x) {
     const unsigned c = (t % C4) * 4;
     const float4 v = reinterpret_cast<const float4*>(x)[t];
@@ -207,7 +240,7 @@ __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, con
     const float4 bv = *reinterpret_cast<const float4*>(b + c);
     float4 o;
     if (BWD) {
-      const float4 d = relu_mask4(reinterpret_cast<const float4*>(g)[t], ym, (size_t)t * 4);
+      const float4 d = relu_mask4(reinterpret_cast<const float4*>(g)[t], ym, (size_t)t * 4, mk);
       if (dres) reinterpret_cast<float4*>(dres)[t] = d;
       if (!out) continue;
       const float4 kv = *reinterpret_cast<const float4*>(k2 + c);
@@ -232,6 +265,9 @@ __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, con
         o.y = nan_relu(o.y);
         o.z = nan_relu(o.z);
         o.w = nan_relu(o.w);
+        if (mk)  // the backward's ReLU mask: bit q = output channel c+q is > 0
+          mk[t] = (uint8_t)((o.x > 0.f ? 1u : 0u) | (o.y > 0.f ? 2u : 0u) | (o.z > 0.f ? 4u : 0u) |
+                            (o.w > 0.f ? 8u : 0u));
       }
     }
     reinterpret_cast<float4*>(out)[t] = o;
@@ -250,10 +286,11 @@ inline int bn_groups(int P, int C) {
 extern "C" int tp_bn_groups(int P, int C) { return tp::bn_groups(P, C); }
 
 // Fused block tail: y = relu?(BN(x) + res?) (res: the residual branch, same shape as x).
-extern "C" hipError_t tp_bn_fwd_train2(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
+// mko (nullable, relu only): the ReLU bit mask, P*C/4 bytes (bit q of byte p*C/4 + c/4 = y[p][c+q] > 0)
+extern "C" hipError_t tp_bn_fwd_train3(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
                                        float eps, float momentum, float* run_mean, float* run_var, float* mean,
                                        float* invstd, float* a, float* b, double* ws, const float* res, int relu,
-                                       hipStream_t st) {
+                                       uint8_t* mko, hipStream_t st) {
   using namespace tp;
   if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
   const int groups = bn_groups(P, C);
@@ -264,8 +301,16 @@ extern "C" hipError_t tp_bn_fwd_train2(const float* x, float* y, int P, int C, c
                                                     mean, invstd, a, b);
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
-      x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu);
+      x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
   return hipGetLastError();
+}
+
+extern "C" hipError_t tp_bn_fwd_train2(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
+                                       float eps, float momentum, float* run_mean, float* run_var, float* mean,
+                                       float* invstd, float* a, float* b, double* ws, const float* res, int relu,
+                                       hipStream_t st) {
+  return tp_bn_fwd_train3(x, y, P, C, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, a, b, ws, res, relu,
+                          nullptr, st);
 }
 
 extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
@@ -277,23 +322,31 @@ extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, co
 
 // Backward of the fused tail: ym = the block output y (ReLU mask; nullable), dres = gradient of
 // the residual input (nullable). dx nullable (dgamma / dbeta only).
-extern "C" hipError_t tp_bn_bwd_train2(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
+// mk (nullable): the forward's ReLU bit mask, used instead of ym
+extern "C" hipError_t tp_bn_bwd_train3(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
                                        const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
                                        float* k1, float* k2, double* ws, const float* ym, float* dres,
-                                       hipStream_t st) {
+                                       const uint8_t* mk, hipStream_t st) {
   using namespace tp;
   if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
   const int groups = bn_groups(P, C);
   const int rpg = (P + groups - 1) / groups;
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
-  bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym);
+  bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym, mk);
   bn_bwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
   if (dx || dres) {
     const unsigned n4 = (unsigned)((long long)P * C / 4);
     bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
-        x, g, a, k1, k2, dx, n4, (unsigned)(C / 4), nullptr, 0, ym, dres);
+        x, g, a, k1, k2, dx, n4, (unsigned)(C / 4), nullptr, 0, ym, dres, const_cast<uint8_t*>(mk));
   }
   return hipGetLastError();
+}
+
+extern "C" hipError_t tp_bn_bwd_train2(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
+                                       const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
+                                       float* k1, float* k2, double* ws, const float* ym, float* dres,
+                                       hipStream_t st) {
+  return tp_bn_bwd_train3(g, x, dx, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2, ws, ym, dres, nullptr, st);
 }
 
 extern "C" hipError_t tp_bn_bwd_train(const float* g, const float* x, float* dx, int P, int C, const float* gamma,

@@ -311,7 +311,7 @@ class _NativeBN2d(torch.autograd.Function):
             xh = xh.contiguous()
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
-        y, mean, invstd = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum))
+        y, mean, invstd, _ = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum))
         ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd)
         ctx.has_w, ctx.has_b = weight is not None, bias is not None
         return _as_nchw(y)
@@ -346,21 +346,21 @@ class _NativeBNAct(torch.autograd.Function):
         rh = _nhwc(res) if res is not None else None
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
-        y, mean, invstd = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
-                                         bool(relu))
-        ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd,
-                              y if relu else torch.empty(0, device=x.device))
+        y, mean, invstd, mk = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
+                                             bool(relu))
+        # the backward masks by the ReLU bit mask (1 byte per 4 channels) instead of re-reading y
+        ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd, mk)
         ctx.has_w, ctx.has_b, ctx.relu, ctx.has_res = weight is not None, bias is not None, relu, res is not None
         return _as_nchw(y)
 
     @staticmethod
     def backward(ctx, gy):
         T = ops.require()
-        xh, w, mean, invstd, y = ctx.saved_tensors
+        xh, w, mean, invstd, mk = ctx.saved_tensors
         g = _nhwc(gy)
         want_res = ctx.has_res and ctx.needs_input_grad[7]
         dx, dgamma, dbeta, dres = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
-                                                 ctx.needs_input_grad[0], y if ctx.relu else None, want_res)
+                                                 ctx.needs_input_grad[0], None, want_res, mk if ctx.relu else None)
         return (_as_nchw(dx) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
                 dbeta if ctx.has_b else None, None, None, None, None, _as_nchw(dres) if want_res else None, None)
 
