@@ -308,7 +308,7 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
   need_u(u, C, K);
-  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "Winograd F(2x2,3x3) needs even H, W");
+  TORCH_CHECK(!pool || (H % 2 == 0 && W % 2 == 0), "Winograd with pooling needs even H, W");
   TORCH_CHECK(C % 8 == 0 && K % 32 == 0, "Winograd needs C % 8 == 0 and K % 32 == 0");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   const float* sc = opt_ptr(scale, K, "scale");
@@ -356,7 +356,7 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
     TORCH_CHECK(g.size(1) == H && g.size(2) == W, "grad shape mismatch");
   }
   TORCH_CHECK(g.size(0) == B, "batch mismatch");
-  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "Winograd F(2x2,3x3) needs even H, W");
+  TORCH_CHECK(!unpool || (H % 2 == 0 && W % 2 == 0), "Winograd with unpooling needs even H, W");
   TORCH_CHECK(Cout % 8 == 0 && Cin % 32 == 0, "Winograd dgrad needs Cout % 8 == 0 and Cin % 32 == 0");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
   const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");

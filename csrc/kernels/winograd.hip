@@ -146,7 +146,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, float* lds_base
 // the (R, B, K) taylor slab — a single-writer +=; score_fold sums the R slots in slot order.
 // The result is bit-reproducible run to run (no float atomics on the engine's Taylor path).
 __host__ __device__ inline int wino_taylor_slots(int H, int W) {
-  const int T_img = (H / 2) * (W / 2);
+  const int T_img = ((H + 1) / 2) * ((W + 1) / 2);  // odd sizes: the last tile row / column is partial
   if (T_img <= 0) return 1;
   if (T_img % 64 == 0) return T_img / 64;
   if (64 % T_img == 0) return 1;
@@ -168,7 +168,7 @@ __device__ __forceinline__ int pbuf_row(int t) { return t ^ ((t >> 2) & 1); }
 template <int EPI>
 __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16][2], int pw0, int k0, int g, int j,
                                               int blk_p, float* yb0, float* yb1, const float* al0, const float* al1) {
-  const int H2 = p.H >> 1, W2 = p.W >> 1, T_img = H2 * W2;
+  const int H2 = (p.H + 1) >> 1, W2 = (p.W + 1) >> 1, T_img = H2 * W2;
   const int t0 = blk_p * 64;
   const int tid = threadIdx.x;
   const int tl_base = (pw0 - t0) + 4 * g;  // block-local index of this lane's first output tile
@@ -269,6 +269,7 @@ phase2:
       const int bb = p.fd_timg.div(pt), rr = pt - bb * T_img;
       const int oh2 = p.fd_w2.div(rr), ow2 = rr - oh2 * W2;
       const int oh = 2 * oh2 + (q >> 1), ow = 2 * ow2 + (q & 1);
+      if (oh >= p.H || ow >= p.W) continue;  // outside an odd-sized image: nothing to store or sum
       const long long pix = ((long long)bb * p.H + oh) * p.W + ow;
       if constexpr (EPI == W_FWD) {
         float4 v;
@@ -369,7 +370,8 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   const int kb = tile % n_k, k0 = kb * W_TK;
   const int blk_p = tile / n_k;
   const int pw0 = blk_p * 64 + wave * 16;  // first tile of this wave
-  const int H2 = p.H >> 1, W2 = p.W >> 1, T_img = H2 * W2;
+  // tile grid: odd H / W (X_DIRECT only) get a partial last tile row / column
+  const int H2 = (p.H + 1) >> 1, W2 = (p.W + 1) >> 1, T_img = H2 * W2;
   const int c_begin = blockIdx.y * p.c_per_split;
   const int c_end = min(p.C, c_begin + p.c_per_split);
   constexpr unsigned OOB = 0x80000000u;
@@ -996,7 +998,10 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
                                    const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
                                    float* taylor, float* apoz, float* ws, int tay_mode, hipStream_t st) {
   using namespace tp;
-  if ((H & 1) || (W & 1) || C % 8 != 0 || K % 32 != 0) return hipErrorInvalidValue;
+  // odd H / W: a partial last tile row / column, direct loads only (no pooling / unpooling)
+  const bool odd = (H & 1) || (W & 1);
+  if ((odd && (unpool || epi == W_FWD_POOL)) || C % 8 != 0 || K % 32 != 0) return hipErrorInvalidValue;
+  if (odd) staged = 0;
   WinoArgs a{};
   a.x = x;
   a.x_argmax = x_argmax;
@@ -1006,7 +1011,7 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.W = W;
   a.C = C;
   a.K = K;
-  a.P = B * (H / 2) * (W / 2);
+  a.P = B * ((H + 1) / 2) * ((W + 1) / 2);
   a.x_elems = unpool ? (long long)B * (H / 2) * (W / 2) * C : (long long)B * H * W * C;
   if (a.x_elems * 4 >= (1ll << 31) || 16ll * C * K * 4 >= (1ll << 31)) return hipErrorInvalidValue;
   if (epi == W_BWD && (long long)B * H * W * K * 4 >= (1ll << 31)) return hipErrorInvalidValue;  // act rsrc
@@ -1025,8 +1030,8 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.apoz = (epi == W_FWD || epi == W_FWD_POOL) ? apoz : nullptr;
   if (apoz && epi != W_FWD && epi != W_FWD_POOL) return hipErrorInvalidValue;
   a.tay_slots = wino_taylor_slots(H, W);
-  a.fd_timg = FastDiv((unsigned)std::max(1, (H / 2) * (W / 2)));
-  a.fd_w2 = FastDiv((unsigned)std::max(1, W / 2));
+  a.fd_timg = FastDiv((unsigned)std::max(1, ((H + 1) / 2) * ((W + 1) / 2)));
+  a.fd_w2 = FastDiv((unsigned)std::max(1, (W + 1) / 2));
 #ifdef TP_WINO_DEBUG
   static const int dbg_bits = [] {
     const char* d = getenv("TP_WINO_DBG");

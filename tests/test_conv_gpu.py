@@ -293,6 +293,56 @@ def test_wino_fwd(cuda, shape, splits, pool, staged):
         assert (am.cpu().long() == am_ref).float().mean() > 0.999
 
 
+WINO_ODD_SHAPES = [(3, 7, 7, 64, 64), (2, 5, 9, 32, 32), (2, 7, 14, 64, 32), (4, 3, 3, 32, 64), (2, 1, 5, 32, 32)]
+
+
+@pytest.mark.parametrize("shape", WINO_ODD_SHAPES)
+@pytest.mark.parametrize("splits", [1, 3])
+def test_wino_fwd_odd(cuda, shape, splits):
+    """Odd H / W (ResNet-50 layer4's 7x7): a partial last tile row / column, direct loads."""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import winograd_weights
+    T = ops.require()
+    B, H, W, Cin, Cout = shape
+    g = torch.Generator().manual_seed(21 + H * W)
+    x = _rand(B, H, W, Cin, gen=g)
+    w = _rand(Cout, Cin, 3, 3, gen=g) * (2.0 / (9 * Cin)) ** 0.5
+    scale = _rand(Cout, gen=g).abs() + 0.5
+    shift = _rand(Cout, gen=g) * 0.1
+    ref, _ = _ref_fwd(x, w, scale, shift, True, False)
+    u = winograd_weights(w.to(cuda))
+    apoz = torch.zeros(B, Cout, device=cuda)
+    out, _ = T.conv_wino_fwd(x.to(cuda), u, scale.to(cuda), shift.to(cuda), True, False, splits, True, apoz)
+    torch.testing.assert_close(out.cpu(), ref, rtol=3e-4, atol=3e-4)
+    if splits == 1:  # the fused APoZ counts see only in-image pixels
+        assert torch.equal(apoz.cpu(), (out.cpu() > 0).float().sum((1, 2)))
+
+
+@pytest.mark.parametrize("shape", WINO_ODD_SHAPES)
+@pytest.mark.parametrize("splits", [1, 4])
+def test_wino_dgrad_taylor_odd(cuda, shape, splits):
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import taylor_slots, winograd_weights
+    T = ops.require()
+    B, H, W, Cin, Cout = shape
+    g = torch.Generator().manual_seed(7 + H * W)
+    w = _rand(Cout, Cin, 3, 3, gen=g) * (1.0 / (9 * Cin)) ** 0.5
+    act = torch.relu(_rand(B, H, W, Cin, gen=g))
+    bn_scale = _rand(Cin, gen=g).abs() + 0.5
+    gfull = _rand(B, H, W, Cout, gen=g)
+    dx = torch.nn.grad.conv2d_input((B, Cin, H, W), w.double(), gfull.permute(0, 3, 1, 2).double(), padding=1)
+    dx = dx.permute(0, 2, 3, 1)
+    tay_ref = (-(dx * act.double())).sum((1, 2))
+    out_ref = torch.where(act > 0, dx * bn_scale.double(), torch.zeros((), dtype=torch.float64))
+    ut = winograd_weights(w.flip(2, 3).transpose(0, 1).to(cuda))
+    R = taylor_slots(H, W)
+    assert R >= T.wino_taylor_slots(H, W)
+    tay = torch.zeros(R, B, Cin, device=cuda)
+    out = T.conv_wino_dgrad(gfull.to(cuda), None, ut, act.to(cuda), bn_scale.to(cuda), tay, True, splits, True)
+    torch.testing.assert_close(out.cpu(), out_ref.float(), rtol=3e-4, atol=3e-4)
+    torch.testing.assert_close(tay.sum(0).cpu(), tay_ref.float(), rtol=3e-4, atol=3e-3)
+
+
 @pytest.mark.parametrize("shape", WINO_SHAPES)
 @pytest.mark.parametrize("splits", [1, 4])
 @pytest.mark.parametrize("unpool", [False, True])

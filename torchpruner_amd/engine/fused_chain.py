@@ -75,7 +75,7 @@ def taylor_slots(H: int, W: int) -> int:
     wino_taylor_slots() in winograd.hip). score_fold sums the slots in order."""
     if H == 2 and W == 2:
         return 4  # dense-GEMM layers (2x2 images) keep one slot per pixel
-    T = (H // 2) * (W // 2)
+    T = ((H + 1) // 2) * ((W + 1) // 2)  # odd sizes: partial last tile row / column
     if T <= 0:
         return 1
     if T % 64 == 0:

@@ -174,8 +174,8 @@ class ResNetEngine:
         Ho, Wo = (H + 2 * pd - ks) // s + 1, (W + 2 * pd - ks) // s + 1
         M, N, K = B * Ho * Wo, e["scale"].numel(), e["w"].shape[1]
         cands = TUNER.candidates(M, N, K)
-        if "u" in e and res is None and H % 2 == 0 and W % 2 == 0:
-            sp0 = _wino_splits(B * (H // 2) * (W // 2), N, C)
+        if "u" in e and res is None:  # odd H / W: partial last tile row / column (direct loads)
+            sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + ([(WINO_LDS, 1)] if sp0 > 1 else []) + cands
         key = ("gen", tuple(h.shape), N, ks, s, res is not None)
 
@@ -340,9 +340,9 @@ class ResNetEngine:
             cands = [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
         else:
             cands = TUNER.candidates(M, N, K)
-        wino_ok = "ut" in e and res is None and mask is not None and H % 2 == 0 and W % 2 == 0
+        wino_ok = "ut" in e and res is None and mask is not None
         if wino_ok:
-            sp0 = _wino_splits(B * (H // 2) * (W // 2), N, C)
+            sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
         key = ("rbwd", tuple(g.shape), N, ks, s, transposed, res is not None, res_stride, mask is not None)
 

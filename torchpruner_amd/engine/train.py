@@ -40,8 +40,8 @@ from .fused_chain import _CU, TUNER, WINO, WINO_LDS, _wino_splits, cpad
 
 
 def _wino_ok(ks, stride, pad, H, W, cin, cout) -> bool:
-    """Winograd F(2x2,3x3) applies: 3x3, stride 1, 'same' padding, even H/W, the kernel's granules."""
-    return ks == 3 and stride == 1 and pad == 1 and H % 2 == 0 and W % 2 == 0 and cin % 8 == 0 and cout % 32 == 0
+    """Winograd F(2x2,3x3) applies: 3x3, stride 1, "same" padding, the kernels' granules."""
+    return ks == 3 and stride == 1 and pad == 1 and cin % 8 == 0 and cout % 32 == 0  # odd H / W: partial tiles
 
 
 def _as_nchw(t: torch.Tensor) -> torch.Tensor:
@@ -121,7 +121,7 @@ def _conv_fwd(x, weight, bias, ks, stride, pad):
 
     cands = TUNER.candidates(M, cout_p, kk)
     if wino:
-        sp0 = _wino_splits(B * (H // 2) * (W // 2), cout_p, cin_p)
+        sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cout_p, cin_p)
         cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
     cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
     y = run(cfg, sp)
@@ -169,7 +169,7 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
 
     cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
     if wino:
-        cands = [(WINO_LDS, _wino_splits(B * (H // 2) * (W // 2), cin_p, cout_p)), (WINO, 1)] + cands
+        cands = [(WINO_LDS, _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cin_p, cout_p)), (WINO, 1)] + cands
     key = ("tdgrad", tuple(g.shape), cin_p, ks, stride, pad, res is not None and res_stride)
     cfg, sp = TUNER.choose(key, M, cin_p, K, run, cands=cands)
     return run(cfg, sp)
