@@ -7,9 +7,6 @@
 
 #include "tp_launchers.h"
 
-#include <map>
-#include <mutex>
-
 extern "C" {
 hipError_t tp_conv_igemm(const float* x, const uint8_t* x_argmax, const float* w, int B, int H, int W, int Cin,
                          int Cout, int ks, int pooled_m, int unpool, int epi, int cfg, int splits, const float* scale,
@@ -53,11 +50,12 @@ hipError_t tp_unpool2_nhwc(const float* g, const uint8_t* am, float* out, int B,
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
 int tp_wino_taylor_slots(int H, int W);
+int tp_wino_lds_bytes();
 hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C, int H, int W, int Cp, hipStream_t st);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
-                        int tay_mode, unsigned* fold_ctr, long long fold_ctr_len, hipStream_t st);
+                        int tay_mode, hipStream_t st);
 hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st);
 hipError_t tp_wino_weights2(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
 hipError_t tp_pack_conv_weight(const float* w, float* out, int O, int I, int KS, int rows, int cols, int cpad, int mode,
@@ -303,30 +301,6 @@ void need_u(const at::Tensor& u, int64_t C, int64_t K) {
               u.sizes());
 }
 
-// Split-K Winograd launches fold their split combine into the kernel (the last block of each
-// output tile sums the splits): one zero-initialised counter per tile, per device, reset to zero
-// by the kernels themselves. TP_WINO_FOLD=0 restores the separate combine launch.
-std::pair<unsigned*, long long> wino_fold_counters(const at::Device& dev, long long need) {
-  static const bool enabled = [] {
-    const char* e = getenv("TP_WINO_FOLD");
-    return !(e && e[0] == '0');
-  }();
-  if (!enabled) return {nullptr, 0};
-  static std::mutex mu;
-  static std::map<int, at::Tensor> bufs;
-  std::lock_guard<std::mutex> lock(mu);
-  at::Tensor& t = bufs[dev.index()];
-  if (!t.defined() || t.numel() < need)
-    t = at::zeros({std::max<long long>(need, 1 << 16)}, at::TensorOptions().device(dev).dtype(at::kInt));
-  return {reinterpret_cast<unsigned*>(t.data_ptr<int>()), (long long)t.numel()};
-}
-
-// split-K workspace of a Winograd launch: max(partial slabs, folded per-tile images)
-int64_t wino_ws_elems(int64_t sp, int64_t B, int64_t H, int64_t W, int64_t K) {
-  const int64_t P = B * ((H + 1) / 2) * ((W + 1) / 2);
-  return sp * std::max<int64_t>(B * H * W * K, (P + 63) / 64 * 256 * K);
-}
-
 // Winograd F(2x2,3x3) forward: x (B,H,W,C) NHWC, u (16, C, K) from winograd_weights().
 std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::Tensor& u,
                                                  const c10::optional<at::Tensor>& scale,
@@ -349,9 +323,7 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
   }
   const int64_t sp = wino_splits(splits, C);
   at::Tensor ws;
-  if (sp > 1) ws = at::empty({wino_ws_elems(sp, B, H, W, K)}, x.options());
-  const auto fc = sp > 1 ? wino_fold_counters(x.device(), ((B * ((H + 1) / 2) * ((W + 1) / 2) + 63) / 64) * (K / 32))
-                         : std::pair<unsigned*, long long>{nullptr, 0};
+  if (sp > 1) ws = at::empty({sp * B * H * W * K}, x.options());
   float* ap = nullptr;
   if (apoz.has_value() && apoz->defined()) {
     TORCH_CHECK(apoz->is_cuda() && apoz->scalar_type() == at::kFloat && apoz->is_contiguous() &&
@@ -362,8 +334,7 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
                             0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, staged ? 1 : 0, sc, sh, relu ? 1 : 0,
                             out.data_ptr<float>(),
                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap,
-                            sp > 1 ? ws.data_ptr<float>() : nullptr, 0, pool ? nullptr : fc.first, fc.second,
-                            cur_stream()));
+                            sp > 1 ? ws.data_ptr<float>() : nullptr, 0, cur_stream()));
   return {out, am};
 }
 
@@ -403,14 +374,12 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
   if (want_out) out = at::empty({B, H, W, Cin}, g.options());
   const int64_t sp = wino_splits(splits, Cout);
   at::Tensor ws;
-  if (sp > 1) ws = at::empty({wino_ws_elems(sp, B, H, W, Cin)}, g.options());
-  const auto fc = sp > 1 ? wino_fold_counters(g.device(), ((B * ((H + 1) / 2) * ((W + 1) / 2) + 63) / 64) * (Cin / 32))
-                         : std::pair<unsigned*, long long>{nullptr, 0};
+  if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
   TP_CHECK_HIP(tp_conv_wino(g.data_ptr<float>(), unpool ? g_argmax->data_ptr<uint8_t>() : nullptr,
                             ut.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, unpool ? 1 : 0, EPI_BWD,
                             (int)sp, staged ? 1 : 0, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
                             act.data_ptr<float>(), tay, nullptr, sp > 1 ? ws.data_ptr<float>() : nullptr,
-                            (int)tay_mode, fc.first, fc.second, cur_stream()));
+                            (int)tay_mode, cur_stream()));
   return out;
 }
 
@@ -734,6 +703,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
 
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
+  m.def("wino_lds_bytes() -> int", []() -> int64_t { return tp_wino_lds_bytes(); });
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
   m.def("maxpool2_nhwc(Tensor x) -> (Tensor, Tensor)");
   m.def("maxpool_nhwc(Tensor x, int k, int s, int pad) -> Tensor");

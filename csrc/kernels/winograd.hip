@@ -80,14 +80,6 @@ struct WinoArgs {
   float* apoz;              // W_FWD: [B][K] counts of positive outputs (exact integers), nullable
   int dbg;                  // experiment switches (TP_WINO_DBG): 1 no epilogue, 2 no restaging, 4 no transform
   int tay_mode;             // W_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
-  // split-K folded into the kernel (W_FWD / W_BWD): every split block parks its transformed
-  // 2x2 outputs (the 2 x 4096-float LDS image) in fold_ws[split][tile]; the LAST block of a tile
-  // to arrive (per-tile counter) sums the images in split order and runs the epilogue — no
-  // separate combine launch, and the same summation order as the combine kernel
-  int fold;
-  float* fold_ws;
-  unsigned* fold_ctr;       // n_tiles counters, zero between launches (the last block resets)
-  long long fold_tiles;
 };
 
 // Phase-attribution switches for profiling experiments only: they skip barriers / stores and
@@ -225,45 +217,6 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
     }
   }
   __syncthreads();
-  if constexpr (EPI == W_FWD || EPI == W_BWD) {
-    if (p.fold) {
-      __shared__ int s_last;
-      const long long tile_id = (long long)blk_p * (p.K / W_TK) + k0 / W_TK;
-      const int S = gridDim.y, me = blockIdx.y;
-      float* mine = p.fold_ws + ((long long)me * p.fold_tiles + tile_id) * 8192;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int f = tid + 256 * i;  // float4 index over [yb0 | yb1]
-        *reinterpret_cast<float4*>(mine + 4 * f) = *reinterpret_cast<const float4*>((f < 1024 ? yb0 : yb1) + 4 * (f & 1023));
-      }
-      __threadfence();  // release: this block's image is visible device-wide before the count
-      __syncthreads();
-      if (tid == 0) s_last = atomicAdd(p.fold_ctr + tile_id, 1u) == (unsigned)(S - 1);
-      __syncthreads();
-      if (!s_last) return;
-      __threadfence();  // acquire: the other splits' images
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int f = tid + 256 * i;
-        float4* dst = reinterpret_cast<float4*>((f < 1024 ? yb0 : yb1) + 4 * (f & 1023));
-        const float4 own = *dst;
-        float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int sp = 0; sp < S; ++sp) {
-          float4 v = own;
-          if (sp != me) {  // streamed past this XCD's L2 (written by other blocks, read once)
-            const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
-                p.fold_ws + ((long long)sp * p.fold_tiles + tile_id) * 8192 + 4 * f));
-            v = make_float4(t[0], t[1], t[2], t[3]);
-          }
-          if (sp == 0) sum = v;
-          else sum = make_float4(sum.x + v.x, sum.y + v.y, sum.z + v.z, sum.w + v.w);
-        }
-        *dst = sum;
-      }
-      if (tid == 0) p.fold_ctr[tile_id] = 0u;  // ready for the next launch
-      __syncthreads();
-    }
-  }
 phase2:
   // ---- phase 2: coalesced global traffic ------------------------------------------------
   if WDBG(p, 8) return;
@@ -404,7 +357,9 @@ template <int EPI, int XMODE>
 __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   constexpr bool STAGED = XMODE == X_STAGED || XMODE == X_STAGED_UNPOOL || XMODE == X_SPAN;
   constexpr bool UNPOOL = XMODE == X_UNPOOL;
-  // separate objects per buffer so the compiler's LDS-DMA alias tracking can tell them apart
+  // separate objects per buffer so the compiler's LDS-DMA alias tracking can tell them apart.
+  // The staged modes use exactly 80 KB: two blocks per CU (160 KB). ANY extra __shared__ byte
+  // halves the occupancy (tests/test_conv_gpu.py::test_wino_lds_budget guards this).
   __shared__ __attribute__((aligned(16))) float us0[W_UIMG];
   __shared__ __attribute__((aligned(16))) float us1[W_UIMG];
   __shared__ __attribute__((aligned(16))) float xs0[STAGED ? W_XS : 4];
@@ -1028,6 +983,21 @@ extern "C" hipError_t tp_wino_weights(const float* w, float* u, int K, int C, in
   return tp_wino_weights2(w, u, K, C, flip_t, flip_t ? C : K, flip_t ? K : C, st);
 }
 
+// static LDS bytes of the largest Winograd kernel instantiations (occupancy guard)
+extern "C" int tp_wino_lds_bytes() {
+  using namespace tp;
+  const void* fns[] = {(const void*)wino_f2x3<W_FWD, X_STAGED>, (const void*)wino_f2x3<W_FWD_POOL, X_STAGED>,
+                       (const void*)wino_f2x3<W_BWD, X_STAGED_UNPOOL>, (const void*)wino_f2x3<W_BWD, X_SPAN>,
+                       (const void*)wino_f2x3<W_PARTIAL, X_STAGED>};
+  int worst = 0;
+  for (const void* f : fns) {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, f) != hipSuccess) return -1;
+    worst = std::max(worst, (int)a.sharedSizeBytes);
+  }
+  return worst;
+}
+
 extern "C" int tp_wino_staged_ok(int H, int W, int unpool) {
   return tp::staged_geometry(H, W, unpool != 0).ok ? 1 : 0;
 }
@@ -1043,8 +1013,7 @@ extern "C" void tp_wino_geometry(int H, int W, int unpool, int* out9) {
 extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W,
                                    int C, int K, int unpool, int epi, int splits, int staged, const float* scale,
                                    const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
-                                   float* taylor, float* apoz, float* ws, int tay_mode, unsigned* fold_ctr,
-                                   long long fold_ctr_len, hipStream_t st) {
+                                   float* taylor, float* apoz, float* ws, int tay_mode, hipStream_t st) {
   using namespace tp;
   // odd H / W: a partial last tile row / column, direct loads only (no pooling / unpooling)
   const bool odd = (H & 1) || (W & 1);
@@ -1117,14 +1086,7 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   const int n_p = (a.P + 63) / 64, n_k = K / 32;
   dim3 grid(n_p * n_k, splits);
   int e_launch = epi;
-  const bool fold = splits > 1 && (epi == W_FWD || epi == W_BWD) && fold_ctr && fold_ctr_len >= (long long)n_p * n_k;
-  if (fold) {
-    if (!ws) return hipErrorInvalidValue;
-    a.fold = 1;
-    a.fold_ws = ws;
-    a.fold_ctr = fold_ctr;
-    a.fold_tiles = (long long)n_p * n_k;
-  } else if (splits > 1) {
+  if (splits > 1) {
     if (!ws) return hipErrorInvalidValue;
     a.out = ws;
     a.pooled_m = epi == W_FWD_POOL ? 1 : 0;
@@ -1146,7 +1108,7 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   else TP_W(W_PARTIAL);
 #undef TP_W
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || splits == 1 || fold) return e;
+  if (e != hipSuccess || splits == 1) return e;
   return tp_conv_epilogue_slabs(ws, splits, B, H, W, K, epi, scale, shift, relu, out, out_argmax, act, taylor,
                                 a.apoz, tay_mode, st);
 }

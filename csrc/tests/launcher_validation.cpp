@@ -23,7 +23,7 @@ hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, i
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
-                        int tay_mode, unsigned* fold_ctr, long long fold_ctr_len, hipStream_t st);
+                        int tay_mode, hipStream_t st);
 hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
                            float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
                            float* b, double* ws, hipStream_t st);
@@ -70,11 +70,11 @@ int main() {
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 6, 64, 3, 1, 1, 64, 0, 1, 0) == hipErrorInvalidValue);   // Cin % 4
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 96, 0, 1, 0) == hipErrorInvalidValue);  // Kpad small
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 576, 7, 1, 0) == hipErrorInvalidValue); // bad cfg
-  EXPECT(tp_conv_wino(n, nullptr, n, 2, 7, 8, 64, 64, 0, 1, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, nullptr, 0, 0) ==
+  EXPECT(tp_conv_wino(n, nullptr, n, 2, 7, 8, 64, 64, 0, 1, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
          hipErrorInvalidValue);  // odd H with 2x2 pooling
-  EXPECT(tp_conv_wino(n, nullptr, n, 2, 7, 8, 64, 64, 1, 2, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, nullptr, 0, 0) ==
+  EXPECT(tp_conv_wino(n, nullptr, n, 2, 7, 8, 64, 64, 1, 2, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
          hipErrorInvalidValue);  // odd H with unpooling
-  EXPECT(tp_conv_wino(n, nullptr, n, 2, 8, 8, 12, 64, 0, 0, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, nullptr, 0, 0) ==
+  EXPECT(tp_conv_wino(n, nullptr, n, 2, 8, 8, 12, 64, 0, 0, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
          hipErrorInvalidValue);  // C % 8
   EXPECT(tp_bn_fwd_train(n, n, 16, 6, n, n, 1e-5f, 0.1f, n, n, n, n, n, n, nullptr, 0) == hipErrorInvalidValue);
 

@@ -293,6 +293,14 @@ def test_wino_fwd(cuda, shape, splits, pool, staged):
         assert (am.cpu().long() == am_ref).float().mean() > 0.999
 
 
+def test_wino_lds_budget(cuda):
+    """The staged Winograd kernels fit two blocks per CU (<= 80 KB of the 160 KB LDS): one more
+    __shared__ word would silently halve their occupancy (a 17% headline regression, measured)."""
+    from torchpruner_amd import ops
+    lds = ops.require().wino_lds_bytes()
+    assert 0 < lds <= 80 * 1024, lds
+
+
 WINO_ODD_SHAPES = [(3, 7, 7, 64, 64), (2, 5, 9, 32, 32), (2, 7, 14, 64, 32), (4, 3, 3, 32, 64), (2, 1, 5, 32, 32)]
 
 
