@@ -485,3 +485,39 @@ def test_wino_fwd_apoz_counts(cuda, staged, splits):
     torch.testing.assert_close(out.cpu(), ref, rtol=3e-4, atol=3e-4)
     cnt = (ref > 0).sum((1, 2)).float()
     assert (apoz.cpu() - cnt).abs().max() <= 2
+
+
+def _mse_onehot(out, y, reduction="mean"):
+    """A non-cross-entropy criterion (MSE to one-hot targets), reference-style signature."""
+    return F.mse_loss(out, F.one_hot(y, out.shape[1]).float(), reduction=reduction)
+
+
+@pytest.mark.parametrize("arch", ["vgg", "resnet"])
+@pytest.mark.parametrize("metric", ["taylor", "sensitivity"])
+def test_engines_any_criterion(cuda, arch, metric):
+    """Gradient metrics with a criterion other than cross-entropy stay on the native engines
+    (dL/dlogits through autograd on the logits) and match the fp64 CPU oracle."""
+    import copy
+    from torchpruner_amd import SensitivityAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models import vgg_cifar
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    torch.manual_seed(3)
+    if arch == "vgg":
+        model = vgg_cifar(11).to(cuda).eval()
+        mods = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+        x = torch.randn(32, 3, 32, 32, device=cuda)
+    else:
+        model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=10, width=32).to(cuda).eval()
+        mods = [b.conv1 for b in model.modules() if isinstance(b, Bottleneck)]
+        x = torch.randn(16, 3, 64, 64, device=cuda)
+    y = torch.randint(0, 10, (x.shape[0],), device=cuda)
+    cls = TaylorAttributionMetric if metric == "taylor" else SensitivityAttributionMetric
+    m = cls(model, DeviceLoader(x, y, 8), _mse_onehot, cuda)
+    got = m.run_many(mods, find_best_evaluation_module=True)
+    assert m.last_path["path"] == ("fused" if arch == "vgg" else "resnet"), m.last_path
+    m64 = copy.deepcopy(model).double().cpu()
+    mods64 = [dict(m64.named_modules())[n] for n, mm in model.named_modules() if any(mm is q for q in mods)]
+    ref = cls(m64, DeviceLoader(x.double().cpu(), y.cpu(), 8), _mse_onehot, "cpu").run_many(mods64, True)
+    for a, e in zip(got, ref):
+        assert np.abs(a - e).max() / (np.abs(e).max() + 1e-30) < 5e-3

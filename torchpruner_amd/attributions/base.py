@@ -411,27 +411,29 @@ class _AttributionMetric(ABC):
         """Gradient metrics on the fused VGG-chain engine: per batch ONE fused forward +
         input-gradient backward writes every block's per-sample partials (``mode`` taylor /
         sensitivity), and ONE fold launch turns all layers' sums into fp64 accumulators."""
+        from ..engine.fused_chain import engine_criterion
         owner = {}
         for k, b in enumerate(blocks):
             owner.setdefault(b, k)
         uniq = sorted(owner)
         stats = accs[0].mode == "stats"
+        crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
         for i, x, y in self._batches():
             B = x.shape[0]
             if stats:
                 arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
                 with trace_range("tp.forward_backward"):
                     if engine.graphs_enabled(B):  # small batches are launch-bound: replay a HIP graph
-                        engine.taylor_graphed(x, y, set(uniq), arena, mode=mode)
+                        engine.taylor_graphed(x, y, set(uniq), arena, mode=mode, criterion=crit)
                     else:
-                        engine.taylor(x, y, set(uniq), arena, mode=mode)
+                        engine.taylor(x, y, set(uniq), arena, mode=mode, criterion=crit)
                 sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device, engine.real_width(b)) for b in uniq]
                 with trace_range("tp.fold"):
                     ops.score_fold_([arena[b] for b in uniq], sums, take_abs, 2)
                 for b in uniq:
                     accs[owner[b]].count += B
             else:
-                res = engine.taylor(x, y, set(uniq), mode=mode)
+                res = engine.taylor(x, y, set(uniq), mode=mode, criterion=crit)
                 ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), take_abs, 1)
                 for b in uniq:
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
@@ -439,17 +441,12 @@ class _AttributionMetric(ABC):
 
     def _resnet_grad_engine(self, eval_modules, why=None):
         """The ResNet engine when it can produce gradient scores for ``eval_modules`` (eval-mode
-        torchvision-layout ResNet, block BNs, mean cross-entropy criterion), else None."""
-        from ..engine.fused_chain import _reject, criterion_is_cross_entropy
+        torchvision-layout ResNet, block BNs; any differentiable criterion), else None."""
+        from ..engine.fused_chain import _reject
         from ..engine.resnet_engine import maybe_resnet_engine
         if not self._engines_allowed():
             return _reject(why, f"compute_dtype={self.compute_dtype} runs the generic autocast path")
-        eng = maybe_resnet_engine(self.model, eval_modules, self.device, grad=True, why=why)
-        if eng is None:
-            return None
-        if not criterion_is_cross_entropy(self.criterion, self.device):
-            return _reject(why, "resnet engine: criterion is not mean cross-entropy")
-        return eng
+        return maybe_resnet_engine(self.model, eval_modules, self.device, grad=True, why=why)
 
     def _fused_engine(self, eval_modules, why=None, need_ce=True, pre_act_ok=False):
         """The fused chain engine (engine, block indices) for ``eval_modules``, else None."""
@@ -462,15 +459,17 @@ class _AttributionMetric(ABC):
     def _resnet_grad_pass(self, eng, eval_modules, accs, mode):
         """Per batch: one engine forward + input-gradient backward scores every module; the
         (B, C_padded) slabs are folded into fp64 accumulators (16 layers per launch)."""
+        from ..engine.fused_chain import engine_criterion
         uniq = list(dict.fromkeys(eval_modules))
         first = {}
         for k, m in enumerate(eval_modules):
             first.setdefault(m, k)
         stats = accs[0].mode == "stats"
+        crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
         with torch.no_grad():
             for i, x, y in self._batches():
                 with trace_range("tp.forward_backward"):
-                    res = eng.grad_scores(x, y, set(uniq), mode)
+                    res = eng.grad_scores(x, y, set(uniq), mode, crit)
                 if stats:
                     slabs = [res[m] for m in uniq]
                     sums = [accs[first[m]].ensure_sum(res[m].shape[1], x.device, m.num_features) for m in uniq]

@@ -20,7 +20,7 @@ class SensitivityAttributionMetric(_AttributionMetric):
         self._begin_run(accs, eval_modules)
         try:
             why = []
-            fused = self._fused_engine(eval_modules, why)
+            fused = self._fused_engine(eval_modules, why, need_ce=False)  # any criterion (autograd on the logits)
             rn = None if fused is not None else self._resnet_grad_engine(eval_modules, why)
             self._record_path("fused" if fused else "resnet" if rn else "generic", eval_modules, why)
             if fused is not None:  # VGG-style chains: |dL/da| partials from the fused dgrad epilogues

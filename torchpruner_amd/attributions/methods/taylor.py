@@ -31,7 +31,7 @@ class TaylorAttributionMetric(_AttributionMetric):
 
     def _run_loop(self, eval_modules, accs, mode):
         why = []
-        fused = self._fused_engine(eval_modules, why)
+        fused = self._fused_engine(eval_modules, why, need_ce=False)  # any criterion (autograd on the logits)
         rn = None if fused is not None else self._resnet_grad_engine(eval_modules, why)
         self._record_path("fused" if fused else "resnet" if rn else "generic", eval_modules, why)
         if fused is not None:

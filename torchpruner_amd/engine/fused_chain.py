@@ -685,7 +685,8 @@ class FusedChainEngine:
         mode = os.environ.get("TORCHPRUNER_GRAPHS", "0")
         return mode == "all" or (mode == "1" and B <= self.GRAPH_MAX_B)
 
-    def taylor_graphed(self, x: torch.Tensor, y: torch.Tensor, want: set, arena: dict, mode="taylor"):
+    def taylor_graphed(self, x: torch.Tensor, y: torch.Tensor, want: set, arena: dict, mode="taylor",
+                       criterion=None):
         """``taylor()`` replayed from a captured HIP graph: the ~40 launches of one fused
         forward + input-gradient backward become one graph launch, which is what small,
         launch-bound batches need. One graph per (input shapes, blocks, mode, score arena,
@@ -694,6 +695,8 @@ class FusedChainEngine:
         into the graph's static inputs and replay. Re-packed weights (pruning, training) or a
         new arena invalidate the graph. ``arena`` must be zero before each call, as for
         ``taylor()`` (ops.score_fold_ with after=2 leaves it so)."""
+        if criterion is not None:  # a user criterion runs through autograd: eager launches
+            return self.taylor(x, y, want, arena, mode, criterion)
         P = self._pack()
         key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device))
         g = self._graphs.get(key)
@@ -719,8 +722,9 @@ class FusedChainEngine:
         g["graph"].replay()
         return {b: arena[b] for b in want}
 
-    def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None, mode="taylor"):
-        """One fused forward+backward; returns {block index: per-sample signed Taylor sums
+    def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None, mode="taylor",
+               criterion=None):
+        """One fused forward+backward (``criterion``: see :func:`logits_grad`); returns {block index: per-sample signed Taylor sums
         sum_hw -(dL/da * a)} (``mode="sensitivity"``: sum_hw |dL/da|) for every requested block
         (conv blocks first, then linear blocks; the final linear has none) as (R, B, C) partial
         slots for conv blocks (sum over R, or fold with ops.score_fold_) and (B, C) for linear
@@ -736,7 +740,7 @@ class FusedChainEngine:
                      for b, sh in self._arena_shapes(x.shape[0], want, x.shape[2], x.shape[3]).items()}
         logits, saved = self.forward(x)
         B = logits.shape[0]
-        _, g = ops.cross_entropy(logits, y, 1.0 / B, True)
+        g = logits_grad(logits, y, criterion)
         lin_acts = saved["lin_acts"]
         acts = saved["acts"]
         res = {}
@@ -798,6 +802,25 @@ class FusedChainEngine:
         return res
 
 
+def logits_grad(logits: torch.Tensor, y: torch.Tensor, criterion=None) -> torch.Tensor:
+    """dL/dlogits of the batch loss the engines back-propagate: the fused HIP log-softmax + NLL
+    kernel for mean cross-entropy (``criterion=None``), else autograd through the user's
+    criterion on the (detached) logits, with its default reduction — exactly the gradient the
+    reference's ``criterion(out, y).backward()`` feeds into the network (attributions.py:64-68)."""
+    if criterion is None:
+        return ops.cross_entropy(logits, y, 1.0 / logits.shape[0], True)[1]
+    lg = logits.detach().requires_grad_(True)
+    with torch.enable_grad():
+        loss = criterion(lg, y)
+    return torch.autograd.grad(loss, lg)[0].float().contiguous()
+
+
+def engine_criterion(criterion, device):
+    """``None`` (the fused cross-entropy) when ``criterion`` is plain mean cross-entropy, else the
+    criterion itself (engines then differentiate it with autograd on the logits)."""
+    return None if criterion is None or criterion_is_cross_entropy(criterion, device) else criterion
+
+
 def criterion_is_cross_entropy(criterion, device) -> bool:
     """Numerically probe whether ``criterion(out, y[, reduction])`` is plain mean cross-entropy."""
     try:
@@ -820,7 +843,8 @@ def _reject(why, reason):
 
 def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None, pre_act_ok=False):
     """Return (engine, block indices of eval_modules) when the fused path applies, else None.
-    ``need_ce=False``: forward-only use (APoZ), any criterion. ``why``: a list that receives the
+    ``need_ce=False``: forward-only use (APoZ) or gradient metrics with any criterion (the caller
+    passes ``engine_criterion(criterion)`` to :meth:`FusedChainEngine.taylor`). ``why``: a list that receives the
     rejection reason when the engine does not apply. ``pre_act_ok``: a classifier block's Linear
     may stand for its activation output (valid for sign counts (APoZ) and zero-masking
     (Shapley): ReLU / LeakyReLU keep the sign and map 0 to 0; not for Taylor / Sensitivity)."""

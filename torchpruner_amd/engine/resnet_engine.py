@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, cpad, winograd_weights
+from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, cpad, logits_grad, winograd_weights
 
 
 @dataclass
@@ -355,8 +355,9 @@ class ResNetEngine:
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands)
         return run(cfg, sp)
 
-    def grad_scores(self, x: torch.Tensor, y: torch.Tensor, want, mode: str):
-        """One engine forward + input-gradient-only backward of the mean cross-entropy; returns
+    def grad_scores(self, x: torch.Tensor, y: torch.Tensor, want, mode: str, criterion=None):
+        """One engine forward + input-gradient-only backward of the loss (mean cross-entropy on
+        the fused kernel, or ``criterion`` through autograd on the logits); returns
         {BN module: (B, C_padded) per-sample ``ops.channel_reduce`` score} for the block BNs in
         ``want`` (evaluation modules of conv1/conv2 of each block). No weight gradients, no
         autograd graph; the backward stops at the earliest block holding a wanted BN."""
@@ -365,7 +366,7 @@ class ResNetEngine:
         logits, saved = self.forward(x, save=True)
         feat = saved.pop()
         B = logits.shape[0]
-        _, g_log = ops.cross_entropy(logits, y, 1.0 / B, True)
+        g_log = logits_grad(logits, y, criterion)
         g_feat = self._fc_bwd(T, P, g_log, feat)  # (B, C_last padded)
         y_last = saved[-1][2]
         HW = y_last.shape[1] * y_last.shape[2]
