@@ -521,3 +521,36 @@ def test_engines_any_criterion(cuda, arch, metric):
     ref = cls(m64, DeviceLoader(x.double().cpu(), y.cpu(), 8), _mse_onehot, "cpu").run_many(mods64, True)
     for a, e in zip(got, ref):
         assert np.abs(a - e).max() / (np.abs(e).max() + 1e-30) < 5e-3
+
+
+@pytest.mark.parametrize("arch", ["vgg", "resnet"])
+def test_engines_shapley_any_criterion(cuda, arch):
+    """Shapley with a non-cross-entropy criterion on the native engines == the fp64 CPU oracle
+    (same permutations); per-sample losses from criterion(out, y, reduction="none")."""
+    import copy
+    from torchpruner_amd import ShapleyAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models import vgg_cifar
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(5)
+    if arch == "vgg":
+        model = vgg_cifar(11).to(cuda).eval()
+        module = [m for m in model.features if isinstance(m, torch.nn.Conv2d)][5]
+        x = torch.randn(12, 3, 32, 32, device=cuda)
+    else:
+        model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=10, width=32).to(cuda).eval()
+        module = [b.conv2 for b in model.modules() if isinstance(b, Bottleneck)][2]
+        x = torch.randn(8, 3, 64, 64, device=cuda)
+    y = torch.randint(0, 10, (x.shape[0],), device=cuda)
+    np.random.seed(3)
+    m = ShapleyAttributionMetric(model, DeviceLoader(x, y, 4), _mse_onehot, cuda, sv_samples=2, reduction="none")
+    got = m.run(module, find_best_evaluation_module=True)
+    assert m.last_path["path"] == ("fused" if arch == "vgg" else "resnet"), m.last_path
+    m64 = copy.deepcopy(model).double().cpu()
+    name = [n for n, mm in model.named_modules() if mm is module][0]
+    np.random.seed(3)
+    ref = ShapleyAttributionMetric(m64, DeviceLoader(x.double().cpu(), y.cpu(), 4), _mse_onehot, "cpu", sv_samples=2,
+                                   reduction="none").run(dict(m64.named_modules())[name],
+                                                         find_best_evaluation_module=True)
+    assert np.abs(got - ref).max() / (np.abs(ref).max() + 1e-12) < 2e-3

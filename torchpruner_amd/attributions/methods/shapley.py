@@ -207,15 +207,17 @@ class ShapleyAttributionMetric(_AttributionMetric):
 
     # ------------------------------------------------------------------ native path
     def _fused_prepare(self, module, why=None):
-        """Prefix evaluation on the fused HIP engine (eval-mode VGG-style chains, CE loss):
+        """Prefix evaluation on the fused HIP engine (eval-mode VGG-style chains, any per-sample loss):
         the evaluation module's activation is produced once per batch, K prefix-masked copies
         are stacked by one kernel and pushed through the remaining fused layers in ONE forward.
         Masking a post-ReLU activation commutes with the following 2x2 max-pool, so the
         engine masks its pooled output (4x less data) with identical results."""
-        fused = self._fused_engine([module], why, pre_act_ok=True)
+        from ...engine.fused_chain import engine_criterion
+        fused = self._fused_engine([module], why, need_ce=False, pre_act_ok=True)  # any per-sample criterion
         if fused is None:
             return None
         engine, (k,) = fused
+        crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
 
         n = engine.real_width(k)
         pad_rank = _RankPadder(n)
@@ -234,14 +236,14 @@ class ShapleyAttributionMetric(_AttributionMetric):
             zk, _ = engine.forward(x, stop_after=k)  # engine layout (B, H, W, C padded)
             B = zk.shape[0]
             z_cl = zk.permute(0, 3, 1, 2)  # (B, C, H, W) view, channels_last strides
-            base = engine.loss_from(k, zk, y)
+            base = engine.loss_from(k, zk, y, crit)
 
             def evaluate(rank_t, p_first, cnt):
                 if delta:  # next block is a Linear: prefix-delta GEMM (no masked copies)
                     return engine.prefix_delta_loss(k, zk, perm_of(rank_t), pad_rank(rank_t, zk.shape[3]), p_first,
-                                                    cnt, y)
+                                                    cnt, y, crit)
                 masked = ops.prefix_mask(z_cl, pad_rank(rank_t, zk.shape[3]), p_first, cnt)  # channels_last
-                loss = engine.loss_from(k, masked.permute(0, 2, 3, 1), y.repeat(cnt))
+                loss = engine.loss_from(k, masked.permute(0, 2, 3, 1), y.repeat(cnt), crit)
                 return loss.view(cnt, B)
 
             return n, B, zk[0].numel(), base, evaluate
@@ -249,13 +251,15 @@ class ShapleyAttributionMetric(_AttributionMetric):
         return prepare
 
     def _resnet_prepare(self, module, why=None):
-        """Prefix evaluation on the ResNet engine (block-internal BN evaluation modules, CE loss):
+        """Prefix evaluation on the ResNet engine (block-internal BN evaluation modules, any loss):
         the masked activation and the block's residual operand are produced once per batch,
         K prefix-masked copies are pushed through the rest of the block and the network in ONE
         engine forward."""
+        from ...engine.fused_chain import engine_criterion, per_sample_loss
         eng = self._resnet_grad_engine([module], why)
         if eng is None:
             return None
+        crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
         bi, ci = eng.locate(module)
         n = module.num_features
         pad_rank = _RankPadder(n)
@@ -264,13 +268,13 @@ class ShapleyAttributionMetric(_AttributionMetric):
             a, idn = eng.forward_to(x, bi, ci)
             B = a.shape[0]
             a_cl = a.permute(0, 3, 1, 2)
-            base, _ = ops.cross_entropy(eng.logits_from(bi, ci, a, idn), y, 1.0, False)
+            base = per_sample_loss(eng.logits_from(bi, ci, a, idn), y, crit)
 
             def evaluate(rank_t, p_first, cnt):
                 masked = ops.prefix_mask(a_cl, pad_rank(rank_t, a.shape[3]), p_first, cnt)
                 idn_k = idn.repeat(cnt, 1, 1, 1) if cnt > 1 else idn
-                loss, _ = ops.cross_entropy(eng.logits_from(bi, ci, masked.permute(0, 2, 3, 1), idn_k),
-                                            y.repeat(cnt), 1.0, False)
+                loss = per_sample_loss(eng.logits_from(bi, ci, masked.permute(0, 2, 3, 1), idn_k), y.repeat(cnt),
+                                       crit)
                 return loss.view(cnt, B)
 
             return n, B, 2 * a[0].numel(), base, evaluate

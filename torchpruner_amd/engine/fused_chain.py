@@ -581,7 +581,7 @@ class FusedChainEngine:
         return e
 
     def prefix_delta_loss(self, k: int, zk: torch.Tensor, perm_t: torch.Tensor, rank_t: torch.Tensor, p0: int,
-                          cnt: int, y: torch.Tensor) -> torch.Tensor:
+                          cnt: int, y: torch.Tensor, criterion=None) -> torch.Tensor:
         """Per-sample losses (cnt, B) of prefixes p0 .. p0+cnt-1 (units of rank < p0+j zeroed in
         copy j) of block ``k``'s output ``zk``, without materialising the cnt masked copies:
 
@@ -613,15 +613,15 @@ class FusedChainEngine:
         if j == len(self.plan.linears) - 1:  # the delta GEMM produced the logits
             n = self.plan.linears[-1].linear.out_features
             logits = out if n == N4 else out[:, :n].contiguous()
-            loss, _ = ops.cross_entropy(logits, yy, 1.0, False)
+            loss = per_sample_loss(logits, yy, criterion)
         else:
-            loss = self.loss_from(k + 1, out.view(cnt * B, 1, 1, N4), yy)
+            loss = self.loss_from(k + 1, out.view(cnt * B, 1, 1, N4), yy, criterion)
         return loss.view(cnt, B)
 
-    def loss_from(self, k: int, h: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-        """Per-sample cross-entropy of the network continued from block ``k``'s output."""
-        loss, _ = ops.cross_entropy(self.forward_from(k, h), y, 1.0, False)
-        return loss
+    def loss_from(self, k: int, h: torch.Tensor, y: torch.Tensor, criterion=None) -> torch.Tensor:
+        """Per-sample loss (cross-entropy, or ``criterion``: :func:`per_sample_loss`) of the
+        network continued from block ``k``'s output."""
+        return per_sample_loss(self.forward_from(k, h), y, criterion)
 
     def _block_hw(self, b, H0, W0):
         """Spatial size of block b's output activation for an H0 x W0 input."""
@@ -813,6 +813,16 @@ def logits_grad(logits: torch.Tensor, y: torch.Tensor, criterion=None) -> torch.
     with torch.enable_grad():
         loss = criterion(lg, y)
     return torch.autograd.grad(loss, lg)[0].float().contiguous()
+
+
+def per_sample_loss(logits: torch.Tensor, y: torch.Tensor, criterion=None) -> torch.Tensor:
+    """Per-sample losses (B,) of ``criterion(out, y, reduction="none")`` (attributions.py:50,87),
+    trailing dims summed as on the generic path; the fused HIP cross-entropy for ``None``."""
+    if criterion is None:
+        return ops.cross_entropy(logits, y, 1.0, False)[0]
+    with torch.no_grad():
+        loss = criterion(logits, y, reduction="none")
+    return loss.reshape(logits.shape[0], -1).sum(-1).float()
 
 
 def engine_criterion(criterion, device):
