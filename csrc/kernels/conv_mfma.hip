@@ -258,31 +258,58 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
 
   float4 ra[T::A_CHUNKS], rb[T::B_CHUNKS];
 
+  // GEN 1: the K slice's (tap, channel block) advance incrementally with the (strictly
+  // sequential) load_tile calls instead of a runtime division per slice; a 1x1 conv's operand
+  // address is loop-invariant up to the channel offset, so it is formed once (a_k1).
+  int ld_tap = 0, ld_cs = 0;
+  unsigned a_k1[GEN == 1 && KS == 1 ? T::A_CHUNKS : 1];
+  if constexpr (GEN == 3) {
+    ld_tap = tmask ? __builtin_ctz(tmask) : KS * KS;  // kt_begin == 0 (GEN 3 never splits K)
+  }
+  if constexpr (GEN == 1) {
+    ld_tap = kt_begin / cin_tiles;
+    ld_cs = kt_begin - ld_tap * cin_tiles;
+    if constexpr (KS == 1) {
+#pragma unroll
+      for (int i = 0; i < T::A_CHUNKS; ++i) {
+        const int ih = a_oh[i], iw = a_ow[i];
+        const bool ok = a_mask[i] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        a_k1[i] = ok ? (unsigned)(a_off[i] + (ih * p.W + iw) * p.Cin + a_c4[i] * 4) * 4u : OOB;
+      }
+    }
+  }
+
   auto load_tile = [&](int kt) {
     int kb = kt;  // K slice of the weight operand
     if constexpr (GEN == 3) {
-      const int ti = kt / cin_tiles, cs = kt - ti * cin_tiles;
-      int tap = 0;
-      for (int t = 0, left = ti; t < KS * KS; ++t) {  // ti-th set bit of the tile's tap mask
-        if ((tmask >> t) & 1u) {
-          if (left == 0) {
-            tap = t;
-            break;
-          }
-          --left;
-        }
-      }
+      // (tap, channel block) advance with the sequential calls: the next tap is the next set
+      // bit of the tile's tap mask (no division / bit search per slice)
+      const int tap = ld_tap, cs = ld_cs;
       kb = tap * cin_tiles + cs;
       const int kh = tap / KS, kw = tap % KS, s = p.stride;
+      const bool s2 = s == 2;  // the common stride: shifts instead of integer divisions
 #pragma unroll
       for (int i = 0; i < T::A_CHUNKS; ++i) {
         const int th = a_oh[i] - kh, tw = a_ow[i] - kw;
-        const int yh = th / s, yw = tw / s;
+        const int yh = s2 ? th >> 1 : th / s, yw = s2 ? tw >> 1 : tw / s;
         const bool ok = a_mask[i] && th >= 0 && tw >= 0 && yh * s == th && yw * s == tw && yh < p.H && yw < p.W;
         const unsigned vo = ok ? (unsigned)(a_off[i] + (yh * p.W + yw) * p.Cin + cs * BK + a_c4[i] * 4) * 4u : OOB;
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
         ra[i] = make_float4(g[0], g[1], g[2], g[3]);
       }
+      if (++ld_cs == cin_tiles) {
+        ld_cs = 0;
+        const unsigned rest = tmask & ~((2u << tap) - 1u);
+        ld_tap = rest ? __builtin_ctz(rest) : KS * KS;
+      }
+    } else if constexpr (GEN == 1 && KS == 1) {
+      const unsigned coff = (unsigned)(ld_cs * BK) * 4u;
+#pragma unroll
+      for (int i = 0; i < T::A_CHUNKS; ++i) {
+        const f32x4 g = buf_load_f32x4(xr, (int)(a_k1[i] != OOB ? a_k1[i] + coff : OOB), 0, 0);
+        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+      }
+      ++ld_cs;
     } else if constexpr (GEN != 0) {
 #pragma unroll
       for (int i = 0; i < T::A_CHUNKS; ++i) {
@@ -291,14 +318,20 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           tap = kt * 8 + a_c4[i];
           c = 0;
         } else {
-          tap = kt / cin_tiles;
-          c = (kt - tap * cin_tiles) * BK + a_c4[i] * 4;
+          tap = ld_tap;
+          c = ld_cs * BK + a_c4[i] * 4;
         }
         const int ih = a_oh[i] + tap / KS, iw = a_ow[i] + tap % KS;
         const bool ok = a_mask[i] && tap < KS * KS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
         const unsigned vo = ok ? (unsigned)(a_off[i] + (ih * p.W + iw) * p.Cin + c) * 4u : OOB;
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
         ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+      }
+      if constexpr (GEN == 1) {
+        if (++ld_cs == cin_tiles) {
+          ld_cs = 0;
+          ++ld_tap;
+        }
       }
     } else {
     const int tap = kt / cin_tiles;
