@@ -256,7 +256,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     b_off[i] = n < p.N ? (n * p.K + b_c4[i] * 4) * 4 : -1;
   }
 
-  float4 ra[T::A_CHUNKS], rb[T::B_CHUNKS];
+  f32x4 ra[T::A_CHUNKS], rb[T::B_CHUNKS];  // the buffer-load results as they are (no repacking moves)
 
   // GEN 1: the K slice's (tap, channel block) advance incrementally with the (strictly
   // sequential) load_tile calls instead of a runtime division per slice; a 1x1 conv's operand
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         const bool ok = a_mask[i] && th >= 0 && tw >= 0 && yh * s == th && yw * s == tw && yh < p.H && yw < p.W;
         const unsigned vo = ok ? (unsigned)(a_off[i] + (yh * p.W + yw) * p.Cin + cs * BK + a_c4[i] * 4) * 4u : OOB;
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
-        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+        ra[i] = g;
       }
       if (++ld_cs == cin_tiles) {
         ld_cs = 0;
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
 #pragma unroll
       for (int i = 0; i < T::A_CHUNKS; ++i) {
         const f32x4 g = buf_load_f32x4(xr, (int)(a_k1[i] != OOB ? a_k1[i] + coff : OOB), 0, 0);
-        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+        ra[i] = g;
       }
       ++ld_cs;
     } else if constexpr (GEN != 0) {
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         const bool ok = a_mask[i] && tap < KS * KS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
         const unsigned vo = ok ? (unsigned)(a_off[i] + (ih * p.W + iw) * p.Cin + c) * 4u : OOB;
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
-        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+        ra[i] = g;
       }
       if constexpr (GEN == 1) {
         if (++ld_cs == cin_tiles) {
@@ -352,12 +352,12 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         v.y = ((am >> 8) & 0xffu) == q ? g[1] : 0.f;
         v.z = ((am >> 16) & 0xffu) == q ? g[2] : 0.f;
         v.w = ((am >> 24) & 0xffu) == q ? g[3] : 0.f;
-        ra[i] = v;
+        ra[i] = f32x4{v.x, v.y, v.z, v.w};
       } else {
         const int delta = (dh * p.W + dw) * p.Cin + c0;  // wave-uniform
         const unsigned vo = ok ? (unsigned)(a_off[i] + delta) * 4u : OOB;
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
-        ra[i] = make_float4(g[0], g[1], g[2], g[3]);
+        ra[i] = g;
       }
     }
     }
@@ -365,16 +365,16 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     for (int i = 0; i < T::B_CHUNKS; ++i) {
       const unsigned vo = b_off[i] >= 0 ? (unsigned)(b_off[i] + kb * BK * 4) : OOB;
       const f32x4 g = buf_load_f32x4(wr, (int)vo, 0, 0);
-      rb[i] = make_float4(g[0], g[1], g[2], g[3]);
+      rb[i] = g;
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < T::A_CHUNKS; ++i)
-      *reinterpret_cast<float4*>(smem + buf * STAGE + a_row[i] * LDK + a_c4[i] * 4) = ra[i];
+      *reinterpret_cast<f32x4*>(smem + buf * STAGE + a_row[i] * LDK + a_c4[i] * 4) = ra[i];
 #pragma unroll
     for (int i = 0; i < T::B_CHUNKS; ++i)
-      *reinterpret_cast<float4*>(smem + buf * STAGE + (BM + b_row[i]) * LDK + b_c4[i] * 4) = rb[i];
+      *reinterpret_cast<f32x4*>(smem + buf * STAGE + (BM + b_row[i]) * LDK + b_c4[i] * 4) = rb[i];
   };
 
   f32x16 acc[T::TM][T::TN];
