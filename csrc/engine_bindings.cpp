@@ -63,6 +63,15 @@ hipError_t tp_pack_conv_weight(const float* w, float* out, int O, int I, int KS,
 long long tp_wino_wgrad_ws_elems(int B, int H, int W, int Cin, int Cout, int splits);
 hipError_t tp_wino_wgrad(const float* g, const float* x, float* ws, int B, int H, int W, int Cin, int Cout, int cfg,
                          int splits, float* fin, int fin_co, int fin_ci, const long long* fs, hipStream_t st);
+hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                        int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
+                        const float* shift, int relu, const float* res, int res_stride, const float* mask,
+                        float* apoz, float* out, float* ws, double* bnpart, hipStream_t st);
+int tp_conv_tile_m(int cfg);
+hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
+                               float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
+                               float* b, double* ws, const double* pre, int G, const float* res, int relu, uint8_t* mko,
+                               hipStream_t st);
 hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                           int ks, int stride, int pad, int Kpad, int cfg, int splits, float* fin, int fin_co,
                           int fin_ci, const long long* fs, hipStream_t st);
@@ -591,6 +600,31 @@ at::Tensor conv_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t ks, int6
   return fin ? at::empty({0}, g.options()) : dw;  // with ``out`` the result is in ``out``
 }
 
+// Training conv forward that also returns the BatchNorm statistics of its output: y (B, Ho, Wo,
+// Cout) and per M tile the column sums / sums of squares, (ceil(M / tile_m(cfg)), 2, Cout) fp64
+// (fold with bn_train_fwd(..., pre=)). No split-K, no epilogue besides the bias.
+std::tuple<at::Tensor, at::Tensor> conv_gen_stats(const at::Tensor& x, const at::Tensor& w,
+                                                  const c10::optional<at::Tensor>& shift, int64_t ks, int64_t stride,
+                                                  int64_t pad, int64_t cfg) {
+  need(x, "x", 4);
+  need(w, "w", 2);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
+  TORCH_CHECK((Cin % 32 == 0 && (ks == 1 || ks == 3 || ks == 5)) || (Cin == 4 && (ks == 3 || ks == 5 || ks == 7)),
+              "conv_gen_stats supports ks 1/3/5 with Cin % 32 == 0, or ks 3/5/7 with a 4-channel input");
+  TORCH_CHECK(w.size(1) == tp_conv_gen_k((int)ks, (int)Cin), "weight K mismatch");
+  TORCH_CHECK(stride >= 1 && pad >= 0 && Cout % 4 == 0, "bad geometry / Cout % 4");
+  const int64_t Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const float* sh = opt_ptr(shift, Cout, "shift");
+  auto out = at::empty({B, Ho, Wo, Cout}, x.options());
+  const int64_t M = B * Ho * Wo, tm = tp_conv_tile_m((int)cfg);
+  auto part = at::empty({(M + tm - 1) / tm, 2, Cout}, x.options().dtype(at::kDouble));
+  TP_CHECK_HIP(tp_conv_gen3(x.data_ptr<float>(), w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin, (int)Cout,
+                            (int)ks, (int)stride, (int)pad, 0, 0, 0, (int)cfg, 1, nullptr, sh, 0, nullptr, 1, nullptr,
+                            nullptr, out.data_ptr<float>(), nullptr, part.data_ptr<double>(), cur_stream()));
+  return {out, part};
+}
+
 // Winograd F(2x2,3x3) weight gradient of a stride-1 pad-1 3x3 conv: g (B, H, W, Cout), x (B, H, W,
 // Cin) NHWC (H, W even, Cin % 32 == 0) -> ``out`` (Cout_r, Cin_r, 3, 3), any strides (real channels).
 void wino_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t cfg, int64_t splits, at::Tensor& out) {
@@ -626,7 +660,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
                                                              const c10::optional<at::Tensor>& running_mean,
                                                              const c10::optional<at::Tensor>& running_var, double eps,
                                                              double momentum, const c10::optional<at::Tensor>& res,
-                                                             bool relu) {
+                                                             bool relu, const c10::optional<at::Tensor>& pre) {
   need(x, "x", -1);
   const int64_t C = x.size(-1), P = x.numel() / std::max<int64_t>(C, 1);
   TORCH_CHECK(C % 4 == 0 && P > 0, "bn_train_fwd needs C % 4 == 0 and a non-empty batch");
@@ -651,8 +685,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
   auto y = at::empty_like(x);
   auto mk = at::empty({relu ? P * C / 4 : 0}, x.options().dtype(at::kByte));
   auto stats = at::empty({4, C}, x.options());  // mean, invstd, a, b
-  auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   float* sp = stats.data_ptr<float>();
+  if (pre.has_value() && pre->defined()) {  // statistics reduced per tile by the producing conv
+    TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kDouble && pre->is_contiguous() && pre->dim() == 3 &&
+                    pre->size(1) == 2 && pre->size(2) == C && pre->device() == x.device(),
+                "pre must be conv_gen_stats' (G, 2, C) fp64 tile statistics");
+    const int64_t G = pre->size(0);
+    auto ws = at::empty({2 * std::min<int64_t>(G, 256) * C}, x.options().dtype(at::kDouble));
+    TP_CHECK_HIP(tp_bn_fwd_train_pre(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
+                                     (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(),
+                                     pre->data_ptr<double>(), (int)G, rp, relu ? 1 : 0,
+                                     relu ? mk.data_ptr<uint8_t>() : nullptr, cur_stream()));
+    return {y, stats[0], stats[1], mk};
+  }
+  auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   TP_CHECK_HIP(tp_bn_fwd_train3(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
                                 (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(), rp,
                                 relu ? 1 : 0, relu ? mk.data_ptr<uint8_t>() : nullptr, cur_stream()));
@@ -712,12 +758,14 @@ void register_engine_ops_def(torch::Library& m) {
         "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
   m.def("bn_train_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float eps, float momentum, Tensor? res=None, bool relu=False) -> (Tensor, Tensor, Tensor, Tensor)");
+        "float eps, float momentum, Tensor? res=None, bool relu=False, Tensor? pre=None) -> (Tensor, Tensor, Tensor, "
+        "Tensor)");
   m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx, Tensor? ym=None, "
         "bool want_dres=False, Tensor? mask=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "
         "-> Tensor");
   m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");
+  m.def("conv_gen_stats(Tensor x, Tensor w, Tensor? shift, int ks, int stride, int pad, int cfg) -> (Tensor, Tensor)");
   m.def("wino_wgrad(Tensor g, Tensor x, int cfg, int splits, Tensor(a!) out) -> ()");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
@@ -752,6 +800,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_gen_bwd", &conv_gen_bwd);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("pack_conv_weight", &pack_conv_weight);
+  m.impl("conv_gen_stats", &conv_gen_stats);
   m.impl("wino_wgrad", &wino_wgrad);
   m.impl("bn_train_fwd", &bn_train_fwd);
   m.impl("bn_train_bwd", &bn_train_bwd);

@@ -274,6 +274,29 @@ __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, con
   }
 }
 
+// Fold [G][2][C] per-tile statistics (written by a conv epilogue) into [G2][2][C] groups for
+// bn_fwd_finalize: block (64-channel slice, output group) sums its tiles with 4 lanes per
+// channel and a fixed-order LDS fold (deterministic).
+__global__ __launch_bounds__(256) void bn_fold_tiles(const double* __restrict__ in, int G, int C,
+                                                     double* __restrict__ out, int per) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  const int g0 = blockIdx.y * per, g1 = min(G, g0 + per);
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int g = g0 + lane; g < g1; g += 4) {
+      s += in[(size_t)(2 * g) * C + c];
+      q += in[(size_t)(2 * g + 1) * C + c];
+    }
+  red[0][lane][cl] = s;
+  red[1][lane][cl] = q;
+  __syncthreads();
+  if (lane < 2 && c < C) {
+    const double t = red[lane][0][cl] + red[lane][1][cl] + red[lane][2][cl] + red[lane][3][cl];
+    out[((size_t)blockIdx.y * 2 + lane) * C + c] = t;
+  }
+}
+
 inline int bn_groups(int P, int C) {
   const int col_blocks = (C + BN_CQ * 4 - 1) / (BN_CQ * 4);
   int groups = std::max(1, std::min(1024, 1024 / std::max(1, col_blocks)));
@@ -297,6 +320,27 @@ extern "C" hipError_t tp_bn_fwd_train3(const float* x, float* y, int P, int C, c
   const int rpg = (P + groups - 1) / groups;
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<0><<<grid, BN_T, 0, st>>>(x, nullptr, nullptr, nullptr, ws, P, C, rpg);
+  bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
+                                                    mean, invstd, a, b);
+  const unsigned n4 = (unsigned)((long long)P * C / 4);
+  bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
+      x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
+  return hipGetLastError();
+}
+
+// Forward with the batch statistics already reduced per conv tile (``pre``: [G][2][C] sums and
+// sums of squares over the tiles' rows, from the producing conv's epilogue): no statistics pass
+// over x. ws holds 2 * min(G, 256) * C doubles.
+extern "C" hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C, const float* gamma,
+                                          const float* beta, float eps, float momentum, float* run_mean,
+                                          float* run_var, float* mean, float* invstd, float* a, float* b,
+                                          double* ws, const double* pre, int G, const float* res, int relu,
+                                          uint8_t* mko, hipStream_t st) {
+  using namespace tp;
+  if (C % 4 || G <= 0 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int G2 = std::min(G, 256), per = (G + G2 - 1) / G2;
+  const int groups = (G + per - 1) / per;
+  bn_fold_tiles<<<dim3((C + 63) / 64, groups), 256, 0, st>>>(pre, G, C, ws, per);
   bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
                                                     mean, invstd, a, b);
   const unsigned n4 = (unsigned)((long long)P * C / 4);

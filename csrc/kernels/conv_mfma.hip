@@ -68,6 +68,8 @@ struct ConvArgs {
                             // EPI_BWD mask of the consumer activation)
   int res_rows;             // > 0: residual row = output row % res_rows (one (res_rows, N) residual
                             // broadcast over row blocks: Shapley prefix-delta GEMM)
+  double* bnpart;           // GEN EPI_FWD LDS epilogue, no split: per M tile the column sums and sums of
+                            // squares of the stored outputs, [m_tile][2][N] (training BN statistics)
 };
 
 // GEN 3 output row m -> (image, oh, ow). Parity order makes each stride-2 phase class one
@@ -465,6 +467,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     }
     int cur_b = -1;
     float4 cnt = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 bs = make_float4(0.f, 0.f, 0.f, 0.f), bq = bs;  // bnpart: this thread's column-quad sums
     // rows are visited in passes of RSTEP; the residual / mask quads of PF passes are loaded
     // together first (PF global loads in flight per thread instead of one round trip per row)
     constexpr int RSTEP = T::NT / C4, RPT = BM / RSTEP, PF = RPT < 4 ? RPT : 4;
@@ -524,6 +527,16 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           v.w = nan_act(v.w, p.slope);
         }
         *reinterpret_cast<float4*>(p.out + o) = v;
+        if (p.bnpart) {
+          bs.x += v.x;
+          bs.y += v.y;
+          bs.z += v.z;
+          bs.w += v.w;
+          bq.x += v.x * v.x;
+          bq.y += v.y * v.y;
+          bq.z += v.z * v.z;
+          bq.w += v.w * v.w;
+        }
         if (p.apoz) {  // exact integer counts: atomics are order-free
           const int b = m / p.HWo;
           if (b != cur_b) {
@@ -559,6 +572,20 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         for (int t = tid; t < n_img * BN; t += T::NT) {
           const int col = n0 + t % BN;
           if (cb[t] > 0.f && col < p.N) atomicAdd(p.apoz + (long long)(b_first + t / BN) * p.N + col, cb[t]);
+        }
+      }
+      if (p.bnpart) {  // fold the RSTEP row lanes of every column in a fixed order (deterministic)
+        __syncthreads();  // the tile in ts is no longer read
+        float* red = ts;  // [2][RSTEP][BN]
+        *reinterpret_cast<float4*>(red + row0 * BN + c4 * 4) = bs;
+        *reinterpret_cast<float4*>(red + (RSTEP + row0) * BN + c4 * 4) = bq;
+        __syncthreads();
+        for (int t = tid; t < 2 * BN; t += T::NT) {
+          const int which = t / BN, col = t - which * BN;
+          double acc = 0.0;
+#pragma unroll 4
+          for (int r = 0; r < RSTEP; ++r) acc += (double)red[(which * RSTEP + r) * BN + col];
+          if (n0 + col < p.N) p.bnpart[((long long)(m0 / BM) * 2 + which) * p.N + n0 + col] = acc;
         }
       }
     }
@@ -1199,11 +1226,37 @@ extern "C" hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, co
 // Full entry: ``transposed`` = data gradient of a strided conv (GEN 3) producing Ho_t x Wo_t
 // (the forward conv's input size); ``mask`` = ReLU-backward activation; ``res_stride``: see
 // ConvArgs. Forward convs pass transposed = 0 (Ho_t/Wo_t ignored), mask = null, res_stride = 1.
+extern "C" hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   double* bnpart, hipStream_t st);
+
 extern "C" hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
                                    int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
                                    const float* scale, const float* shift, int relu, const float* res,
                                    int res_stride, const float* mask, float* apoz, float* out, float* ws,
                                    hipStream_t st) {
+  return tp_conv_gen3(x, w, B, H, W, Cin, Cout, ks, stride, pad, transposed, Ho_t, Wo_t, cfg, splits, scale, shift,
+                      relu, res, res_stride, mask, apoz, out, ws, nullptr, st);
+}
+
+// M tile height of an implicit-GEMM tile config (the row count of a bnpart slab is ceil(M / it))
+extern "C" int tp_conv_tile_m(int cfg) {
+  switch (cfg) {
+    case 1: case 5: return 256;
+    case 2: return 64;
+    default: return 128;
+  }
+}
+
+// ``bnpart`` (nullable): [ceil(M / tile_m(cfg))][2][Cout] doubles receiving the per-tile column
+// sums / sums of squares of the output (training BatchNorm statistics); no split-K then.
+extern "C" hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   double* bnpart, hipStream_t st) {
   using namespace tp;
   const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
   if ((gen != 2 && Cin % 32 != 0) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
@@ -1241,9 +1294,16 @@ extern "C" hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H,
   a.mask = mask;
   a.apoz = apoz;
   a.out = out;
-  const char* ge = getenv("TP_GEN_EPI");
-  a.epi_lds = ge ? atoi(ge) : 1;
-  if (gen == 3 || mask || res_stride > 1) a.epi_lds = 1;  // only the LDS epilogue implements these
+  static const int gen_epi = [] {  // TP_GEN_EPI=0: per-lane epilogue stores (experiments); read once
+    const char* ge = getenv("TP_GEN_EPI");
+    return ge ? atoi(ge) : 1;
+  }();
+  a.epi_lds = gen_epi;
+  if (gen == 3 || mask || res_stride > 1 || bnpart) a.epi_lds = 1;  // only the LDS epilogue implements these
+  if (bnpart) {
+    if (splits > 1) return hipErrorInvalidValue;
+    a.bnpart = bnpart;
+  }
   if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);
   if (!ws) return hipErrorInvalidValue;
   ConvArgs b = a;

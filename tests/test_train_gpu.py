@@ -388,3 +388,30 @@ def test_wino_wgrad(cuda, B, H, W, Cin, Cout, cin_r, cout_r, splits, cfg):
     out = torch.full((cout_r, cin_r, 3, 3), float("nan"), device=cuda)
     T.wino_wgrad(gy.to(cuda), x.to(cuda), cfg, splits, out)
     torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("cfg", [0, 2, 4, 1])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 7, 9, 64, 36), (3, 14, 14, 128, 256)])
+def test_conv_gen_stats(cuda, cfg, B, H, W, Cin, Cout):
+    """1x1 conv forward with the BN statistics reduced in its epilogue: tile sums fold to the
+    fp64 column sums of the output, and bn_train_fwd(pre=) == the statistics-pass forward."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    g = torch.Generator().manual_seed(cfg * 7 + Cin)
+    x = torch.randn(B, H, W, Cin, generator=g).to(cuda)
+    w = (torch.randn(Cout, Cin, generator=g) * 0.1).to(cuda)
+    y, part = T.conv_gen_stats(x, w, None, 1, 1, 0, cfg)
+    ref = (x.reshape(-1, Cin).double() @ w.double().t())
+    torch.testing.assert_close(y.reshape(-1, Cout).double(), ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(part[:, 0].sum(0), y.reshape(-1, Cout).double().sum(0), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(part[:, 1].sum(0), (y.reshape(-1, Cout).double() ** 2).sum(0), rtol=1e-6, atol=1e-6)
+    gamma = torch.rand(Cout, device=cuda) + 0.5
+    beta = torch.randn(Cout, device=cuda)
+    outs = []
+    for pre in (None, part):
+        rm, rv = torch.zeros(Cout, device=cuda), torch.ones(Cout, device=cuda)
+        o = T.bn_train_fwd(y, gamma, beta, rm, rv, 1e-5, 0.1, None, True, pre)
+        outs.append((o[0], rm, rv))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-6, atol=1e-6)

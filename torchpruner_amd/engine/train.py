@@ -90,8 +90,11 @@ def _wgrad_splits(P, tiles):
     return sp
 
 
-def _conv_fwd(x, weight, bias, ks, stride, pad):
-    """Forward of one native conv: returns (y NHWC (B, Ho, Wo, Cout), saved (xh, w32), meta)."""
+def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
+    """Forward of one native conv: returns (y NHWC (B, Ho, Wo, Cout), saved (xh, w32), meta,
+    part). With ``stats``, ``part`` is the per-tile BatchNorm statistics of y from the GEMM
+    epilogue ((G, 2, Cout) fp64, for ``bn_act(..., pre=part)``) when the tuned kernel is a
+    single-pass implicit GEMM, else None."""
     T = ops.require()
     B, Cin, H, W = x.shape
     Cout = weight.shape[0]
@@ -124,11 +127,19 @@ def _conv_fwd(x, weight, bias, ks, stride, pad):
         sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cout_p, cin_p)
         cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
     cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
-    y = run(cfg, sp)
+    part = None
+    if stats and cfg not in (WINO, WINO_LDS) and sp == 1:
+        if "wk" not in cache:
+            cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
+        y, part = T.conv_gen_stats(xh, cache["wk"], shift, ks, stride, pad, cfg)
+        if cout_p != Cout:
+            part = part[..., :Cout].contiguous()
+    else:
+        y = run(cfg, sp)
     if cout_p != Cout:
         y = y[..., :Cout].contiguous()
     meta = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride(), cin_p, cout_p)
-    return y, (xh, w32), meta
+    return y, (xh, w32), meta, part
 
 
 def _grad_nhwc(gy, meta):
@@ -213,7 +224,7 @@ def _conv_wgrad(g, xh, meta):
 class _NativeConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, ks, stride, pad):
-        y, saved, ctx.meta = _conv_fwd(x, weight, bias, ks, stride, pad)
+        y, saved, ctx.meta, _ = _conv_fwd(x, weight, bias, ks, stride, pad)
         ctx.save_for_backward(*saved)
         return _as_nchw(y)
 
@@ -236,6 +247,34 @@ class _NativeConv2d(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+class _NativeConv2dStats(torch.autograd.Function):
+    """:class:`_NativeConv2d` that also returns its output's BatchNorm tile statistics (or
+    None), computed in the GEMM epilogue: the following training BN skips its statistics pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, ks, stride, pad):
+        y, saved, ctx.meta, part = _conv_fwd(x, weight, bias, ks, stride, pad, stats=True)
+        ctx.save_for_backward(*saved)
+        if part is not None:
+            ctx.mark_non_differentiable(part)
+        return _as_nchw(y), part
+
+    @staticmethod
+    def backward(ctx, gy, _gpart):
+        return _NativeConv2d.backward(ctx, gy)
+
+
+def conv_stats(conv: nn.Conv2d, x: torch.Tensor):
+    """``(conv(x), tile statistics or None)`` — a native 1x1 conv computes its output's BN
+    statistics in the GEMM epilogue; anything else runs the module (statistics None)."""
+    if "forward" in conv.__dict__ and conv.forward.__func__ is _native_forward and _geom(conv)[0] == 1 \
+            and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.weight.dtype == torch.float32 \
+            and _fits(conv, x):
+        ks, s, p = _geom(conv)
+        return _NativeConv2dStats.apply(x, conv.weight, conv.bias, ks, s, p)
+    return conv(x), None
+
+
 class _NativeBlockEntry(torch.autograd.Function):
     """The two readers of a residual block's input x, as one autograd node: conv1 (1x1, stride 1)
     and the identity branch — x itself, or the downsample conv (1x1, stride s). Returns
@@ -246,17 +285,24 @@ class _NativeBlockEntry(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, wd, bd, ds_stride):
-        y1, saved1, ctx.meta1 = _conv_fwd(x, w1, b1, 1, 1, 0)
+        # (conv1 output, identity-branch pre-BN, and the two outputs' BN tile statistics or None)
+        y1, saved1, ctx.meta1, p1 = _conv_fwd(x, w1, b1, 1, 1, 0, stats=True)
         ctx.has_ds = wd is not None
+        pd = None
         if ctx.has_ds:
-            yd, saved_d, ctx.meta_d = _conv_fwd(x, wd, bd, 1, ds_stride, 0)
+            yd, saved_d, ctx.meta_d, pd = _conv_fwd(x, wd, bd, 1, ds_stride, 0, stats=True)
             ctx.save_for_backward(*saved1, saved_d[1])
-            return _as_nchw(y1), _as_nchw(yd)
-        ctx.save_for_backward(*saved1)
-        return _as_nchw(y1), x
+            out = (_as_nchw(y1), _as_nchw(yd))
+        else:
+            ctx.save_for_backward(*saved1)
+            out = (_as_nchw(y1), x)
+        for t in (p1, pd):
+            if t is not None:
+                ctx.mark_non_differentiable(t)
+        return out + (p1, pd)
 
     @staticmethod
-    def backward(ctx, g1, gid):
+    def backward(ctx, g1, gid, _gp1=None, _gpd=None):
         if ctx.has_ds:
             xh, w1, wd = ctx.saved_tensors
         else:
@@ -340,14 +386,14 @@ class _NativeBNAct(torch.autograd.Function):
     ATen ReLU / add / threshold-backward passes of the unfused block disappear."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu, pre=None):
         T = ops.require()
         xh = _nhwc(x)
         rh = _nhwc(res) if res is not None else None
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         y, mean, invstd, mk = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
-                                             bool(relu))
+                                             bool(relu), pre)
         # the backward masks by the ReLU bit mask (1 byte per 4 channels) instead of re-reading y
         ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd, mk)
         ctx.has_w, ctx.has_b, ctx.relu, ctx.has_res = weight is not None, bias is not None, relu, res is not None
@@ -362,7 +408,8 @@ class _NativeBNAct(torch.autograd.Function):
         dx, dgamma, dbeta, dres = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
                                                  ctx.needs_input_grad[0], None, want_res, mk if ctx.relu else None)
         return (_as_nchw(dx) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
-                dbeta if ctx.has_b else None, None, None, None, None, _as_nchw(dres) if want_res else None, None)
+                dbeta if ctx.has_b else None, None, None, None, None, _as_nchw(dres) if want_res else None, None,
+                None)
 
 
 def _bn_fusable(bn, x, res=None) -> bool:
@@ -372,9 +419,12 @@ def _bn_fusable(bn, x, res=None) -> bool:
             and (res is None or (res.shape == x.shape and res.dtype == x.dtype and res.is_cuda)))
 
 
-def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: bool = True) -> torch.Tensor:
+def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: bool = True,
+           pre: torch.Tensor = None) -> torch.Tensor:
     """``relu?(bn(x) + res?)`` — fused on the native kernels in training mode, the module's own
-    ops otherwise (eval mode, unsupported inputs)."""
+    ops otherwise (eval mode, unsupported inputs). ``pre``: x's batch statistics already reduced
+    per tile by the producing conv's epilogue (:func:`conv_stats`), which skips the statistics
+    pass over x."""
     if not _bn_fusable(bn, x, res):
         y = bn(x)
         if res is not None:
@@ -387,8 +437,10 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: 
             momentum = 1.0 / float(bn.num_batches_tracked)
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
+    if pre is not None and (pre.dim() != 3 or pre.shape[2] != x.shape[1]):
+        pre = None
     return _NativeBNAct.apply(x, bn.weight, bn.bias, rm, rv, bn.eps, momentum if momentum is not None else 0.0, res,
-                              relu)
+                              relu, pre)
 
 
 def _block_kind(m) -> str | None:
@@ -427,17 +479,18 @@ def _native_block_forward(self, x):
     entry = _entry_convs(self, x)
     if entry is not None:
         c1, dconv, dbn = entry
-        y1, idp = _NativeBlockEntry.apply(x, c1.weight, c1.bias, dconv.weight if dconv is not None else None,
-                                          dconv.bias if dconv is not None else None,
-                                          dconv.stride[0] if dconv is not None else 1)
-        identity = bn_act(dbn, idp, relu=False) if dbn is not None else idp
-        out = bn_act(self.bn1, y1, relu=True)
+        y1, idp, p1, pd = _NativeBlockEntry.apply(x, c1.weight, c1.bias, dconv.weight if dconv is not None else None,
+                                                  dconv.bias if dconv is not None else None,
+                                                  dconv.stride[0] if dconv is not None else 1)
+        identity = bn_act(dbn, idp, relu=False, pre=pd) if dbn is not None else idp
+        out = bn_act(self.bn1, y1, relu=True, pre=p1)
     else:
         identity = self.downsample(x) if self.downsample is not None else x
         out = bn_act(self.bn1, self.conv1(x), relu=True)
     if _block_kind(self) == "bottleneck":
         out = bn_act(self.bn2, self.conv2(out), relu=True)
-        return bn_act(self.bn3, self.conv3(out), res=identity, relu=True)
+        y3, p3 = conv_stats(self.conv3, out)
+        return bn_act(self.bn3, y3, res=identity, relu=True, pre=p3)
     return bn_act(self.bn2, self.conv2(out), res=identity, relu=True)
 
 
