@@ -403,8 +403,10 @@ def test_conv_gen_stats(cuda, cfg, B, H, W, Cin, Cout):
     y, part = T.conv_gen_stats(x, w, None, 1, 1, 0, cfg)
     ref = (x.reshape(-1, Cin).double() @ w.double().t())
     torch.testing.assert_close(y.reshape(-1, Cout).double(), ref, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(part[:, 0].sum(0), y.reshape(-1, Cout).double().sum(0), rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(part[:, 1].sum(0), (y.reshape(-1, Cout).double() ** 2).sum(0), rtol=1e-6, atol=1e-6)
+    yd = y.reshape(-1, Cout).double()
+    # per-thread fp32 partials over a few rows, folded in fp64: error ~1e-7 of the sum of |terms|
+    torch.testing.assert_close(part[:, 0].sum(0), yd.sum(0), rtol=0, atol=1e-6 * float(yd.abs().sum(0).max()))
+    torch.testing.assert_close(part[:, 1].sum(0), (yd ** 2).sum(0), rtol=1e-6, atol=1e-6)
     gamma = torch.rand(Cout, device=cuda) + 0.5
     beta = torch.randn(Cout, device=cuda)
     outs = []
