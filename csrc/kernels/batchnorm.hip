@@ -135,35 +135,11 @@ __device__ __forceinline__ void fold_groups(const double* __restrict__ part, int
   __shared__ double red[2][16][16];
   s = 0.0;
   q = 0.0;
-  if (c < C) {
-    // 8 groups per lane in flight (independent partial sums, folded in a fixed order): the fold is
-    // L2-latency bound, one dependent load per iteration took ~10 us per call
-    constexpr int U = 8;
-    double ps[U], pq[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) ps[u] = pq[u] = 0.0;
-    int i = gl;
-    for (; i + 16 * (U - 1) < groups; i += 16 * U) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        ps[u] += part[(size_t)(2 * (i + 16 * u)) * C + c];
-        pq[u] += part[(size_t)(2 * (i + 16 * u) + 1) * C + c];
-      }
+  if (c < C)
+    for (int i = gl; i < groups; i += 16) {
+      s += part[(size_t)(2 * i) * C + c];
+      q += part[(size_t)(2 * i + 1) * C + c];
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {  // the < U remaining groups of this lane (static register indexing)
-      const int j = i + 16 * u;
-      if (j < groups) {
-        ps[u] += part[(size_t)(2 * j) * C + c];
-        pq[u] += part[(size_t)(2 * j + 1) * C + c];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      s += ps[u];
-      q += pq[u];
-    }
-  }
   red[0][gl][cl] = s;
   red[1][gl][cl] = q;
   __syncthreads();

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 import types
 
 import torch
@@ -90,6 +91,10 @@ def _wgrad_splits(P, tiles):
     return sp
 
 
+# TORCHPRUNER_BN_EPI_STATS=0: training BN always runs its own statistics pass (A/B switch)
+_EPI_STATS = os.environ.get("TORCHPRUNER_BN_EPI_STATS", "1") != "0"
+
+
 def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
     """Forward of one native conv: returns (y NHWC (B, Ho, Wo, Cout), saved (xh, w32), meta,
     part). With ``stats``, ``part`` is the per-tile BatchNorm statistics of y from the GEMM
@@ -128,7 +133,7 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
         cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
     cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
     part = None
-    if stats and cfg not in (WINO, WINO_LDS) and sp == 1:
+    if stats and _EPI_STATS and cfg not in (WINO, WINO_LDS) and sp == 1:
         if "wk" not in cache:
             cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
         y, part = T.conv_gen_stats(xh, cache["wk"], shift, ks, stride, pad, cfg)
