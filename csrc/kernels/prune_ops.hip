@@ -154,6 +154,34 @@ __global__ __launch_bounds__(256) void unpool2_nhwc(const float* __restrict__ g,
     out[t] = am[o] == (uint8_t)((ih & 1) * 2 + (iw & 1)) ? g[o] : 0.f;
   }
 }
+
+// C % 4 == 0: one thread per (pooled pixel, 4-channel group) reads a float4 of the pooled grad
+// and its 4 argmax bytes once and writes the 2x2 window as four float4 rows (16-B stores,
+// consecutive lanes on consecutive channel groups). Feeds the staged Winograd dgrad a dense
+// full-resolution operand instead of rebuilding it per MFMA chunk.
+__global__ __launch_bounds__(256) void unpool2_nhwc_v4(const float4* __restrict__ g, const uint32_t* __restrict__ am,
+                                                       float4* __restrict__ out, int W2, int C4, long long total) {
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(t % C4);
+    const long long p = t / C4;  // pooled pixel (b, ph, pw) = b * H2 * W2 + ph * W2 + pw
+    const long long row = p / W2;  // b * H2 + ph
+    const int pw = (int)(p - row * W2);
+    const float4 v = g[t];
+    const uint32_t a = am[t];
+    const long long o00 = ((row * 2) * (2 * W2) + 2 * pw) * C4 + c4;  // full-res (2ph, 2pw)
+    const long long drow = (long long)(2 * W2) * C4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 r;
+      r.x = ((a >> 0) & 0xffu) == (uint32_t)q ? v.x : 0.f;
+      r.y = ((a >> 8) & 0xffu) == (uint32_t)q ? v.y : 0.f;
+      r.z = ((a >> 16) & 0xffu) == (uint32_t)q ? v.z : 0.f;
+      r.w = ((a >> 24) & 0xffu) == (uint32_t)q ? v.w : 0.f;
+      out[o00 + (q >> 1) * drow + (q & 1) * C4] = r;
+    }
+  }
+}
 }  // namespace tp
 
 extern "C" hipError_t tp_maxpool2_nhwc(const float* x, float* y, uint8_t* am, int B, int H, int W, int C,
@@ -166,6 +194,15 @@ extern "C" hipError_t tp_maxpool2_nhwc(const float* x, float* y, uint8_t* am, in
 
 extern "C" hipError_t tp_unpool2_nhwc(const float* g, const uint8_t* am, float* out, int B, int H, int W, int C,
                                       hipStream_t st) {
+  if (C % 4 == 0 && H % 2 == 0 && W % 2 == 0 && (reinterpret_cast<uintptr_t>(g) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(am) & 3) == 0) {
+    const long long total = (long long)B * (H / 2) * (W / 2) * (C / 4);
+    const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
+    tp::unpool2_nhwc_v4<<<grid, 256, 0, st>>>(reinterpret_cast<const float4*>(g),
+                                              reinterpret_cast<const uint32_t*>(am), reinterpret_cast<float4*>(out),
+                                              W / 2, C / 4, total);
+    return hipGetLastError();
+  }
   const long long total = (long long)B * H * W * C;
   const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
   tp::unpool2_nhwc<<<grid, 256, 0, st>>>(g, am, out, B, H, W, C);

@@ -401,6 +401,47 @@ def test_wino_dgrad_taylor(cuda, shape, splits, unpool, staged):
     assert torch.equal(tay, tay2)
 
 
+@pytest.mark.parametrize("shape", [(3, 8, 8, 64), (2, 32, 32, 32), (5, 4, 6, 36), (2, 4, 4, 6)])
+def test_unpool2_nhwc(cuda, shape):
+    """unpool2_nhwc (vectorised path for C % 4 == 0, scalar otherwise) == scatter by argmax."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    B, H, W, C = shape
+    g = torch.Generator().manual_seed(11)
+    gp = _rand(B, H // 2, W // 2, C, gen=g)
+    am = torch.randint(0, 4, (B, H // 2, W // 2, C), generator=g, dtype=torch.uint8)
+    ref = torch.zeros(B, H, W, C)
+    for q in range(4):
+        ref[:, q // 2::2, q % 2::2, :] = torch.where(am == q, gp, torch.zeros(()))
+    out = T.unpool2_nhwc(gp.to(cuda), am.to(cuda))
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_wino_dgrad_unpooled_staged_matches_fused_unpool(cuda):
+    """The engine's WINO_UNP dgrad (explicit unpool + staged kernel on the dense gradient) gives
+    the same output and the same Taylor partial slots, bit for bit, as the staged-unpool kernel
+    that rebuilds the full-resolution operand from pooled cells (same operand values, same
+    reduction order)."""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import taylor_slots, winograd_weights
+    T = ops.require()
+    B, H, W, Cin, Cout = 4, 16, 16, 64, 128
+    g = torch.Generator().manual_seed(21)
+    w = _rand(Cout, Cin, 3, 3, gen=g) * (1.0 / (9 * Cin)) ** 0.5
+    act = torch.relu(_rand(B, H, W, Cin, gen=g)).to(cuda)
+    bn_scale = (_rand(Cin, gen=g).abs() + 0.5).to(cuda)
+    gp = _rand(B, H // 2, W // 2, Cout, gen=g).to(cuda)
+    am = torch.randint(0, 4, (B, H // 2, W // 2, Cout), generator=g, dtype=torch.uint8).to(cuda)
+    ut = winograd_weights(w.flip(2, 3).transpose(0, 1).to(cuda))
+    R = taylor_slots(H, W)
+    for splits in (1, 2):
+        t1, t2 = torch.zeros(R, B, Cin, device=cuda), torch.zeros(R, B, Cin, device=cuda)
+        o1 = T.conv_wino_dgrad(gp, am, ut, act, bn_scale, t1, True, splits, True)
+        o2 = T.conv_wino_dgrad(T.unpool2_nhwc(gp, am), None, ut, act, bn_scale, t2, True, splits, True)
+        assert torch.equal(o1, o2)
+        assert torch.equal(t1, t2)
+
+
 def test_wino_nan_propagation(cuda):
     from torchpruner_amd import ops
     from torchpruner_amd.engine.fused_chain import winograd_weights

@@ -45,6 +45,8 @@ _CU = 256
 _TILES = {0: (128, 128), 1: (256, 64), 2: (64, 64), 3: (128, 64), 4: (128, 128), 5: (256, 64), 6: (128, 64)}
 WINO = -1  # pseudo tile cfg: fused Winograd F(2x2,3x3) kernel (winograd.hip), direct patch loads
 WINO_LDS = -2  # the same with the block input region staged through LDS
+WINO_UNP = -3  # dgrad of a pooled layer: explicit vectorised unpool, then the staged kernel on the
+               # dense full-resolution gradient (vs rebuilding it from pooled cells per chunk)
 
 # Winograd F(2x2,3x3) weight transform G g G^T
 _G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
@@ -484,6 +486,9 @@ class FusedChainEngine:
 
     def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0):
         """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
+        if cfg == WINO_UNP:
+            return T.conv_wino_dgrad(T.unpool2_nhwc(g, am), None, e["ut"], act, sc, taylor, want_out, sp, True,
+                                     tay_mode=tm)
         if cfg in (WINO, WINO_LDS):
             return T.conv_wino_dgrad(g, am, e["ut"], act, sc, taylor, want_out, sp, cfg == WINO_LDS, tay_mode=tm)
         if cfg >= self.DENSE:
@@ -793,6 +798,10 @@ class FusedChainEngine:
                 # dense GEMM dgrad: one writer per Taylor element (deterministic as well)
                 cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * Cin, 4 * Cg)] + \
                     TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
+            elif wino is not None and am is not None:
+                wc = TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
+                wc = [c for c in wc if c[0] == WINO_LDS] + [c for c in wc if c[0] != WINO_LDS]  # [0]: untuned pick
+                cands = wc + [(WINO_UNP, s_) for k, s_ in wc if k == WINO_LDS]
             cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None),
                                    M, Cin, e["wt"].shape[1],
                                    lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4:
