@@ -600,3 +600,47 @@ def test_engines_shapley_any_criterion(cuda, arch):
                                    reduction="none").run(dict(m64.named_modules())[name],
                                                          find_best_evaluation_module=True)
     assert np.abs(got - ref).max() / (np.abs(ref).max() + 1e-12) < 2e-3
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_fused_first_layer_candidates(cuda, pool):
+    """Every first-layer candidate of the fused VGG engine (staged / direct Winograd, VALU direct)
+    == fp64 conv + eval BN + ReLU (+ 2x2 max-pool), APoZ counts exact. (A packed-tap implicit-GEMM
+    candidate, conv_igemm GEN 2 on a 4-channel input, was measured slower than the staged
+    Winograd kernel at B=2048 and dropped.)"""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.engine.fused_chain import WINO, WINO_LDS
+    from torchpruner_amd.models import prunable_vgg16
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    T = ops.require()
+    torch.manual_seed(3)
+    model = prunable_vgg16().to(cuda).eval()
+    with torch.no_grad():
+        bn = model.features[1]
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 1.5)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    conv = model.features[0]
+    eng, _ = maybe_engine(model, [find_best_module_for_attributions(model, conv)], F.cross_entropy, cuda)
+    e = eng._pack()["convs"][0]
+    e = dict(e, pool=pool)
+    x = torch.randn(6, 3, 32, 32, device=cuda)
+    ref = F.conv2d(x.double().cpu(), conv.weight.double().cpu(), conv.bias.double().cpu() if conv.bias is not None
+                   else None, padding=1)
+    ref = F.batch_norm(ref, bn.running_mean.double().cpu(), bn.running_var.double().cpu(), bn.weight.double().cpu(),
+                       bn.bias.double().cpu(), False, 0.0, bn.eps)
+    pre = torch.relu(ref)
+    cnt_ref = (pre > 0).sum((2, 3)).float()
+    if pool:
+        ref = F.max_pool2d(pre, 2)
+    else:
+        ref = pre
+    ref = ref.permute(0, 2, 3, 1).float()
+    cands = [(WINO_LDS, 1), (WINO, 1), (eng.FIRST_DIRECT, 1)]
+    for cfg, sp in cands:
+        ap = torch.zeros(6, e["scale"].numel(), device=cuda)
+        out, _ = eng._first_run(T, e, x, cfg, sp, ap)
+        torch.testing.assert_close(out[..., :64].cpu(), ref, rtol=1e-4, atol=1e-4, msg=f"cfg {cfg}")
+        assert torch.equal(ap[:, :64].cpu(), cnt_ref), f"cfg {cfg}"

@@ -7,7 +7,7 @@ from torchpruner_amd import ops
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(4, 64, 32, 32), (8, 128, 16, 16), (16, 512, 4, 4), (32, 512, 2, 2), (8, 512), (3, 7, 5, 3), (2, 3, 1, 1),
-          (2, 64, 112, 112), (3, 80, 56, 56)]
+          (2, 64, 112, 112), (3, 80, 56, 56), (2, 96, 7, 7), (5, 1056, 3, 3), (256, 32, 9, 9)]
 
 
 def _ref(fn, *ts):
