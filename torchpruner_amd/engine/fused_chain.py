@@ -153,7 +153,7 @@ class Autotuner:
         if wino is not None:
             sp = _wino_splits(wino[0], N, wino[1])
             for kind in (WINO, WINO_LDS):
-                out += [(kind, sp)] + ([(kind, max(1, sp // 2))] if sp > 1 else [])
+                out += [(kind, sp)] + ([(kind, max(1, sp // 2))] if sp > 1 else []) + ([(kind, 1)] if sp > 2 else [])
             if wino_only:
                 return out
         for cfg, (bm, bn) in _TILES.items():
@@ -163,6 +163,8 @@ class Autotuner:
             out.append((cfg, sp))
             if sp > 1:
                 out.append((cfg, max(1, sp // 2)))
+            if sp > 2:  # small batches: one K pass without the partial-slab combine launch
+                out.append((cfg, 1))
         return out
 
     def choose(self, key, M, N, K, run, wino=None, wino_only=False, cands=None):
