@@ -802,8 +802,11 @@ class FusedChainEngine:
                     TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
             elif wino is not None and am is not None:
                 wc = TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
-                wc = [c for c in wc if c[0] == WINO_LDS] + [c for c in wc if c[0] != WINO_LDS]  # [0]: untuned pick
-                cands = wc + [(WINO_UNP, s_) for k, s_ in wc if k == WINO_LDS]
+                wc = [c for c in wc if c[0] == WINO_LDS] + [c for c in wc if c[0] != WINO_LDS]
+                unp = [(WINO_UNP, s_) for k, s_ in wc if k == WINO_LDS]
+                # [0] = the untuned pick: explicit unpool from 16x16 down (measured faster at
+                # B=2048 for the 16/8/4-pixel layers, slower at 32x32); bit-identical either way
+                cands = unp + wc if H <= 16 else wc + unp
             cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None),
                                    M, Cin, e["wt"].shape[1],
                                    lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4:
