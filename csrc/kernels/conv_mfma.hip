@@ -174,7 +174,11 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   const int lane = tid & 63, wave = tid >> 6;
   const int n_tiles = (p.N + BN - 1) / BN;
   const int m_tiles = (p.M + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // GEN 3 parity order puts the 4-, 2- and 1-tap phase classes in consecutive M ranges: the
+  // contiguous XCD remap would hand the two heaviest XCDs all 4-tap tiles and the last two all
+  // 1-tap tiles (max/mean work 4/2.25 -> the kernel ran ~1.7x long). Plain round-robin dispatch
+  // spreads every class over all XCDs; the A operand here is the small low-resolution gradient.
+  const int tile = (GEN == 3 && p.parity) ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (tile / n_tiles) * BM;
   const int n0 = (tile % n_tiles) * BN;
   if (m0 >= m_tiles * BM) return;
