@@ -64,3 +64,33 @@ def test_graph_invalidated_by_new_weights(cuda):
     ref = _scores(model, x, y, 32, "0")
     for a, r in zip(got, ref):
         np.testing.assert_array_equal(a, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sensitivity", [False, True])
+def test_two_stream_pipeline_bit_identical(cuda, sensitivity):
+    """Small batches run two in flight on two HIP streams (attributions/base.py _BatchPipeline):
+    the accumulated scores must equal the one-stream loop bit for bit (per-stream arenas, folds
+    chained in batch order), including a ragged last batch (its own, sequential first run)."""
+    from torchpruner_amd import SensitivityAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(1)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    x = torch.randn(330, 3, 32, 32, device=cuda)  # 8 batches of 40 + a ragged 10
+    y = torch.randint(0, 10, (330,), device=cuda)
+    metric = SensitivityAttributionMetric if sensitivity else TaylorAttributionMetric
+    out = {}
+    for env in ("0", "1"):
+        old = os.environ.get("TORCHPRUNER_STREAMS")
+        os.environ["TORCHPRUNER_STREAMS"] = env
+        try:
+            out[env] = metric(model, DeviceLoader(x, y, 40), F.cross_entropy, cuda).run_many(convs, True)
+        finally:
+            if old is None:
+                del os.environ["TORCHPRUNER_STREAMS"]
+            else:
+                os.environ["TORCHPRUNER_STREAMS"] = old
+    for a, b in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, b)

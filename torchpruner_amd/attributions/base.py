@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import math
 import os
 from abc import ABC, abstractmethod
 
@@ -418,8 +419,16 @@ class _AttributionMetric(ABC):
         uniq = sorted(owner)
         stats = accs[0].mode == "stats"
         crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
+        pipe = _BatchPipeline(engine, uniq) if stats and self._ckpt is None else None
         for i, x, y in self._batches():
             B = x.shape[0]
+            if pipe is not None and pipe.take(x, y, mode, crit, take_abs,
+                                              lambda arena: [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device,
+                                                                                       engine.real_width(b))
+                                                             for b in uniq]):
+                for b in uniq:
+                    accs[owner[b]].count += B
+                continue
             if stats:
                 arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
                 with trace_range("tp.forward_backward"):
@@ -437,6 +446,8 @@ class _AttributionMetric(ABC):
                 ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), take_abs, 1)
                 for b in uniq:
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
+        if pipe is not None:
+            pipe.join()
         return [accs[owner[b]] for b in blocks]
 
     def _resnet_grad_engine(self, eval_modules, why=None):
@@ -522,3 +533,60 @@ def _to(t, device):
     if isinstance(t, torch.Tensor):
         return t.to(device, non_blocking=True)
     return t
+
+
+class _BatchPipeline:
+    """Two batches in flight for small batches on the fused engine (stats reductions only).
+
+    A small batch leaves most of the 256 CUs idle in every layer (a few hundred workgroups, each
+    latency-bound), so consecutive batches run on two HIP streams and their kernels co-execute.
+    Each stream owns its own score arena; the per-batch fold into the fp64 sums is chained by an
+    event in batch order, so the accumulated scores are bit-identical to the sequential loop.
+    The first batch of every new shape runs alone on the current stream (kernel autotuning,
+    arena allocation, lazily packed operands). Off for batches of >= 2^20 output pixels of the
+    first layer (B >= 1024 at 32x32: the GPU is already full) and with TORCHPRUNER_STREAMS=0."""
+
+    MAX_PIXELS = 1 << 20
+
+    def __init__(self, engine, uniq):
+        self.engine, self.uniq = engine, uniq
+        self.enabled = os.environ.get("TORCHPRUNER_STREAMS", "1") != "0"
+        self.max_pixels = int(os.environ.get("TORCHPRUNER_STREAMS_MAX_PIXELS", self.MAX_PIXELS))
+        self.streams = None
+        self.seen = set()
+        self.n = 0
+        self.fold_done = None  # event: the previous pipelined batch's fold
+
+    def take(self, x, y, mode, crit, take_abs, sums_of) -> bool:
+        """Run batch (x, y) pipelined and return True, or return False (caller runs it)."""
+        if not self.enabled or not x.is_cuda or crit is not None or \
+                x.shape[0] * math.prod(x.shape[2:]) >= self.max_pixels or self.engine.graphs_enabled(x.shape[0]):
+            return False
+        key = (tuple(x.shape), tuple(y.shape))
+        if key not in self.seen:  # autotune / allocate alone, after everything in flight
+            self.join()
+            self.seen.add(key)
+            return False
+        if self.streams is None:
+            self.streams = [torch.cuda.Stream(x.device) for _ in range(2)]
+        cur = torch.cuda.current_stream(x.device)
+        st = self.streams[self.n % 2]
+        st.wait_stream(cur)  # the batch's copy (and everything before this run) is done
+        with torch.cuda.stream(st):
+            arena = self.engine.score_arena(x.shape[0], self.uniq, x.device, tuple(x.shape[2:]), slot=self.n % 2)
+            self.engine.taylor(x, y, set(self.uniq), arena, mode=mode)
+            if self.fold_done is not None:
+                st.wait_event(self.fold_done)
+            ops.score_fold_([arena[b] for b in self.uniq], sums_of(arena), take_abs, 2)
+            self.fold_done = torch.cuda.Event()
+            self.fold_done.record(st)
+        x.record_stream(st)
+        y.record_stream(st)
+        self.n += 1
+        return True
+
+    def join(self):
+        if self.streams is not None:
+            cur = torch.cuda.current_stream(self.streams[0].device)
+            for st in self.streams:
+                cur.wait_stream(st)

@@ -651,11 +651,12 @@ class FusedChainEngine:
                 shapes[b] = (B, c)
         return shapes
 
-    def score_arena(self, B: int, want, device, hw=(32, 32)):
+    def score_arena(self, B: int, want, device, hw=(32, 32), slot: int = 0):
         """Persistent zeroed score slabs for the blocks in ``want`` (one allocation): (R, B, C)
         partial slots for conv blocks (see taylor_slots), (B, C) for linear blocks. The caller
-        must leave them zeroed (ops.score_fold_ with after=2) for reuse."""
-        key = (B, tuple(sorted(want)), str(device), tuple(hw))
+        must leave them zeroed (ops.score_fold_ with after=2) for reuse. ``slot``: independent
+        arenas for batches in flight on different streams."""
+        key = (B, tuple(sorted(want)), str(device), tuple(hw), slot)
         arena = self._arenas.get(key)
         if arena is None:
             shapes = self._arena_shapes(B, want, *hw)
