@@ -67,12 +67,12 @@ def test_graph_invalidated_by_new_weights(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sensitivity", [False, True])
-def test_two_stream_pipeline_bit_identical(cuda, sensitivity):
+@pytest.mark.parametrize("which", ["taylor", "sensitivity", "apoz"])
+def test_two_stream_pipeline_bit_identical(cuda, which):
     """Small batches run two in flight on two HIP streams (attributions/base.py _BatchPipeline):
     the accumulated scores must equal the one-stream loop bit for bit (per-stream arenas, folds
     chained in batch order), including a ragged last batch (its own, sequential first run)."""
-    from torchpruner_amd import SensitivityAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd import APoZAttributionMetric, SensitivityAttributionMetric, TaylorAttributionMetric
     from torchpruner_amd.data import DeviceLoader
     from torchpruner_amd.models import prunable_vgg16
     torch.manual_seed(1)
@@ -80,7 +80,8 @@ def test_two_stream_pipeline_bit_identical(cuda, sensitivity):
     convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
     x = torch.randn(330, 3, 32, 32, device=cuda)  # 8 batches of 40 + a ragged 10
     y = torch.randint(0, 10, (330,), device=cuda)
-    metric = SensitivityAttributionMetric if sensitivity else TaylorAttributionMetric
+    metric = {"taylor": TaylorAttributionMetric, "sensitivity": SensitivityAttributionMetric,
+              "apoz": APoZAttributionMetric}[which]
     out = {}
     for env in ("0", "1"):
         old = os.environ.get("TORCHPRUNER_STREAMS")

@@ -11,7 +11,7 @@ import torch
 
 from ... import ops
 from ...engine.resnet_engine import maybe_resnet_engine
-from ..base import _AttributionMetric
+from ..base import _AttributionMetric, _BatchPipeline
 
 
 class APoZAttributionMetric(_AttributionMetric):
@@ -50,9 +50,24 @@ class APoZAttributionMetric(_AttributionMetric):
             owner.setdefault(b, k)
         uniq = sorted(owner)
         stats = accs[0].mode == "stats"
+        pipe = _BatchPipeline(engine) if stats and self._ckpt is None else None
         with torch.no_grad():
             for i, x, _y in self._batches():
                 B = x.shape[0]
+
+                def launch(slot, x=x):
+                    bufs = {b: torch.zeros(x.shape[0], engine._block_width(b), device=x.device) for b in uniq}
+                    engine.forward(x, stop_after=uniq[-1], apoz=bufs)
+                    return bufs
+
+                def fold(bufs, dev=x.device):
+                    sums = [accs[owner[b]].ensure_sum(bufs[b].shape[1], dev, engine.real_width(b)) for b in uniq]
+                    ops.score_fold_([bufs[b] for b in uniq], sums, False, 0)
+
+                if pipe is not None and pipe.take(x, None, launch, fold):  # two batches in flight (small B)
+                    for b in uniq:
+                        accs[owner[b]].count += B
+                    continue
                 bufs = {b: torch.zeros(B, engine._block_width(b), device=x.device) for b in uniq}
                 engine.forward(x, stop_after=uniq[-1], apoz=bufs)
                 if stats:
@@ -63,6 +78,8 @@ class APoZAttributionMetric(_AttributionMetric):
                 else:
                     for b in uniq:
                         accs[owner[b]].add(bufs[b][:, :engine.real_width(b)], i)
+        if pipe is not None:
+            pipe.join()
         return [accs[owner[b]] for b in blocks]
 
     def _engine_pass(self, eng, eval_modules, accs):
