@@ -97,3 +97,36 @@ def test_resnet_engine_apoz_matches_generic(cuda):
     with torch.no_grad():
         torch.testing.assert_close(eng.forward(x), model(x), rtol=2e-3, atol=2e-3)
     assert resnet50 is not None
+
+
+@pytest.mark.parametrize("which", ["apoz", "taylor", "sensitivity"])
+def test_resnet_two_stream_pipeline_bit_identical(cuda, which):
+    """ResNet engine runs with two batches in flight (attributions/base.py _BatchPipeline) give
+    the one-stream scores bit for bit, ragged last batch included."""
+    import os
+    from torchpruner_amd import (APoZAttributionMetric, SensitivityAttributionMetric, TaylorAttributionMetric,
+                                 get_resnet_pruning_graph)
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    torch.manual_seed(2)
+    model = ResNet(Bottleneck, [1, 2, 1, 1], num_classes=10, width=32).to(cuda).eval()
+    x = torch.randn(22, 3, 64, 64, device=cuda)  # 5 batches of 4 + a ragged 2
+    y = torch.randint(0, 10, (22,), device=cuda)
+    mods = [m for m, _ in get_resnet_pruning_graph(model)]
+    metric = {"apoz": APoZAttributionMetric, "taylor": TaylorAttributionMetric,
+              "sensitivity": SensitivityAttributionMetric}[which]
+    out = {}
+    for env in ("0", "1"):
+        old = os.environ.get("TORCHPRUNER_STREAMS")
+        os.environ["TORCHPRUNER_STREAMS"] = env
+        try:
+            m = metric(model, DeviceLoader(x, y, 4), F.cross_entropy, cuda)
+            out[env] = m.run_many(mods, True)
+            assert m.last_path["path"] == "resnet", m.last_path
+        finally:
+            if old is None:
+                del os.environ["TORCHPRUNER_STREAMS"]
+            else:
+                os.environ["TORCHPRUNER_STREAMS"] = old
+    for a, b in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, b)

@@ -484,8 +484,20 @@ class _AttributionMetric(ABC):
             first.setdefault(m, k)
         stats = accs[0].mode == "stats"
         crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
+        pipe = _BatchPipeline(eng) if stats and self._ckpt is None and crit is None else None
         with torch.no_grad():
             for i, x, y in self._batches():
+                def fold(res, dev=x.device):
+                    slabs = [res[m] for m in uniq]
+                    sums = [accs[first[m]].ensure_sum(res[m].shape[1], dev, m.num_features) for m in uniq]
+                    for j in range(0, len(slabs), 16):
+                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], False, 0)
+
+                if pipe is not None and pipe.take(x, y, lambda slot, x=x, y=y: eng.grad_scores(x, y, set(uniq), mode),
+                                                  fold):
+                    for m in uniq:
+                        accs[first[m]].count += x.shape[0]
+                    continue
                 with trace_range("tp.forward_backward"):
                     res = eng.grad_scores(x, y, set(uniq), mode, crit)
                 if stats:
@@ -498,6 +510,8 @@ class _AttributionMetric(ABC):
                 else:
                     for m in uniq:
                         accs[first[m]].add(res[m][:, :m.num_features].contiguous(), i)
+        if pipe is not None:
+            pipe.join()
         return [accs[first[m]] for m in eval_modules]
 
     def _forward_capture_pass(self, eval_modules, on_out):
@@ -570,8 +584,9 @@ class _BatchPipeline:
 
     def take(self, x, y, launch, fold) -> bool:
         """Run batch (x, y) pipelined and return True, or return False (caller runs it)."""
+        graphs = getattr(self.engine, "graphs_enabled", None)
         if not self.enabled or not x.is_cuda or x.shape[0] * math.prod(x.shape[2:]) >= self.max_pixels or \
-                self.engine.graphs_enabled(x.shape[0]):
+                (graphs is not None and graphs(x.shape[0])):
             return False
         key = (tuple(x.shape), tuple(y.shape) if y is not None else None)
         if key not in self.seen:  # autotune / allocate alone, after everything in flight

@@ -86,9 +86,33 @@ class APoZAttributionMetric(_AttributionMetric):
         uniq = list(dict.fromkeys(eval_modules))
         stats = accs[0].mode == "stats"
         arena = None
+        pipe = _BatchPipeline(eng) if stats and self._ckpt is None else None
+        nf = sum(m.num_features for m in uniq)
+
+        def views(flat, B):
+            bufs, off = {}, 0
+            for m in uniq:
+                bufs[m] = flat[off:off + B * m.num_features].view(B, m.num_features)
+                off += B * m.num_features
+            return bufs
+
         with torch.no_grad():
             for i, x, _y in self._batches():
                 B = x.shape[0]
+
+                def launch(slot, x=x):
+                    bufs = views(torch.zeros(x.shape[0] * nf, device=x.device), x.shape[0])
+                    eng.forward(x, bufs)
+                    return bufs
+
+                def fold(bufs, dev=x.device):
+                    sums = [accs[k].ensure_sum(m.num_features, dev) for k, m in enumerate(eval_modules)]
+                    ops.score_fold_([bufs[m] for m in eval_modules], sums, False, 0)
+
+                if pipe is not None and pipe.take(x, None, launch, fold):  # two batches in flight
+                    for a in accs:
+                        a.count += B
+                    continue
                 if arena is None or arena.shape[0] != B * sum(m.num_features for m in uniq) or not stats:
                     arena = torch.zeros(B * sum(m.num_features for m in uniq), device=x.device)
                 else:
@@ -106,3 +130,5 @@ class APoZAttributionMetric(_AttributionMetric):
                 else:
                     for k, m in enumerate(eval_modules):
                         accs[k].add(bufs[m], i)
+        if pipe is not None:
+            pipe.join()
