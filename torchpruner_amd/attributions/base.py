@@ -578,6 +578,7 @@ class _BatchPipeline:
         self.engine = engine
         self.enabled = os.environ.get("TORCHPRUNER_STREAMS", "1") != "0"
         self.max_pixels = int(os.environ.get("TORCHPRUNER_STREAMS_MAX_PIXELS", self.MAX_PIXELS))
+        self.depth = max(2, int(os.environ.get("TORCHPRUNER_STREAMS_DEPTH", "2")))  # batches in flight
         self.streams = None
         self.seen = set()
         self.n = 0
@@ -595,12 +596,13 @@ class _BatchPipeline:
             self.seen.add(key)
             return False
         if self.streams is None:
-            self.streams = [torch.cuda.Stream(x.device) for _ in range(2)]
+            self.streams = [torch.cuda.Stream(x.device) for _ in range(self.depth)]
         cur = torch.cuda.current_stream(x.device)
-        st = self.streams[self.n % 2]
+        slot = self.n % self.depth
+        st = self.streams[slot]
         st.wait_stream(cur)  # the batch's copy (and everything before this run) is done
         with torch.cuda.stream(st):
-            bufs = launch(self.n % 2)
+            bufs = launch(slot)
             if self.fold_done is not None:
                 st.wait_event(self.fold_done)
             fold(bufs)
