@@ -47,6 +47,8 @@ hipError_t tp_maxpool_nhwc(const float* x, float* y, int B, int H, int W, int C,
 hipError_t tp_avgpool_nhwc(const float* x, float* y, int B, int HW, int C, hipStream_t st);
 hipError_t tp_maxpool2_nhwc(const float* x, float* y, uint8_t* am, int B, int H, int W, int C, hipStream_t st);
 hipError_t tp_unpool2_nhwc(const float* g, const uint8_t* am, float* out, int B, int H, int W, int C, hipStream_t st);
+hipError_t tp_conv_first_wave(const float* x, const float* wt, const float* scale, const float* shift, float* out,
+                              int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
 hipError_t tp_conv_first_direct(const float* x, const float* w, const float* scale, const float* shift, float* out,
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
 int tp_wino_taylor_slots(int H, int W);
@@ -218,6 +220,13 @@ at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor
   need(shift, "shift", 1);
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   auto out = at::empty({B, H, W, Cout}, x.options());
+  if ((Cout == 16 || Cout == 32 || Cout == 64) && Cin <= 16) {  // wave-uniform weights (scalar loads)
+    const at::Tensor wt = w.permute({1, 2, 3, 0}).contiguous();  // [Cin][3][3][Cout]
+    TP_CHECK_HIP(tp_conv_first_wave(x.data_ptr<float>(), wt.data_ptr<float>(), scale.data_ptr<float>(),
+                                    shift.data_ptr<float>(), out.data_ptr<float>(), (int)B, (int)Cin, (int)H, (int)W,
+                                    (int)Cout, relu ? 1 : 0, cur_stream()));
+    return out;
+  }
   TP_CHECK_HIP(tp_conv_first_direct(x.data_ptr<float>(), w.data_ptr<float>(), scale.data_ptr<float>(),
                                     shift.data_ptr<float>(), out.data_ptr<float>(), (int)B, (int)Cin, (int)H, (int)W,
                                     (int)Cout, relu ? 1 : 0, cur_stream()));

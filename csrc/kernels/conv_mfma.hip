@@ -924,6 +924,86 @@ __global__ __launch_bounds__(256) void conv_first_direct(const float* __restrict
   }
 }
 
+// First conv layer, wave-uniform channels: a wave owns 64 consecutive output pixels (one per
+// lane) x ALL COUT channels, so every weight is the same for the 64 lanes and comes from the
+// scalar cache (s_load, an SGPR operand of the FMA) instead of LDS; each input tap is loaded once
+// per lane and feeds COUT FMAs. The wave's 64 x COUT output tile is one contiguous NHWC region:
+// it is transposed through LDS (rows padded by 4 floats) and written with 1-KB coalesced
+// float4 stores. The conv_first_direct version above was LDS-bandwidth bound (every lane read
+// its weights from LDS, 4 FMAs per 16-B read).
+template <int COUT>
+__global__ __launch_bounds__(256) void conv_first_wave(const float* __restrict__ x, const float* __restrict__ wt,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, float* __restrict__ out,
+                                                       int B, int Cin, int H, int W, int relu) {
+  constexpr int HC = COUT >= 32 ? 32 : COUT;  // channels per transpose pass
+  constexpr int LD = HC + 4;                  // padded LDS row (floats)
+  __shared__ __attribute__((aligned(16))) float tile[4][64 * LD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long npix = (long long)B * H * W;
+  const long long pix0 = ((long long)blockIdx.x * 4 + wave) * 64;
+  if (pix0 >= npix) return;  // whole wave past the end (no block-wide barrier below)
+  const long long pix = pix0 + lane;
+  const bool valid = pix < npix;
+  const int HW = H * W;
+  const int b = valid ? (int)(pix / HW) : 0;
+  const int r = valid ? (int)(pix - (long long)b * HW) : 0;
+  const int oh = r / W, ow = r - (r / W) * W;
+  float acc[COUT];
+#pragma unroll
+  for (int j = 0; j < COUT; ++j) acc[j] = 0.f;
+  for (int c = 0; c < Cin; ++c) {
+    const float* xc = x + ((long long)b * Cin + c) * HW;
+    float v[9];  // the 9 taps' loads in flight together
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh + t / 3 - 1, iw = ow + t % 3 - 1;
+      v[t] = (valid && ih >= 0 && ih < H && iw >= 0 && iw < W) ? xc[ih * W + iw] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      // compiler fence: one tap's COUT wave-uniform weights (scalar loads) live in SGPRs at a
+      // time — hoisting all taps' loads spills SGPRs
+      asm volatile("" ::: "memory");
+      const float* wr = wt + (c * 9 + t) * COUT;
+#pragma unroll
+      for (int j = 0; j < COUT; ++j) acc[j] = fmaf(v[t], wr[j], acc[j]);
+    }
+  }
+  float* tw = tile[wave];
+  constexpr int Q = HC / 4;  // float4 per pixel row of one pass
+#pragma unroll
+  for (int h = 0; h < COUT / HC; ++h) {
+#pragma unroll
+    for (int j = 0; j < HC; j += 4) {
+      const int n = h * HC + j;
+      float4 y;
+      y.x = acc[n] * scale[n] + shift[n];
+      y.y = acc[n + 1] * scale[n + 1] + shift[n + 1];
+      y.z = acc[n + 2] * scale[n + 2] + shift[n + 2];
+      y.w = acc[n + 3] * scale[n + 3] + shift[n + 3];
+      if (relu) {
+        y.x = nan_relu(y.x);
+        y.y = nan_relu(y.y);
+        y.z = nan_relu(y.z);
+        y.w = nan_relu(y.w);
+      }
+      *reinterpret_cast<float4*>(tw + lane * LD + j) = y;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+      const int idx = i * 64 + lane;  // float4 index in the wave's [64][HC] tile, row-major
+      const int px = idx / Q, c4 = idx - px * Q;
+      const float4 o = *reinterpret_cast<const float4*>(tw + px * LD + 4 * c4);
+      if (pix0 + px < npix) *reinterpret_cast<float4*>(out + (pix0 + px) * COUT + h * HC + 4 * c4) = o;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // reads done before the next pass overwrites the tile
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace tp
 
 // ------------------------------------------------------------------------------------------
@@ -1082,6 +1162,20 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
   else if (epi == EPI_BWD && a.HWo >= BWD_IMG_MIN_HW)
     conv_epilogue_bwd_img<<<dim3((unsigned)ceil_div(a.N, 64), (unsigned)(a.M / a.HWo)), 1024, 0, st>>>(a, ws, splits);
   else if (epi == EPI_BWD) conv_epilogue<EPI_BWD><<<grid, 256, 0, st>>>(a, ws, splits);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// ``wt``: the weight as [Cin*9][Cout] (tap-major): the wave-uniform kernel for Cout 16/32/64.
+extern "C" hipError_t tp_conv_first_wave(const float* x, const float* wt, const float* scale, const float* shift,
+                                         float* out, int B, int Cin, int H, int W, int Cout, int relu,
+                                         hipStream_t st) {
+  const long long pix = (long long)B * H * W;
+  if (pix <= 0 || Cin < 1 || Cin > 16) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)tp::ceil_div(pix, 256);
+  if (Cout == 64) tp::conv_first_wave<64><<<grid, 256, 0, st>>>(x, wt, scale, shift, out, B, Cin, H, W, relu);
+  else if (Cout == 32) tp::conv_first_wave<32><<<grid, 256, 0, st>>>(x, wt, scale, shift, out, B, Cin, H, W, relu);
+  else if (Cout == 16) tp::conv_first_wave<16><<<grid, 256, 0, st>>>(x, wt, scale, shift, out, B, Cin, H, W, relu);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
