@@ -34,7 +34,7 @@ def main(marker, dirs):
     for d in dirs:
         names, cnt, dur = load(d)
         ids = sorted(names)
-        marks = [i for i in ids if marker in names[i]]
+        marks = [i for i in ids if any(m in names[i] for m in marker.split("|"))]
         if not marks:
             continue
         for i in ids:

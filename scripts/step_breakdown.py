@@ -7,9 +7,9 @@ import re
 import sys
 
 
-def main(path, marker="nchw_to_nhwc_pad", top=30):
+def main(path, marker="nchw_to_nhwc_pad|conv_first_wave", top=30):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if any(m in r["Kernel_Name"] for m in marker.split("|"))]
     a, b = idx[-2], idx[-1]
     step = rows[a:b]
     agg = collections.defaultdict(lambda: [0, 0.0])

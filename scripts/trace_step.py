@@ -13,7 +13,7 @@ def short(name):
 def main(path, marker="conv_first", which=-2):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if any(m in r["Kernel_Name"] for m in marker.split("|"))]
     if len(idx) < 2:
         print("marker not found twice")
         return
