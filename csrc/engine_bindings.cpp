@@ -210,8 +210,10 @@ at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_ar
 }
 
 // First conv layer (tiny Cin) on the VALU: NCHW input -> NHWC output, BN affine + ReLU fused.
+// ``wt``: optional tap-major copy of w, [Cin][3][3][Cout], packed once by the caller (the
+// wave-uniform kernel's operand layout); built here per call when absent.
 at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor& scale, const at::Tensor& shift,
-                      bool relu) {
+                      bool relu, const c10::optional<at::Tensor>& wt_packed) {
   need(x, "x", 4);
   need(w, "w", 4);
   const int64_t B = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = w.size(0);
@@ -221,7 +223,15 @@ at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   auto out = at::empty({B, H, W, Cout}, x.options());
   if ((Cout == 16 || Cout == 32 || Cout == 64) && Cin <= 16) {  // wave-uniform weights (scalar loads)
-    const at::Tensor wt = w.permute({1, 2, 3, 0}).contiguous();  // [Cin][3][3][Cout]
+    at::Tensor wt;
+    if (wt_packed.has_value() && wt_packed->defined()) {
+      wt = *wt_packed;
+      need(wt, "wt", 4);
+      TORCH_CHECK(wt.size(0) == Cin && wt.size(1) == 3 && wt.size(2) == 3 && wt.size(3) == Cout,
+                  "wt must be (Cin, 3, 3, Cout)");
+    } else {
+      wt = w.permute({1, 2, 3, 0}).contiguous();  // [Cin][3][3][Cout]
+    }
     TP_CHECK_HIP(tp_conv_first_wave(x.data_ptr<float>(), wt.data_ptr<float>(), scale.data_ptr<float>(),
                                     shift.data_ptr<float>(), out.data_ptr<float>(), (int)B, (int)Cin, (int)H, (int)W,
                                     (int)Cout, relu ? 1 : 0, cur_stream()));
@@ -783,7 +793,7 @@ void register_engine_ops_def(torch::Library& m) {
         "int splits, Tensor(a!)? apoz=None, float slope=0.0) -> (Tensor, Tensor)");
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
         "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0, float slope=0.0) -> Tensor");
-  m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu) -> Tensor");
+  m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu, Tensor? wt=None) -> Tensor");
   m.def("wino_weights(Tensor w, bool flip_t, int K=0, int C=0) -> Tensor");
   m.def("prefix_tri_operands(Tensor z, Tensor w, Tensor perm, int p0, int cnt, int Kc) -> (Tensor, Tensor)");
   m.def("prefix_delta(Tensor T, Tensor wsub, Tensor neg_one, Tensor y0, bool relu, float slope, int cfg) -> Tensor");

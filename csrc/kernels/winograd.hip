@@ -1059,7 +1059,8 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   a.dbg = dbg_bits;
 #endif
   int xmode = unpool ? X_UNPOOL : X_DIRECT;
-  if (staged && !unpool && !staged_geometry(H, W, false).ok && getenv("TP_WINO_NOSPAN") == nullptr) {
+  static const bool span_ok = getenv("TP_WINO_NOSPAN") == nullptr;  // experiments only; read once at load
+  if (staged && !unpool && !staged_geometry(H, W, false).ok && span_ok) {
     const SpanGeom sg = span_geometry(H, W);
     if (sg.ok) {
       xmode = X_SPAN;

@@ -173,3 +173,28 @@ def test_shapley_work_split_modes():
     assert run_loopback(3, body) == ["batches"] * 3
     assert run_loopback(8, body) == ["prefixes"] * 8
     assert ShapleyAttributionMetric(model, dl, F.cross_entropy, torch.device("cpu"))._work_split() is None
+
+
+def test_pruner_lower_level_api_syncs_indices():
+    """R5 at every API level: prune_module / prune_parameter called with rank-local indices
+    prune rank 0's indices on every replica (one broadcast at the outermost call)."""
+    import torch.nn as nn
+
+    w0 = torch.arange(24, dtype=torch.float32).view(6, 4)
+
+    def body(comm):  # (threads share the global RNG: deterministic weights instead of a seed)
+        lin = nn.Linear(4, 6)
+        lin.weight.data.copy_(w0)
+        bn = nn.BatchNorm1d(6)
+        p = Pruner(nn.Sequential(lin, bn), (4,), "cpu", group=comm)
+        p.prune_module(lin, [comm.rank, 5], direction="out")  # rank-local indices
+        p.prune_parameters(bn, ["weight", "bias", "running_mean", "running_var"], [comm.rank + 1])
+        p.prune_parameter(lin, "weight", [comm.rank], axis=1)
+        return lin.weight.detach().clone(), bn.weight.shape[0]
+
+    outs = run_loopback(3, body)
+    for w, nbn in outs:
+        assert torch.equal(w, outs[0][0]) and w.shape == (4, 3) and nbn == 5
+    # rank 0's choices: out rows {0, 5} removed, then input column 0
+    ref = w0[[1, 2, 3, 4]][:, [1, 2, 3]]
+    assert torch.equal(outs[0][0], ref)

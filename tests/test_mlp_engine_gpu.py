@@ -155,3 +155,49 @@ def test_shapley_prefix_delta_matches_masked_copies(cuda, where):
     err_copies = np.abs(res["copies"] - res["fp64"]).max()
     assert res["delta"].shape == res["fp64"].shape
     assert err_delta <= 3 * err_copies + 2e-6, (err_delta, err_copies)
+
+
+def test_mlp_plan_input_shape_checks():
+    """A plain Linear chain given a (B, T, F) batch runs per token in PyTorch; the engine would
+    read it as one flat vector, so such inputs reject the plan (CPU: lowering decision only)."""
+    from torchpruner_amd.engine.fused_chain import build_plan
+    plain, _ = build_plan(nn.Sequential(nn.Linear(8, 16), nn.ReLU(), nn.Linear(16, 4)))
+    assert plain is not None and not plain.flatten
+    assert plain.input_error((5, 8)) is None
+    assert plain.input_error((5, 3, 8)) is not None  # per-token in PyTorch
+    assert plain.input_error((5, 9)) is not None
+    flat, _ = build_plan(_fcnet(in_features=784, hidden=64))
+    assert flat.flatten and flat.input_error((5, 1, 28, 28)) is None
+    assert flat.input_error((5, 1, 28, 29)) is not None  # wider than in_features
+    from torchpruner_amd.models import prunable_vgg16
+    vgg, _ = build_plan(prunable_vgg16().eval())
+    assert vgg.input_error((2, 3, 32, 32)) is None
+    assert vgg.input_error((2, 3, 64, 64)) is not None  # features would not end at 1x1
+
+
+@pytest.mark.gpu
+def test_mlp_engine_rejects_per_token_input(cuda):
+    """(B, T, F) input to Sequential(Linear, ReLU, Linear): the metrics take the generic path and
+    agree with an fp64 CPU run; native_logits declines."""
+    from torchpruner_amd import APoZAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.engine import native_logits
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(8, 16), nn.ReLU(), nn.Linear(16, 4)).eval()
+    x = torch.randn(12, 3, 8)
+    y = torch.randint(0, 4, (12, 3))
+
+    def crit(out, t, reduction="mean"):
+        return F.cross_entropy(out.reshape(-1, 4), t.reshape(-1), reduction=reduction)
+
+    md = copy.deepcopy(m).to(cuda)
+    assert native_logits(md, x.to(cuda)) is None
+    dl = [(x[i:i + 4].to(cuda), y[i:i + 4].to(cuda)) for i in range(0, 12, 4)]
+    for M in (TaylorAttributionMetric, APoZAttributionMetric):
+        met = M(md, dl, crit, cuda)
+        got = met.run(md[0], find_best_evaluation_module=True)
+        assert met.last_path["path"] == "generic", met.last_path
+        mc = copy.deepcopy(m).double()
+        ref = M(mc, [(a.double(), b) for a, b in zip(x.split(4), y.split(4))], crit, torch.device("cpu")).run(
+            mc[0], find_best_evaluation_module=True)
+        assert got.shape == (16,)
+        np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-6)

@@ -246,13 +246,16 @@ class _AttributionMetric(ABC):
 
     # ------------------------------------------------------------------ engine internals
     def _native_ctx(self):
-        """Generic path on the native kernels: every eligible ``nn.Conv2d`` (and training-mode
-        BatchNorm) of the model runs the HIP implicit-GEMM kernels through autograd instead of
-        MIOpen (TORCHPRUNER_GENERIC_NATIVE=0 disables; reduced compute dtypes keep autocast)."""
+        """Generic path on the native kernels: every eligible ``nn.Conv2d``, ``nn.Linear``,
+        ``nn.MaxPool2d``, ``nn.AdaptiveAvgPool2d`` and training-mode ``BatchNorm2d`` of the model
+        runs the HIP kernels through autograd instead of MIOpen / hipBLASLt, unfused so that every
+        module's hooks fire (TORCHPRUNER_GENERIC_NATIVE=0 disables; reduced compute dtypes keep
+        autocast). ``nn.Dropout`` stays on PyTorch: a model scored in training mode draws its
+        dropout masks from the same RNG stream as with the reference."""
         from ..engine.train import native_convs
         enable = (torch.device(self.device).type == "cuda" and not self._reduced_precision()
                   and os.environ.get("TORCHPRUNER_GENERIC_NATIVE", "1") != "0" and ops.backend() != "torch")
-        return native_convs(self.model, enable=enable, fuse=False)  # hooks must see every module
+        return native_convs(self.model, enable=enable, fuse=False, dropout=False)  # hooks must see every module
 
     def _record_path(self, path: str, eval_modules, why=()):
         """Remember and log (once per run, ``torchpruner`` logger) which path served it:
@@ -472,7 +475,24 @@ class _AttributionMetric(ABC):
         if not self._engines_allowed():
             return _reject(why, f"compute_dtype={self.compute_dtype} runs the generic autocast path")
         return maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=need_ce, why=why,
-                            pre_act_ok=pre_act_ok)
+                            pre_act_ok=pre_act_ok, input_shape=self._first_input_shape())
+
+    def _first_input_shape(self):
+        """Shape of the data generator's first input batch, or None when it cannot be peeked at
+        without consuming it (one-shot iterators)."""
+        dg = self.data_gen
+        try:
+            if getattr(dg, "local_only", False):  # a per-rank ShardLoader
+                first = next(iter(dg.batches.values()), None)
+            else:
+                it = iter(dg)
+                if it is dg:
+                    return None
+                first = next(it, None)
+        except Exception:
+            return None
+        x = first[0] if isinstance(first, (tuple, list)) and first else None
+        return tuple(x.shape) if isinstance(x, torch.Tensor) else None
 
     def _resnet_grad_pass(self, eng, eval_modules, accs, mode):
         """Per batch: one engine forward + input-gradient backward scores every module; the

@@ -91,22 +91,22 @@ class ShapleyAttributionMetric(_AttributionMetric):
             perms = pdist.broadcast_object(perms, 0, self.group)
         return perms
 
-    def _segments(self, S, n, split):
+    def _segments(self, S, n, split, K):
         """This rank's share of the flattened (permutation j, prefix p in 1..n) work (all of it
-        unless ``split``)."""
+        unless ``split``). The work is cut on the K-prefix chunk grid of the single-rank run
+        (chunk c of a permutation covers prefixes c*K+1 .. (c+1)*K), so every stacked
+        evaluation has exactly the shape and prefix range it has on one rank and the sharded
+        scores are bit-identical to the single-rank ones."""
         world, rank = self._world()
-        if split:
-            lo, hi = pdist.split_range(S * n, rank, world)
-        else:
-            lo, hi = 0, S * n
+        per = -(-n // K)  # chunks per permutation
+        lo, hi = pdist.split_range(S * per, rank, world) if split else (0, S * per)
         segs = []
-        u = lo
-        while u < hi:
-            j = u // n
-            p_lo = u % n + 1
-            p_hi = min(n, p_lo + (hi - u) - 1)
-            segs.append((j, p_lo, p_hi))
-            u += p_hi - p_lo + 1
+        c = lo
+        while c < hi:
+            j, c0 = divmod(c, per)
+            c1 = min(per, c0 + (hi - c))  # chunks c0 .. c1-1 of permutation j
+            segs.append((j, c0 * K + 1, min(n, c1 * K)))
+            c += c1 - c0
         return segs
 
     def _work_split(self):
@@ -118,6 +118,10 @@ class ShapleyAttributionMetric(_AttributionMetric):
         world, _ = self._world()
         if world == 1 or self.shard_data is False:
             return None
+        if getattr(self.data_gen, "local_only", False):
+            # a per-rank loader (ShardLoader) cannot be iterated whole: shard by batches even
+            # with fewer batches than ranks (ranks without a batch contribute zeros)
+            return "batches"
         try:
             nb = len(self.data_gen)
         except TypeError:
@@ -134,7 +138,9 @@ class ShapleyAttributionMetric(_AttributionMetric):
     def _accumulate_permutation(self, perm_t, rank_t, p_lo, p_hi, base_loss, evaluate, K, S, sink):
         """Evaluate prefixes p_lo..p_hi of one permutation and add their deltas to ``sink``."""
         B = base_loss.shape[0]
-        prev = base_loss if p_lo == 1 else evaluate(rank_t, p_lo - 1, 1)[0]
+        # a range that starts inside the permutation takes its boundary loss L_{p_lo-1} from the
+        # previous full chunk (the same stacked evaluation the single-rank run makes)
+        prev = base_loss if p_lo == 1 else evaluate(rank_t, max(1, p_lo - K), min(K, p_lo - 1))[-1]
         cur = p_lo
         while cur <= p_hi:
             cnt = min(K, p_hi - cur + 1)
@@ -163,18 +169,21 @@ class ShapleyAttributionMetric(_AttributionMetric):
                     perms = self._permutations(n, S)  # drawn on rank 0, broadcast (R3)
                     perm_ts = [torch.as_tensor(p, dtype=torch.int32).to(base_loss.device) for p in perms]
                     rank_ts = [self._rank_of(p, base_loss.device) for p in perms]
-                    segs = self._segments(S, n, split == "prefixes")
                 K = self._prefix_chunk(B, per_sample)
+                if segs is None or segs[0] != K:
+                    segs = (K, self._segments(S, n, split == "prefixes", K))
+                # deltas are summed unscaled (fp64 sums of fp32 loss differences: exact, so any
+                # rank split / collective order gives the same bits) and divided by S at the end
                 if stats:
                     if sv_col is None:
                         sv_col = torch.zeros(n, dtype=torch.float64, device=base_loss.device)
-                    sink = lambda L, pt, k0: ops.shapley_column(L, pt, sv_col, k0, 1.0 / S)
+                    sink = lambda L, pt, k0: ops.shapley_column(L, pt, sv_col, k0, 1.0)
                 else:
                     slab = torch.zeros(B, n, dtype=torch.float64, device=base_loss.device)
                     slabs.append((bidx, slab))
-                    sink = lambda L, pt, k0, slab=slab: ops.shapley_scatter(L, pt, slab, 0, k0, 1.0 / S)
+                    sink = lambda L, pt, k0, slab=slab: ops.shapley_scatter(L, pt, slab, 0, k0, 1.0)
                 with trace_range("tp.shapley.prefixes"):
-                    for j, p_lo, p_hi in segs:
+                    for j, p_lo, p_hi in segs[1]:
                         self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi, base_loss, evaluate, K, S,
                                                      sink)
                 count += B
@@ -193,7 +202,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
                         count = float(buf[n].item())
             if sv_col is None:
                 return np.zeros(0)
-            total = sv_col.cpu().numpy()
+            total = sv_col.cpu().numpy() / max(S, 1)
             return total / max(count, 1) if self.reduction == "mean" else total
         if split == "batches":
             with trace_range("tp.collective"):
@@ -203,7 +212,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
             if split == "prefixes":
                 with trace_range("tp.collective"):
                     pdist.all_reduce_sum_(sv, self.group)
-        return self.aggregate_over_samples(sv.cpu().numpy())
+        return self.aggregate_over_samples(sv.cpu().numpy() / max(S, 1))
 
     # ------------------------------------------------------------------ native path
     def _fused_prepare(self, module, why=None):

@@ -86,6 +86,11 @@ class ShardLoader:
     def __len__(self):
         return self.num_batches
 
+    @property
+    def local_only(self) -> bool:
+        """True when this loader holds only its rank's batches (plain iteration would fail)."""
+        return len(self.batches) != self.num_batches
+
     def __iter__(self):
         if len(self.batches) != self.num_batches:
             raise RuntimeError("ShardLoader holds one rank's batches; iterate it through shard(rank, world)")

@@ -17,7 +17,7 @@ def native_logits(model, x: torch.Tensor):
     MLPs; ResNet engine), or None when neither applies (training mode, CPU, other models)."""
     if not isinstance(x, torch.Tensor) or not x.is_cuda or model.training:
         return None
-    r = maybe_engine(model, [], None, x.device, need_ce=False)
+    r = maybe_engine(model, [], None, x.device, need_ce=False, input_shape=tuple(x.shape))
     if r is not None:
         return r[0].forward(x)[0]
     eng = maybe_resnet_engine(model, [], x.device)

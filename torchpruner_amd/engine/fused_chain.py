@@ -238,6 +238,24 @@ def _is_block_act(m) -> bool:
 class Plan:
     convs: list = field(default_factory=list)
     linears: list = field(default_factory=list)
+    flatten: bool = False  # the chain has an explicit Flatten stage
+
+    def input_error(self, shape) -> Optional[str]:
+        """Why an input of ``shape`` is not what this chain computes on (None when it is): the
+        engine would otherwise silently read a differently shaped input as the planned one."""
+        shape = tuple(shape)
+        if self.convs:
+            npool = sum(b.pool is not None for b in self.convs)
+            side = 1 << npool
+            cin = self.convs[0].conv.in_channels
+            if len(shape) != 4 or shape[1] != cin or shape[2] != side or shape[3] != side:
+                return f"input {shape} is not (B, {cin}, {side}, {side}) (features must end at 1x1)"
+            return None
+        fin = self.linears[0].linear.in_features
+        feat = math.prod(shape[1:]) if len(shape) > 1 else 0
+        if feat != fin or (len(shape) != 2 and not self.flatten):
+            return f"input {shape} is not (B, {fin})" + ("" if self.flatten else " (no Flatten stage)")
+        return None
 
     def eval_module_of(self, i):
         blk = self.blocks[i]
@@ -301,6 +319,7 @@ def build_plan(model: nn.Module):
     # flatten (a conv-less MLP may start with it or take flattened inputs)
     if i < n and (isinstance(stages[i], nn.Flatten) or getattr(stages[i], "__name__", "") == "_flatten"):
         i += 1
+        plan.flatten = True
     elif plan.convs:
         return None, "expected flatten after the conv stack"
     while i < n:
@@ -378,6 +397,7 @@ class FusedChainEngine:
             entry = {"scale": scale.contiguous(), "shift": shift.contiguous(), "pool": b.pool is not None}
             if b.first:
                 entry["w_first"] = w.contiguous()
+                entry["w_first_t"] = w.permute(1, 2, 3, 0).contiguous()  # tap-major VALU operand, packed once
                 if self.use_wino and w.shape[1] <= 8 and cout % 32 == 0:
                     # tiny-Cin first layer on the Winograd MFMA kernel: input padded to 8 channels
                     entry["u_first"] = winograd_weights(F.pad(w, (0, 0, 0, 0, 0, 8 - w.shape[1])))
@@ -418,7 +438,7 @@ class FusedChainEngine:
         """First (tiny-Cin) conv block -> (output, argmax or None): the block's 2x2 max-pool is
         fused into the Winograd epilogue, or applied after the VALU direct conv."""
         if cfg == self.FIRST_DIRECT:
-            h = T.conv_first(xf, e["w_first"], e["scale"], e["shift"], True)
+            h = T.conv_first(xf, e["w_first"], e["scale"], e["shift"], True, e["w_first_t"])
             if apoz is not None:
                 apoz += ops.channel_reduce(h.permute(0, 3, 1, 2), None, "apoz")
             return T.maxpool2_nhwc(h) if e["pool"] else (h, None)
@@ -526,6 +546,9 @@ class FusedChainEngine:
         NHWC (pooled when the block pools) for conv blocks, (B,1,1,N) for linear blocks.
         ``apoz`` maps block indices to zeroed (B, padded width) buffers that receive, per sample
         and unit, the count of positive outputs of the block's ReLU (before pooling)."""
+        err = self.plan.input_error(x.shape)
+        if err:
+            raise ValueError(f"fused chain engine: {err}")
         T = ops.require()
         P = self._pack()
         B = x.shape[0]
@@ -859,6 +882,13 @@ def criterion_is_cross_entropy(criterion, device) -> bool:
         return False
 
 
+def engines_enabled() -> bool:
+    """``TORCHPRUNER_ENGINES=0`` sends every metric to the generic module/hook path (the
+    same-algorithm library baseline of bench.py: one pass, PyTorch modules; add
+    ``TORCHPRUNER_GENERIC_NATIVE=0`` for MIOpen / hipBLASLt convolutions)."""
+    return os.environ.get("TORCHPRUNER_ENGINES", "1") != "0"
+
+
 def _reject(why, reason):
     """Record why an engine did not apply (path transparency) and return None."""
     if why is not None:
@@ -866,18 +896,23 @@ def _reject(why, reason):
     return None
 
 
-def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None, pre_act_ok=False):
+def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None, pre_act_ok=False,
+                 input_shape=None):
     """Return (engine, block indices of eval_modules) when the fused path applies, else None.
     ``need_ce=False``: forward-only use (APoZ) or gradient metrics with any criterion (the caller
     passes ``engine_criterion(criterion)`` to :meth:`FusedChainEngine.taylor`). ``why``: a list that receives the
     rejection reason when the engine does not apply. ``pre_act_ok``: a classifier block's Linear
     may stand for its activation output (valid for sign counts (APoZ) and zero-masking
-    (Shapley): ReLU / LeakyReLU keep the sign and map 0 to 0; not for Taylor / Sensitivity)."""
+    (Shapley): ReLU / LeakyReLU keep the sign and map 0 to 0; not for Taylor / Sensitivity).
+    ``input_shape``: shape of a data batch; an input the chain does not compute on (e.g. a
+    (B, T, F) batch for a Linear MLP) rejects the engine."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda":
         return _reject(why, f"device {dev} is not a GPU")
     if ops.backend() == "torch" or not ops.available():
         return _reject(why, "native extension disabled (TORCHPRUNER_BACKEND=torch) or not built")
+    if not engines_enabled():
+        return _reject(why, "fused engines disabled (TORCHPRUNER_ENGINES=0)")
     if model.training:
         return _reject(why, "model is in training mode (engines fold eval-mode BatchNorm)")
     if any(p.dtype != torch.float32 for p in model.parameters()):
@@ -885,6 +920,10 @@ def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None,
     plan, reason = build_plan(model)
     if plan is None:
         return _reject(why, f"fused chain: {reason}")
+    if input_shape is not None:
+        err = plan.input_error(input_shape)
+        if err:
+            return _reject(why, f"fused chain: {err}")
     idx = []
     blocks = plan.blocks
     for m in eval_modules:

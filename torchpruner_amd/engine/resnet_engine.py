@@ -411,8 +411,10 @@ _ENGINES: "weakref.WeakKeyDictionary[nn.Module, ResNetEngine]" = weakref.WeakKey
 def maybe_resnet_engine(model, eval_modules, device, grad=False, why=None):
     """A ResNetEngine when every eval module is a BN the engine counts (``grad``: scores by
     :meth:`ResNetEngine.grad_scores`, block BNs only), else None (``why`` receives the reason)."""
-    from .fused_chain import _reject
+    from .fused_chain import _reject, engines_enabled
     dev = torch.device(device) if not isinstance(device, torch.device) else device
+    if not engines_enabled():
+        return _reject(why, "resnet engine: engines disabled (TORCHPRUNER_ENGINES=0)")
     if dev.type != "cuda" or ops.backend() == "torch" or not ops.available() or model.training:
         return _reject(why, "resnet engine: needs an eval-mode model on a GPU with the native extension")
     if any(p.dtype != torch.float32 for p in model.parameters()):

@@ -663,15 +663,17 @@ def _native_forward(self, x):
     return _NativeConv2d.apply(x, self.weight, self.bias, ks, s, p)
 
 
-def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True) -> list:
+def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True, dropout: bool = True) -> list:
     """Route every eligible ``nn.Conv2d`` of ``model`` (and, with ``bn``, every ``BatchNorm2d`` in
     training mode) through the native kernels (instance-level ``forward`` override; pruning keeps
     working because weights are re-packed per call). With ``bn`` and ``fuse``, residual blocks,
     ResNet stems and ``nn.Sequential`` containers also fuse their BN(+residual)+ReLU tails in
     training mode — the fused BN / ReLU modules (and a bottleneck's conv1 / downsample conv, run by
     the block's entry node) are then not called, so forward hooks on them do not fire (attribution
-    passes use ``fuse=False``). Returns the switched modules; undo with
-    :func:`disable_native_convs`."""
+    passes use ``fuse=False``). Also switched: ``nn.Linear`` (MFMA GEMM), ``nn.MaxPool2d``,
+    ``nn.AdaptiveAvgPool2d`` and, with ``dropout``, training-mode ``nn.Dropout`` (Philox masks
+    seeded from torch's CPU RNG: a different random stream than PyTorch's dropout). Returns the
+    switched modules; undo with :func:`disable_native_convs`."""
     if not ops.available() or ops.backend() == "torch":
         return []
     from .resnet_engine import _is_resnet
@@ -691,7 +693,7 @@ def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True) ->
         elif eligible(m):
             m.forward = types.MethodType(_native_forward, m)
             switched.append(m)
-        elif type(m) is nn.Dropout:
+        elif dropout and type(m) is nn.Dropout:
             m.forward = types.MethodType(_native_dropout_forward, m)
             switched.append(m)
         elif type(m) is nn.Linear:
@@ -715,9 +717,9 @@ def disable_native_convs(modules) -> None:
 
 
 @contextlib.contextmanager
-def native_convs(model: nn.Module, enable: bool = True, bn: bool = True, fuse: bool = True):
+def native_convs(model: nn.Module, enable: bool = True, bn: bool = True, fuse: bool = True, dropout: bool = True):
     """``with native_convs(model): loss.backward()`` — scoped :func:`enable_native_convs`."""
-    switched = enable_native_convs(model, bn, fuse) if enable else []
+    switched = enable_native_convs(model, bn, fuse, dropout) if enable else []
     try:
         yield switched
     finally:

@@ -167,6 +167,46 @@ def barrier(group=None):
         group.barrier() if _comm(group) else dist.barrier(group=group)
 
 
+def all_gather_object(obj: Any, group=None) -> list:
+    if get_world_size(group) == 1:
+        return [obj]
+    if _comm(group):
+        return group.all_gather_object(obj)
+    out = [None] * get_world_size(group)
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def state_digest(model: torch.nn.Module) -> str:
+    """sha256 (16 hex) over every parameter and buffer of ``model`` (bytes, in state_dict order)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k, t in model.state_dict().items():
+        h.update(k.encode())
+        h.update(t.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
+def sync_module(model: torch.nn.Module, src: int = 0, group=None) -> dict:
+    """Make every rank hold rank ``src``'s parameters and buffers, and report whether they
+    already agreed: the digests are all-gathered BEFORE the broadcast (a replicated
+    "deterministic" initialisation that diverged shows up as ``agreed_before: False``) and
+    again after it (asserted equal). Data-parallel scores are only meaningful when every rank
+    scores the same model."""
+    world = get_world_size(group)
+    mine = state_digest(model)
+    if world == 1:
+        return {"agreed_before": True, "digest": mine, "ranks": 1}
+    before = all_gather_object(mine, group)
+    with torch.no_grad():
+        for t in model.state_dict().values():
+            broadcast_tensor_(t, src, group)
+    after = all_gather_object(state_digest(model), group)
+    assert len(set(after)) == 1, f"model digests differ after broadcast: {after}"
+    return {"agreed_before": len(set(before)) == 1, "digest": after[0], "ranks": world,
+            "digests_before": before if len(set(before)) > 1 else None}
+
+
 def gather_ordered_rows(slabs: list[tuple[int, torch.Tensor]], group=None) -> torch.Tensor:
     """All-gather per-batch ``(global_batch_index, (B_i, C) tensor)`` slabs from every rank
     and return the ``(sum B_i, C)`` concatenation in global batch order (R2).

@@ -19,6 +19,7 @@ Differences (deliberate fixes):
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 
@@ -55,15 +56,15 @@ class Pruner:
         self.optimizer = optimizer
         self.group = group
         self.sync_indices = sync_indices
+        self._depth = 0  # > 0 inside a public call: nested calls use already-agreed indices
 
     # ------------------------------------------------------------------ public API
     def prune_model(self, module, indices, cascading_modules=None):
         """Prune output units ``indices`` of ``module`` and cascade into ``cascading_modules``."""
-        with trace_range("tp.prune"):
-            return self._prune_model(module, indices, cascading_modules)
+        with trace_range("tp.prune"), self._entry():
+            return self._prune_model(module, self._sync(_as_index_array(indices)), cascading_modules)
 
     def _prune_model(self, module, indices, cascading_modules=None):
-        indices = self._sync(_as_index_array(indices))
         if cascading_modules is None:
             logger.warning("no cascading modules defined")
             cascading_modules = []
@@ -83,14 +84,18 @@ class Pruner:
             if hasattr(next_module, "_nan_indices"):
                 idx = getattr(next_module, "_nan_indices")
                 length = getattr(next_module, "_activation_len", None)
-                self.prune_module(next_module, idx, direction="in", original_len=length)
+                self._prune_module(next_module, _as_index_array(idx), direction="in", original_len=length)
                 delattr(next_module, "_nan_indices")
             if hasattr(next_module, "_activation_len"):
                 delattr(next_module, "_activation_len")
-        self.prune_module(module, indices, direction="out")
+        self._prune_module(module, indices, direction="out")
 
     def prune_module(self, module, indices, direction="out", original_len=None):
         """Prune a module's parameters along its output (``"out"``) or input (``"in"``) units."""
+        with self._entry():
+            return self._prune_module(module, self._sync(_as_index_array(indices)), direction, original_len)
+
+    def _prune_module(self, module, indices, direction="out", original_len=None):
         assert direction in ["out", "in"], "direction should be 'out' or 'in'"
         if direction == "out":
             assert any(isinstance(module, t) for t in SUPPORTED_OUT_PRUNING_MODULES), \
@@ -127,7 +132,11 @@ class Pruner:
 
     def prune_parameters(self, module, names, indices, axis=0):
         """Slice several same-length tensors of ``module`` along ``axis`` in ONE gather launch."""
-        indices = _as_index_array(indices)
+        with self._entry():
+            indices = self._sync(_as_index_array(indices))
+            return self._prune_parameters(module, names, indices, axis)
+
+    def _prune_parameters(self, module, names, indices, axis=0):
         tensors, axes, sinks = [], [], []
         keep = None
         for name in names:
@@ -169,10 +178,26 @@ class Pruner:
                 self.optimizer.state[p][key] = new
 
     # ------------------------------------------------------------------ internals
+    @contextlib.contextmanager
+    def _entry(self):
+        self._depth += 1
+        try:
+            yield
+        finally:
+            self._depth -= 1
+
     def _sync(self, indices: np.ndarray) -> np.ndarray:
-        if self.sync_indices and pdist.get_world_size(self.group) > 1:
-            indices = np.asarray(pdist.broadcast_object(indices, 0, self.group))
-        return indices
+        """R5: at the outermost public call of a data-parallel job every rank takes rank 0's
+        indices (broadcast), and a rank whose own indices differed says so — every replica must
+        prune identically, whichever API level the caller uses (prune_model / prune_module /
+        prune_parameter(s)). Nested calls reuse the agreed indices (no extra collective)."""
+        if self._depth > 1 or not self.sync_indices or pdist.get_world_size(self.group) <= 1:
+            return indices
+        agreed = np.asarray(pdist.broadcast_object(indices, 0, self.group), dtype=np.int64).reshape(-1)
+        if not np.array_equal(agreed, indices):
+            logger.warning("rank %d: pruning indices differ from rank 0's (%d vs %d units); using rank 0's",
+                           pdist.get_rank(self.group), len(indices), len(agreed))
+        return agreed
 
     def _adjust_dropout(self, module, indices, original_len):
         """Keep the expected number of active units: p *= 1 - pruned/original (pruner.py:117-127)."""
