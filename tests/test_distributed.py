@@ -53,6 +53,14 @@ def _compute(world_rank=None):
     np.random.seed(7)
     out["sv_none"] = ShapleyAttributionMetric(model, dl, F.cross_entropy, dev, sv_samples=2,
                                               reduction="none").run(model[0], find_best_evaluation_module=True)
+    # a per-rank ShardLoader with fewer batches (2) than ranks: sharded by batches
+    from torchpruner_amd.data import ShardLoader
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rk = dist.get_rank() if dist.is_initialized() else 0
+    xs, ys = next(iter(dl))
+    sl = ShardLoader.build(lambda i: (xs + i, ys), 2, xs.shape[0], rk, world)
+    np.random.seed(5)
+    out["sv_shard"] = ShapleyAttributionMetric(model, sl, F.cross_entropy, dev, sv_samples=2).run(model[4])
     # pruner: rank-dependent indices must be replaced by rank 0's
     rank = dist.get_rank() if dist.is_initialized() else 0
     Pruner(model, (3, 8, 8), dev).prune_model(model[4], [rank, 3], [model[7]])
@@ -81,11 +89,12 @@ def test_dp_matches_single_process(world):
         mp.spawn(_worker, args=(world, port, path), nprocs=world, join=True)
         got = torch.load(path, weights_only=False)
     # fp64 device accumulators: the sharded reductions agree with one process to <= 1e-6
-    # relative; Shapley prefix losses are re-batched per rank (rounding level)
+    # relative; Shapley work is cut on the single-rank prefix-chunk grid and its
+    # deltas summed unscaled, so it is bit-identical (world 8: 6 batches -> prefix split)
     for k in ["taylor", "taylor_none", "sens_sum"]:
         np.testing.assert_allclose(got[k], ref[k], rtol=1e-6, atol=1e-9, err_msg=k)
-    for k in ["sv", "sv_none"]:
-        np.testing.assert_allclose(got[k], ref[k], rtol=1e-5, atol=1e-8, err_msg=k)
+    for k in ["sv", "sv_none", "sv_shard"]:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     for a, b in zip(got["apoz_many"], ref["apoz_many"]):
         np.testing.assert_allclose(a, b, rtol=1e-6)
     assert got["taylor_none"].shape == (22, 5)

@@ -187,6 +187,8 @@ class ShapleyAttributionMetric(_AttributionMetric):
                         self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi, base_loss, evaluate, K, S,
                                                      sink)
                 count += B
+        if split == "batches" and perms is None:
+            self._permutations(0, S)  # a rank without batches still joins the permutation broadcast (R3)
         if stats:
             if split is not None:
                 with trace_range("tp.collective"):

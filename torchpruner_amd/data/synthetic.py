@@ -71,25 +71,27 @@ class ShardLoader:
     of the data instead of all of it); iterating it plainly is only valid when it owns all
     batches (world 1)."""
 
-    def __init__(self, batches: dict, num_batches: int, batch_size: int):
+    def __init__(self, batches: dict, num_batches: int, batch_size: int, world: int = 1):
         self.batches = batches
         self.num_batches = num_batches
         self.batch_size = batch_size
+        self.world = world
         self.dataset = _Len(num_batches * batch_size)
 
     @classmethod
     def build(cls, make_batch: Callable, num_batches: int, batch_size: int, rank: int = 0, world: int = 1):
         """``make_batch(i)`` -> (x, y) of global batch ``i`` (e.g. seeded from i); only this rank's
         batches are built."""
-        return cls({i: make_batch(i) for i in range(rank, num_batches, world)}, num_batches, batch_size)
+        return cls({i: make_batch(i) for i in range(rank, num_batches, world)}, num_batches, batch_size, world)
 
     def __len__(self):
         return self.num_batches
 
     @property
     def local_only(self) -> bool:
-        """True when this loader holds only its rank's batches (plain iteration would fail)."""
-        return len(self.batches) != self.num_batches
+        """True when this loader was built for one rank of a multi-rank job (it holds only that
+        rank's batches; every rank answers the same, so they agree on how to split work)."""
+        return self.world > 1 or len(self.batches) != self.num_batches
 
     def __iter__(self):
         if len(self.batches) != self.num_batches:
