@@ -81,6 +81,13 @@ hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, const float* 
                                 int N, int B0, int relu, float slope, int cfg, float* out, hipStream_t st);
 hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* perm, int B, int C, int N, int p0,
                                   int cnt, int Kc, float* T, float* Wsub, hipStream_t st);
+hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
+int tp_wino4_u_img();
+int tp_wino4_ok(int H, int W, int C, int K);
+int tp_wino4_lds_bytes(int S);
+hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
+                         const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act, float* taylor,
+                         float* apoz, int tay_mode, hipStream_t st);
 }
 
 namespace {
@@ -408,6 +415,90 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
                             (int)sp, staged ? 1 : 0, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
                             act.data_ptr<float>(), tay, nullptr, sp > 1 ? ws.data_ptr<float>() : nullptr,
                             (int)tay_mode, cur_stream()));
+  return out;
+}
+
+// ---- Winograd F(4x4,3x3) (wino4.hip): square 4/8/16/32-pixel maps --------------------------------
+at::Tensor wino4_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C) {
+  need(w, "w", 4);
+  TORCH_CHECK(w.size(2) == 3 && w.size(3) == 3, "w must be (.., .., 3, 3)");
+  if (K <= 0) K = flip_t ? w.size(1) : w.size(0);
+  if (C <= 0) C = flip_t ? w.size(0) : w.size(1);
+  TORCH_CHECK(K % 32 == 0 && C % 8 == 0, "F(4x4) U images need K % 32 == 0 and C % 8 == 0");
+  TORCH_CHECK(flip_t ? (w.size(0) <= C && w.size(1) <= K) : (w.size(0) <= K && w.size(1) <= C),
+              "weight wider than the padded GEMM");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(w.device());
+  auto u = at::empty({C / 8, K / 32, (int64_t)tp_wino4_u_img()}, w.options());
+  TP_CHECK_HIP(tp_wino4_weights(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
+                                (int)w.size(0), (int)w.size(1), cur_stream()));
+  return u;
+}
+
+void need_u4(const at::Tensor& u, int64_t C, int64_t K) {
+  need(u, "u", 3);
+  TORCH_CHECK(C % 8 == 0 && K % 32 == 0 && u.size(0) == C / 8 && u.size(1) == K / 32 && u.size(2) == tp_wino4_u_img(),
+              "u must be the F(4x4) U images (C/8, K/32, ", tp_wino4_u_img(), "), got ", u.sizes());
+}
+
+std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at::Tensor& u,
+                                                  const c10::optional<at::Tensor>& scale,
+                                                  const c10::optional<at::Tensor>& shift, bool relu, bool pool,
+                                                  const c10::optional<at::Tensor>& apoz) {
+  need(x, "x", 4);
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
+  need_u4(u, C, K);
+  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)C, (int)K), "F(4x4) Winograd needs square 4/8/16/32 maps, C % 8 == 0, "
+              "K % 32 == 0; got ", x.sizes(), " K=", K);
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const float* sc = opt_ptr(scale, K, "scale");
+  const float* sh = opt_ptr(shift, K, "shift");
+  at::Tensor out, am;
+  if (pool) {
+    out = at::empty({B, H / 2, W / 2, K}, x.options());
+    am = at::empty({B, H / 2, W / 2, K}, x.options().dtype(at::kByte));
+  } else {
+    out = at::empty({B, H, W, K}, x.options());
+  }
+  float* ap = nullptr;
+  if (apoz.has_value() && apoz->defined()) {
+    TORCH_CHECK(apoz->is_cuda() && apoz->scalar_type() == at::kFloat && apoz->is_contiguous() &&
+                    apoz->numel() == B * K, "apoz must be a contiguous float32 (B, K) tensor");
+    ap = apoz->data_ptr<float>();
+  }
+  TP_CHECK_HIP(tp_conv_wino4(x.data_ptr<float>(), u.data_ptr<float>(), (int)B, (int)H, (int)C, (int)K,
+                             pool ? EPI_FWD_POOL : EPI_FWD, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
+                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap, 0, cur_stream()));
+  return {out, am};
+}
+
+// F(4x4) dgrad with the conv_wino_dgrad epilogue contract (no unpooling: pass the unpooled grad)
+at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at::Tensor& act,
+                            const c10::optional<at::Tensor>& bn_scale, const c10::optional<at::Tensor>& taylor,
+                            bool want_out, int64_t tay_mode) {
+  need(g, "g", 4);
+  need(act, "act", 4);
+  const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
+  need_u4(ut, Cout, Cin);
+  TORCH_CHECK(g.size(0) == B && g.size(1) == H && g.size(2) == W, "grad shape mismatch");
+  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)Cout, (int)Cin), "F(4x4) dgrad needs square 4/8/16/32 maps, "
+              "Cout % 8 == 0, Cin % 32 == 0");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
+  float* tay = nullptr;
+  if (taylor.has_value() && taylor->defined()) {
+    const int64_t R = std::max<int64_t>(tp_wino_taylor_slots((int)H, (int)W), 2);
+    TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
+                    taylor->numel() % (B * Cin) == 0 && taylor->numel() >= (H == 32 ? 2 : 1) * B * Cin,
+                "taylor must be a contiguous float32 (R', B, Cin) GPU tensor with R' >= ", H == 32 ? 2 : 1,
+                " partial slots");
+    (void)R;
+    tay = taylor->data_ptr<float>();
+  }
+  at::Tensor out;
+  if (want_out) out = at::empty({B, H, W, Cin}, g.options());
+  TP_CHECK_HIP(tp_conv_wino4(g.data_ptr<float>(), ut.data_ptr<float>(), (int)B, (int)H, (int)Cout, (int)Cin, EPI_BWD,
+                             sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(),
+                             tay, nullptr, (int)tay_mode, cur_stream()));
   return out;
 }
 
@@ -769,6 +860,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("wino_lds_bytes() -> int", []() -> int64_t { return tp_wino_lds_bytes(); });
+  m.def("wino4_lds_bytes(int S) -> int", [](int64_t S) -> int64_t { return tp_wino4_lds_bytes((int)S); });
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
   m.def("maxpool2_nhwc(Tensor x) -> (Tensor, Tensor)");
   m.def("maxpool_nhwc(Tensor x, int k, int s, int pad) -> Tensor");
@@ -801,6 +893,11 @@ void register_engine_ops_def(torch::Library& m) {
         "bool staged=True, Tensor(a!)? apoz=None) -> (Tensor, Tensor)");
   m.def("conv_wino_dgrad(Tensor g, Tensor? g_argmax, Tensor ut, Tensor act, Tensor? bn_scale, "
         "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True, int tay_mode=0) -> Tensor");
+  m.def("wino4_weights(Tensor w, bool flip_t, int K=0, int C=0) -> Tensor");
+  m.def("conv_wino4_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, "
+        "Tensor(a!)? apoz=None) -> (Tensor, Tensor)");
+  m.def("conv_wino4_dgrad(Tensor g, Tensor ut, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, bool want_out, "
+        "int tay_mode=0) -> Tensor");
 }
 
 void register_engine_ops_impl(torch::Library& m) {
@@ -825,4 +922,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("bn_train_bwd", &bn_train_bwd);
   m.impl("unpool2_nhwc", &unpool2_nhwc);
   m.impl("conv_wino_dgrad", &conv_wino_dgrad);
+  m.impl("wino4_weights", &wino4_weights);
+  m.impl("conv_wino4_fwd", &conv_wino4_fwd);
+  m.impl("conv_wino4_dgrad", &conv_wino4_dgrad);
 }

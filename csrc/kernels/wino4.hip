@@ -1,0 +1,530 @@
+// Winograd F(4x4, 3x3) convolution on fp32 MFMA (v_mfma_f32_16x16x4_f32) for the stride-1 3x3
+// layers of square S x S feature maps, S in {4, 8, 16, 32} (VGG's 32/16/8/4-pixel stages):
+// 36 multiplies per 4x4 output tile instead of 144 (direct) or 64 (F(2x2,3x3), winograd.hip),
+// i.e. 1.78x fewer MFMAs than F(2x2) at the same LDS bytes per MFMA.
+//
+//   * a block = 4 waves = 32 output tiles (4x4 pixels) x 32 output channels; wave w owns the 16
+//     tiles of half (w & 1) (MFMA rows, lane & 15) x the 16 channels of half (w >> 1) x all 36
+//     transform points: 36 accumulator tiles, 144 registers;
+//   * input channels advance in chunks of 8: lane (j, g) holds channels 2g, 2g+1 (MFMA k = g) of
+//     its tile's 6x6 patch, read as float2 from a 2-plane (channels 0-3 / 4-7) LDS image of the
+//     block's input region (halos shared, one 16-B slot per pixel and plane, DMA'd with
+//     `buffer_load_dwordx4 ... lds`); the row / image pitches and a pad slot after every 4 columns
+//     make the 16 tiles of a wave hit 16 different bank quads (conflict-free ds_read_b64) with
+//     compile-time patch offsets; S = 4 stages image interiors only (the border is a constant 0);
+//   * the transformed weights U = G g G^T of (8 channels x 32 outputs x 36 points) are one 36-KB
+//     pre-arranged LDS image per chunk: one conflict-free ds_read_b64 = the B operands of both
+//     channel halves of a point;
+//   * software pipeline: the DMA of chunk c+1 is issued at the top of chunk c; after the first
+//     half of chunk c's MFMAs the waves wait for it (one barrier), read their next patch and form
+//     V = B^T d B for chunk c+1 under the second half of chunk c's MFMAs;
+//   * epilogue: Y = A^T m A in registers, parked in LDS, then coalesced 128-B stores with the
+//     fused epilogue contract of winograd.hip — BN affine + NaN-propagating ReLU (+ 2x2 max-pool
+//     with argmax bytes), APoZ counts, and for the data gradient the ReLU-mask / BN-scale output
+//     and the Taylor / Sensitivity partials — summed per (image, channel) in a fixed order with
+//     one writer per sum (every image lies in a single block): deterministic, no atomics.
+//
+// Transform points 0, +-1, +-2, inf (Lavin & Gray); fp32 error ~2e-6 relative (64-channel
+// reduction), well inside the engine's fp64-oracle tolerances.
+#include "tp_common.h"
+
+#include <type_traits>
+
+namespace tp {
+namespace w4 {
+
+enum Epi : int { FWD = 0, FWD_POOL = 1, BWD = 2 };
+
+constexpr int TILES = 32;                 // output tiles per block
+constexpr int TK = 32;                    // output channels per block
+constexpr int NPT = 36;                   // transform points
+constexpr int U_IMG = NPT * 2 * 16 * 8;   // 9216 floats per (8-channel chunk, 32-output) image
+constexpr int U_ROUNDS = U_IMG / 1024;    // 9 DMA rounds of 256 16-B slots
+constexpr int TPL = 16 * 16 + 4;          // epilogue LDS floats per tile (16 px x 16 ch + bank pad)
+constexpr unsigned OOB = 0x80000000u;
+
+// Staged input region per spatial size, per plane: NI images per block (32 tiles), image pitch
+// IP slots, row pitch RWP slots, RH rows; for S >= 8 the region carries the 1-pixel halo and a
+// pad slot after every 4 columns (col' = x' + x'/4, x' = x + 1); S = 4 holds the 4x4 interiors.
+// Conflict rule (ds_read_b64 of 8 B at slot s, bank = 4s + 2(g & 1) mod 64): the 16 slot bases of
+// a wave's tiles must be distinct mod 16. XR = DMA rounds of 256 slots for both planes.
+template <int S> struct Geo;
+template <> struct Geo<32> { static constexpr int NI = 1, RH = 18, RWP = 42, IP = 18 * 42; };
+template <> struct Geo<16> { static constexpr int NI = 2, RH = 18, RWP = 23, IP = 18 * 23; };
+template <> struct Geo<8> { static constexpr int NI = 8, RH = 10, RWP = 14, IP = 146; };
+template <> struct Geo<4> { static constexpr int NI = 32, RH = 4, RWP = 4, IP = 17; };
+template <int S> constexpr int plane_slots() { return Geo<S>::NI * Geo<S>::IP; }
+template <int S> constexpr int x_rounds() { return (2 * plane_slots<S>() + 255) / 256; }
+
+struct Args {
+  const float* x;     // NHWC (B, S, S, C): the input (forward) or the output gradient (dgrad)
+  const float* u;     // U images [C/8][K/32][U_IMG]
+  int B, C, K, P;     // P = output tiles = B * (S/4)^2
+  long long x_elems;
+  const float* scale; // FWD: BN scale (K); BWD: previous layer's BN scale (K), nullable
+  const float* shift; // FWD: BN shift (K), nullable
+  int relu;
+  float* out;         // FWD: (B,S,S,K) or pooled (B,S/2,S/2,K); BWD: (B,S,S,K) masked grad, nullable
+  uint8_t* out_argmax;
+  const float* act;   // BWD: the activation the gradient belongs to, (B,S,S,K)
+  float* taylor;      // BWD: (R, B, K) slab, slot 0 written (+=), nullable
+  float* apoz;        // FWD / FWD_POOL: (B, K) counts of positive outputs (+=), nullable
+  int tay_mode;       // BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, float* lds_base, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)lds_base, 16, voff, soff, 0, 0);
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// one length-6 column / row of V = B^T d B, B^T rows: [4,0,-5,0,1,0] [0,-4,-4,1,1,0] [0,4,-4,-1,1,0]
+// [0,-2,-1,2,1,0] [0,2,-1,-2,1,0] [0,4,0,-5,0,1]
+__device__ __forceinline__ void bt6(float& a0, float& a1, float& a2, float& a3, float& a4, float& a5) {
+  const float s12 = a1 + a2, s34 = a3 + a4, d12 = a1 - a2, d43 = a4 - a3, d42 = a4 - a2, d31 = a3 - a1;
+  const float o0 = fmaf(4.f, a0, fmaf(-5.f, a2, a4));
+  const float o5 = fmaf(4.f, a1, fmaf(-5.f, a3, a5));
+  a0 = o0;
+  a1 = fmaf(-4.f, s12, s34);
+  a2 = fmaf(4.f, d12, d43);
+  a3 = fmaf(2.f, d31, d42);
+  a4 = fmaf(-2.f, d31, d42);
+  a5 = o5;
+}
+
+__device__ __forceinline__ void input_transform(float (&d)[36]) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) bt6(d[c], d[6 + c], d[12 + c], d[18 + c], d[24 + c], d[30 + c]);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) bt6(d[6 * r], d[6 * r + 1], d[6 * r + 2], d[6 * r + 3], d[6 * r + 4], d[6 * r + 5]);
+}
+
+// Y = A^T m A, A^T = [[1,1,1,1,1,0],[0,1,-1,2,-2,0],[0,1,1,4,4,0],[0,1,-1,8,-8,1]]
+__device__ __forceinline__ void at6(const float m0, const float m1, const float m2, const float m3, const float m4,
+                                    const float m5, float& y0, float& y1, float& y2, float& y3) {
+  const float a = m1 + m2, b = m1 - m2, c = m3 + m4, d = m3 - m4;
+  y0 = m0 + a + c;
+  y1 = fmaf(2.f, d, b);
+  y2 = fmaf(4.f, c, a);
+  y3 = fmaf(8.f, d, b) + m5;
+}
+
+__device__ __forceinline__ void output_transform(const float (&m)[36], float (&y)[16]) {
+  float t[24];  // 4 x 6
+#pragma unroll
+  for (int c = 0; c < 6; ++c)
+    at6(m[c], m[6 + c], m[12 + c], m[18 + c], m[24 + c], m[30 + c], t[c], t[6 + c], t[12 + c], t[18 + c]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    at6(t[6 * r], t[6 * r + 1], t[6 * r + 2], t[6 * r + 3], t[6 * r + 4], t[6 * r + 5], y[4 * r], y[4 * r + 1],
+        y[4 * r + 2], y[4 * r + 3]);
+}
+
+template <int EPI, int S>
+__device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[NPT], int blk_p, int k0, float* ya, float* yb,
+                                         float* part) {
+  constexpr int TPR = S / 4, TI = TPR * TPR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int t0 = blk_p * TILES;
+  const bool want_part = EPI == BWD ? p.taylor != nullptr : p.apoz != nullptr;
+
+  // ---- phase 1: output transform; park 32 tiles x 16 px x (16 + 16) channels in LDS -----------
+  {
+    float* ybuf = (wave >> 1) ? yb : ya;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tl = (wave & 1) * 16 + 4 * g + r;
+      float m[36], y[16];
+#pragma unroll
+      for (int x = 0; x < NPT; ++x) m[x] = acc[x][r];
+      output_transform(m, y);
+      float* dst = ybuf + tl * TPL + j;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dst[q * 16] = y[q];
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: coalesced traffic; 8 lanes cover one pixel's 32 channels (128 B) --------------
+  const int c4 = lane & 7;
+  const int k = k0 + 4 * c4;
+  const float* ysrc = (c4 < 4 ? ya : yb) + (c4 & 3) * 4;
+  f32x4 sc4 = {1.f, 1.f, 1.f, 1.f}, sh4 = {0.f, 0.f, 0.f, 0.f};
+  if (p.scale) sc4 = *reinterpret_cast<const f32x4*>(p.scale + k);
+  if (EPI != BWD && p.shift) sh4 = *reinterpret_cast<const f32x4*>(p.shift + k);
+  if constexpr (EPI == FWD_POOL) {
+    const int pp = (lane >> 3) & 3;  // pooled pixel (py, px) of the tile
+    const int py = pp >> 1, px = pp & 1;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int tl = wave * 8 + 2 * tt + (lane >> 5);
+      const int pt = t0 + tl;
+      f32x4 cnt = {0.f, 0.f, 0.f, 0.f};
+      if (pt < p.P) {
+        f32x4 best = {0.f, 0.f, 0.f, 0.f};
+        unsigned arg = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int q = (2 * py + (w >> 1)) * 4 + 2 * px + (w & 1);
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = yv[e] * sc4[e] + sh4[e];
+            if (p.relu) v = nan_relu(v);
+            cnt[e] += v > 0.f ? 1.f : 0.f;
+            if (w == 0 || v > best[e] || (v != v && best[e] == best[e])) {
+              best[e] = v;
+              arg = (arg & ~(0xffu << (8 * e))) | ((unsigned)w << (8 * e));
+            }
+          }
+        }
+        const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
+        const long long o = (((long long)b * (S / 2) + 2 * tr + py) * (S / 2) + 2 * tc + px) * p.K + k;
+        *reinterpret_cast<f32x4*>(p.out + o) = best;
+        *reinterpret_cast<unsigned*>(p.out_argmax + o) = arg;
+      }
+      if (want_part) {  // per-(tile, channel) count over the 4 pooled pixels (lanes ^8, ^16)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          cnt[e] += __shfl_xor(cnt[e], 8);
+          cnt[e] += __shfl_xor(cnt[e], 16);
+        }
+        if (pp == 0) *reinterpret_cast<f32x4*>(part + tl * TK + 4 * c4) = cnt;
+      }
+    }
+  } else {
+    const int qq = lane >> 3;  // pixels qq and qq + 8 of the tile
+#pragma unroll 2
+    for (int tt = 0; tt < 8; ++tt) {
+      const int tl = wave * 8 + tt;
+      const int pt = t0 + tl;
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      if (pt < p.P) {
+        const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int q = qq + 8 * h2;
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
+          const long long pix = ((long long)b * S + 4 * tr + (q >> 2)) * S + 4 * tc + (q & 3);
+          if constexpr (EPI == FWD) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = yv[e] * sc4[e] + sh4[e];
+              if (p.relu) v[e] = nan_relu(v[e]);
+              sum[e] += v[e] > 0.f ? 1.f : 0.f;
+            }
+            *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+          } else {  // BWD
+            const f32x4 a = *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sum[e] += p.tay_mode ? fabsf(yv[e]) : -(yv[e] * a[e]);
+            if (p.out) {
+              f32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = a[e] > 0.f ? yv[e] * sc4[e] : 0.f;
+              *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+            }
+          }
+        }
+      }
+      if (want_part) {  // per-(tile, channel) sum over the 16 pixels: lanes ^8, ^16, ^32 (fixed order)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sum[e] += __shfl_xor(sum[e], 8);
+          sum[e] += __shfl_xor(sum[e], 16);
+          sum[e] += __shfl_xor(sum[e], 32);
+        }
+        if (qq == 0) *reinterpret_cast<f32x4*>(part + tl * TK + 4 * c4) = sum;
+      }
+    }
+  }
+  if (!want_part) return;
+  __syncthreads();
+  // ---- per-(image, channel) sums over the block's tiles of the image, fixed order ------------
+  // S <= 16: whole images per block, one writer per sum. S = 32: two blocks per image (halves):
+  // Taylor partials go to slot (half) of the (R, B, K) slab (single writer per slot); APoZ counts
+  // are exact integers, so their float atomic adds are order-independent.
+  constexpr int NI = Geo<S>::NI;
+  constexpr int TIB = TI < TILES ? TI : TILES;  // tiles of one image in this block
+  const int b0 = t0 / TI;
+  for (int t = tid; t < NI * TK; t += 256) {
+    const int il = t / TK, kk = t - il * TK;
+    const int b = b0 + il;
+    if (b >= p.B) continue;
+    float s = 0.f;
+    for (int ti = 0; ti < TIB; ++ti) s += part[(il * TIB + ti) * TK + kk];
+    if constexpr (EPI == BWD) {
+      const int slot = S == 32 ? (blk_p & 1) : 0;
+      p.taylor[((long long)slot * p.B + b) * p.K + k0 + kk] += s;
+    } else if constexpr (S == 32) {
+      if (s > 0.f) atomicAdd(p.apoz + (long long)b * p.K + k0 + kk, s);
+    } else {
+      p.apoz[(long long)b * p.K + k0 + kk] += s;
+    }
+  }
+}
+
+template <int EPI, int S>
+__global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
+  using G = Geo<S>;
+  constexpr int TPR = S / 4, TI = TPR * TPR;
+  constexpr int PL = plane_slots<S>();
+  constexpr int XR = x_rounds<S>();
+  // separate objects per buffer: the compiler's LDS-DMA alias tracking tells them apart
+  __shared__ __attribute__((aligned(16))) float us0[U_IMG];
+  __shared__ __attribute__((aligned(16))) float us1[U_IMG];
+  __shared__ __attribute__((aligned(16))) float xs0[XR * 1024];
+  __shared__ __attribute__((aligned(16))) float xs1[XR * 1024];
+  static_assert(TILES * TPL <= U_IMG, "epilogue tile buffer must fit a U buffer");
+  static_assert(TILES * TK <= XR * 1024, "partial-sum buffer must fit an X buffer");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int n_k = p.K / TK;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = tile % n_k, k0 = kb * TK;
+  const int blk_p = tile / n_k;
+  const int t0 = blk_p * TILES;
+  const int b0 = t0 / TI;
+  const int nh = wave >> 1;  // output-channel half of this wave
+
+  const __amdgpu_buffer_rsrc_t urs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, (int)((long long)(p.C / 8) * n_k * U_IMG * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)(p.x_elems * 4), 0x00020000);
+
+  // this lane's tile (MFMA row j) and its patch's first slot in a plane of the staged region
+  const int tib = (wave & 1) * 16 + j;
+  const int il = tib / TI, ti = tib - il * TI, tr = ti / TPR, tc = ti - tr * TPR;
+  const int sbase = S == 4 ? il * G::IP : il * G::IP + 4 * tr * G::RWP + 5 * tc;
+  const int poff = ((g >> 1) * PL + sbase) * 4 + (g & 1) * 2;  // float offset: plane g/2, channels 2g, 2g+1
+
+  // DMA source byte offsets (channel 0 of a chunk) of this thread's slot in each round
+  unsigned xsrc[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int slot = i * 256 + tid;
+    const int h = slot / PL, s = slot - h * PL;
+    const int im = s / G::IP, rem = s - im * G::IP;
+    int xx, yy;
+    bool ok;
+    if constexpr (S == 4) {
+      yy = rem / 4;
+      xx = rem - yy * 4;
+      ok = rem < 16;
+    } else {
+      const int row = rem / G::RWP, colp = rem - row * G::RWP;
+      const int blk5 = colp / 5, w5 = colp - blk5 * 5;
+      xx = 4 * blk5 + w5 - 1;
+      yy = row - 1 + (S == 32 ? 16 * (blk_p & 1) : 0);  // S = 32: the block is one image half
+      ok = w5 != 4 && row < G::RH && xx >= 0 && xx < S && yy >= 0 && yy < S;
+    }
+    const int b = b0 + im;
+    ok = ok && h < 2 && im < G::NI && b < p.B;
+    xsrc[i] = ok ? (unsigned)(((((long long)b * S + yy) * S + xx) * p.C + 4 * h) * 4) : OOB;
+  }
+
+  auto stage = [&](int c0, float* ud, float* xd) {
+    const unsigned ub = (unsigned)(((c0 >> 3) * n_k + kb) * U_IMG) * 4u;
+#pragma unroll
+    for (int i = 0; i < U_ROUNDS; ++i) dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ub);
+#pragma unroll
+    for (int i = 0; i < XR; ++i) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
+  };
+
+  // the lane's 6x6 patch of channels (2g, 2g+1) -> V = B^T d B of both
+  auto load_transform = [&](const float* xb, float (&v0)[36], float (&v1)[36]) {
+    const float* p0 = xb + poff;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        float2 d = {0.f, 0.f};
+        if constexpr (S == 4) {
+          if (r >= 1 && r <= 4 && q >= 1 && q <= 4) d = *reinterpret_cast<const float2*>(p0 + ((r - 1) * 4 + (q - 1)) * 4);
+        } else {
+          d = *reinterpret_cast<const float2*>(p0 + (r * G::RWP + q + (q >= 4 ? 1 : 0)) * 4);
+        }
+        v0[r * 6 + q] = d.x;
+        v1[r * 6 + q] = d.y;
+      }
+    input_transform(v0);
+    input_transform(v1);
+  };
+
+  f32x4 acc[NPT];
+#pragma unroll
+  for (int x = 0; x < NPT; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // B operands of lane (j, g): U[x][c = 2g + e][k = 16 nh + j], e = 0, 1 as one float2 (g slot
+  // XOR-swizzled by j >> 3: conflict-free ds_read_b64)
+  const int uoff = nh * 128 + j * 8 + 2 * (g ^ ((j >> 3) << 1));
+
+  auto mfmas = [&](const float* ub, const float (&v0)[36], const float (&v1)[36], auto x0c, auto x1c) {
+    constexpr int X0 = decltype(x0c)::value, X1 = decltype(x1c)::value;
+    const float* ul = ub + uoff;
+#pragma unroll
+    for (int x = X0; x < X1; x += 2) {
+      const float2 wa = *reinterpret_cast<const float2*>(ul + x * 256);
+      const float2 wb = *reinterpret_cast<const float2*>(ul + (x + 1) * 256);
+      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x], wa.x, acc[x], 0, 0, 0);
+      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x + 1], wb.x, acc[x + 1], 0, 0, 0);
+      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x], wa.y, acc[x], 0, 0, 0);
+      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x + 1], wb.y, acc[x + 1], 0, 0, 0);
+    }
+  };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, NPT / 2>;
+  using H2 = std::integral_constant<int, NPT>;
+
+  // one chunk: MFMAs of chunk c (va0/va1, U in ub) with the next chunk's staging and transform
+  // overlapped (un / xn: the other buffers; vn0 / vn1 receive V of chunk c + 1)
+  auto chunk = [&](int c0, const float* ub, float* un, float* xn, const float (&va0)[36], const float (&va1)[36],
+                   float (&vn0)[36], float (&vn1)[36], bool more) {
+    __syncthreads();  // chunk c-1 is done everywhere: un / xn are free
+    if (more) stage(c0 + 8, un, xn);
+    mfmas(ub, va0, va1, H0{}, H1{});
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // every wave's part of the next chunk has landed
+      load_transform(xn, vn0, vn1);
+    }
+    mfmas(ub, va0, va1, H1{}, H2{});
+  };
+
+  const int nc = p.C / 8;
+  float a0[36], a1[36], b0v[36], b1v[36];
+  stage(0, us0, xs0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  load_transform(xs0, a0, a1);
+  for (int c = 0; c < nc; c += 2) {
+    chunk(8 * c, us0, us1, xs1, a0, a1, b0v, b1v, c + 1 < nc);
+    if (c + 1 < nc) chunk(8 * (c + 1), us1, us0, xs0, b0v, b1v, a0, a1, c + 2 < nc);
+  }
+  __syncthreads();  // the main loop's LDS reads are done: reuse us0/us1 (outputs), xs0 (partials)
+  epilogue<EPI, S>(p, acc, blk_p, k0, us0, us1, xs0);
+}
+
+// U = G g G^T into the LDS images: word ((x*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + e of image
+// (cb, kb) holds U[x][c = 8cb + 2g + e][k = 32kb + 16nh + j]. fp64, rounded once. flip_t: the
+// data-gradient operand (w'[k][c] = w[c][k], taps rotated 180 degrees).
+__global__ __launch_bounds__(256) void weight_transform(const float* __restrict__ w, float* __restrict__ u, int K, int C,
+                                                        int flip_t, int S0, int S1) {
+  const double Gm[6][3] = {{0.25, 0.0, 0.0},
+                           {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                           {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                           {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                           {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                           {0.0, 0.0, 1.0}};
+  const long long total = (long long)(C / 8) * (K / TK) * U_IMG;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int word = (int)(t % U_IMG);
+    const long long img = t / U_IMG;
+    const int kb = (int)(img % (K / TK)), cb = (int)(img / (K / TK));
+    const int e = word & 1, gs = (word >> 1) & 3, j = (word >> 3) & 15, nh = (word >> 7) & 1, x = word >> 8;
+    const int g = gs ^ ((j >> 3) << 1);
+    const int c = 8 * cb + 2 * g + e, k = TK * kb + 16 * nh + j;
+    const int i = x / 6, jj = x % 6;
+    const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
+    double acc = 0.0;
+    if (r0 < S0 && r1 < S1) {
+      const float* src = w + ((long long)r0 * S1 + r1) * 9;
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+          const int tap = flip_t ? (2 - a) * 3 + (2 - b) : a * 3 + b;
+          acc += Gm[i][a] * (double)src[tap] * Gm[jj][b];
+        }
+    }
+    u[t] = (float)acc;
+  }
+}
+
+}  // namespace w4
+}  // namespace tp
+
+// U images of a 3x3 weight for wino4: (C/8, K/32, 9216) floats. w: (S0, S1, 3, 3) = the forward
+// weight (Cout, Cin, 3, 3), possibly narrower than the padded GEMM; flip_t as tp_wino_weights2.
+extern "C" hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1,
+                                       hipStream_t st) {
+  if (K % 32 || C % 8 || K <= 0 || C <= 0 || S0 <= 0 || S1 <= 0) return hipErrorInvalidValue;
+  if (flip_t ? (S0 > C || S1 > K) : (S0 > K || S1 > C)) return hipErrorInvalidValue;
+  const long long total = (long long)(C / 8) * (K / 32) * tp::w4::U_IMG;
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
+  tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1);
+  return hipGetLastError();
+}
+
+extern "C" int tp_wino4_u_img() { return tp::w4::U_IMG; }
+
+extern "C" int tp_wino4_ok(int H, int W, int C, int K) {
+  return H == W && (H == 4 || H == 8 || H == 16 || H == 32) && C % 8 == 0 && C >= 8 && K % 32 == 0 && K >= 32;
+}
+
+// F(4x4,3x3) conv, S x S maps. epi: 0 fwd (BN affine + ReLU), 1 fwd + 2x2 max-pool (+ argmax),
+// 2 dgrad epilogue (x = output gradient, act / scale / taylor as conv_wino). apoz (fwd) and taylor
+// (dgrad, slot 0 of the (R, B, K) slab) are summed per (image, channel) with one writer each (+=).
+extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi,
+                                    const float* scale, const float* shift, int relu, float* out, uint8_t* out_argmax,
+                                    const float* act, float* taylor, float* apoz, int tay_mode, hipStream_t st) {
+  using namespace tp::w4;
+  if (!tp_wino4_ok(S, S, C, K) || B <= 0) return hipErrorInvalidValue;
+  if (epi < 0 || epi > 2 || (epi == BWD && !act) || (epi != BWD && !out) || (epi == FWD_POOL && !out_argmax))
+    return hipErrorInvalidValue;
+  Args a{};
+  a.x = x;
+  a.u = u;
+  a.B = B;
+  a.C = C;
+  a.K = K;
+  const int tpr = S / 4;
+  a.P = B * tpr * tpr;
+  a.x_elems = (long long)B * S * S * C;
+  if (a.x_elems * 4 >= (1ll << 31) || (long long)(C / 8) * (K / 32) * U_IMG * 4 >= (1ll << 31))
+    return hipErrorInvalidValue;
+  if (epi == BWD && (long long)B * S * S * K * 4 >= (1ll << 31)) return hipErrorInvalidValue;
+  a.scale = scale;
+  a.shift = shift;
+  a.relu = relu;
+  a.out = out;
+  a.out_argmax = out_argmax;
+  a.act = act;
+  a.taylor = epi == BWD ? taylor : nullptr;
+  a.apoz = epi == BWD ? nullptr : apoz;
+  a.tay_mode = tay_mode;
+  const int n_p = (a.P + TILES - 1) / TILES, n_k = K / TK;
+  const dim3 grid(n_p * n_k);
+#define TP_W4(E, SS) wino4_f4x3<E, SS><<<grid, 256, 0, st>>>(a)
+#define TP_W4S(E)                   \
+  do {                              \
+    if (S == 32) TP_W4(E, 32);      \
+    else if (S == 16) TP_W4(E, 16); \
+    else if (S == 8) TP_W4(E, 8);   \
+    else TP_W4(E, 4);               \
+  } while (0)
+  if (epi == FWD) TP_W4S(FWD);
+  else if (epi == FWD_POOL) TP_W4S(FWD_POOL);
+  else TP_W4S(BWD);
+#undef TP_W4S
+#undef TP_W4
+  return hipGetLastError();
+}
+
+// static LDS bytes of a wino4 instantiation (occupancy / budget guard)
+extern "C" int tp_wino4_lds_bytes(int S) {
+  using namespace tp::w4;
+  const void* f = S == 32 ? (const void*)wino4_f4x3<BWD, 32>
+                  : S == 16 ? (const void*)wino4_f4x3<BWD, 16>
+                  : S == 8 ? (const void*)wino4_f4x3<BWD, 8>
+                           : (const void*)wino4_f4x3<BWD, 4>;
+  hipFuncAttributes at{};
+  if (hipFuncGetAttributes(&at, f) != hipSuccess) return -1;
+  return (int)at.sharedSizeBytes;
+}

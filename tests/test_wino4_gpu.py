@@ -1,0 +1,110 @@
+"""Winograd F(4x4,3x3) kernels (csrc/kernels/wino4.hip) against fp64 PyTorch references:
+forward with BN affine + ReLU (+ 2x2 max-pool / argmax, APoZ counts) and the data gradient with
+the ReLU-mask / BN-scale output and the Taylor / Sensitivity partials, on the 4/8/16/32-pixel
+maps of VGG16-CIFAR, with ragged batches (partial last blocks) and odd channel paddings."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(32, 16, 32, 3), (32, 64, 64, 2), (16, 64, 128, 3), (16, 128, 96, 1), (8, 128, 256, 5), (8, 24, 32, 2),
+          (4, 256, 512, 3), (4, 64, 32, 37)]
+
+
+def _ops():
+    from torchpruner_amd import ops
+    return ops.require()
+
+
+def _fwd_ref(x, w, sc, sh):
+    y = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), padding=1)
+    y = y * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1)
+    return torch.relu(y).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("S,C,K,B", SHAPES)
+def test_wino4_forward(cuda, S, C, K, B):
+    T = _ops()
+    g = torch.Generator(device=cuda).manual_seed(S * 1000 + C + K)
+    x = torch.randn(B, S, S, C, device=cuda, generator=g)
+    w = torch.randn(K, C, 3, 3, device=cuda, generator=g) / (3 * C ** 0.5)
+    sc = torch.rand(K, device=cuda, generator=g) + 0.5
+    sh = torch.randn(K, device=cuda, generator=g) * 0.1
+    u = T.wino4_weights(w, False, 0, 0)
+    apoz = torch.zeros(B, K, device=cuda)
+    y, _ = T.conv_wino4_fwd(x, u, sc, sh, True, False, apoz)
+    ref = _fwd_ref(x, w, sc, sh)
+    err = ((y.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-5, err
+    cnt = (ref > 0).sum((1, 2)).float()
+    assert (apoz - cnt).abs().max().item() <= max(2.0, 1e-3 * S * S), (apoz - cnt).abs().max()
+    # pooled epilogue
+    apoz2 = torch.zeros(B, K, device=cuda)
+    yp, am = T.conv_wino4_fwd(x, u, sc, sh, True, True, apoz2)
+    r4 = ref.permute(0, 3, 1, 2)
+    pooled, idx = F.max_pool2d(r4, 2, return_indices=True)
+    errp = ((yp.double() - pooled.permute(0, 2, 3, 1)).abs().max() / pooled.abs().max()).item()
+    assert errp < 2e-5, errp
+    # argmax byte = (dy << 1) | dx of the window; compare where the window max is unique enough
+    H2 = S // 2
+    ii = idx.permute(0, 2, 3, 1)
+    dy = (ii // S) % 2
+    dx = (ii % S) % 2
+    want = (dy * 2 + dx).to(torch.uint8)
+    top2 = r4.unfold(2, 2, 2).unfold(3, 2, 2).reshape(B, K, H2, H2, 4).sort(-1).values
+    clear = ((top2[..., 3] - top2[..., 2]) > 1e-4 * pooled.abs().max()).permute(0, 2, 3, 1) & (pooled.permute(0, 2, 3, 1) > 0)
+    assert torch.equal((am & 3)[clear], want[clear])
+    assert (apoz2 - cnt).abs().max().item() <= max(2.0, 1e-3 * S * S)
+
+
+@pytest.mark.parametrize("S,C,K,B", SHAPES)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_wino4_dgrad(cuda, S, C, K, B, mode):
+    """dgrad of conv(Cin=K -> Cout=C): g (B,S,S,C) -> dL/dact (B,S,S,K) with the W_BWD epilogue."""
+    T = _ops()
+    Cout, Cin = C, K
+    gen = torch.Generator(device=cuda).manual_seed(S * 7 + C * 3 + K)
+    w = torch.randn(Cout, Cin, 3, 3, device=cuda, generator=gen) / (3 * Cin ** 0.5)
+    go = torch.randn(B, S, S, Cout, device=cuda, generator=gen)
+    act = torch.relu(torch.randn(B, S, S, Cin, device=cuda, generator=gen))
+    sc = torch.rand(Cin, device=cuda, generator=gen) + 0.5
+    ut = T.wino4_weights(w, True, 0, 0)
+    R = 2
+    tay = torch.zeros(R, B, Cin, device=cuda)
+    out = T.conv_wino4_dgrad(go, ut, act, sc, tay, True, mode)
+    dx = torch.nn.grad.conv2d_input((B, Cin, S, S), w.double(), go.double().permute(0, 3, 1, 2), padding=1)
+    dx = dx.permute(0, 2, 3, 1)
+    ref_out = torch.where(act.double() > 0, dx * sc.double(), torch.zeros((), dtype=torch.float64, device=cuda))
+    err = ((out.double() - ref_out).abs().max() / ref_out.abs().max()).item()
+    assert err < 2e-5, err
+    part = dx.abs() if mode else -(dx * act.double())
+    ref_t = part.sum((1, 2))
+    got_t = tay.double().sum(0)
+    errt = ((got_t - ref_t).abs().max() / ref_t.abs().max()).item()
+    assert errt < 2e-5, errt
+    if S != 32:
+        assert tay[1].abs().max().item() == 0.0  # whole images per block: slot 0 only
+
+
+def test_wino4_deterministic_and_lds_budget(cuda):
+    T = _ops()
+    x = torch.randn(7, 16, 16, 64, device=cuda)
+    w = torch.randn(128, 64, 3, 3, device=cuda) * 0.05
+    u = T.wino4_weights(w, False, 0, 0)
+    a1, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None)
+    a2, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None)
+    assert torch.equal(a1, a2)
+    for S in (4, 8, 16, 32):
+        assert 0 < T.wino4_lds_bytes(S) <= 160 * 1024
+
+
+def test_wino4_rejects_bad_shapes(cuda):
+    T = _ops()
+    w = torch.randn(32, 8, 3, 3, device=cuda)
+    u = T.wino4_weights(w, False, 0, 0)
+    with pytest.raises(RuntimeError):
+        T.conv_wino4_fwd(torch.randn(2, 12, 12, 8, device=cuda), u, None, None, True, False, None)
+    with pytest.raises(RuntimeError):
+        T.conv_wino4_fwd(torch.randn(2, 16, 8, 8, device=cuda), u, None, None, True, False, None)
