@@ -28,6 +28,8 @@
 // reduction), well inside the engine's fp64-oracle tolerances.
 #include "tp_common.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace tp {
@@ -70,6 +72,8 @@ struct Args {
   float* taylor;      // BWD: (R, B, K) slab, slot 0 written (+=), nullable
   float* apoz;        // FWD / FWD_POOL: (B, K) counts of positive outputs (+=), nullable
   int tay_mode;       // BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
+  int dbg;            // phase-cost experiments only (TP_W4_DBG; results are WRONG when set): 1 no U DMA,
+                      // 2 no X DMA, 4 no transform, 8 no MFMAs, 16 no epilogue
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -331,10 +335,14 @@ __global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
     xsrc[i] = ok ? (unsigned)(((((long long)b * S + yy) * S + xx) * p.C + 4 * h) * 4) : OOB;
   }
 
-  auto stage = [&](int c0, float* ud, float* xd) {
+  auto stage_u = [&](int c0, float* ud) {
+    if (p.dbg & 1) return;
     const unsigned ub = (unsigned)(((c0 >> 3) * n_k + kb) * U_IMG) * 4u;
 #pragma unroll
     for (int i = 0; i < U_ROUNDS; ++i) dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ub);
+  };
+  auto stage_x = [&](int c0, float* xd) {
+    if (p.dbg & 2) return;
 #pragma unroll
     for (int i = 0; i < XR; ++i) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
   };
@@ -355,10 +363,12 @@ __global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
         v0[r * 6 + q] = d.x;
         v1[r * 6 + q] = d.y;
       }
+    if (p.dbg & 4) return;
     input_transform(v0);
     input_transform(v1);
   };
 
+  const int nc = p.C / 8;
   f32x4 acc[NPT];
 #pragma unroll
   for (int x = 0; x < NPT; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -369,6 +379,7 @@ __global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
 
   auto mfmas = [&](const float* ub, const float (&v0)[36], const float (&v1)[36], auto x0c, auto x1c) {
     constexpr int X0 = decltype(x0c)::value, X1 = decltype(x1c)::value;
+    if (p.dbg & 8) return;
     const float* ul = ub + uoff;
 #pragma unroll
     for (int x = X0; x < X1; x += 2) {
@@ -384,32 +395,48 @@ __global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
   using H1 = std::integral_constant<int, NPT / 2>;
   using H2 = std::integral_constant<int, NPT>;
 
-  // one chunk: MFMAs of chunk c (va0/va1, U in ub) with the next chunk's staging and transform
-  // overlapped (un / xn: the other buffers; vn0 / vn1 receive V of chunk c + 1)
-  auto chunk = [&](int c0, const float* ub, float* un, float* xn, const float (&va0)[36], const float (&va1)[36],
-                   float (&vn0)[36], float (&vn1)[36], bool more) {
-    __syncthreads();  // chunk c-1 is done everywhere: un / xn are free
-    if (more) stage(c0 + 8, un, xn);
+  // One chunk c: MFMAs of chunk c (va, U(c) in ub) with the next chunk's patch read + transform
+  // under its second half. DMA lead: U(c+1) is issued at the top of chunk c (its buffer held U(c-1),
+  // free after the top barrier) and needed at the top of c+1; X(c+1) is issued in the middle of
+  // chunk c-1 (its buffer held X(c-1), read one chunk earlier) and read in the middle of chunk c:
+  // both have a full chunk of MFMAs to land. The counted waits rely on the issue order
+  // ... X(c+1) [mid c-1], U(c+1) [top c], X(c+2) [mid c] ... (vmcnt retires in order).
+  auto chunk = [&](int c, const float* ub, float* un, float* xn, float* xf, const float (&va0)[36],
+                   const float (&va1)[36], float (&vn0)[36], float (&vn1)[36]) {
+    const bool more = c + 1 < nc, more2 = c + 2 < nc;
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XR) : "memory");  // U(c) landed, X(c+1) may fly
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's U(c) landed; chunk c-1 is done everywhere (un is free)
+    if (more) stage_u(8 * (c + 1), un);
     mfmas(ub, va0, va1, H0{}, H1{});
     if (more) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // every wave's part of the next chunk has landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U_ROUNDS) : "memory");  // X(c+1) landed, U(c+1) may fly
+      __syncthreads();  // every wave's part of X(c+1) has landed
+      if (more2) stage_x(8 * (c + 2), xf);  // xf held X(c), read by every wave before the top barrier
       load_transform(xn, vn0, vn1);
     }
     mfmas(ub, va0, va1, H1{}, H2{});
   };
 
-  const int nc = p.C / 8;
   float a0[36], a1[36], b0v[36], b1v[36];
-  stage(0, us0, xs0);
+  stage_u(0, us0);
+  stage_x(0, xs0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   load_transform(xs0, a0, a1);
+  if (nc > 1) stage_x(8, xs1);
   for (int c = 0; c < nc; c += 2) {
-    chunk(8 * c, us0, us1, xs1, a0, a1, b0v, b1v, c + 1 < nc);
-    if (c + 1 < nc) chunk(8 * (c + 1), us1, us0, xs0, b0v, b1v, a0, a1, c + 2 < nc);
+    chunk(c, us0, us1, xs1, xs0, a0, a1, b0v, b1v);
+    if (c + 1 < nc) chunk(c + 1, us1, us0, xs0, xs1, b0v, b1v, a0, a1);
   }
   __syncthreads();  // the main loop's LDS reads are done: reuse us0/us1 (outputs), xs0 (partials)
+  if (p.dbg & 16) {
+    float t = 0.f;
+#pragma unroll
+    for (int x = 0; x < NPT; ++x) t += acc[x][0] + a0[x] + a1[x];
+    if (t == 1234.5f) p.out[0] = t;  // keeps the main loop alive
+    return;
+  }
   epilogue<EPI, S>(p, acc, blk_p, k0, us0, us1, xs0);
 }
 
@@ -499,6 +526,13 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   a.taylor = epi == BWD ? taylor : nullptr;
   a.apoz = epi == BWD ? nullptr : apoz;
   a.tay_mode = tay_mode;
+  static const int dbg = [] {
+    const char* d = getenv("TP_W4_DBG");
+    const int v = d ? atoi(d) : 0;
+    if (v) fprintf(stderr, "[tpamd] WARNING: TP_W4_DBG=%d: F(4x4) results are WRONG (phase-cost experiment)\n", v);
+    return v;
+  }();
+  a.dbg = dbg;
   const int n_p = (a.P + TILES - 1) / TILES, n_k = K / TK;
   const dim3 grid(n_p * n_k);
 #define TP_W4(E, SS) wino4_f4x3<E, SS><<<grid, 256, 0, st>>>(a)

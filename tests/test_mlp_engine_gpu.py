@@ -199,5 +199,5 @@ def test_mlp_engine_rejects_per_token_input(cuda):
         mc = copy.deepcopy(m).double()
         ref = M(mc, [(a.double(), b) for a, b in zip(x.split(4), y.split(4))], crit, torch.device("cpu")).run(
             mc[0], find_best_evaluation_module=True)
-        assert got.shape == (16,)
+        assert got.shape == ref.shape == (3,)  # units along dim 1 (T), as the reference's hooks reduce
         np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-6)

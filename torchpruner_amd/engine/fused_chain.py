@@ -47,6 +47,8 @@ WINO = -1  # pseudo tile cfg: fused Winograd F(2x2,3x3) kernel (winograd.hip), d
 WINO_LDS = -2  # the same with the block input region staged through LDS
 WINO_UNP = -3  # dgrad of a pooled layer: explicit vectorised unpool, then the staged kernel on the
                # dense full-resolution gradient (vs rebuilding it from pooled cells per chunk)
+WINO4 = -4  # Winograd F(4x4,3x3) kernel (wino4.hip): square 4/8/16/32-pixel maps, 1.78x fewer MFMAs
+            # than F(2x2); dgrads of pooled layers take the explicit unpool first
 
 # Winograd F(2x2,3x3) weight transform G g G^T
 _G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
@@ -89,6 +91,10 @@ def taylor_slots(H: int, W: int) -> int:
 
 def _wino_ok(H, W, C, K):
     return H % 2 == 0 and W % 2 == 0 and C % 8 == 0 and K % 32 == 0
+
+
+def _wino4_ok(H, W, C, K):
+    return H == W and H in (4, 8, 16, 32) and C % 8 == 0 and K % 32 == 0
 
 
 def _wino_splits(P, K, C):
@@ -394,7 +400,8 @@ class FusedChainEngine:
             w = F.pad(w, (0, 0, 0, 0, 0, (cin_p - w.shape[1]) if cin_p is not None else 0, 0, wp))
             scale, shift = F.pad(scale, (0, wp)), F.pad(shift, (0, wp))
             cin_p, cout = b.width, b.width
-            entry = {"scale": scale.contiguous(), "shift": shift.contiguous(), "pool": b.pool is not None}
+            entry = {"scale": scale.contiguous(), "shift": shift.contiguous(), "pool": b.pool is not None,
+                     "w4d": w.contiguous()}
             if b.first:
                 entry["w_first"] = w.contiguous()
                 entry["w_first_t"] = w.permute(1, 2, 3, 0).contiguous()  # tap-major VALU operand, packed once
@@ -456,6 +463,16 @@ class FusedChainEngine:
                                lambda c, s_, e=e, xf=xf: self._first_run(T, e, xf, c, s_), cands=cands)
         return self._first_run(T, e, xf, cfg, sp, apoz)
 
+    @staticmethod
+    def _u4(e, dgrad=False):
+        """F(4x4,3x3) U images of the entry's weight (forward, or the flipped/transposed data-gradient
+        operand), built on first use and cached in the packed entry."""
+        key = "ut4" if dgrad else "u4"
+        u = e.get(key)
+        if u is None:
+            u = e[key] = ops.require().wino4_weights(e["w4d"], dgrad, 0, 0)
+        return u
+
     # A 3x3/pad-1 conv on a 2x2 image is a dense GEMM: every output pixel q sees input pixel p
     # through tap (p - q + 1): y(B, 4K) = x(B, 4C) @ Wbig^T with Wbig (4K, 4C) — the same 2.25x
     # fewer multiplies as Winograd, on the implicit-GEMM kernel (ks=1) with no transforms.
@@ -480,6 +497,8 @@ class FusedChainEngine:
 
     def _conv_run(self, T, e, h, cfg, sp, apoz=None):
         """``apoz``: (B, N) buffer that receives the counts of positive (pre-pool) outputs."""
+        if cfg == WINO4:
+            return T.conv_wino4_fwd(h, self._u4(e), e["scale"], e["shift"], True, e["pool"], apoz)
         if cfg in (WINO, WINO_LDS):
             return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS, apoz)
         if cfg >= self.DENSE:
@@ -502,12 +521,18 @@ class FusedChainEngine:
         if H == 2 and W == 2 and C % 32 == 0:
             cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * N, 4 * C)] + \
                 TUNER.candidates(M, N, K, wino)
+        elif self.use_wino and _wino4_ok(H, W, C, N) and "w4d" in e:
+            cands = [(WINO4, 1)] + TUNER.candidates(M, N, K, wino)  # [0] = the untuned pick
         cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"], wino is not None), M, N, K,
                                lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino, cands=cands)
         return self._conv_run(T, e, h, cfg, sp, apoz)
 
     def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0):
         """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
+        if cfg == WINO4:
+            if am is not None:
+                g = T.unpool2_nhwc(g, am)
+            return T.conv_wino4_dgrad(g, self._u4(e, True), act, sc, taylor, want_out, tm)
         if cfg == WINO_UNP:
             return T.conv_wino_dgrad(T.unpool2_nhwc(g, am), None, e["ut"], act, sc, taylor, want_out, sp, True,
                                      tay_mode=tm)
@@ -831,6 +856,10 @@ class FusedChainEngine:
                 # [0] = the untuned pick: explicit unpool from 16x16 down (measured faster at
                 # B=2048 for the 16/8/4-pixel layers, slower at 32x32); bit-identical either way
                 cands = unp + wc if H <= 16 else wc + unp
+            if self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is None and wino is not None:
+                cands = TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
+            if self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is not None:
+                cands = [(WINO4, 1)] + cands  # [0] = the untuned pick
             cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None),
                                    M, Cin, e["wt"].shape[1],
                                    lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4:
