@@ -73,7 +73,7 @@ struct Args {
   float* apoz;        // FWD / FWD_POOL: (B, K) counts of positive outputs (+=), nullable
   int tay_mode;       // BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
   int dbg;            // phase-cost experiments only (TP_W4_DBG; results are WRONG when set): 1 no U DMA,
-                      // 2 no X DMA, 4 no transform, 8 no MFMAs, 16 no epilogue
+                      // 2 no X DMA, 16 no epilogue
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -107,6 +107,20 @@ __device__ __forceinline__ void input_transform(float (&d)[36]) {
   for (int c = 0; c < 6; ++c) bt6(d[c], d[6 + c], d[12 + c], d[18 + c], d[24 + c], d[30 + c]);
 #pragma unroll
   for (int r = 0; r < 6; ++r) bt6(d[6 * r], d[6 * r + 1], d[6 * r + 2], d[6 * r + 3], d[6 * r + 4], d[6 * r + 5]);
+}
+
+// step k (0..23) of V = B^T d B for two channels: k < 12 column passes (channel k / 6, column
+// k % 6), then row passes (channel (k - 12) / 6, row (k - 12) % 6); in this order every row pass
+// follows its channel's column passes.
+__device__ __forceinline__ void transform_step(float (&d0)[36], float (&d1)[36], int k) {
+  float(&d)[36] = (k < 12 ? (k < 6) : (k < 18)) ? d0 : d1;
+  if (k < 12) {
+    const int c = k % 6;
+    bt6(d[c], d[6 + c], d[12 + c], d[18 + c], d[24 + c], d[30 + c]);
+  } else {
+    const int r = (k - 12) % 6;
+    bt6(d[6 * r], d[6 * r + 1], d[6 * r + 2], d[6 * r + 3], d[6 * r + 4], d[6 * r + 5]);
+  }
 }
 
 // Y = A^T m A, A^T = [[1,1,1,1,1,0],[0,1,-1,2,-2,0],[0,1,1,4,4,0],[0,1,-1,8,-8,1]]
@@ -275,18 +289,24 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[NPT], int b
   }
 }
 
-template <int EPI, int S>
-__global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
+// MODE 0: one block per CU, U and X double-buffered, the next chunk's DMA and transform
+// software-pipelined under the current chunk's MFMAs (one wave per SIMD).
+// MODE 1: two blocks per CU (<= 80 KB of LDS each), single-buffered: each block stages, waits,
+// transforms and multiplies in turn, and the other block's waves fill the SIMDs meanwhile.
+template <int EPI, int S, int MODE>
+__global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
   using G = Geo<S>;
   constexpr int TPR = S / 4, TI = TPR * TPR;
   constexpr int PL = plane_slots<S>();
   constexpr int XR = x_rounds<S>();
+  constexpr int XB = MODE ? (XR > 9 ? XR : 9) * 1024 : XR * 1024;
   // separate objects per buffer: the compiler's LDS-DMA alias tracking tells them apart
   __shared__ __attribute__((aligned(16))) float us0[U_IMG];
-  __shared__ __attribute__((aligned(16))) float us1[U_IMG];
-  __shared__ __attribute__((aligned(16))) float xs0[XR * 1024];
-  __shared__ __attribute__((aligned(16))) float xs1[XR * 1024];
-  static_assert(TILES * TPL <= U_IMG, "epilogue tile buffer must fit a U buffer");
+  __shared__ __attribute__((aligned(16))) float us1[MODE ? 4 : U_IMG];
+  __shared__ __attribute__((aligned(16))) float xs0[XB];
+  __shared__ __attribute__((aligned(16))) float xs1[MODE ? 4 : XB];
+  __shared__ __attribute__((aligned(16))) float pts[MODE ? TILES * TK : 4];
+  static_assert(TILES * TPL <= U_IMG && TILES * TPL <= (MODE ? XB : U_IMG), "epilogue tile buffers");
   static_assert(TILES * TK <= XR * 1024, "partial-sum buffer must fit an X buffer");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -347,13 +367,15 @@ __global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
     for (int i = 0; i < XR; ++i) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
   };
 
-  // the lane's 6x6 patch of channels (2g, 2g+1) -> V = B^T d B of both
-  auto load_transform = [&](const float* xb, float (&v0)[36], float (&v1)[36]) {
+  // the lane's 6x6 patch of channels (2g, 2g+1) (raw; transformed in place by transform())
+  auto load_patch = [&](const float* xb, float (&v0)[36], float (&v1)[36]) {
     const float* p0 = xb + poff;
+    // column-major issue order: the first column transform can start after 6 reads (lgkmcnt
+    // retires in order)
 #pragma unroll
-    for (int r = 0; r < 6; ++r)
+    for (int q = 0; q < 6; ++q)
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
+      for (int r = 0; r < 6; ++r) {
         float2 d = {0.f, 0.f};
         if constexpr (S == 4) {
           if (r >= 1 && r <= 4 && q >= 1 && q <= 4) d = *reinterpret_cast<const float2*>(p0 + ((r - 1) * 4 + (q - 1)) * 4);
@@ -363,9 +385,6 @@ __global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
         v0[r * 6 + q] = d.x;
         v1[r * 6 + q] = d.y;
       }
-    if (p.dbg & 4) return;
-    input_transform(v0);
-    input_transform(v1);
   };
 
   const int nc = p.C / 8;
@@ -377,57 +396,104 @@ __global__ __launch_bounds__(256, 1) void wino4_f4x3(Args p) {
   // XOR-swizzled by j >> 3: conflict-free ds_read_b64)
   const int uoff = nh * 128 + j * 8 + 2 * (g ^ ((j >> 3) << 1));
 
-  auto mfmas = [&](const float* ub, const float (&v0)[36], const float (&v1)[36], auto x0c, auto x1c) {
-    constexpr int X0 = decltype(x0c)::value, X1 = decltype(x1c)::value;
-    if (p.dbg & 8) return;
-    const float* ul = ub + uoff;
-#pragma unroll
-    for (int x = X0; x < X1; x += 2) {
-      const float2 wa = *reinterpret_cast<const float2*>(ul + x * 256);
-      const float2 wb = *reinterpret_cast<const float2*>(ul + (x + 1) * 256);
-      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x], wa.x, acc[x], 0, 0, 0);
-      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x + 1], wb.x, acc[x + 1], 0, 0, 0);
-      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x], wa.y, acc[x], 0, 0, 0);
-      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x + 1], wb.y, acc[x + 1], 0, 0, 0);
-    }
-  };
-  using H0 = std::integral_constant<int, 0>;
-  using H1 = std::integral_constant<int, NPT / 2>;
-  using H2 = std::integral_constant<int, NPT>;
-
-  // One chunk c: MFMAs of chunk c (va, U(c) in ub) with the next chunk's patch read + transform
-  // under its second half. DMA lead: U(c+1) is issued at the top of chunk c (its buffer held U(c-1),
-  // free after the top barrier) and needed at the top of c+1; X(c+1) is issued in the middle of
-  // chunk c-1 (its buffer held X(c-1), read one chunk earlier) and read in the middle of chunk c:
-  // both have a full chunk of MFMAs to land. The counted waits rely on the issue order
-  // ... X(c+1) [mid c-1], U(c+1) [top c], X(c+2) [mid c] ... (vmcnt retires in order).
-  auto chunk = [&](int c, const float* ub, float* un, float* xn, float* xf, const float (&va0)[36],
+  // One chunk c, ONE barrier: on entry U(c) and X(c+1) (both issued at the top of chunk c-1) must
+  // have landed; after the barrier U(c+1) (into the buffer of U(c-1)) and X(c+2) (into the buffer
+  // of X(c), whose patches every wave read at the top of chunk c-1) are issued — a full chunk of
+  // lead each — and the next patch is read. The 72 MFMAs of chunk c are then interleaved with
+  // the transform of chunk c+1 (in-order issue: one wave per SIMD hides the VALU work only if
+  // it sits between the MFMAs, so the schedule is pinned with sched_group_barrier).
+  auto chunk = [&](int c, const float* ub, float* un, const float* xn, float* xf, const float (&va0)[36],
                    const float (&va1)[36], float (&vn0)[36], float (&vn1)[36]) {
-    const bool more = c + 1 < nc, more2 = c + 2 < nc;
-    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XR) : "memory");  // U(c) landed, X(c+1) may fly
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave's U(c) landed; chunk c-1 is done everywhere (un is free)
-    if (more) stage_u(8 * (c + 1), un);
-    mfmas(ub, va0, va1, H0{}, H1{});
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U_ROUNDS) : "memory");  // X(c+1) landed, U(c+1) may fly
-      __syncthreads();  // every wave's part of X(c+1) has landed
-      if (more2) stage_x(8 * (c + 2), xf);  // xf held X(c), read by every wave before the top barrier
-      load_transform(xn, vn0, vn1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (c + 1 < nc) stage_u(8 * (c + 1), un);
+    if (c + 2 < nc) stage_x(8 * (c + 2), xf);
+    // 18 steps of 4 MFMAs (points 2i, 2i+1 x both channel halves). Steps 0-8 only run MFMAs (the
+    // current V dies as they go); step 8 issues the next patch's 36 reads (column-major), steps
+    // 10-17 run its 24 length-6 transforms (12 column passes, then 12 row passes), 3 per step.
+    // This keeps the live set at ~36 current + 72 next V registers (accumulators in AGPRs), and
+    // one sched_barrier per step pins the interleave: the wave is alone on its SIMD, so VALU work
+    // only hides between its own MFMAs. (The last chunk reads and transforms a stale patch:
+    // harmless, keeps the schedule uniform.)
+    const float* ul = ub + uoff;
+    float2 wq[2][2];  // B operands of two point pairs ahead
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      wq[s2][0] = *reinterpret_cast<const float2*>(ul + (2 * s2) * 256);
+      wq[s2][1] = *reinterpret_cast<const float2*>(ul + (2 * s2 + 1) * 256);
     }
-    mfmas(ub, va0, va1, H1{}, H2{});
+#pragma unroll
+    for (int i = 0; i < NPT / 2; ++i) {
+      const int x = 2 * i;
+      const float2 wa = wq[i & 1][0], wb = wq[i & 1][1];
+      if (i + 2 < NPT / 2) {
+        wq[i & 1][0] = *reinterpret_cast<const float2*>(ul + (x + 4) * 256);
+        wq[i & 1][1] = *reinterpret_cast<const float2*>(ul + (x + 5) * 256);
+      }
+      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(va0[x], wa.x, acc[x], 0, 0, 0);
+      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(va0[x + 1], wb.x, acc[x + 1], 0, 0, 0);
+      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(va1[x], wa.y, acc[x], 0, 0, 0);
+      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(va1[x + 1], wb.y, acc[x + 1], 0, 0, 0);
+      if (i == 8) load_patch(xn, vn0, vn1);
+      constexpr int T0 = 10;  // first transform step
+      const int k_lo = i < T0 ? 0 : (i - T0) * 3, k_hi = i < T0 ? 0 : (i - T0 + 1) * 3;
+#pragma unroll
+      for (int k = k_lo; k < k_hi; ++k) transform_step(vn0, vn1, k);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
 
+  if constexpr (MODE == 1) {
+    float v0[36], v1[36];
+    for (int c = 0; c < nc; ++c) {
+      __syncthreads();  // the previous chunk's patch and U reads are done: the buffers are free
+      stage_u(8 * c, us0);
+      stage_x(8 * c, xs0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      load_patch(xs0, v0, v1);
+      input_transform(v0);
+      input_transform(v1);
+      const float* ul = us0 + uoff;
+#pragma unroll
+      for (int x = 0; x < NPT; x += 2) {
+        const float2 wa = *reinterpret_cast<const float2*>(ul + x * 256);
+        const float2 wb = *reinterpret_cast<const float2*>(ul + (x + 1) * 256);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x], wa.x, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x + 1], wb.x, acc[x + 1], 0, 0, 0);
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x], wa.y, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x + 1], wb.y, acc[x + 1], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (p.dbg & 16) {
+      float t = 0.f;
+#pragma unroll
+      for (int x = 0; x < NPT; ++x) t += acc[x][0];
+      if (t == 1234.5f) p.out[0] = t;
+      return;
+    }
+    epilogue<EPI, S>(p, acc, blk_p, k0, us0, xs0, pts);
+    return;
+  }
   float a0[36], a1[36], b0v[36], b1v[36];
+  // prologue: U(0), X(0), X(1) in flight; V(0) formed before the loop
   stage_u(0, us0);
   stage_x(0, xs0);
+  if (nc > 1) stage_x(8, xs1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  load_transform(xs0, a0, a1);
-  if (nc > 1) stage_x(8, xs1);
-  for (int c = 0; c < nc; c += 2) {
-    chunk(c, us0, us1, xs1, xs0, a0, a1, b0v, b1v);
-    if (c + 1 < nc) chunk(c + 1, us1, us0, xs0, xs1, b0v, b1v, a0, a1);
+  load_patch(xs0, a0, a1);
+  input_transform(a0);
+  input_transform(a1);
+  for (int c = 0; c < nc; ++c) {
+    const bool odd = c & 1;
+    chunk(c, odd ? us1 : us0, odd ? us0 : us1, odd ? xs0 : xs1, odd ? xs1 : xs0, a0, a1, b0v, b1v);
+#pragma unroll
+    for (int t = 0; t < 36; ++t) {
+      a0[t] = b0v[t];
+      a1[t] = b1v[t];
+    }
   }
   __syncthreads();  // the main loop's LDS reads are done: reuse us0/us1 (outputs), xs0 (partials)
   if (p.dbg & 16) {
@@ -535,7 +601,15 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   a.dbg = dbg;
   const int n_p = (a.P + TILES - 1) / TILES, n_k = K / TK;
   const dim3 grid(n_p * n_k);
-#define TP_W4(E, SS) wino4_f4x3<E, SS><<<grid, 256, 0, st>>>(a)
+  static const int mode = [] {  // TP_W4_MODE=1: two-blocks-per-CU single-buffered variant (experiments)
+    const char* m = getenv("TP_W4_MODE");
+    return m ? atoi(m) : 0;
+  }();
+#define TP_W4(E, SS)                                         \
+  do {                                                       \
+    if (mode == 1) wino4_f4x3<E, SS, 1><<<grid, 256, 0, st>>>(a); \
+    else wino4_f4x3<E, SS, 0><<<grid, 256, 0, st>>>(a);          \
+  } while (0)
 #define TP_W4S(E)                   \
   do {                              \
     if (S == 32) TP_W4(E, 32);      \
@@ -554,10 +628,10 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 // static LDS bytes of a wino4 instantiation (occupancy / budget guard)
 extern "C" int tp_wino4_lds_bytes(int S) {
   using namespace tp::w4;
-  const void* f = S == 32 ? (const void*)wino4_f4x3<BWD, 32>
-                  : S == 16 ? (const void*)wino4_f4x3<BWD, 16>
-                  : S == 8 ? (const void*)wino4_f4x3<BWD, 8>
-                           : (const void*)wino4_f4x3<BWD, 4>;
+  const void* f = S == 32 ? (const void*)wino4_f4x3<BWD, 32, 0>
+                  : S == 16 ? (const void*)wino4_f4x3<BWD, 16, 0>
+                  : S == 8 ? (const void*)wino4_f4x3<BWD, 8, 0>
+                           : (const void*)wino4_f4x3<BWD, 4, 0>;
   hipFuncAttributes at{};
   if (hipFuncGetAttributes(&at, f) != hipSuccess) return -1;
   return (int)at.sharedSizeBytes;
