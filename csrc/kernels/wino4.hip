@@ -144,144 +144,154 @@ __device__ __forceinline__ void output_transform(const float (&m)[36], float (&y
         y[4 * r + 2], y[4 * r + 3]);
 }
 
-template <int EPI, int S>
-__device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[NPT], int blk_p, int k0, float* ya, float* yb,
+// Epilogue of a block of NW waves = NW/2 groups of 16 tiles x 2 output halves of 16 channels:
+// outputs staged in LDS per half of 32 tiles (ya: channels 0-15, yb: 16-31), then coalesced
+// 128-B traffic; ``part`` receives per-(tile, channel) partial sums (TB x 32 floats).
+template <int EPI, int S, int NW>
+__device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[NPT], int t0, int k0, float* ya, float* yb,
                                          float* part) {
   constexpr int TPR = S / 4, TI = TPR * TPR;
+  constexpr int GROUPS = NW / 2, TB = 16 * GROUPS, HALVES = TB / 32, TPW = 32 / NW;  // tiles per wave (phase 2)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int t0 = blk_p * TILES;
+  const int grp = wave % GROUPS, nh = wave / GROUPS;
   const bool want_part = EPI == BWD ? p.taylor != nullptr : p.apoz != nullptr;
-
-  // ---- phase 1: output transform; park 32 tiles x 16 px x (16 + 16) channels in LDS -----------
-  {
-    float* ybuf = (wave >> 1) ? yb : ya;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int tl = (wave & 1) * 16 + 4 * g + r;
-      float m[36], y[16];
-#pragma unroll
-      for (int x = 0; x < NPT; ++x) m[x] = acc[x][r];
-      output_transform(m, y);
-      float* dst = ybuf + tl * TPL + j;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) dst[q * 16] = y[q];
-    }
-  }
-  __syncthreads();
-  // ---- phase 2: coalesced traffic; 8 lanes cover one pixel's 32 channels (128 B) --------------
   const int c4 = lane & 7;
   const int k = k0 + 4 * c4;
   const float* ysrc = (c4 < 4 ? ya : yb) + (c4 & 3) * 4;
   f32x4 sc4 = {1.f, 1.f, 1.f, 1.f}, sh4 = {0.f, 0.f, 0.f, 0.f};
   if (p.scale) sc4 = *reinterpret_cast<const f32x4*>(p.scale + k);
   if (EPI != BWD && p.shift) sh4 = *reinterpret_cast<const f32x4*>(p.shift + k);
-  if constexpr (EPI == FWD_POOL) {
-    const int pp = (lane >> 3) & 3;  // pooled pixel (py, px) of the tile
-    const int py = pp >> 1, px = pp & 1;
+
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      const int tl = wave * 8 + 2 * tt + (lane >> 5);
-      const int pt = t0 + tl;
-      f32x4 cnt = {0.f, 0.f, 0.f, 0.f};
-      if (pt < p.P) {
-        f32x4 best = {0.f, 0.f, 0.f, 0.f};
-        unsigned arg = 0;
+  for (int hf = 0; hf < HALVES; ++hf) {
+    // ---- phase 1: output transform; park this half's 32 tiles x 16 px x (16 + 16) ch -------
+    if (grp / 2 == hf) {
+      float* ybuf = nh ? yb : ya;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int q = (2 * py + (w >> 1)) * 4 + 2 * px + (w & 1);
-          const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
+      for (int r = 0; r < 4; ++r) {
+        const int tl = (grp & 1) * 16 + 4 * g + r;
+        float m[36], y[16];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float v = yv[e] * sc4[e] + sh4[e];
-            if (p.relu) v = nan_relu(v);
-            cnt[e] += v > 0.f ? 1.f : 0.f;
-            if (w == 0 || v > best[e] || (v != v && best[e] == best[e])) {
-              best[e] = v;
-              arg = (arg & ~(0xffu << (8 * e))) | ((unsigned)w << (8 * e));
-            }
-          }
-        }
-        const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
-        const long long o = (((long long)b * (S / 2) + 2 * tr + py) * (S / 2) + 2 * tc + px) * p.K + k;
-        *reinterpret_cast<f32x4*>(p.out + o) = best;
-        *reinterpret_cast<unsigned*>(p.out_argmax + o) = arg;
-      }
-      if (want_part) {  // per-(tile, channel) count over the 4 pooled pixels (lanes ^8, ^16)
+        for (int x = 0; x < NPT; ++x) m[x] = acc[x][r];
+        output_transform(m, y);
+        float* dst = ybuf + tl * TPL + j;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          cnt[e] += __shfl_xor(cnt[e], 8);
-          cnt[e] += __shfl_xor(cnt[e], 16);
-        }
-        if (pp == 0) *reinterpret_cast<f32x4*>(part + tl * TK + 4 * c4) = cnt;
+        for (int q = 0; q < 16; ++q) dst[q * 16] = y[q];
       }
     }
-  } else {
-    const int qq = lane >> 3;  // pixels qq and qq + 8 of the tile
-#pragma unroll 2
-    for (int tt = 0; tt < 8; ++tt) {
-      const int tl = wave * 8 + tt;
-      const int pt = t0 + tl;
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-      if (pt < p.P) {
-        const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
+    __syncthreads();
+    // ---- phase 2: coalesced traffic; 8 lanes cover one pixel's 32 channels (128 B) ----------
+    if constexpr (EPI == FWD_POOL) {
+      const int pp = (lane >> 3) & 3;  // pooled pixel (py, px) of the tile
+      const int py = pp >> 1, px = pp & 1;
 #pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const int q = qq + 8 * h2;
-          const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
-          const long long pix = ((long long)b * S + 4 * tr + (q >> 2)) * S + 4 * tc + (q & 3);
-          if constexpr (EPI == FWD) {
-            f32x4 v;
+      for (int tt = 0; tt < TPW / 2; ++tt) {
+        const int tl = wave * TPW + 2 * tt + (lane >> 5);
+        const int tb = hf * 32 + tl;
+        const int pt = t0 + tb;
+        f32x4 cnt = {0.f, 0.f, 0.f, 0.f};
+        if (pt < p.P) {
+          f32x4 best = {0.f, 0.f, 0.f, 0.f};
+          unsigned arg = 0;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const int q = (2 * py + (w >> 1)) * 4 + 2 * px + (w & 1);
+            const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              v[e] = yv[e] * sc4[e] + sh4[e];
-              if (p.relu) v[e] = nan_relu(v[e]);
-              sum[e] += v[e] > 0.f ? 1.f : 0.f;
+              float v = yv[e] * sc4[e] + sh4[e];
+              if (p.relu) v = nan_relu(v);
+              cnt[e] += v > 0.f ? 1.f : 0.f;
+              if (w == 0 || v > best[e] || (v != v && best[e] == best[e])) {
+                best[e] = v;
+                arg = (arg & ~(0xffu << (8 * e))) | ((unsigned)w << (8 * e));
+              }
             }
-            *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
-          } else {  // BWD
-            const f32x4 a = *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k);
+          }
+          const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
+          const long long o = (((long long)b * (S / 2) + 2 * tr + py) * (S / 2) + 2 * tc + px) * p.K + k;
+          *reinterpret_cast<f32x4*>(p.out + o) = best;
+          *reinterpret_cast<unsigned*>(p.out_argmax + o) = arg;
+        }
+        if (want_part) {  // per-(tile, channel) count over the 4 pooled pixels (lanes ^8, ^16)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) sum[e] += p.tay_mode ? fabsf(yv[e]) : -(yv[e] * a[e]);
-            if (p.out) {
+          for (int e = 0; e < 4; ++e) {
+            cnt[e] += __shfl_xor(cnt[e], 8);
+            cnt[e] += __shfl_xor(cnt[e], 16);
+          }
+          if (pp == 0) *reinterpret_cast<f32x4*>(part + tb * TK + 4 * c4) = cnt;
+        }
+      }
+    } else {
+      const int qq = lane >> 3;  // pixels qq and qq + 8 of the tile
+#pragma unroll 2
+      for (int tt = 0; tt < TPW; ++tt) {
+        const int tl = wave * TPW + tt;
+        const int tb = hf * 32 + tl;
+        const int pt = t0 + tb;
+        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+        if (pt < p.P) {
+          const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int q = qq + 8 * h2;
+            const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
+            const long long pix = ((long long)b * S + 4 * tr + (q >> 2)) * S + 4 * tc + (q & 3);
+            if constexpr (EPI == FWD) {
               f32x4 v;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = a[e] > 0.f ? yv[e] * sc4[e] : 0.f;
+              for (int e = 0; e < 4; ++e) {
+                v[e] = yv[e] * sc4[e] + sh4[e];
+                if (p.relu) v[e] = nan_relu(v[e]);
+                sum[e] += v[e] > 0.f ? 1.f : 0.f;
+              }
               *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+            } else {  // BWD
+              const f32x4 a = *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) sum[e] += p.tay_mode ? fabsf(yv[e]) : -(yv[e] * a[e]);
+              if (p.out) {
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = a[e] > 0.f ? yv[e] * sc4[e] : 0.f;
+                *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+              }
             }
           }
         }
-      }
-      if (want_part) {  // per-(tile, channel) sum over the 16 pixels: lanes ^8, ^16, ^32 (fixed order)
+        if (want_part) {  // per-(tile, channel) sum over the 16 pixels: lanes ^8, ^16, ^32 (fixed order)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          sum[e] += __shfl_xor(sum[e], 8);
-          sum[e] += __shfl_xor(sum[e], 16);
-          sum[e] += __shfl_xor(sum[e], 32);
+          for (int e = 0; e < 4; ++e) {
+            sum[e] += __shfl_xor(sum[e], 8);
+            sum[e] += __shfl_xor(sum[e], 16);
+            sum[e] += __shfl_xor(sum[e], 32);
+          }
+          if (qq == 0) *reinterpret_cast<f32x4*>(part + tb * TK + 4 * c4) = sum;
         }
-        if (qq == 0) *reinterpret_cast<f32x4*>(part + tl * TK + 4 * c4) = sum;
       }
     }
+    __syncthreads();  // ya / yb are rewritten by the next half
   }
   if (!want_part) return;
-  __syncthreads();
   // ---- per-(image, channel) sums over the block's tiles of the image, fixed order ------------
-  // S <= 16: whole images per block, one writer per sum. S = 32: two blocks per image (halves):
+  // Whole images per block: one writer per sum. A block of half an image (S = 32, 32 tiles):
   // Taylor partials go to slot (half) of the (R, B, K) slab (single writer per slot); APoZ counts
   // are exact integers, so their float atomic adds are order-independent.
-  constexpr int NI = Geo<S>::NI;
-  constexpr int TIB = TI < TILES ? TI : TILES;  // tiles of one image in this block
+  constexpr int TIB = TI < TB ? TI : TB;  // tiles of one image in this block
+  constexpr int NIB = TB / TIB;           // images in this block
   const int b0 = t0 / TI;
-  for (int t = tid; t < NI * TK; t += 256) {
+  for (int t = tid; t < NIB * TK; t += 64 * NW) {
     const int il = t / TK, kk = t - il * TK;
     const int b = b0 + il;
     if (b >= p.B) continue;
     float s = 0.f;
     for (int ti = 0; ti < TIB; ++ti) s += part[(il * TIB + ti) * TK + kk];
+    constexpr bool split_img = TI > TB;
     if constexpr (EPI == BWD) {
-      const int slot = S == 32 ? (blk_p & 1) : 0;
+      const int slot = split_img ? (t0 / TB) % (TI / TB) : 0;
       p.taylor[((long long)slot * p.B + b) * p.K + k0 + kk] += s;
-    } else if constexpr (S == 32) {
+    } else if constexpr (split_img) {
       if (s > 0.f) atomicAdd(p.apoz + (long long)b * p.K + k0 + kk, s);
     } else {
       p.apoz[(long long)b * p.K + k0 + kk] += s;
@@ -384,6 +394,10 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
         }
         v0[r * 6 + q] = d.x;
         v1[r * 6 + q] = d.y;
+        // keep every read a single ds_read_b64: a merged ds_read2_b64 is banked in 16-lane groups
+        // mod 32 banks, where the 16 tiles of a wave can only cover 8 bank quads (2-way conflicts);
+        // the layout is conflict-free for ds_read_b64's 32-lane groups mod 64 banks
+        __builtin_amdgcn_sched_barrier(0);
       }
   };
 
@@ -420,7 +434,9 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       wq[s2][0] = *reinterpret_cast<const float2*>(ul + (2 * s2) * 256);
+      __builtin_amdgcn_sched_barrier(0);
       wq[s2][1] = *reinterpret_cast<const float2*>(ul + (2 * s2 + 1) * 256);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int i = 0; i < NPT / 2; ++i) {
@@ -428,6 +444,7 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
       const float2 wa = wq[i & 1][0], wb = wq[i & 1][1];
       if (i + 2 < NPT / 2) {
         wq[i & 1][0] = *reinterpret_cast<const float2*>(ul + (x + 4) * 256);
+        __builtin_amdgcn_sched_barrier(0);  // two ds_read_b64, not one ds_read2st64_b64
         wq[i & 1][1] = *reinterpret_cast<const float2*>(ul + (x + 5) * 256);
       }
       acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(va0[x], wa.x, acc[x], 0, 0, 0);
@@ -455,14 +472,24 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
       input_transform(v0);
       input_transform(v1);
       const float* ul = us0 + uoff;
+      // B operands one point pair ahead, each read its own ds_read_b64 (see load_patch)
+      float2 qa = *reinterpret_cast<const float2*>(ul);
+      __builtin_amdgcn_sched_barrier(0);
+      float2 qb = *reinterpret_cast<const float2*>(ul + 256);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int x = 0; x < NPT; x += 2) {
-        const float2 wa = *reinterpret_cast<const float2*>(ul + x * 256);
-        const float2 wb = *reinterpret_cast<const float2*>(ul + (x + 1) * 256);
+        const float2 wa = qa, wb = qb;
+        if (x + 2 < NPT) {
+          qa = *reinterpret_cast<const float2*>(ul + (x + 2) * 256);
+          __builtin_amdgcn_sched_barrier(0);
+          qb = *reinterpret_cast<const float2*>(ul + (x + 3) * 256);
+        }
         acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x], wa.x, acc[x], 0, 0, 0);
         acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x + 1], wb.x, acc[x + 1], 0, 0, 0);
         acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x], wa.y, acc[x], 0, 0, 0);
         acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x + 1], wb.y, acc[x + 1], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     __syncthreads();
@@ -473,7 +500,7 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
       if (t == 1234.5f) p.out[0] = t;
       return;
     }
-    epilogue<EPI, S>(p, acc, blk_p, k0, us0, xs0, pts);
+    epilogue<EPI, S, 4>(p, acc, t0, k0, us0, xs0, pts);
     return;
   }
   float a0[36], a1[36], b0v[36], b1v[36];
@@ -503,7 +530,7 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
     if (t == 1234.5f) p.out[0] = t;  // keeps the main loop alive
     return;
   }
-  epilogue<EPI, S>(p, acc, blk_p, k0, us0, us1, xs0);
+  epilogue<EPI, S, 4>(p, acc, t0, k0, us0, us1, xs0);
 }
 
 // U = G g G^T into the LDS images: word ((x*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + e of image
