@@ -56,6 +56,18 @@ template <> struct Geo<16> { static constexpr int NI = 2, RH = 18, RWP = 23, IP 
 template <> struct Geo<8> { static constexpr int NI = 8, RH = 10, RWP = 14, IP = 146; };
 template <> struct Geo<4> { static constexpr int NI = 32, RH = 4, RWP = 4, IP = 17; };
 template <int S> constexpr int plane_slots() { return Geo<S>::NI * Geo<S>::IP; }
+// MODE 2 (64-tile blocks): S = 32 holds a whole image (34 rows); otherwise twice the images
+// Staged input geometry of a TB-tile block (MODE 2/3). PAD: a pad slot after every 4 columns
+// (col' = x' + x'/4) keeps the slot bases of the 16 tiles of a wave distinct mod 16 when a wave
+// spans tile rows of one image (S = 32, 16); S = 8 packs its 10 x 10 halo'd images densely
+// (IP = 101: 16 tiles = 4 images x 2 x 2 cover all 16 classes). S = 32, TB = 32: half an image.
+template <int S, int TB> struct GeoT;
+template <int TB> struct GeoT<32, TB> {
+  static constexpr int NI = 1, RH = TB / 2 + 2, RWP = 42, IP = (TB / 2 + 2) * 42, PAD = 1;
+};
+template <int TB> struct GeoT<16, TB> { static constexpr int NI = TB / 16, RH = 18, RWP = 23, IP = 18 * 23, PAD = 1; };
+template <int TB> struct GeoT<8, TB> { static constexpr int NI = TB / 4, RH = 10, RWP = 10, IP = 101, PAD = 0; };
+template <int TB> struct GeoT<4, TB> { static constexpr int NI = TB, RH = 4, RWP = 4, IP = 17, PAD = 0; };
 template <int S> constexpr int x_rounds() { return (2 * plane_slots<S>() + 255) / 256; }
 
 struct Args {
@@ -533,11 +545,252 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
   epilogue<EPI, S, 4>(p, acc, t0, k0, us0, us1, xs0);
 }
 
-// U = G g G^T into the LDS images: word ((x*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + e of image
-// (cb, kb) holds U[x][c = 8cb + 2g + e][k = 32kb + 16nh + j]. fp64, rounded once. flip_t: the
+
+// LDS DMA issued from inline asm: invisible to the compiler's wait-count tracking, which would
+// otherwise wait for every DMA in flight before any LDS read of a buffer it cannot tell apart
+// (runtime-selected double buffers). The caller owns the vmcnt waits. rsrc: raw 4-dword buffer
+// descriptor (base, stride 0, num_records, raw-buffer flags); lds: wave-uniform LDS byte address.
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4v raw_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  return i32x4v{(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
+}
+__device__ __forceinline__ unsigned lds_addr(const float* p) { return (unsigned)(size_t)(lds_ptr_t)p; }
+__device__ __forceinline__ void dma16_asm(const i32x4v& rs, unsigned lds, unsigned voff, unsigned soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(rs), "s"(soff)
+               : "memory", "m0");
+}
+
+__device__ __forceinline__ void lds_barrier() {  // LDS reads done + s_barrier, leaving DMA (vmcnt) in flight
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// MODE 2: one block of 8 waves per CU (two per SIMD) = 64 tiles x 32 outputs; wave w owns the 16
+// tiles of group (w & 3) x the 16 channels of half (w >> 2).
+//
+// Cost model (measured, scripts/micro/mfma_valu.hip): on gfx950 fp32 MFMAs and fp32 VALU work
+// share the SIMD's issue — VALU between MFMAs does not hide, not even across the two waves of a
+// SIMD — so the kernel minimises VALU instructions instead of interleaving them: the input
+// transform runs on packed pairs (v_pk_fma_f32 / v_pk_add_f32: both channels of a lane, one
+// instruction), the patch of a lane is read as float2 pairs (channels 2g, 2g+1; conflict-free
+// ds_read_b64), and the MFMA k of parity e is channel 2g + e. The U image uses layout 1 (one
+// float2 = points 2i, 2i+1 of one parity; parity 0 in the first half, parity 1 in the second).
+//
+// Per chunk c: top barrier (U0(c), X(c) landed) -> issue U1(c) -> read + transform the patch ->
+// 36 MFMAs of parity 0 -> barrier (U1(c) landed; U0 and X(c) free) -> issue U0(c+1), X(c+2) ->
+// 36 MFMAs of parity 1. X is double-buffered (1.5 chunks of lead), U single-buffered in halves
+// (half a chunk of lead). DMA is issued from inline asm; the waits are explicit.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void bt6p(f2v& a0, f2v& a1, f2v& a2, f2v& a3, f2v& a4, f2v& a5) {
+  const f2v s12 = a1 + a2, s34 = a3 + a4, d12 = a1 - a2, d43 = a4 - a3, d42 = a4 - a2, d31 = a3 - a1;
+  const f2v o0 = 4.f * a0 + (-5.f * a2 + a4);
+  const f2v o5 = 4.f * a1 + (-5.f * a3 + a5);
+  a0 = o0;
+  a1 = -4.f * s12 + s34;
+  a2 = 4.f * d12 + d43;
+  a3 = 2.f * d31 + d42;
+  a4 = -2.f * d31 + d42;
+  a5 = o5;
+}
+
+template <int EPI, int S, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
+  constexpr int TB = 8 * NW, NG = NW / 2;  // tiles per block, 16-tile groups
+  constexpr bool XDBL = NW == 8;           // X double-buffered (one block per CU)
+  using G = GeoT<S, TB>;
+  constexpr int TPR = S / 4, TI = TPR * TPR;
+  constexpr int PL = G::NI * G::IP;
+  constexpr int NXI = (2 * PL + 63) / 64;  // X DMA wave-instructions (64 16-B slots each)
+  constexpr int KX = (NXI + NW - 1) / NW;
+  constexpr int XN = (XDBL ? (NXI > 34 ? NXI : 34) : (NXI > 33 ? NXI : 33)) * 256;
+  __shared__ __attribute__((aligned(16))) float us[U_IMG];
+  __shared__ __attribute__((aligned(16))) float xs0[XN];
+  __shared__ __attribute__((aligned(16))) float xs1[XDBL ? XN : TB * TK];  // NW = 4: partial sums
+  static_assert(32 * TPL <= XN && TB * TK <= U_IMG && 32 * TPL <= U_IMG, "epilogue buffers");
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const int n_k = p.K / TK;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = tile % n_k, k0 = kb * TK;
+  const int blk_p = tile / n_k;
+  const int t0 = blk_p * TB;
+  const int b0 = t0 / TI;
+  const int grp = wave % NG, nh = wave / NG;
+
+  const i32x4v urs = raw_rsrc(p.u, (unsigned)((long long)(p.C / 8) * n_k * U_IMG * 4));
+  const i32x4v xrs = raw_rsrc(p.x, (unsigned)(p.x_elems * 4));
+
+  const int tib = grp * 16 + j;
+  const int il = tib / TI, ti = tib - il * TI, tr = ti / TPR, tc = ti - tr * TPR;
+  const int sbase = S == 4 ? il * G::IP : il * G::IP + 4 * tr * G::RWP + (G::PAD ? 5 : 4) * tc;
+  const int poff = ((g >> 1) * PL + sbase) * 4 + (g & 1) * 2;  // plane g/2, channels 2g, 2g+1
+
+  // X DMA sources, 16 bits per instruction: pixel index relative to the block's first image (11
+  // bits), plane (1), valid (1); the byte offset is rebuilt at issue (3 VALU) — half the registers
+  unsigned xcode[(KX + 1) / 2];
+#pragma unroll
+  for (int i = 0; i < (KX + 1) / 2; ++i) xcode[i] = 0u;
+#pragma unroll
+  for (int i = 0; i < KX; ++i) {
+    const int slot = (wave + NW * i) * 64 + lane;
+    const int h = slot / PL, s = slot - h * PL;
+    const int im = s / G::IP, rem = s - im * G::IP;
+    int xx, yy;
+    bool ok;
+    if constexpr (S == 4) {
+      yy = rem / 4;
+      xx = rem - yy * 4;
+      ok = rem < 16;
+    } else {
+      const int row = rem / G::RWP, colp = rem - row * G::RWP;
+      int w5 = 0;
+      if constexpr (G::PAD) {
+        const int blk5 = colp / 5;
+        w5 = colp - blk5 * 5;
+        xx = 4 * blk5 + w5 - 1;
+      } else {
+        xx = colp - 1;
+      }
+      yy = row - 1 + (S == 32 && TB == 32 ? 16 * (blk_p & 1) : 0);
+      ok = w5 != 4 && row < G::RH && xx >= 0 && xx < S && yy >= 0 && yy < S;
+    }
+    ok = ok && h < 2 && im < G::NI && b0 + im < p.B;
+    const unsigned code = ok ? (unsigned)((im * S + yy) * S + xx) | ((unsigned)h << 11) | 0x1000u : 0u;
+    xcode[i >> 1] |= code << (16 * (i & 1));
+  }
+  static_assert(G::NI * S * S <= 2048, "X pixel code");
+  const unsigned xbase = (unsigned)b0 * S * S * (unsigned)p.C * 4u;
+  const unsigned lane16 = (unsigned)lane * 16u;
+  const unsigned c4 = (unsigned)p.C * 4u;
+
+  // U half hf (18 point pairs = 18 wave-instructions) of chunk c0/8
+  auto stage_u = [&](int c0, int hf) {
+    if (p.dbg & 1) return;
+    const unsigned ub = (unsigned)(((c0 >> 3) * n_k + kb) * U_IMG) * 4u;
+#pragma unroll
+    for (int i = 0; i < (18 + NW - 1) / NW; ++i) {
+      const int pt = wave + NW * i;
+      if (pt < 18) {
+        const int q = hf * 18 + pt;
+        dma16_asm(urs, lds_addr(us + q * 256), lane16, ub + (unsigned)q * 1024u);  // point pair q: soffset
+      }
+    }
+  };
+  auto stage_x = [&](int c0, float* xd) {
+    if (p.dbg & 2) return;
+#pragma unroll
+    for (int i = 0; i < KX; ++i)
+      if (wave + NW * i < NXI) {
+        const unsigned code = xcode[i >> 1] >> (16 * (i & 1));
+        const unsigned off = (code & 0x1000u) ? xbase + (code & 0x7ffu) * c4 + ((code >> 7) & 16u) : OOB;
+        dma16_asm(xrs, lds_addr(xd + (wave + NW * i) * 256), off, (unsigned)c0 * 4u);
+      }
+  };
+
+  const int nc = p.C / 8;
+  f32x4 acc[NPT];
+#pragma unroll
+  for (int x = 0; x < NPT; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* ul = us + nh * 128 + j * 8 + 2 * (g ^ ((j >> 3) << 1));
+  const bool full_x = (NXI - wave + NW - 1) / NW == KX;  // this wave issues KX (else KX - 1) X DMAs
+  // Wait until at most this wave's X DMAs of one chunk (issued last) are in flight
+  auto wait_but_x = [&]() {
+    if (full_x) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KX) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KX - 1) : "memory");
+  };
+
+  // prologue: X(0) (and X(1)), U0(0) in flight
+  stage_x(0, xs0);
+  if (XDBL && nc > 1) stage_x(8, xs1);
+  stage_u(0, 0);
+  for (int c = 0; c < nc; ++c) {
+    float* xb = (XDBL && (c & 1)) ? xs1 : xs0;  // X(c)
+    // top: U0(c) and X(c) landed everywhere (NW = 8: X(c+1), issued after U0(c), may still be in
+    // flight); every wave is done with U1(c-1)
+    if (XDBL && c + 1 < nc && c > 0) wait_but_x();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    stage_u(8 * c, 1);
+    f2v v[36];
+    {
+      const float* p0 = xb + poff;
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          f2v d = {0.f, 0.f};
+          if constexpr (S == 4) {
+            if (r >= 1 && r <= 4 && q >= 1 && q <= 4) d = *reinterpret_cast<const f2v*>(p0 + ((r - 1) * 4 + (q - 1)) * 4);
+          } else {
+            d = *reinterpret_cast<const f2v*>(p0 + (r * G::RWP + q + (G::PAD && q >= 4 ? 1 : 0)) * 4);
+          }
+          v[r * 6 + q] = d;
+          __builtin_amdgcn_sched_barrier(0);  // one ds_read_b64 each (no ds_read2 merging)
+        }
+    }
+    if constexpr (!XDBL) {  // every wave has its patch: X(c+1) into the single buffer
+      lds_barrier();
+      if (c + 1 < nc) stage_x(8 * (c + 1), xs0);
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) bt6p(v[q], v[6 + q], v[12 + q], v[18 + q], v[24 + q], v[30 + q]);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) bt6p(v[6 * r], v[6 * r + 1], v[6 * r + 2], v[6 * r + 3], v[6 * r + 4], v[6 * r + 5]);
+    float2 wq[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (e == 1) {
+        // U1(c) landed everywhere (NW = 4: X(c+1), issued after it, may still be in flight);
+        // every wave is done with U0(c) (and NW = 8: X(c))
+        if (!XDBL && c + 1 < nc) wait_but_x();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (c + 1 < nc) stage_u(8 * (c + 1), 0);
+        if (XDBL && c + 2 < nc) stage_x(8 * (c + 2), xb);
+      }
+      const float* ue = ul + e * 18 * 256;
+      wq[0] = *reinterpret_cast<const float2*>(ue);
+      __builtin_amdgcn_sched_barrier(0);
+      wq[1] = *reinterpret_cast<const float2*>(ue + 256);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 18; ++i) {
+        const float2 w = wq[i & 1];
+        if (i + 2 < 18) {
+          wq[i & 1] = *reinterpret_cast<const float2*>(ue + (i + 2) * 256);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const int x = 2 * i;
+        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(e ? v[x].y : v[x].x, w.x, acc[x], 0, 0, 0);
+        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(e ? v[x + 1].y : v[x + 1].x, w.y, acc[x + 1], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (p.dbg & 16) {
+    float t = 0.f;
+#pragma unroll
+    for (int x = 0; x < NPT; ++x) t += acc[x][0];
+    if (t == 1234.5f) p.out[0] = t;
+    return;
+  }
+  if constexpr (XDBL) epilogue<EPI, S, 8>(p, acc, t0, k0, xs0, xs1, us);
+  else epilogue<EPI, S, 4>(p, acc, t0, k0, us, xs0, xs1);
+}
+
+// U = G g G^T into the LDS images: layout 0 (MODE 0/1): word ((x*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + e
+// of image (cb, kb) holds U[x][c = 8cb + 2g + e][k = 32kb + 16nh + j]; layout 1 (MODE 2): word
+// (((e*18 + x/2)*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + (x & 1) holds U[x][c = 8cb + 2g + e][k]. fp64, rounded once. flip_t: the
 // data-gradient operand (w'[k][c] = w[c][k], taps rotated 180 degrees).
 __global__ __launch_bounds__(256) void weight_transform(const float* __restrict__ w, float* __restrict__ u, int K, int C,
-                                                        int flip_t, int S0, int S1) {
+                                                        int flip_t, int S0, int S1, int lay) {
   const double Gm[6][3] = {{0.25, 0.0, 0.0},
                            {-1.0 / 6, -1.0 / 6, -1.0 / 6},
                            {-1.0 / 6, 1.0 / 6, -1.0 / 6},
@@ -549,7 +802,8 @@ __global__ __launch_bounds__(256) void weight_transform(const float* __restrict_
     const int word = (int)(t % U_IMG);
     const long long img = t / U_IMG;
     const int kb = (int)(img % (K / TK)), cb = (int)(img / (K / TK));
-    const int e = word & 1, gs = (word >> 1) & 3, j = (word >> 3) & 15, nh = (word >> 7) & 1, x = word >> 8;
+    const int lo = word & 1, gs = (word >> 1) & 3, j = (word >> 3) & 15, nh = (word >> 7) & 1, hi = word >> 8;
+    const int e = lay ? hi / 18 : lo, x = lay ? 2 * (hi % 18) + lo : hi;
     const int g = gs ^ ((j >> 3) << 1);
     const int c = 8 * cb + 2 * g + e, k = TK * kb + 16 * nh + j;
     const int i = x / 6, jj = x % 6;
@@ -567,6 +821,17 @@ __global__ __launch_bounds__(256) void weight_transform(const float* __restrict_
   }
 }
 
+// TP_W4_MODE (read once): 0 pipelined 1 block/CU, 1 two blocks/CU, 2 packed transforms, 8 waves per
+// block, 3 (default) packed transforms, two 4-wave blocks per CU (the blocks' barriers are
+// independent, so one block's patch reads / transform run under the other's MFMAs: 1.3x MODE 2)
+static int kernel_mode() {
+  static const int mode = [] {
+    const char* m = getenv("TP_W4_MODE");
+    return m ? atoi(m) : 3;
+  }();
+  return mode;
+}
+
 }  // namespace w4
 }  // namespace tp
 
@@ -578,7 +843,7 @@ extern "C" hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, i
   if (flip_t ? (S0 > C || S1 > K) : (S0 > K || S1 > C)) return hipErrorInvalidValue;
   const long long total = (long long)(C / 8) * (K / 32) * tp::w4::U_IMG;
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
-  tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1);
+  tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1, tp::w4::kernel_mode() >= 2);
   return hipGetLastError();
 }
 
@@ -626,15 +891,15 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
     return v;
   }();
   a.dbg = dbg;
-  const int n_p = (a.P + TILES - 1) / TILES, n_k = K / TK;
+  const int mode = kernel_mode();
+  const int tb = mode == 2 ? 64 : TILES;  // MODE 3: 32-tile blocks
+  const int n_p = (a.P + tb - 1) / tb, n_k = K / TK;
   const dim3 grid(n_p * n_k);
-  static const int mode = [] {  // TP_W4_MODE=1: two-blocks-per-CU single-buffered variant (experiments)
-    const char* m = getenv("TP_W4_MODE");
-    return m ? atoi(m) : 0;
-  }();
-#define TP_W4(E, SS)                                         \
-  do {                                                       \
-    if (mode == 1) wino4_f4x3<E, SS, 1><<<grid, 256, 0, st>>>(a); \
+#define TP_W4(E, SS)                                              \
+  do {                                                            \
+    if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a);   \
+    else if (mode == 3) wino4_m2<E, SS, 4><<<grid, 256, 0, st>>>(a); \
+    else if (mode == 1) wino4_f4x3<E, SS, 1><<<grid, 256, 0, st>>>(a); \
     else wino4_f4x3<E, SS, 0><<<grid, 256, 0, st>>>(a);          \
   } while (0)
 #define TP_W4S(E)                   \
@@ -655,10 +920,16 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 // static LDS bytes of a wino4 instantiation (occupancy / budget guard)
 extern "C" int tp_wino4_lds_bytes(int S) {
   using namespace tp::w4;
-  const void* f = S == 32 ? (const void*)wino4_f4x3<BWD, 32, 0>
-                  : S == 16 ? (const void*)wino4_f4x3<BWD, 16, 0>
-                  : S == 8 ? (const void*)wino4_f4x3<BWD, 8, 0>
-                           : (const void*)wino4_f4x3<BWD, 4, 0>;
+  const int m = kernel_mode();
+  const void* f = nullptr;
+#define TP_W4F(SS)                                                                            \
+  f = m == 2 ? (const void*)wino4_m2<BWD, SS, 8>                                              \
+             : m == 3 ? (const void*)wino4_m2<BWD, SS, 4> : (const void*)wino4_f4x3<BWD, SS, 0>
+  if (S == 32) TP_W4F(32);
+  else if (S == 16) TP_W4F(16);
+  else if (S == 8) TP_W4F(8);
+  else TP_W4F(4);
+#undef TP_W4F
   hipFuncAttributes at{};
   if (hipFuncGetAttributes(&at, f) != hipSuccess) return -1;
   return (int)at.sharedSizeBytes;
