@@ -12,7 +12,8 @@ rank 0); (2) prune ``--frac`` of the lowest-scored channels of each (indices bro
 the pruner's multi-tensor gather.
 
     torchrun --nproc-per-node 8 experiments/prune_finetune.py --rounds 3 --frac 0.2
-    python experiments/prune_finetune.py --compare taylor,apoz,random --seeds 0,1,2 --modes 8 --noise 2.5
+    python experiments/prune_finetune.py --compare taylor,apoz,random --seeds 0,1,2 --classes 20 --modes 8 \
+        --noise 2.5 --teacher-target 0.85 --pretrain-steps 400 --rounds 3 --steps 15
 
 ``--compare``: for every seed one teacher is trained (``--pretrain-steps``), then EVERY method
 prunes a copy of that same teacher with the same budgets (rounds, fraction, finetune steps,
@@ -62,7 +63,12 @@ def parse():
     ap.add_argument("--modes", type=int, default=1, help="prototypes per class (task difficulty)")
     ap.add_argument("--noise", type=float, default=1.0)
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--pretrain-steps", type=int, default=60, help="SGD steps before the first prune")
+    ap.add_argument("--pretrain-steps", type=int, default=60, help="SGD steps before the first prune (max with "
+                                                                   "--teacher-target)")
+    ap.add_argument("--teacher-target", type=float, default=None,
+                    help="stop pretraining once val top-1 reaches this (checked every --check-every steps): an "
+                         "unsaturated teacher, so recovery and method differences stay measurable")
+    ap.add_argument("--check-every", type=int, default=20)
     ap.add_argument("--val-batches", type=int, default=4)
     ap.add_argument("--recal-batches", type=int, default=8,
                     help="BN running statistics re-estimated after each prune (same batches on every rank)")
@@ -151,7 +157,7 @@ def main():
     for m in methods:
         assert m in METRICS, f"unknown method {m}"
     seeds = [int(s) for s in args.seeds.split(",")]
-    all_rows = []
+    all_rows, teachers = [], []
     for seed in seeds:
         np.random.seed(seed)
         task = PrototypeTask((3, args.res, args.res), args.classes, noise=args.noise, seed=seed, device=dev,
@@ -159,12 +165,21 @@ def main():
         val = task.stream(args.val_batches * world, args.batch, seed=seed * 1000 + 999, channels_last=True)
         model, wrapper, opt, pruner = build(args, dev, seed)
         t0 = time.perf_counter()
-        pre_loss, _ = train(wrapper, dev, F.cross_entropy, task.stream(args.pretrain_steps * world, args.batch,
-                                                                       seed=seed * 1000 + 1, channels_last=True),
-                            opt, -1, log_every=0)
-        _, pre_top1 = test(model, dev, F.cross_entropy, val, verbose=0, shard=True)
-        emit({"seed": seed, "pretrain_steps": args.pretrain_steps, "train_loss": round(pre_loss, 4),
+        done, part = 0, 0
+        while done < args.pretrain_steps:
+            n = args.pretrain_steps - done if args.teacher_target is None else min(args.check_every,
+                                                                                   args.pretrain_steps - done)
+            pre_loss, _ = train(wrapper, dev, F.cross_entropy, task.stream(n * world, args.batch,
+                                                                           seed=seed * 1000 + 1 + 7 * part,
+                                                                           channels_last=True), opt, -1, log_every=0)
+            done += n
+            part += 1
+            _, pre_top1 = test(model, dev, F.cross_entropy, val, verbose=0, shard=True)
+            if args.teacher_target is not None and pre_top1 >= args.teacher_target:
+                break
+        emit({"seed": seed, "pretrain_steps": done, "train_loss": round(pre_loss, 4),
               "val_top1": round(pre_top1, 4), "params": count_parameters(model), "s": round(time.perf_counter() - t0, 1)})
+        teachers.append(round(pre_top1, 4))
         if len(methods) == 1:
             all_rows += prune_rounds(args, model, wrapper, opt, pruner, task, val, methods[0], seed, world, rank, emit)
             continue
@@ -191,8 +206,21 @@ def main():
                                   "after_finetune_mean": round(float(np.mean(ft)), 4),
                                   "after_finetune_std": round(float(np.std(ft)), 4)})
             summary[method] = per_round
-        emit({"summary": summary, "seeds": seeds, "rounds": args.rounds, "frac": args.frac, "steps": args.steps,
-              "world": world})
+        # separation of each method from random in units of the seeds' spread (per round, after prune)
+        sep = {}
+        if "random" in methods:
+            for method in methods:
+                if method == "random":
+                    continue
+                sep[method] = []
+                for r in range(args.rounds):
+                    a = [x["val_top1_after_prune"] for x in all_rows if x["method"] == method and x["round"] == r]
+                    b = [x["val_top1_after_prune"] for x in all_rows if x["method"] == "random" and x["round"] == r]
+                    spread = float(np.sqrt(np.var(a) + np.var(b))) or 1e-9
+                    sep[method].append(round((float(np.mean(a)) - float(np.mean(b))) / spread, 2))
+        emit({"summary": summary, "teacher_top1": teachers, "separation_vs_random_after_prune": sep, "seeds": seeds,
+              "rounds": args.rounds, "frac": args.frac, "steps": args.steps, "world": world,
+              "task": {"classes": args.classes, "modes": args.modes, "noise": args.noise, "res": args.res}})
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -31,6 +31,7 @@ def load(d):
 
 def main(marker, dirs):
     per = collections.defaultdict(lambda: collections.defaultdict(list))
+    extra = set()
     for d in dirs:
         names, cnt, dur = load(d)
         ids = sorted(names)
@@ -51,10 +52,11 @@ def main(marker, dirs):
                     per[k]["read_GBs"].append(c["FETCH_SIZE"] * 1024 / (us * 1e-6) / 1e9)
                 if "WRITE_SIZE" in c:
                     per[k]["write_GBs"].append(c["WRITE_SIZE"] * 1024 / (us * 1e-6) / 1e9)
-            for n in ("SQ_LDS_BANK_CONFLICT", "SQ_INSTS_LDS"):
-                if n in c:
+            for n in c:
+                if n not in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "FETCH_SIZE", "WRITE_SIZE"):
                     per[k][n].append(c[n])
-    cols = ["us", "mfma_util", "read_GBs", "write_GBs", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_LDS"]
+                    extra.add(n)
+    cols = ["us", "mfma_util", "read_GBs", "write_GBs"] + sorted(extra)
     print(f"{'kernel':72s} " + " ".join(f"{c[:12]:>12s}" for c in cols))
     for k, m in sorted(per.items(), key=lambda kv: -sum(kv[1].get("us", [0]))):
         vals = [(sum(m[c]) / len(m[c]) if m.get(c) else float("nan")) for c in cols]
