@@ -292,6 +292,27 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
     log(f"[bench] generic path (MIOpen/hipBLASLt, same one-pass run_many): {generic:.0f} img/s -> engine "
         f"x{value / generic:.2f} ({time.perf_counter() - t0:.1f}s)")
 
+    # 1b. opt-in bf16 operands on the same engine (never the headline): throughput, and per-layer
+    # rank agreement of the bf16 scores with the exact fp32 ones on the same batches
+    t0 = time.perf_counter()
+    TaylorAttributionMetric(model, loader(1, args.seed + 13, B), F.cross_entropy, dev,
+                            compute_dtype=torch.bfloat16).run_many(convs, find_best_evaluation_module=True)  # tune
+    bm = TaylorAttributionMetric(model, loader(args.steps, args.seed + 14, B), F.cross_entropy, dev,
+                                 compute_dtype=torch.bfloat16)
+    s_bf, bdt = timed_run(bm, convs)
+    assert bm.last_path["path"] == "fused", bm.last_path
+    s_fp = TaylorAttributionMetric(model, loader(args.steps, args.seed + 14, B), F.cross_entropy, dev).run_many(
+        convs, find_best_evaluation_module=True)
+    from scipy.stats import spearmanr
+    rho = [float(spearmanr(a, b).correlation) for a, b in zip(s_bf, s_fp)]
+    out["vgg_taylor_bf16_img_s"] = round(args.steps * B * world / bdt, 1)
+    out["bf16_vs_fp32_engine"] = round(out["vgg_taylor_bf16_img_s"] / value, 2)
+    out["bf16_score_spearman_min"] = round(min(rho), 5)
+    out["bf16_config"] = {"compute_dtype": "bfloat16 operands (3x3 convs), fp32 accumulation/activations, fp64 "
+                                           "score accumulators", "spearman_per_layer": [round(r, 5) for r in rho]}
+    log(f"[bench] opt-in bf16 engine: {out['vgg_taylor_bf16_img_s']:.0f} img/s (x{out['bf16_vs_fp32_engine']} "
+        f"fp32), min per-layer Spearman vs fp32 {min(rho):.4f} ({time.perf_counter() - t0:.1f}s)")
+
     # 2. config #3: ResNet-50, ImageNet shape, B=256 per GPU, every prunable bottleneck conv
     t0 = time.perf_counter()
     torch.manual_seed(0)

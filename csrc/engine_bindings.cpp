@@ -138,7 +138,8 @@ std::tuple<at::Tensor, at::Tensor> conv_fwd(const at::Tensor& x, const at::Tenso
   TORCH_CHECK(w.size(1) == ks * ks * Cin, "weight K mismatch: ", w.size(1), " vs ", ks * ks * Cin);
   TORCH_CHECK(Cin % 32 == 0, "Cin must be a multiple of 32");
   TORCH_CHECK(!pool || (H % 2 == 0 && W % 2 == 0), "pooling needs even H, W");
-  TORCH_CHECK(cfg >= 0 && cfg <= 6, "bad tile config");
+  TORCH_CHECK((cfg >= 0 && cfg <= 6) || (ks == 3 && (cfg == 256 || cfg == 258 || cfg == 259)),
+              "bad tile config (bf16 operands: 256 + {0, 2, 3}, 3x3 only)");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   const float* sc = opt_ptr(scale, Cout, "scale");
   const float* sh = opt_ptr(shift, Cout, "shift");
@@ -193,6 +194,8 @@ at::Tensor conv_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>& g_ar
   TORCH_CHECK(wt.size(0) == Cin && wt.size(1) == ks * ks * Cout, "wt must be (Cin, ks*ks*Cout)");
   TORCH_CHECK(Cout % 32 == 0, "Cout must be a multiple of 32 for dgrad");
   TORCH_CHECK(tay_group >= 0 && (tay_group == 0 || Cin % tay_group == 0), "tay_group must divide Cin");
+  TORCH_CHECK((cfg >= 0 && cfg <= 6) || (ks == 3 && (cfg == 256 || cfg == 258 || cfg == 259)),
+              "bad tile config (bf16 operands: 256 + {0, 2, 3}, 3x3 only)");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
   const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
   float* tay = nullptr;

@@ -24,6 +24,15 @@
 namespace tp {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// 4 fp32 -> 4 bf16 (round to nearest even: v_cvt_pk_bf16_f32), packed in 2 dwords
+__device__ __forceinline__ uint2 bf16x4_of(const f32x4 v) {
+  return __builtin_bit_cast(uint2, __builtin_convertvector(v, bf16x4));
+}
+
+constexpr int CFG_BF16 = 256;  // tile-config flag: bf16 operands (conv_igemm BF), fp32 accumulation
 
 enum Epi : int {
   EPI_FWD = 0,       // y = relu?(acc*scale[n] + shift[n]) stored NHWC
@@ -163,12 +172,20 @@ __device__ __forceinline__ float4 res_quad(const ConvArgs& p, long long pix, int
 // pixel (oh, ow) gathers y pixel ((oh + pad - kh) / s, (ow + pad - kw) / s) through tap (kh, kw)
 // when the division is exact; w[n = forward ci][k = (kh, kw, co)]. With parity row order a
 // tile only iterates the taps its stride phases use (1/4 of the 3x3 taps on average).
-template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI, int GEN = 0>
+// BF (opt-in, compute_dtype=bfloat16; GEN 0 only): operands rounded to bf16 (RNE) as they are
+// staged into LDS (rows of 32 bf16 = 16 dwords, padded to 20: 80-B rows keep the 16-B fragment
+// reads conflict-free), products on v_mfma_f32_32x32x16_bf16 with fp32 accumulation; loads,
+// epilogues and every output stay fp32. 16x the fp32 MFMA rate: the K slice is 2 MFMAs, not 16.
+template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI, int GEN = 0, bool BF = false>
 __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, WM, WN) / 128) void conv_igemm(ConvArgs p) {
   using T = Tile<BM, BN, WM, WN>;
   constexpr int BK = T::BK, LDK = T::LDK;
   __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
   constexpr int STAGE = (BM + BN) * LDK;  // floats per pipeline stage: A rows then B rows
+  constexpr int LDKB = 20;                // BF: dwords per LDS row (32 bf16 + pad)
+  constexpr int STAGEB = (BM + BN) * LDKB;
+  static_assert(!BF || GEN == 0, "bf16 operands: GEN 0 only");
+  unsigned* smu = reinterpret_cast<unsigned*>(smem);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -375,6 +392,15 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     }
   };
   auto store_tile = [&](int buf) {
+    if constexpr (BF) {  // round to bf16 (RNE) on the way into LDS: 4 fp32 -> 2 dwords
+#pragma unroll
+      for (int i = 0; i < T::A_CHUNKS; ++i)
+        *reinterpret_cast<uint2*>(smu + buf * STAGEB + a_row[i] * LDKB + a_c4[i] * 2) = bf16x4_of(ra[i]);
+#pragma unroll
+      for (int i = 0; i < T::B_CHUNKS; ++i)
+        *reinterpret_cast<uint2*>(smu + buf * STAGEB + (BM + b_row[i]) * LDKB + b_c4[i] * 2) = bf16x4_of(rb[i]);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < T::A_CHUNKS; ++i)
       *reinterpret_cast<f32x4*>(smem + buf * STAGE + a_row[i] * LDK + a_c4[i] * 4) = ra[i];
@@ -403,6 +429,30 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     for (int kt = kt_begin; kt < kt_end; ++kt) {
       const bool more = kt + 1 < kt_end;
       if (more) load_tile(kt + 1);  // global loads in flight under the MFMAs below
+      if constexpr (BF) {
+        // lane (li, lh) feeds k = 16 s2 + 8 lh + e of the slice (A and B agree): one 16-B read
+        // per fragment per MFMA
+        const unsigned* a_bb = smu + buf * STAGEB + (wm0 + li) * LDKB + lh * 4;
+        const unsigned* b_bb = smu + buf * STAGEB + (BM + wn0 + li) * LDKB + lh * 4;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          u32x4 afb[T::TM], bfb[T::TN];
+#pragma unroll
+          for (int i = 0; i < T::TM; ++i) afb[i] = *reinterpret_cast<const u32x4*>(a_bb + i * 32 * LDKB + s2 * 8);
+#pragma unroll
+          for (int j = 0; j < T::TN; ++j) bfb[j] = *reinterpret_cast<const u32x4*>(b_bb + j * 32 * LDKB + s2 * 8);
+#pragma unroll
+          for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+            for (int j = 0; j < T::TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, afb[i]),
+                                                                  __builtin_bit_cast(bf16x8, bfb[j]), acc[i][j], 0, 0, 0);
+        }
+        if (more) store_tile(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+        continue;
+      }
       const float* a_base = smem + buf * STAGE + (wm0 + li) * LDK + lh * 16;
       const float* b_base = smem + buf * STAGE + (BM + wn0 + li) * LDK + lh * 16;
       // software-pipelined fragment reads: chunk c+1 is read while chunk c feeds the MFMAs
@@ -1013,19 +1063,30 @@ namespace {
 
 using tp::ConvArgs;
 
-template <int BM, int BN, int WM, int WN, int KS, bool PM, bool UP, int EPI>
+template <int BM, int BN, int WM, int WN, int KS, bool PM, bool UP, int EPI, bool BF = false>
 hipError_t launch_cfg(const ConvArgs& a, int splits, hipStream_t st) {
   const int m_tiles = (a.M + BM - 1) / BM, n_tiles = (a.N + BN - 1) / BN;
   dim3 grid(m_tiles * n_tiles, splits);
-  tp::conv_igemm<BM, BN, WM, WN, KS, PM, UP, EPI><<<grid, tp::Tile<BM, BN, WM, WN>::NT, 0, st>>>(a);
+  tp::conv_igemm<BM, BN, WM, WN, KS, PM, UP, EPI, 0, BF><<<grid, tp::Tile<BM, BN, WM, WN>::NT, 0, st>>>(a);
   return hipGetLastError();
 }
 
 // cfg: 0 = 128x128 (waves 2x2 of 64x64), 1 = 256x64 (4x1 of 64x64), 2 = 64x64 (2x2 of 32x32),
 //      4 = 128x128 (8 waves 2x4 of 64x32), 5 = 256x64 (8 waves 4x2 of 64x32), 6 = 128x64 (8 waves 4x2 of 32x32),
 //      3 = 128x64 (2x2 of 64x32)
+// cfg | CFG_BF16 (3x3 only): the bf16-operand variants of cfgs 0, 2, 3
 template <int KS, bool PM, bool UP, int EPI>
 hipError_t launch_any(int cfg, const ConvArgs& a, int splits, hipStream_t st) {
+  if (cfg & tp::CFG_BF16) {
+    if constexpr (KS == 3) {
+      switch (cfg & ~tp::CFG_BF16) {
+        case 0: return launch_cfg<128, 128, 64, 64, KS, PM, UP, EPI, true>(a, splits, st);
+        case 2: return launch_cfg<64, 64, 32, 32, KS, PM, UP, EPI, true>(a, splits, st);
+        case 3: return launch_cfg<128, 64, 64, 32, KS, PM, UP, EPI, true>(a, splits, st);
+      }
+    }
+    return hipErrorInvalidValue;
+  }
   switch (cfg) {
     case 0: return launch_cfg<128, 128, 64, 64, KS, PM, UP, EPI>(a, splits, st);
     case 1: return launch_cfg<256, 64, 64, 64, KS, PM, UP, EPI>(a, splits, st);

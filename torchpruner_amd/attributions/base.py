@@ -470,12 +470,18 @@ class _AttributionMetric(ABC):
         return maybe_resnet_engine(self.model, eval_modules, self.device, grad=True, why=why)
 
     def _fused_engine(self, eval_modules, why=None, need_ce=True, pre_act_ok=False):
-        """The fused chain engine (engine, block indices) for ``eval_modules``, else None."""
+        """The fused chain engine (engine, block indices) for ``eval_modules``, else None.
+        ``compute_dtype=torch.bfloat16`` runs it with bf16-operand 3x3 convs (fp32 accumulation,
+        fp32 activations / gradients, fp64 score accumulators); fp16 uses the generic path."""
         from ..engine.fused_chain import _reject, maybe_engine
-        if not self._engines_allowed():
+        bf16 = self.compute_dtype == torch.bfloat16
+        if not self._engines_allowed() and not bf16:
             return _reject(why, f"compute_dtype={self.compute_dtype} runs the generic autocast path")
-        return maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=need_ce, why=why,
-                            pre_act_ok=pre_act_ok, input_shape=self._first_input_shape())
+        res = maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=need_ce, why=why,
+                           pre_act_ok=pre_act_ok, input_shape=self._first_input_shape())
+        if res is not None:
+            res[0].bf16 = bf16
+        return res
 
     def _first_input_shape(self):
         """Shape of the data generator's first input batch, or None when it cannot be peeked at

@@ -48,6 +48,8 @@ WINO_LDS = -2  # the same with the block input region staged through LDS
 WINO_UNP = -3  # dgrad of a pooled layer: explicit vectorised unpool, then the staged kernel on the
                # dense full-resolution gradient (vs rebuilding it from pooled cells per chunk)
 WINO4 = -4  # Winograd F(4x4,3x3) kernel (wino4.hip): square 4/8/16/32-pixel maps, 1.78x fewer MFMAs
+CFG_BF16 = 256  # tile-config flag of conv_igemm: bf16 operands / fp32 accumulation (opt-in, compute_dtype)
+_BF16_CFGS = (0, 2, 3)  # the implicit-GEMM tiles built with bf16 variants (conv_mfma.hip launch_any)
             # than F(2x2); dgrads of pooled layers take the explicit unpool first
 
 # Winograd F(2x2,3x3) weight transform G g G^T
@@ -361,6 +363,10 @@ class FusedChainEngine:
         self._arenas = {}
         self._graphs = {}  # HIP graphs of taylor() per (shapes, blocks, mode)
         self.use_wino = os.environ.get("TORCHPRUNER_WINOGRAD", "1") != "0"
+        # opt-in bf16 operands for the 3x3 convs (compute_dtype=torch.bfloat16): products on
+        # v_mfma_f32_32x32x16_bf16 with fp32 accumulation; activations, epilogues, gradients and
+        # score accumulators stay fp32 / fp64. Never the default (the headline is exact fp32).
+        self.bf16 = False
 
     # ------------------------------------------------------------------ weights
     def _params_key(self):
@@ -497,6 +503,8 @@ class FusedChainEngine:
 
     def _conv_run(self, T, e, h, cfg, sp, apoz=None):
         """``apoz``: (B, N) buffer that receives the counts of positive (pre-pool) outputs."""
+        if cfg >= CFG_BF16:
+            return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp, apoz)
         if cfg == WINO4:
             return T.conv_wino4_fwd(h, self._u4(e), e["scale"], e["shift"], True, e["pool"], apoz)
         if cfg in (WINO, WINO_LDS):
@@ -518,17 +526,26 @@ class FusedChainEngine:
         N, K = e["scale"].numel(), e["w"].shape[1]
         wino = (B * (H // 2) * (W // 2), C) if "u" in e and _wino_ok(H, W, C, N) else None
         cands = None
-        if H == 2 and W == 2 and C % 32 == 0:
+        if self.bf16 and C % 32 == 0:
+            cands = self._bf16_cands(M, N, K)
+        elif H == 2 and W == 2 and C % 32 == 0:
             cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * N, 4 * C)] + \
                 TUNER.candidates(M, N, K, wino)
         elif self.use_wino and _wino4_ok(H, W, C, N) and "w4d" in e:
             cands = [(WINO4, 1)] + TUNER.candidates(M, N, K, wino)  # [0] = the untuned pick
-        cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"], wino is not None), M, N, K,
+        cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"], wino is not None, self.bf16), M, N, K,
                                lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino, cands=cands)
         return self._conv_run(T, e, h, cfg, sp, apoz)
 
+    @staticmethod
+    def _bf16_cands(M, N, K):
+        """bf16-operand implicit-GEMM candidates ([0] = the untuned pick)."""
+        return [(CFG_BF16 + c, s_) for c, s_ in TUNER.candidates(M, N, K) if c in _BF16_CFGS]
+
     def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0):
         """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
+        if cfg >= CFG_BF16:
+            return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp, tay_mode=tm)
         if cfg == WINO4:
             if am is not None:
                 g = T.unpool2_nhwc(g, am)
@@ -754,7 +771,7 @@ class FusedChainEngine:
         if criterion is not None:  # a user criterion runs through autograd: eager launches
             return self.taylor(x, y, want, arena, mode, criterion)
         P = self._pack()
-        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device))
+        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device), self.bf16)
         g = self._graphs.get(key)
         if g is not None and (g["P"] is not P or g["arena"] is not arena):
             g = None
@@ -841,7 +858,9 @@ class FusedChainEngine:
             Cin, Cg = prev_act.shape[3], g.shape[3]
             wino = (B * (H // 2) * (W // 2), Cg) if "ut" in e and _wino_ok(H, W, Cg, Cin) else None
             sc4, cands = None, None
-            if H == 2 and W == 2 and Cg % 32 == 0 and Cin % 32 == 0:
+            if self.bf16 and Cg % 32 == 0:
+                cands = self._bf16_cands(M, Cin, e["wt"].shape[1])
+            elif H == 2 and W == 2 and Cg % 32 == 0 and Cin % 32 == 0:
                 pe = P["convs"][ci - 1]
                 sc4 = pe.get("scale4")
                 if sc4 is None:
@@ -856,11 +875,13 @@ class FusedChainEngine:
                 # [0] = the untuned pick: explicit unpool from 16x16 down (measured faster at
                 # B=2048 for the 16/8/4-pixel layers, slower at 32x32); bit-identical either way
                 cands = unp + wc if H <= 16 else wc + unp
-            if self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is None and wino is not None:
+            if not self.bf16 and self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is None \
+                    and wino is not None:
                 cands = TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
-            if self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is not None:
+            if not self.bf16 and self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is not None:
                 cands = [(WINO4, 1)] + cands  # [0] = the untuned pick
-            cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None),
+            cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None,
+                                    self.bf16),
                                    M, Cin, e["wt"].shape[1],
                                    lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4:
                                    self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_, s4), wino, wino_only=True,
@@ -973,6 +994,7 @@ def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None,
             for a, b in zip(eng.plan.blocks, plan.blocks)):
         eng = FusedChainEngine(model, plan)
         _ENGINES[model] = eng
+    eng.bf16 = False  # exact fp32 unless the caller opts in (AttributionMetric compute_dtype=bfloat16)
     return eng, idx
 
 
