@@ -87,7 +87,7 @@ int tp_wino4_ok(int H, int W, int C, int K);
 int tp_wino4_lds_bytes(int S);
 hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act, float* taylor,
-                         float* apoz, int tay_mode, hipStream_t st);
+                         float* apoz, int tay_mode, int splits, float* ws, hipStream_t st);
 }
 
 namespace {
@@ -446,7 +446,7 @@ void need_u4(const at::Tensor& u, int64_t C, int64_t K) {
 std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at::Tensor& u,
                                                   const c10::optional<at::Tensor>& scale,
                                                   const c10::optional<at::Tensor>& shift, bool relu, bool pool,
-                                                  const c10::optional<at::Tensor>& apoz) {
+                                                  const c10::optional<at::Tensor>& apoz, int64_t splits) {
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
   need_u4(u, C, K);
@@ -468,16 +468,20 @@ std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at:
                     apoz->numel() == B * K, "apoz must be a contiguous float32 (B, K) tensor");
     ap = apoz->data_ptr<float>();
   }
+  const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, C / 8));
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * H * W * K}, x.options());
   TP_CHECK_HIP(tp_conv_wino4(x.data_ptr<float>(), u.data_ptr<float>(), (int)B, (int)H, (int)C, (int)K,
                              pool ? EPI_FWD_POOL : EPI_FWD, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
-                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap, 0, cur_stream()));
+                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap, 0, (int)sp,
+                             sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
   return {out, am};
 }
 
 // F(4x4) dgrad with the conv_wino_dgrad epilogue contract (no unpooling: pass the unpooled grad)
 at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at::Tensor& act,
                             const c10::optional<at::Tensor>& bn_scale, const c10::optional<at::Tensor>& taylor,
-                            bool want_out, int64_t tay_mode) {
+                            bool want_out, int64_t tay_mode, int64_t splits) {
   need(g, "g", 4);
   need(act, "act", 4);
   const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
@@ -499,9 +503,13 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
   }
   at::Tensor out;
   if (want_out) out = at::empty({B, H, W, Cin}, g.options());
+  const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, Cout / 8));
+  at::Tensor ws;
+  if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
   TP_CHECK_HIP(tp_conv_wino4(g.data_ptr<float>(), ut.data_ptr<float>(), (int)B, (int)H, (int)Cout, (int)Cin, EPI_BWD,
                              sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(),
-                             tay, nullptr, (int)tay_mode, cur_stream()));
+                             tay, nullptr, (int)tay_mode, (int)sp, sp > 1 ? ws.data_ptr<float>() : nullptr,
+                             cur_stream()));
   return out;
 }
 
@@ -898,9 +906,9 @@ void register_engine_ops_def(torch::Library& m) {
         "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True, int tay_mode=0) -> Tensor");
   m.def("wino4_weights(Tensor w, bool flip_t, int K=0, int C=0) -> Tensor");
   m.def("conv_wino4_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, "
-        "Tensor(a!)? apoz=None) -> (Tensor, Tensor)");
+        "Tensor(a!)? apoz=None, int splits=1) -> (Tensor, Tensor)");
   m.def("conv_wino4_dgrad(Tensor g, Tensor ut, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, bool want_out, "
-        "int tay_mode=0) -> Tensor");
+        "int tay_mode=0, int splits=1) -> Tensor");
 }
 
 void register_engine_ops_impl(torch::Library& m) {

@@ -28,6 +28,7 @@
 // reduction), well inside the engine's fp64-oracle tolerances.
 #include "tp_common.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -35,7 +36,7 @@
 namespace tp {
 namespace w4 {
 
-enum Epi : int { FWD = 0, FWD_POOL = 1, BWD = 2 };
+enum Epi : int { FWD = 0, FWD_POOL = 1, BWD = 2, PARTIAL = 3 };  // PARTIAL: raw split-K slab (MODE 2/3)
 
 constexpr int TILES = 32;                 // output tiles per block
 constexpr int TK = 32;                    // output channels per block
@@ -84,6 +85,8 @@ struct Args {
   float* taylor;      // BWD: (R, B, K) slab, slot 0 written (+=), nullable
   float* apoz;        // FWD / FWD_POOL: (B, K) counts of positive outputs (+=), nullable
   int tay_mode;       // BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
+  long long slab;     // PARTIAL: floats per split slab (M * K); slab s = blockIdx.y
+  int pool_order;     // PARTIAL: rows in pooled order (b, y/2, x/2, y&1, x&1) for a pooled combine
   int dbg;            // phase-cost experiments only (TP_W4_DBG; results are WRONG when set): 1 no U DMA,
                       // 2 no X DMA, 16 no epilogue
 };
@@ -250,7 +253,14 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[NPT], int t
             const int q = qq + 8 * h2;
             const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
             const long long pix = ((long long)b * S + 4 * tr + (q >> 2)) * S + 4 * tc + (q & 3);
-            if constexpr (EPI == FWD) {
+            if constexpr (EPI == PARTIAL) {
+              const int yy = 4 * tr + (q >> 2), xx = 4 * tc + (q & 3);
+              const long long row = p.pool_order
+                                        ? ((((long long)b * (S / 2) + (yy >> 1)) * (S / 2) + (xx >> 1)) * 4 +
+                                           (yy & 1) * 2 + (xx & 1))
+                                        : pix;
+              *reinterpret_cast<f32x4*>(p.out + (long long)blockIdx.y * p.slab + row * p.K + k) = yv;
+            } else if constexpr (EPI == FWD) {
               f32x4 v;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
@@ -692,7 +702,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
       }
   };
 
-  const int nc = p.C / 8;
+  // split-K over channel chunks: blockIdx.y owns chunks [c_lo, c_hi) (host: no empty split)
+  const int nc_all = p.C / 8, cps = (nc_all + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c_lo = (int)blockIdx.y * cps, nc = min(nc_all, c_lo + cps);
   f32x4 acc[NPT];
 #pragma unroll
   for (int x = 0; x < NPT; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -705,14 +717,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   };
 
   // prologue: X(0) (and X(1)), U0(0) in flight
-  stage_x(0, xs0);
-  if (XDBL && nc > 1) stage_x(8, xs1);
-  stage_u(0, 0);
-  for (int c = 0; c < nc; ++c) {
-    float* xb = (XDBL && (c & 1)) ? xs1 : xs0;  // X(c)
+  stage_x(8 * c_lo, xs0);
+  if (XDBL && c_lo + 1 < nc) stage_x(8 * (c_lo + 1), xs1);
+  stage_u(8 * c_lo, 0);
+  for (int c = c_lo; c < nc; ++c) {
+    float* xb = (XDBL && ((c - c_lo) & 1)) ? xs1 : xs0;  // X(c)
     // top: U0(c) and X(c) landed everywhere (NW = 8: X(c+1), issued after U0(c), may still be in
     // flight); every wave is done with U1(c-1)
-    if (XDBL && c + 1 < nc && c > 0) wait_but_x();
+    if (XDBL && c + 1 < nc && c > c_lo) wait_but_x();
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     stage_u(8 * c, 1);
@@ -856,11 +868,24 @@ extern "C" int tp_wino4_ok(int H, int W, int C, int K) {
 // F(4x4,3x3) conv, S x S maps. epi: 0 fwd (BN affine + ReLU), 1 fwd + 2x2 max-pool (+ argmax),
 // 2 dgrad epilogue (x = output gradient, act / scale / taylor as conv_wino). apoz (fwd) and taylor
 // (dgrad, slot 0 of the (R, B, K) slab) are summed per (image, channel) with one writer each (+=).
+// splits > 1 (MODE 2/3): the channel chunks are split over gridDim.y blocks that write raw slabs
+// into ws (splits x M x K floats; pooled row order for epi 1), combined in a fixed order by the
+// shared split-K epilogue (conv_mfma.hip) — small batches get enough blocks to fill the chip.
+extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
+                                              const float* scale, const float* shift, int relu, float* out,
+                                              uint8_t* out_argmax, const float* act, float* taylor,
+                                              float* apoz, int tay_mode, hipStream_t st);
+
 extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi,
                                     const float* scale, const float* shift, int relu, float* out, uint8_t* out_argmax,
-                                    const float* act, float* taylor, float* apoz, int tay_mode, hipStream_t st) {
+                                    const float* act, float* taylor, float* apoz, int tay_mode, int splits,
+                                    float* ws, hipStream_t st) {
   using namespace tp::w4;
   if (!tp_wino4_ok(S, S, C, K) || B <= 0) return hipErrorInvalidValue;
+  const int nc = C / 8;
+  splits = std::max(1, std::min(splits, nc));
+  splits = (nc + (nc + splits - 1) / splits - 1) / ((nc + splits - 1) / splits);  // no empty split
+  if (splits > 1 && (kernel_mode() < 2 || !ws)) return hipErrorInvalidValue;
   if (epi < 0 || epi > 2 || (epi == BWD && !act) || (epi != BWD && !out) || (epi == FWD_POOL && !out_argmax))
     return hipErrorInvalidValue;
   Args a{};
@@ -894,7 +919,35 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   const int mode = kernel_mode();
   const int tb = mode == 2 ? 64 : TILES;  // MODE 3: 32-tile blocks
   const int n_p = (a.P + tb - 1) / tb, n_k = K / TK;
-  const dim3 grid(n_p * n_k);
+  const dim3 grid(n_p * n_k, splits);
+  if (splits > 1) {
+    Args b = a;
+    b.out = ws;
+    b.out_argmax = nullptr;
+    b.act = nullptr;
+    b.taylor = nullptr;
+    b.apoz = nullptr;
+    b.scale = nullptr;
+    b.shift = nullptr;
+    b.slab = (long long)B * S * S * K;
+    b.pool_order = epi == FWD_POOL;
+    if (b.slab * splits >= (1ll << 31)) return hipErrorInvalidValue;
+#define TP_W4P(SS)                                                                      \
+  do {                                                                                  \
+    if (mode == 2) wino4_m2<PARTIAL, SS, 8><<<grid, 512, 0, st>>>(b);                   \
+    else wino4_m2<PARTIAL, SS, 4><<<grid, 256, 0, st>>>(b);                             \
+  } while (0)
+    if (S == 32) TP_W4P(32);
+    else if (S == 16) TP_W4P(16);
+    else if (S == 8) TP_W4P(8);
+    else TP_W4P(4);
+#undef TP_W4P
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return tp_conv_epilogue_slabs(ws, splits, B, S, S, K, epi, scale, epi == BWD ? nullptr : shift, relu, out,
+                                  out_argmax, act, epi == BWD ? taylor : nullptr, epi == BWD ? nullptr : apoz,
+                                  tay_mode, st);
+  }
 #define TP_W4(E, SS)                                              \
   do {                                                            \
     if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a);   \

@@ -108,3 +108,46 @@ def test_wino4_rejects_bad_shapes(cuda):
         T.conv_wino4_fwd(torch.randn(2, 12, 12, 8, device=cuda), u, None, None, True, False, None)
     with pytest.raises(RuntimeError):
         T.conv_wino4_fwd(torch.randn(2, 16, 8, 8, device=cuda), u, None, None, True, False, None)
+
+
+@pytest.mark.parametrize("S,C,K,B", [(32, 64, 64, 3), (16, 128, 96, 2), (8, 256, 64, 5), (4, 512, 64, 7)])
+@pytest.mark.parametrize("splits", [2, 4])
+def test_wino4_split_k(cuda, S, C, K, B, splits):
+    """Channel split-K (raw slabs + the deterministic combine) == one K pass, all epilogues."""
+    T = _ops()
+    import os
+    if int(os.environ.get("TP_W4_MODE", "3")) < 2:
+        pytest.skip("split-K needs MODE 2/3")
+    g = torch.Generator(device=cuda).manual_seed(S + C + splits)
+    x = torch.randn(B, S, S, C, device=cuda, generator=g)
+    w = torch.randn(K, C, 3, 3, device=cuda, generator=g) / (3 * C ** 0.5)
+    sc = torch.rand(K, device=cuda, generator=g) + 0.5
+    sh = torch.randn(K, device=cuda, generator=g) * 0.1
+    u = T.wino4_weights(w, False, 0, 0)
+    for pool in (False, True):
+        a1 = torch.zeros(B, K, device=cuda)
+        a2 = torch.zeros(B, K, device=cuda)
+        y1, m1 = T.conv_wino4_fwd(x, u, sc, sh, True, pool, a1, 1)
+        y2, m2 = T.conv_wino4_fwd(x, u, sc, sh, True, pool, a2, splits)
+        assert ((y1 - y2).abs().max() / y1.abs().max()).item() < 1e-4
+        assert (a1 - a2).abs().max().item() <= 2.0
+        if pool:
+            agree = ((m1 & 3) == (m2 & 3)).float().mean().item()
+            assert agree > 0.999, agree
+        ref = _fwd_ref(x, w, sc, sh)
+        if not pool:
+            assert ((y2.double() - ref).abs().max() / ref.abs().max()).item() < 2e-5
+    # dgrad of conv(Cin=K -> Cout=C) with Taylor partials
+    go = torch.randn(B, S, S, C, device=cuda, generator=g)
+    wd = torch.randn(C, K, 3, 3, device=cuda, generator=g) / (3 * K ** 0.5)
+    act = torch.relu(torch.randn(B, S, S, K, device=cuda, generator=g))
+    scp = torch.rand(K, device=cuda, generator=g) + 0.5
+    ut = T.wino4_weights(wd, True, 0, 0)
+    t1, t2 = torch.zeros(2, B, K, device=cuda), torch.zeros(2, B, K, device=cuda)
+    o1 = T.conv_wino4_dgrad(go, ut, act, scp, t1, True, 0, 1)
+    o2 = T.conv_wino4_dgrad(go, ut, act, scp, t2, True, 0, splits)
+    assert ((o1 - o2).abs().max() / o1.abs().max()).item() < 1e-4  # summation order only
+    s1, s2 = t1.double().sum(0), t2.double().sum(0)
+    assert ((s1 - s2).abs().max() / s1.abs().max()).item() < 1e-4
+    o3 = T.conv_wino4_dgrad(go, ut, act, scp, None, True, 0, splits)
+    assert torch.equal(o2, o3)  # deterministic combine

@@ -29,6 +29,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+import sys
 import weakref
 from dataclasses import dataclass, field
 from typing import Optional
@@ -97,6 +98,20 @@ def _wino_ok(H, W, C, K):
 
 def _wino4_ok(H, W, C, K):
     return H == W and H in (4, 8, 16, 32) and C % 8 == 0 and K % 32 == 0
+
+
+_W4_SPLITS = os.environ.get("TORCHPRUNER_W4_SPLITS", "1") != "0"
+_TUNER_LOG = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") != "0"  # print every timed kernel choice
+
+
+def _wino4_cands(B, H, W, K, C):
+    """F(4x4) candidates: one K pass, plus channel-chunk split-K (raw slabs + the shared
+    deterministic combine) when the tile grid alone cannot fill the chip (small batches)."""
+    blocks = math.ceil(B * (H // 4) * (W // 4) / 32) * (K // 32)
+    sp, chunks = 1, C // 8
+    while _W4_SPLITS and blocks * sp < 2 * _CU and sp * 2 <= chunks // 4 and sp < 16:
+        sp *= 2
+    return [(WINO4, 1)] + ([(WINO4, sp)] if sp > 1 else []) + ([(WINO4, sp // 2)] if sp > 2 else [])
 
 
 def _wino_splits(P, K, C):
@@ -201,6 +216,8 @@ class Autotuner:
             if best is None or t < best[0]:
                 best = (t, cand)
         self.cache[key] = best[1]
+        if _TUNER_LOG:
+            print(f"[tuner] {key} -> {best[1]} ({best[0] / 2 * 1e3:.1f} us)", file=sys.stderr, flush=True)
         return best[1]
 
 
@@ -506,7 +523,7 @@ class FusedChainEngine:
         if cfg >= CFG_BF16:
             return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp, apoz)
         if cfg == WINO4:
-            return T.conv_wino4_fwd(h, self._u4(e), e["scale"], e["shift"], True, e["pool"], apoz)
+            return T.conv_wino4_fwd(h, self._u4(e), e["scale"], e["shift"], True, e["pool"], apoz, sp)
         if cfg in (WINO, WINO_LDS):
             return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS, apoz)
         if cfg >= self.DENSE:
@@ -532,7 +549,7 @@ class FusedChainEngine:
             cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * N, 4 * C)] + \
                 TUNER.candidates(M, N, K, wino)
         elif self.use_wino and _wino4_ok(H, W, C, N) and "w4d" in e:
-            cands = [(WINO4, 1)] + TUNER.candidates(M, N, K, wino)  # [0] = the untuned pick
+            cands = _wino4_cands(B, H, W, N, C) + TUNER.candidates(M, N, K, wino)  # [0] = the untuned pick
         cfg, sp = TUNER.choose(("fwd", tuple(h.shape), N, e["pool"], wino is not None, self.bf16), M, N, K,
                                lambda c, s_, e=e, hh=h: self._conv_run(T, e, hh, c, s_), wino, cands=cands)
         return self._conv_run(T, e, h, cfg, sp, apoz)
@@ -549,7 +566,7 @@ class FusedChainEngine:
         if cfg == WINO4:
             if am is not None:
                 g = T.unpool2_nhwc(g, am)
-            return T.conv_wino4_dgrad(g, self._u4(e, True), act, sc, taylor, want_out, tm)
+            return T.conv_wino4_dgrad(g, self._u4(e, True), act, sc, taylor, want_out, tm, sp)
         if cfg == WINO_UNP:
             return T.conv_wino_dgrad(T.unpool2_nhwc(g, am), None, e["ut"], act, sc, taylor, want_out, sp, True,
                                      tay_mode=tm)
@@ -879,7 +896,7 @@ class FusedChainEngine:
                     and wino is not None:
                 cands = TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
             if not self.bf16 and self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is not None:
-                cands = [(WINO4, 1)] + cands  # [0] = the untuned pick
+                cands = _wino4_cands(B, H, W, Cin, Cg) + cands  # [0] = the untuned pick
             cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None,
                                     self.bf16),
                                    M, Cin, e["wt"].shape[1],
