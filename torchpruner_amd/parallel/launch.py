@@ -14,6 +14,14 @@ dies, the others are blocked in a collective that can never complete, so they ge
 seconds to finish on their own and are then terminated (SIGTERM, then SIGKILL). Children get
 ``PR_SET_PDEATHSIG`` so that a killed parent does not leave ranks holding the GPU.
 
+Elastic restart (``max_restarts``, torchrun's ``--max-restarts`` semantics for one node): after a
+failure the whole group is stopped and relaunched on a fresh rendezvous port, up to
+``max_restarts`` times; each generation sees ``TORCHELASTIC_RESTART_COUNT`` (the variable torchrun
+exports). A job that checkpoints per rank (``_AttributionMetric(checkpoint=...)``,
+``checkpoint.save_accumulators``) resumes from its checkpoints and recomputes only unfinished
+work, so a transient rank loss costs one relaunch, not the job. The same scripts work unchanged
+under ``torchrun --max-restarts N``.
+
 The reference has no launcher or distributed code at all; the loop this
 parallelises is the attribution data loop, reference ``torchpruner/attributions/attributions.py:58-68``.
 """
@@ -45,10 +53,18 @@ def under_launcher(env=None) -> bool:
     return "WORLD_SIZE" in env and "RANK" in env
 
 
-def rank_env(rank: int, world: int, port: int, base=None, addr: str = "127.0.0.1") -> dict:
+def restart_count(env=None) -> int:
+    """Generation of this rank process: 0 on the first launch, k after the k-th elastic restart
+    (set by :func:`spawn_local` and by torchrun)."""
+    env = os.environ if env is None else env
+    return int(env.get("TORCHELASTIC_RESTART_COUNT", "0"))
+
+
+def rank_env(rank: int, world: int, port: int, base=None, addr: str = "127.0.0.1", restart: int = 0) -> dict:
     env = dict(os.environ if base is None else base)
     env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
-               MASTER_ADDR=addr, MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
+               MASTER_ADDR=addr, MASTER_PORT=str(port), PYTHONUNBUFFERED="1",
+               TORCHELASTIC_RESTART_COUNT=str(restart))
     # dmabuf IPC only on this platform (RCCL / CUDA-tensor sharing fails without it)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return env
@@ -74,21 +90,32 @@ def _worst(rcs: Sequence[Optional[int]]) -> int:
 
 def spawn_local(nproc: int, argv: Sequence[str], *, python: str = sys.executable, env: Optional[dict] = None,
                 grace: float = 60.0, timeout: Optional[float] = None, cwd: Optional[str] = None,
-                log=None) -> int:
+                log=None, max_restarts: int = 0) -> int:
     """Run ``python argv...`` as ``nproc`` ranks on this node; return the return code of the
     first rank that failed (the root cause; peers blocked in a collective fail after it), 0 if
     none did.
 
     Children inherit stdout/stderr (rank 0's result line reaches the caller unmodified).
     ``grace``: seconds the surviving ranks get after the first failure; ``timeout``: overall
-    limit (None = none)."""
-    assert nproc >= 1
+    limit per generation (None = none); ``max_restarts``: relaunch the whole group this many
+    times after a failure (elastic restart, see the module docstring)."""
+    assert nproc >= 1 and max_restarts >= 0
     log = log or (lambda msg: print(msg, file=sys.stderr, flush=True))
+    for gen in range(max_restarts + 1):
+        rc = _run_group(nproc, argv, python, env, grace, timeout, cwd, log, gen)
+        if rc == 0:
+            return 0
+        if gen < max_restarts:
+            log(f"[launch] group failed (rc {rc}); elastic restart {gen + 1}/{max_restarts}")
+    return rc
+
+
+def _run_group(nproc, argv, python, env, grace, timeout, cwd, log, gen) -> int:
     port = free_port()
     procs = []
     try:
         for r in range(nproc):
-            procs.append(subprocess.Popen([python, *argv], env=rank_env(r, nproc, port, env), cwd=cwd,
+            procs.append(subprocess.Popen([python, *argv], env=rank_env(r, nproc, port, env, restart=gen), cwd=cwd,
                                           preexec_fn=_pdeathsig))
         t0 = time.monotonic()
         failed_at = None
@@ -134,3 +161,22 @@ def maybe_spawn(nproc: int, script: str, args: Sequence[str], **kw) -> Optional[
     if nproc <= 1 or under_launcher():
         return None
     return spawn_local(nproc, [script, *args], **kw)
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    """``python -m torchpruner_amd.parallel.launch --nproc N [--max-restarts K] script.py args...``:
+    a standard-library-only, single-node stand-in for ``torchrun`` (no GPU touched here)."""
+    import argparse
+    ap = argparse.ArgumentParser(prog="python -m torchpruner_amd.parallel.launch")
+    ap.add_argument("--nproc", type=int, default=1, help="ranks (one per GPU)")
+    ap.add_argument("--max-restarts", type=int, default=0, help="elastic relaunches of the group after a failure")
+    ap.add_argument("--grace", type=float, default=60.0, help="seconds survivors get after a rank fails")
+    ap.add_argument("--timeout", type=float, default=None, help="per-generation time limit (seconds)")
+    ap.add_argument("script")
+    ap.add_argument("args", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    return spawn_local(a.nproc, [a.script, *a.args], grace=a.grace, timeout=a.timeout, max_restarts=a.max_restarts)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
