@@ -33,6 +33,8 @@ __device__ __forceinline__ uint2 bf16x4_of(const f32x4 v) {
 }
 
 constexpr int CFG_BF16 = 256;  // tile-config flag: bf16 operands (conv_igemm BF), fp32 accumulation
+constexpr int CFG_WS = 16;     // cfgs 16..18: persistent warp-specialised 1x1 GEMM (gemm_ws.hip), 1x1 stride-s
+                               // GEN 1 convs and their dgrads (no split-K, no bnpart, dense residual)
 
 enum Epi : int {
   EPI_FWD = 0,       // y = relu?(acc*scale[n] + shift[n]) stored NHWC
@@ -1330,6 +1332,10 @@ hipError_t gen_dispatch(int ks, int gen, int cfg, const tp::ConvArgs& a, int spl
 }
 }  // namespace
 
+extern "C" hipError_t tp_gemm1x1_ws(const float* x, const float* w, int B, int H, int W, int Cin, int N, int stride,
+                                    const float* scale, const float* shift, int relu, float slope, const float* res,
+                                    const float* mask, float* apoz, float* out, int variant, hipStream_t st);
+
 extern "C" int tp_conv_gen_k(int ks, int Cin) {
   return Cin == 4 ? (ks * ks * 4 + 31) / 32 * 32 : ks * ks * Cin;
 }
@@ -1419,6 +1425,11 @@ extern "C" hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H,
   using namespace tp;
   const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
   if ((gen != 2 && Cin % 32 != 0) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
+  if (cfg >= CFG_WS && cfg < CFG_WS + 3) {  // persistent warp-specialised 1x1 kernel (gemm_ws.hip)
+    if (gen != 1 || ks != 1 || pad != 0 || res_stride != 1 || bnpart) return hipErrorInvalidValue;
+    return tp_gemm1x1_ws(x, w, B, H, W, Cin, Cout, stride, scale, shift, relu, 0.f, res, mask, apoz, out,
+                         cfg - CFG_WS, st);
+  }
   if (gen == 3 && (ks != 1 && ks != 3)) return hipErrorInvalidValue;
   ConvArgs a{};
   a.x = x;

@@ -47,6 +47,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ws", action="store_true", help="add the warp-specialised 1x1 GEMM cfgs (16-18)")
+    ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
     args = ap.parse_args()
     T = ops.require()
     dev = torch.device("cuda")
@@ -67,6 +69,8 @@ def main():
         shift = torch.zeros(cout, device=dev)
         res = torch.randn(B, Ho, Wo, cout, device=dev) if (ks == 1 and cout >= 256 and s == 1 and cin < cout) else None
         cands = [(c, sp) for c, sp in TUNER.candidates(M, cout, kk)]
+        if args.ws and ks == 1:
+            cands += [(16, 1), (17, 1), (18, 1)]
         wino = ks == 3 and s == 1 and H % 2 == 0 and W % 2 == 0
         if wino:
             sp0 = _wino_splits(B * (H // 2) * (W // 2), cout, cin_p)
@@ -91,6 +95,8 @@ def main():
             torch.cuda.synchronize()
             results.append((e0.elapsed_time(e1) / args.iters * 1e3, cfg, sp))
         us, cfg, sp = min(results)
+        if args.verbose:
+            print("   " + "  ".join(f"{c}/{p_}:{t:.0f}" for t, c, p_ in sorted(results, key=lambda r: (r[1], r[2]))))
         blas = ""
         if ks == 1 and s == 1:  # the same GEMM on hipBLASLt (torch.mm), no epilogue: a reference point
             a2, b2 = x.view(M, cin_p), w.view(cout, cin_p)
