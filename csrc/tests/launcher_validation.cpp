@@ -24,6 +24,9 @@ hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
                         int tay_mode, hipStream_t st);
+hipError_t tp_gemm1x1_ws(const float* x, const float* w, int B, int H, int W, int Cin, int N, int stride,
+                         const float* scale, const float* shift, int relu, float slope, const float* res,
+                         const float* mask, float* apoz, float* out, int variant, hipStream_t st);
 hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
                            float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
                            float* b, double* ws, hipStream_t st);
@@ -77,6 +80,18 @@ int main() {
   EXPECT(tp_conv_wino(n, nullptr, n, 2, 8, 8, 12, 64, 0, 0, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
          hipErrorInvalidValue);  // C % 8
   EXPECT(tp_bn_fwd_train(n, n, 16, 6, n, n, 1e-5f, 0.1f, n, n, n, n, n, n, nullptr, 0) == hipErrorInvalidValue);
+  // warp-specialised 1x1 GEMM (conv_gen cfgs 16-18): Cin % 32, N % 4, stride, slope, variant, 2^31-byte bounds,
+  // and the conv_gen entry's 1x1 / no-pad / dense-residual / no-bnpart gate
+  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 48, 64, 1, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
+  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 62, 1, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
+  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 64, 0, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
+  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 64, 1, n, n, 1, -0.5f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
+  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 64, 1, n, n, 0, 0.f, n, n, n, n, 3, 0) == hipErrorInvalidValue);
+  EXPECT(tp_gemm1x1_ws(n, n, 4096, 128, 128, 64, 64, 1, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 3, 1, 1, 0, 0, 0, 16, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // cfg 16 is 1x1 only
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 17, 1, n, n, 0, n, 2, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // strided residual
 
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);

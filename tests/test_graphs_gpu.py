@@ -95,3 +95,35 @@ def test_two_stream_pipeline_bit_identical(cuda, which):
                 os.environ["TORCHPRUNER_STREAMS"] = old
     for a, b in zip(out["1"], out["0"]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sensitivity", [False, True])
+def test_pipelined_graph_replay_bit_identical(cuda, sensitivity):
+    """Default (TORCHPRUNER_GRAPHS=auto): pipelined small batches replay one captured graph per
+    stream slot (each into its own score arena); scores equal the eager one-stream loop bit for
+    bit, including a ragged last batch, on the capturing run and on a pure-replay rerun."""
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.models import prunable_vgg16
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(2)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    eng, _ = maybe_engine(model, [find_best_module_for_attributions(model, c) for c in convs], F.cross_entropy, cuda)
+    x = torch.randn(430, 3, 32, 32, device=cuda)  # 10 batches of 40 + a ragged 30
+    y = torch.randint(0, 10, (430,), device=cuda)
+    old = os.environ.get("TORCHPRUNER_STREAMS")
+    os.environ["TORCHPRUNER_STREAMS"] = "0"
+    try:
+        ref = _scores(model, x, y, 40, "0", sensitivity=sensitivity)
+    finally:
+        if old is None:
+            del os.environ["TORCHPRUNER_STREAMS"]
+        else:
+            os.environ["TORCHPRUNER_STREAMS"] = old
+    for _ in range(2):
+        got = _scores(model, x, y, 40, "auto", sensitivity=sensitivity)
+        for a, r in zip(got, ref):
+            np.testing.assert_array_equal(a, r)
+    graphs = [k for k in eng._graphs if k[0] != "seen"]
+    assert len({k[-1] for k in graphs}) == 2, "one graph per pipeline slot (score arena)"

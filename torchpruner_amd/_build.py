@@ -124,7 +124,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
     return OUT
 
 
-SANITIZE_SOURCES = ("conv_mfma", "conv_wgrad", "winograd", "batchnorm")
+SANITIZE_SOURCES = ("conv_mfma", "conv_wgrad", "winograd", "batchnorm", "gemm_ws")
 
 
 def build_host_sanitizer(verbose: bool = False) -> Path:

@@ -428,7 +428,10 @@ class _AttributionMetric(ABC):
 
             def launch(slot, x=x, y=y):
                 arena = engine.score_arena(x.shape[0], uniq, x.device, tuple(x.shape[2:]), slot=slot)
-                engine.taylor(x, y, set(uniq), arena, mode=mode)
+                if engine.graphs_enabled(x.shape[0], pipelined=True):  # host-bound otherwise
+                    engine.taylor_graphed(x, y, set(uniq), arena, mode=mode)
+                else:
+                    engine.taylor(x, y, set(uniq), arena, mode=mode)
                 return arena
 
             def fold(arena, dev=x.device):
@@ -595,8 +598,11 @@ class _BatchPipeline:
     The first batch of every new shape runs alone on the current stream (kernel autotuning,
     buffer allocation, lazily packed operands). Two batches' activations are live at once, so it
     is off for inputs of >= 2^24 pixels per batch (B >= 16384 at 32x32, B >= 335 at 224x224;
-    TORCHPRUNER_STREAMS_MAX_PIXELS overrides), with HIP-graph replay, and with
-    TORCHPRUNER_STREAMS=0. ResNet-50 at B=256: APoZ +8%, Taylor +7%."""
+    TORCHPRUNER_STREAMS_MAX_PIXELS overrides), with TORCHPRUNER_GRAPHS=1/all (one graph-replayed
+    batch at a time), and with TORCHPRUNER_STREAMS=0. ResNet-50 at B=256: APoZ +8%, Taylor +7%.
+    On the fused VGG/MLP engine a pipelined batch of up to 1024 images replays a HIP graph of its
+    step per slot (FusedChainEngine.graphs_enabled): with two batches in flight the B=100 step is
+    host-bound otherwise."""
 
     MAX_PIXELS = 1 << 24
 
@@ -614,7 +620,7 @@ class _BatchPipeline:
         """Run batch (x, y) pipelined and return True, or return False (caller runs it)."""
         graphs = getattr(self.engine, "graphs_enabled", None)
         if not self.enabled or not x.is_cuda or x.shape[0] * math.prod(x.shape[2:]) >= self.max_pixels or \
-                (graphs is not None and graphs(x.shape[0])):
+                (graphs is not None and graphs(x.shape[0]) and os.environ.get("TORCHPRUNER_GRAPHS") in ("1", "all")):
             return False
         key = (tuple(x.shape), tuple(y.shape) if y is not None else None)
         if key not in self.seen:  # autotune / allocate alone, after everything in flight

@@ -765,15 +765,22 @@ class FusedChainEngine:
         blk = self.plan.blocks[b]
         return blk.conv.out_channels if isinstance(blk, ConvBlock) else blk.linear.out_features
 
-    # TORCHPRUNER_GRAPHS=1: replay HIP graphs for batches up to GRAPH_MAX_B; "all": any size.
-    # Off by default: measured on MI355X the step is GPU-bound down to B=8 (1.0 ms/step), so
-    # graphs gain nothing there (profiles/hip_graphs_taylor_step.txt); they help when the host
-    # cannot keep the launch queue ahead (contended CPUs).
+    # HIP-graph replay of the fused step (TORCHPRUNER_GRAPHS): "auto" (default) = for batches up to
+    # GRAPH_MAX_B when two or more batches are in flight on the stream pipeline; "1" = also for
+    # one batch at a time; "all" = any batch size; "0" = never. One batch at a time the step is
+    # GPU-bound down to B=8 (profiles/hip_graphs_taylor_step.txt), but with two batches in flight
+    # the GPU finishes a B=100 step (~55 launches) faster than Python enqueues it: the host spent
+    # 0.77-0.99 ms per batch in the pipeline against 0.85-1.04 ms of wall
+    # (scripts/b100_host_probe.py), so the pipelined launches replay one graph per slot.
     GRAPH_MAX_B = 1024
 
-    def graphs_enabled(self, B: int) -> bool:
-        mode = os.environ.get("TORCHPRUNER_GRAPHS", "0")
-        return mode == "all" or (mode == "1" and B <= self.GRAPH_MAX_B)
+    def graphs_enabled(self, B: int, pipelined: bool = False) -> bool:
+        mode = os.environ.get("TORCHPRUNER_GRAPHS", "auto")
+        if mode == "all":
+            return True
+        if mode == "auto":
+            return pipelined and B <= self.GRAPH_MAX_B
+        return mode == "1" and B <= self.GRAPH_MAX_B
 
     def taylor_graphed(self, x: torch.Tensor, y: torch.Tensor, want: set, arena: dict, mode="taylor",
                        criterion=None):
@@ -788,7 +795,9 @@ class FusedChainEngine:
         if criterion is not None:  # a user criterion runs through autograd: eager launches
             return self.taylor(x, y, want, arena, mode, criterion)
         P = self._pack()
-        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device), self.bf16)
+        # one graph per score arena: the stream pipeline replays slot k's graph into slot k's arena
+        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device), self.bf16,
+               id(arena))
         g = self._graphs.get(key)
         if g is not None and (g["P"] is not P or g["arena"] is not arena):
             g = None
@@ -804,7 +813,7 @@ class FusedChainEngine:
             with torch.cuda.graph(graph, stream=side):
                 self.taylor(sx, sy, want, arena, mode)
             torch.cuda.current_stream(x.device).wait_stream(side)
-            if len(self._graphs) > 32:  # bound the graphs' private memory pools
+            if len(self._graphs) > 64:  # bound the graphs' private memory pools
                 self._graphs.clear()
             g = self._graphs[key] = {"graph": graph, "x": sx, "y": sy, "P": P, "arena": arena}
         g["x"].copy_(x)
