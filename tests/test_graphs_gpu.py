@@ -126,4 +126,4 @@ def test_pipelined_graph_replay_bit_identical(cuda, sensitivity):
         for a, r in zip(got, ref):
             np.testing.assert_array_equal(a, r)
     graphs = [k for k in eng._graphs if k[0] != "seen"]
-    assert len({k[-1] for k in graphs}) == 2, "one graph per pipeline slot (score arena)"
+    assert len({k[-1] for k in graphs}) == 4, "one graph per pipeline slot (score arena), 4 slots by default"

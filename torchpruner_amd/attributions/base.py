@@ -422,7 +422,7 @@ class _AttributionMetric(ABC):
         uniq = sorted(owner)
         stats = accs[0].mode == "stats"
         crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
-        pipe = _BatchPipeline(engine) if stats and self._ckpt is None and crit is None else None
+        pipe = _BatchPipeline(engine, graph_replay=True) if stats and self._ckpt is None and crit is None else None
         for i, x, y in self._batches():
             B = x.shape[0]
 
@@ -606,11 +606,16 @@ class _BatchPipeline:
 
     MAX_PIXELS = 1 << 24
 
-    def __init__(self, engine):
+    def __init__(self, engine, graph_replay: bool = False):
         self.engine = engine
+        self.graph_replay = graph_replay  # the caller's launch() replays graphs when graphs_enabled(B, True)
         self.enabled = os.environ.get("TORCHPRUNER_STREAMS", "1") != "0"
         self.max_pixels = int(os.environ.get("TORCHPRUNER_STREAMS_MAX_PIXELS", self.MAX_PIXELS))
-        self.depth = max(2, int(os.environ.get("TORCHPRUNER_STREAMS_DEPTH", "2")))  # batches in flight
+        # batches in flight: 4 when the batches replay graphs (host-light: B=100 +10-19% over 2,
+        # B=256 +4%, profiles/bench/pipeline_depth_graphs.txt), else 2 (eager launches: the host is
+        # the limit beyond two)
+        env_depth = os.environ.get("TORCHPRUNER_STREAMS_DEPTH")
+        self.depth = max(2, int(env_depth)) if env_depth else None
         self.streams = None
         self.seen = set()
         self.n = 0
@@ -628,6 +633,8 @@ class _BatchPipeline:
             self.seen.add(key)
             return False
         if self.streams is None:
+            if self.depth is None:
+                self.depth = 4 if self.graph_replay and graphs is not None and graphs(x.shape[0], pipelined=True) else 2
             self.streams = [torch.cuda.Stream(x.device) for _ in range(self.depth)]
         cur = torch.cuda.current_stream(x.device)
         slot = self.n % self.depth
