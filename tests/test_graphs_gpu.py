@@ -127,3 +127,37 @@ def test_pipelined_graph_replay_bit_identical(cuda, sensitivity):
             np.testing.assert_array_equal(a, r)
     graphs = [k for k in eng._graphs if k[0] != "seen"]
     assert len({k[-1] for k in graphs}) == 4, "one graph per pipeline slot (score arena), 4 slots by default"
+
+
+@pytest.mark.gpu
+def test_pipelined_apoz_graph_replay_matches_eager(cuda):
+    """Fused-chain APoZ: pipelined batches replay one graph per slot (count buffers are graph
+    outputs, re-zeroed inside the graph); the counts equal the one-stream eager loop exactly."""
+    from torchpruner_amd import APoZAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import maybe_engine
+    from torchpruner_amd.models import prunable_vgg16
+    from torchpruner_amd.utils import find_best_module_for_attributions
+    torch.manual_seed(3)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    eng, _ = maybe_engine(model, [find_best_module_for_attributions(model, c) for c in convs], F.cross_entropy, cuda,
+                          need_ce=False)
+    x = torch.randn(450, 3, 32, 32, device=cuda)  # 11 batches of 40 + a ragged 10
+    y = torch.randint(0, 10, (450,), device=cuda)
+    out = {}
+    for env in ("0", "1"):
+        old = os.environ.get("TORCHPRUNER_STREAMS")
+        os.environ["TORCHPRUNER_STREAMS"] = env
+        try:
+            for _ in range(2 if env == "1" else 1):
+                out[env] = APoZAttributionMetric(model, DeviceLoader(x, y, 40), F.cross_entropy, cuda).run_many(
+                    convs, True)
+        finally:
+            if old is None:
+                del os.environ["TORCHPRUNER_STREAMS"]
+            else:
+                os.environ["TORCHPRUNER_STREAMS"] = old
+    for a, b in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, b)
+    assert any(k[0] == "apoz" for k in eng._graphs), "no APoZ graph was captured"

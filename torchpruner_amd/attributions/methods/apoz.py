@@ -50,12 +50,14 @@ class APoZAttributionMetric(_AttributionMetric):
             owner.setdefault(b, k)
         uniq = sorted(owner)
         stats = accs[0].mode == "stats"
-        pipe = _BatchPipeline(engine) if stats and self._ckpt is None else None
+        pipe = _BatchPipeline(engine, graph_replay=True) if stats and self._ckpt is None else None
         with torch.no_grad():
             for i, x, _y in self._batches():
                 B = x.shape[0]
 
                 def launch(slot, x=x):
+                    if engine.graphs_enabled(x.shape[0], pipelined=True):  # host-bound otherwise
+                        return engine.apoz_graphed(x, uniq, slot)
                     bufs = {b: torch.zeros(x.shape[0], engine._block_width(b), device=x.device) for b in uniq}
                     engine.forward(x, stop_after=uniq[-1], apoz=bufs)
                     return bufs

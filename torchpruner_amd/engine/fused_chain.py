@@ -821,6 +821,41 @@ class FusedChainEngine:
         g["graph"].replay()
         return {b: arena[b] for b in want}
 
+    def apoz_graphed(self, x: torch.Tensor, blocks, slot: int = 0) -> dict:
+        """``forward(x, stop_after=max(blocks), apoz=zeroed (B, width) count buffers)`` replayed from
+        a captured HIP graph (one per input shape, blocks and pipeline slot; the first call of a
+        key runs eagerly). Returns the count buffers: graph outputs that stay valid until this
+        slot's next replay (the stream pipeline folds them on the same stream first)."""
+        P = self._pack()
+        blocks = tuple(sorted(blocks))
+        key = ("apoz", tuple(x.shape), x.dtype, str(x.device), blocks, slot, self.bf16)
+        g = self._graphs.get(key)
+        if g is not None and g["P"] is not P:
+            g = None
+
+        def run(xx):
+            bufs = {b: torch.zeros(xx.shape[0], self._block_width(b), device=xx.device) for b in blocks}
+            self.forward(xx, stop_after=blocks[-1], apoz=bufs)
+            return bufs
+
+        if g is None:
+            if self._graphs.get(("seen",) + key) is not P:
+                self._graphs[("seen",) + key] = P
+                return run(x)
+            sx = x.clone()
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(x.device)
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            with torch.cuda.graph(graph, stream=side):
+                bufs = run(sx)
+            torch.cuda.current_stream(x.device).wait_stream(side)
+            if len(self._graphs) > 64:
+                self._graphs.clear()
+            g = self._graphs[key] = {"graph": graph, "x": sx, "P": P, "bufs": bufs}
+        g["x"].copy_(x)
+        g["graph"].replay()
+        return g["bufs"]
+
     def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None, mode="taylor",
                criterion=None):
         """One fused forward+backward (``criterion``: see :func:`logits_grad`); returns {block index: per-sample signed Taylor sums
