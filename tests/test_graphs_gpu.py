@@ -161,3 +161,36 @@ def test_pipelined_apoz_graph_replay_matches_eager(cuda):
     for a, b in zip(out["1"], out["0"]):
         np.testing.assert_array_equal(a, b)
     assert any(k[0] == "apoz" for k in eng._graphs), "no APoZ graph was captured"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layer", [0, 6, 9])
+def test_shapley_graphed_prefix_chunks_bit_identical(cuda, layer):
+    """Shapley on the fused engine replays one graph per prefix-chunk size (the prefix offset
+    enters as a shifted rank vector): scores equal the eager launches bit for bit, on the
+    capturing run and on a pure-replay rerun (ragged last chunk included)."""
+    from torchpruner_amd import ShapleyAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(4)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    x = torch.randn(120, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (120,), device=cuda)
+
+    def run(env):
+        old = os.environ.get("TORCHPRUNER_GRAPHS")
+        os.environ["TORCHPRUNER_GRAPHS"] = env
+        try:
+            np.random.seed(0)
+            m = ShapleyAttributionMetric(model, DeviceLoader(x, y, 40), F.cross_entropy, cuda, sv_samples=2)
+            return m.run(convs[layer], find_best_evaluation_module=True)
+        finally:
+            if old is None:
+                del os.environ["TORCHPRUNER_GRAPHS"]
+            else:
+                os.environ["TORCHPRUNER_GRAPHS"] = old
+
+    ref = run("0")
+    for _ in range(2):
+        np.testing.assert_array_equal(run("auto"), ref)

@@ -25,6 +25,7 @@ MI355X-native execution:
 from __future__ import annotations
 
 import logging
+import os
 
 import numpy as np
 import torch
@@ -248,11 +249,15 @@ class ShapleyAttributionMetric(_AttributionMetric):
             B = zk.shape[0]
             z_cl = zk.permute(0, 3, 1, 2)  # (B, C, H, W) view, channels_last strides
             base = engine.loss_from(k, zk, y, crit)
+            # masked-copy chunks replay a HIP graph per chunk size (fused cross-entropy only)
+            st = engine.shapley_static(k, zk, y) if not delta and crit is None and _graphs_on() else None
 
             def evaluate(rank_t, p_first, cnt):
                 if delta:  # next block is a Linear: prefix-delta GEMM (no masked copies)
                     return engine.prefix_delta_loss(k, zk, perm_of(rank_t), pad_rank(rank_t, zk.shape[3]), p_first,
                                                     cnt, y, crit)
+                if st is not None:
+                    return engine.shapley_eval(st, pad_rank(rank_t, zk.shape[3]), p_first, cnt)
                 masked = ops.prefix_mask(z_cl, pad_rank(rank_t, zk.shape[3]), p_first, cnt)  # channels_last
                 loss = engine.loss_from(k, masked.permute(0, 2, 3, 1), y.repeat(cnt), crit)
                 return loss.view(cnt, B)
@@ -381,6 +386,11 @@ def _mask_stacked(out, rank, p0, K):
     o = out.reshape((K, -1) + tuple(out.shape[1:]))
     keep = keep.view((K, 1, C) + (1,) * (out.dim() - 2))
     return torch.where(keep, o, torch.zeros((), dtype=out.dtype, device=out.device)).reshape(out.shape)
+
+
+def _graphs_on() -> bool:
+    """HIP-graph replay of the fused engine's prefix chunks (TORCHPRUNER_GRAPHS != "0")."""
+    return os.environ.get("TORCHPRUNER_GRAPHS", "auto") != "0"
 
 
 class _RankPadder:

@@ -821,6 +821,56 @@ class FusedChainEngine:
         g["graph"].replay()
         return {b: arena[b] for b in want}
 
+    # ------------------------------------------------------------------ Shapley prefix evaluations
+    def shapley_static(self, k: int, zk: torch.Tensor, y: torch.Tensor) -> dict:
+        """Static device buffers of a Shapley prefix evaluation of block ``k``'s output (one
+        batch): the activation, the labels and the shifted rank vector that the captured graphs
+        of :meth:`shapley_eval` read. Copies this batch in (two launches per batch)."""
+        key = ("sv_static", k, tuple(zk.shape), tuple(y.shape), str(zk.device))
+        st = self._graphs.get(key)
+        if st is None:
+            st = self._graphs[key] = {"z": torch.empty_like(zk), "y": torch.empty_like(y), "rank": None,
+                                      "graphs": {}, "seen": {}, "k": k}
+        st["z"].copy_(zk)
+        st["y"].copy_(y)
+        return st
+
+    def shapley_eval(self, st: dict, rank_padded: torch.Tensor, p_first: int, cnt: int) -> torch.Tensor:
+        """Per-sample losses (cnt, B) of prefixes p_first .. p_first+cnt-1 (units of rank < p
+        zeroed) of the activation in ``st``, replayed from a HIP graph per ``cnt``: the prefix
+        offset enters as a shifted rank vector (rank - p_first, one eager launch) so the graph
+        holds the mask kernel with p0 = 0 (rank < p0 + j <=> rank - p0 < j: the same mask, the
+        same losses bit for bit). A prefix chunk is otherwise ~20-40 launches of small work:
+        shallow layers were host-bound (profiles/bench/host_bound_probe_paths.txt)."""
+        P = self._pack()
+        if st["rank"] is None or st["rank"].shape != rank_padded.shape:
+            st["rank"] = torch.empty_like(rank_padded)
+            st["graphs"].clear()
+        torch.sub(rank_padded, p_first, out=st["rank"])
+        B = st["z"].shape[0]
+
+        def run():
+            z_cl = st["z"].permute(0, 3, 1, 2)  # channels_last view
+            masked = ops.prefix_mask(z_cl, st["rank"], 0, cnt)
+            return self.loss_from(st["k"], masked.permute(0, 2, 3, 1), st["y"].repeat(cnt)).view(cnt, B)
+
+        g = st["graphs"].get(cnt)
+        if g is not None and g["P"] is not P:
+            g = None
+        if g is None:
+            if st["seen"].get(cnt) is not P:  # first use of this chunk size: eager (autotunes, allocates)
+                st["seen"][cnt] = P
+                return run()
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(st["z"].device)
+            side.wait_stream(torch.cuda.current_stream(st["z"].device))
+            with torch.cuda.graph(graph, stream=side):
+                out = run()
+            torch.cuda.current_stream(st["z"].device).wait_stream(side)
+            g = st["graphs"][cnt] = {"graph": graph, "out": out, "P": P}
+        g["graph"].replay()
+        return g["out"].clone()  # the caller keeps the last row across the next replay
+
     def apoz_graphed(self, x: torch.Tensor, blocks, slot: int = 0) -> dict:
         """``forward(x, stop_after=max(blocks), apoz=zeroed (B, width) count buffers)`` replayed from
         a captured HIP graph (one per input shape, blocks and pipeline slot; the first call of a
