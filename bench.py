@@ -33,6 +33,8 @@ Throughput (timed; BASELINE.json config #2, scaled to N GPUs):
 Other BASELINE configs in the same run (all ranks, sharded like the headline):
 * ``resnet50_apoz_img_s`` / ``resnet50_taylor_img_s``: config #3, ResNet-50 224x224 B=256 per
   GPU, every prunable bottleneck conv in one ``run_many`` on the ResNet engine.
+* ``vgg_taylor_b100_img_s``: the headline's fp32 Taylor run_many at the reference's attribution
+  batch B=100 per GPU (200 timed steps; small batches replay HIP graphs, four in flight).
 * ``shapley_vgg_img_evals_s``: config #4, Shapley sv_samples=5 over 1000 images (B=100, the
   nbVGG setup) at conv layers 0 / 6 / 12, downstream image-evaluations per second.
 
@@ -312,6 +314,21 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
                                            "score accumulators", "spearman_per_layer": [round(r, 5) for r in rho]}
     log(f"[bench] opt-in bf16 engine: {out['vgg_taylor_bf16_img_s']:.0f} img/s (x{out['bf16_vs_fp32_engine']} "
         f"fp32), min per-layer Spearman vs fp32 {min(rho):.4f} ({time.perf_counter() - t0:.1f}s)")
+
+    # 1c. the same fp32 Taylor run_many at the reference's attribution batch B=100 (nbVGG:193-196):
+    # small batches run four in flight, each replaying a captured HIP graph of its step
+    t0 = time.perf_counter()
+    sb, s_steps = 100, 200
+    TaylorAttributionMetric(model, loader(12, args.seed + 15, sb), F.cross_entropy, dev).run_many(
+        convs, find_best_evaluation_module=True)  # tune + capture (untimed)
+    sm = TaylorAttributionMetric(model, loader(s_steps, args.seed + 16, sb), F.cross_entropy, dev)
+    _, sdt = timed_run(sm, convs)
+    assert sm.last_path["path"] == "fused", sm.last_path
+    out["vgg_taylor_b100_img_s"] = round(s_steps * sb * world / sdt, 1)
+    out["b100_config"] = {"per_gpu_batch": sb, "steps": s_steps, "dtype": "fp32",
+                          "pipeline": "4 batches in flight on 4 HIP streams, per-slot HIP-graph replay"}
+    log(f"[bench] B=100 (reference attribution batch): {out['vgg_taylor_b100_img_s']:.0f} img/s "
+        f"({time.perf_counter() - t0:.1f}s)")
 
     # 2. config #3: ResNet-50, ImageNet shape, B=256 per GPU, every prunable bottleneck conv
     t0 = time.perf_counter()
