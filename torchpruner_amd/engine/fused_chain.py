@@ -772,7 +772,7 @@ class FusedChainEngine:
     # the GPU finishes a B=100 step (~55 launches) faster than Python enqueues it: the host spent
     # 0.77-0.99 ms per batch in the pipeline against 0.85-1.04 ms of wall
     # (scripts/b100_host_probe.py), so the pipelined launches replay one graph per slot.
-    GRAPH_MAX_B = 1024
+    GRAPH_MAX_B = int(os.environ.get("TORCHPRUNER_GRAPH_MAX_B", "1024"))
 
     def graphs_enabled(self, B: int, pipelined: bool = False) -> bool:
         mode = os.environ.get("TORCHPRUNER_GRAPHS", "auto")
