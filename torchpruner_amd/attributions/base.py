@@ -429,7 +429,7 @@ class _AttributionMetric(ABC):
             def launch(slot, x=x, y=y):
                 arena = engine.score_arena(x.shape[0], uniq, x.device, tuple(x.shape[2:]), slot=slot)
                 if engine.graphs_enabled(x.shape[0], pipelined=True):  # host-bound otherwise
-                    engine.taylor_graphed(x, y, set(uniq), arena, mode=mode)
+                    engine.taylor_graphed(x, y, set(uniq), arena, mode=mode, warm=True)
                 else:
                     engine.taylor(x, y, set(uniq), arena, mode=mode)
                 return arena
@@ -600,20 +600,21 @@ class _BatchPipeline:
     is off for inputs of >= 2^24 pixels per batch (B >= 16384 at 32x32, B >= 335 at 224x224;
     TORCHPRUNER_STREAMS_MAX_PIXELS overrides), with TORCHPRUNER_GRAPHS=1/all (one graph-replayed
     batch at a time), and with TORCHPRUNER_STREAMS=0. ResNet-50 at B=256: APoZ +8%, Taylor +7%.
-    On the fused VGG/MLP engine a pipelined batch of up to 1024 images replays a HIP graph of its
-    step per slot (FusedChainEngine.graphs_enabled): with two batches in flight the B=100 step is
-    host-bound otherwise."""
+    On the fused VGG/MLP engine a pipelined batch replays a HIP graph of its step per slot
+    (FusedChainEngine.graphs_enabled), captured on the slot's first batch: with two batches in
+    flight the B=100 step is host-bound otherwise."""
 
     MAX_PIXELS = 1 << 24
+    DEEP_MAX_PIXELS = 1 << 18  # four in flight up to B=256 at 32x32 (B=512 even, B=1024 / 2048 -4%)
 
     def __init__(self, engine, graph_replay: bool = False):
         self.engine = engine
         self.graph_replay = graph_replay  # the caller's launch() replays graphs when graphs_enabled(B, True)
         self.enabled = os.environ.get("TORCHPRUNER_STREAMS", "1") != "0"
         self.max_pixels = int(os.environ.get("TORCHPRUNER_STREAMS_MAX_PIXELS", self.MAX_PIXELS))
-        # batches in flight: 4 when the batches replay graphs (host-light: B=100 +10-19% over 2,
-        # B=256 +4%, profiles/bench/pipeline_depth_graphs.txt), else 2 (eager launches: the host is
-        # the limit beyond two)
+        # batches in flight: 4 when the batches replay graphs and are small (host-light: B=100
+        # +10-19% over 2, B=256 +4%, profiles/bench/pipeline_depth_graphs.txt; at B=2048 four cost
+        # 4%, profiles/bench/large_batch_graphs_vs_eager.txt), else 2
         env_depth = os.environ.get("TORCHPRUNER_STREAMS_DEPTH")
         self.depth = max(2, int(env_depth)) if env_depth else None
         self.streams = None
@@ -634,7 +635,9 @@ class _BatchPipeline:
             return False
         if self.streams is None:
             if self.depth is None:
-                self.depth = 4 if self.graph_replay and graphs is not None and graphs(x.shape[0], pipelined=True) else 2
+                small = x.shape[0] * math.prod(x.shape[2:]) <= self.DEEP_MAX_PIXELS
+                self.depth = 4 if small and self.graph_replay and graphs is not None and \
+                    graphs(x.shape[0], pipelined=True) else 2
             self.streams = [torch.cuda.Stream(x.device) for _ in range(self.depth)]
         cur = torch.cuda.current_stream(x.device)
         slot = self.n % self.depth

@@ -57,7 +57,7 @@ class APoZAttributionMetric(_AttributionMetric):
 
                 def launch(slot, x=x):
                     if engine.graphs_enabled(x.shape[0], pipelined=True):  # host-bound otherwise
-                        return engine.apoz_graphed(x, uniq, slot)
+                        return engine.apoz_graphed(x, uniq, slot, warm=True)
                     bufs = {b: torch.zeros(x.shape[0], engine._block_width(b), device=x.device) for b in uniq}
                     engine.forward(x, stop_after=uniq[-1], apoz=bufs)
                     return bufs

@@ -771,7 +771,10 @@ class FusedChainEngine:
     # GPU-bound down to B=8 (profiles/hip_graphs_taylor_step.txt), but with two batches in flight
     # the GPU finishes a B=100 step (~55 launches) faster than Python enqueues it: the host spent
     # 0.77-0.99 ms per batch in the pipeline against 0.85-1.04 ms of wall
-    # (scripts/b100_host_probe.py), so the pipelined launches replay one graph per slot.
+    # (scripts/b100_host_probe.py), so the pipelined launches replay one graph per slot. Large
+    # batches are GPU-bound: replay trims ~1% at B=2048, but the graphs' multi-GB private pools
+    # then slowed later small-batch work in the same process by 7-17%
+    # (profiles/bench/large_batch_graphs_vs_eager.txt), so the default stops at 1024.
     GRAPH_MAX_B = int(os.environ.get("TORCHPRUNER_GRAPH_MAX_B", "1024"))
 
     def graphs_enabled(self, B: int, pipelined: bool = False) -> bool:
@@ -783,7 +786,7 @@ class FusedChainEngine:
         return mode == "1" and B <= self.GRAPH_MAX_B
 
     def taylor_graphed(self, x: torch.Tensor, y: torch.Tensor, want: set, arena: dict, mode="taylor",
-                       criterion=None):
+                       criterion=None, warm: bool = False):
         """``taylor()`` replayed from a captured HIP graph: the ~40 launches of one fused
         forward + input-gradient backward become one graph launch, which is what small,
         launch-bound batches need. One graph per (input shapes, blocks, mode, score arena,
@@ -791,7 +794,9 @@ class FusedChainEngine:
         and builds the lazily packed operands), the second captures, later calls copy the batch
         into the graph's static inputs and replay. Re-packed weights (pruning, training) or a
         new arena invalidate the graph. ``arena`` must be zero before each call, as for
-        ``taylor()`` (ops.score_fold_ with after=2 leaves it so)."""
+        ``taylor()`` (ops.score_fold_ with after=2 leaves it so). ``warm=True``: the caller ran
+        this shape eagerly already (kernels tuned, operands packed): capture on the first call
+        (the stream pipeline's first batch of a shape runs alone, eagerly)."""
         if criterion is not None:  # a user criterion runs through autograd: eager launches
             return self.taylor(x, y, want, arena, mode, criterion)
         P = self._pack()
@@ -803,7 +808,7 @@ class FusedChainEngine:
             g = None
         if g is None:
             seen = self._graphs.get(("seen",) + key)
-            if seen is None or seen[0] is not P or seen[1] is not arena:
+            if not warm and (seen is None or seen[0] is not P or seen[1] is not arena):
                 self._graphs[("seen",) + key] = (P, arena)
                 return self.taylor(x, y, want, arena, mode)
             sx, sy = x.clone(), y.clone()
@@ -871,11 +876,12 @@ class FusedChainEngine:
         g["graph"].replay()
         return g["out"].clone()  # the caller keeps the last row across the next replay
 
-    def apoz_graphed(self, x: torch.Tensor, blocks, slot: int = 0) -> dict:
+    def apoz_graphed(self, x: torch.Tensor, blocks, slot: int = 0, warm: bool = False) -> dict:
         """``forward(x, stop_after=max(blocks), apoz=zeroed (B, width) count buffers)`` replayed from
         a captured HIP graph (one per input shape, blocks and pipeline slot; the first call of a
         key runs eagerly). Returns the count buffers: graph outputs that stay valid until this
-        slot's next replay (the stream pipeline folds them on the same stream first)."""
+        slot's next replay (the stream pipeline folds them on the same stream first). ``warm``:
+        as for :meth:`taylor_graphed`."""
         P = self._pack()
         blocks = tuple(sorted(blocks))
         key = ("apoz", tuple(x.shape), x.dtype, str(x.device), blocks, slot, self.bf16)
@@ -889,7 +895,7 @@ class FusedChainEngine:
             return bufs
 
         if g is None:
-            if self._graphs.get(("seen",) + key) is not P:
+            if not warm and self._graphs.get(("seen",) + key) is not P:
                 self._graphs[("seen",) + key] = P
                 return run(x)
             sx = x.clone()
