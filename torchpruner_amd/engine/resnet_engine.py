@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, cpad, logits_grad, winograd_weights
+from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, cpad, logits_grad, taylor_slots, winograd_weights
 
 
 @dataclass
@@ -324,10 +324,14 @@ class ResNetEngine:
             e["wt"] = w4.permute(3, 1, 2, 0).reshape(ci, ks * ks * co).contiguous()
         return e
 
-    def _dgrad(self, T, e, g, mask, res=None, res_stride=1, low_res=False):
+    def _dgrad(self, T, e, g, mask, res=None, res_stride=1, low_res=False, taylor=False):
         """dL/d(input) of conv ``e`` from g = dL/d(conv output) (BN scale folded in), plus
         ``res``, masked by ``mask`` (the input's post-ReLU activation). ``low_res``: a strided
-        1x1 conv's gradient at the output resolution (scattered by the consumer's res_stride)."""
+        1x1 conv's gradient at the output resolution (scattered by the consumer's res_stride).
+        Returns (gradient, Taylor slab or None): with ``taylor`` and a Winograd kernel chosen,
+        the dgrad epilogue also writes the per-(image, channel) partial sums of -(dL/da * a),
+        a = ``mask``, into an (R, B, C) slab (one writer per element: deterministic), which
+        saves the separate channel reduction's read of both tensors."""
         e = self._bwd_operands(e)
         B, H, W, C = g.shape
         ks, s = e["ks"], e["stride"]
@@ -346,14 +350,17 @@ class ResNetEngine:
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
         key = ("rbwd", tuple(g.shape), N, ks, s, transposed, res is not None, res_stride, mask is not None)
 
-        def run(cfg, sp, gg=g, rr=res, mm=mask):
+        def run(cfg, sp, gg=g, rr=res, mm=mask, tay=None):
             if cfg in (WINO, WINO_LDS):
-                return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, None, True, sp, cfg == WINO_LDS)
+                return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, tay, True, sp, cfg == WINO_LDS, 0)
             return T.conv_gen_bwd(gg, e["wt"], rr, res_stride, mm, ks, s if transposed else 1, pad, Ho, Wo,
                                   transposed, cfg, sp)
 
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands)
-        return run(cfg, sp)
+        if taylor and cfg in (WINO, WINO_LDS):
+            tay = torch.zeros(taylor_slots(Ho, Wo), B, N, device=g.device)
+            return run(cfg, sp, tay=tay), tay
+        return run(cfg, sp), None
 
     def grad_scores(self, x: torch.Tensor, y: torch.Tensor, want, mode: str, criterion=None):
         """One engine forward + input-gradient-only backward of the loss (mean cross-entropy on
@@ -383,18 +390,22 @@ class ResNetEngine:
             g = g_s
             for ci in range(len(blk.convs) - 1, 0, -1):
                 a_prev = inner[ci - 1]
-                g = self._dgrad(T, e["convs"][ci], g, a_prev)  # dL/d(bn_{ci} output), ReLU-masked
                 bn = blk.convs[ci - 1].bn
-                if bn in want:
+                fuse = bn in want and mode in ("taylor", "taylor_signed")
+                g, tay = self._dgrad(T, e["convs"][ci], g, a_prev, taylor=fuse)  # dL/d(bn_{ci} output), masked
+                if tay is not None:  # Taylor partials from the Winograd dgrad epilogue
+                    sums = tay.sum(0)
+                    out[bn] = sums.abs_() if mode == "taylor" else sums
+                elif bn in want:
                     out[bn] = ops.channel_reduce(a_prev.permute(0, 3, 1, 2), g.permute(0, 3, 1, 2), mode)
             if bi == first:
                 break
             if e["ds"] is not None:
-                g_res = self._dgrad(T, e["ds"], g_s, None, low_res=True)
+                g_res, _ = self._dgrad(T, e["ds"], g_s, None, low_res=True)
                 rs = e["ds"]["stride"]
             else:
                 g_res, rs = g_s, 1
-            g_s = self._dgrad(T, e["convs"][0], g, x_in, res=g_res, res_stride=rs)
+            g_s, _ = self._dgrad(T, e["convs"][0], g, x_in, res=g_res, res_stride=rs)
         return out
 
     def eval_modules(self):
