@@ -139,6 +139,12 @@ def run(args) -> int:
                   "visible (set TORCHPRUNER_SHARE_GPU=1 with TORCHPRUNER_DIST_BACKEND=gloo to rehearse)",
                   file=sys.stderr, flush=True)
             return 3
+    if world_env > 1:
+        # the generic-path extra runs MIOpen: give every rank its own user perf-db / kernel cache so
+        # N processes finding and compiling the same convolutions never contend for one database
+        tag = f"{os.environ.get('RANK', '0')}_{os.getpid()}"
+        os.environ.setdefault("MIOPEN_USER_DB_PATH", f"/tmp/tp_miopen_db_{tag}")
+        os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", f"/tmp/tp_miopen_cache_{tag}")
     ctx = pdist.init_distributed()
     dev = ctx.device
     world, rank = ctx.world_size, ctx.rank
