@@ -194,3 +194,22 @@ def test_shapley_graphed_prefix_chunks_bit_identical(cuda, layer):
     ref = run("0")
     for _ in range(2):
         np.testing.assert_array_equal(run("auto"), ref)
+
+
+@pytest.mark.gpu
+def test_invalidate_after_data_edit(cuda):
+    """``param.data`` in-place edits bypass the version counter the engines key their packed
+    weights on; ``engine.invalidate(model)`` drops the cached engine (and its graphs)."""
+    from torchpruner_amd.engine import invalidate
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(5)
+    model = prunable_vgg16().to(cuda).eval()
+    x = torch.randn(64, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (64,), device=cuda)
+    _scores(model, x, y, 16, "auto")
+    model.features[0].weight.data.mul_(1.7)  # no version bump
+    assert invalidate(model)
+    got = _scores(model, x, y, 16, "auto")
+    ref = _scores(model, x, y, 16, "0")
+    for a, r in zip(got, ref):
+        np.testing.assert_array_equal(a, r)

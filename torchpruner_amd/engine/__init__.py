@@ -8,7 +8,22 @@ from .fused_chain import FusedChainEngine, Plan, build_plan, criterion_is_cross_
 from .resnet_engine import ResNetEngine, build_resnet_plan, maybe_resnet_engine
 
 __all__ = ["FusedChainEngine", "Plan", "build_plan", "criterion_is_cross_entropy", "maybe_engine", "ResNetEngine",
-           "build_resnet_plan", "maybe_resnet_engine", "native_logits"]
+           "build_resnet_plan", "maybe_resnet_engine", "native_logits", "invalidate"]
+
+
+def invalidate(model) -> bool:
+    """Drop the native engines cached for ``model`` (packed weights, autotuned plans, captured HIP
+    graphs). The engines re-pack when a parameter's storage or version counter changes, which
+    covers optimizer steps, ``load_state_dict``, pruning and in-place edits under ``no_grad``;
+    in-place edits through ``param.data`` bypass the version counter, so call this after them.
+    Returns True when something was cached."""
+    from . import fused_chain, resnet_engine
+    hit = False
+    for cache in (fused_chain._ENGINES, resnet_engine._ENGINES):
+        if model in cache:
+            del cache[model]
+            hit = True
+    return hit
 
 
 @torch.no_grad()
