@@ -70,6 +70,12 @@ hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H, int W, int
                         const float* shift, int relu, const float* res, int res_stride, const float* mask,
                         float* apoz, float* out, float* ws, double* bnpart, hipStream_t st);
 int tp_conv_tile_m(int cfg);
+hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                        int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
+                        const float* shift, int relu, const float* res, int res_stride, const float* mask,
+                        float* apoz, float* out, float* ws, double* bnpart, float* tay_part, int tay_mode,
+                        hipStream_t st);
+int tp_conv_gen_tay_slots(int cfg, int HWo);
 hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
                                float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
                                float* b, double* ws, const double* pre, int G, const float* res, int relu, uint8_t* mko,
@@ -631,7 +637,8 @@ at::Tensor nchw_to_nhwc_pad(const at::Tensor& x, int64_t Cp) {
 // Epilogue: v (+ res, res_stride-scattered) then out = mask > 0 ? v : 0 when mask is given.
 at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::optional<at::Tensor>& res,
                         int64_t res_stride, const c10::optional<at::Tensor>& mask, int64_t ks, int64_t stride,
-                        int64_t pad, int64_t Ho, int64_t Wo, bool transposed, int64_t cfg, int64_t splits) {
+                        int64_t pad, int64_t Ho, int64_t Wo, bool transposed, int64_t cfg, int64_t splits,
+                        const c10::optional<at::Tensor>& taylor, int64_t tay_mode) {
   need(g, "g", 4);
   need(wt, "wt", 2);
   const int64_t B = g.size(0), H = g.size(1), W = g.size(2), C = g.size(3), N = wt.size(0);
@@ -668,14 +675,28 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
   int64_t sp = transposed ? 1 : std::max<int64_t>(1, std::min<int64_t>(splits, kt));
   const int64_t per = (kt + sp - 1) / sp;
   sp = (kt + per - 1) / per;
+  float* tp_ = nullptr;
+  if (taylor.has_value() && taylor->defined()) {
+    // fused Taylor / Sensitivity partials (R, B, N) of the masked output (1x1, stride 1, one K pass)
+    const int R = tp_conv_gen_tay_slots((int)cfg, (int)(Ho * Wo));
+    TORCH_CHECK(!transposed && ks == 1 && mp != nullptr && sp == 1 && R > 0,
+                "conv_gen_bwd taylor partials need a 1x1 stride-1 dgrad with a mask, one K pass, and a tile "
+                "config spanning <= 4 images");
+    TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
+                    taylor->numel() == (int64_t)R * B * N,
+                "taylor must be a contiguous float32 (R, B, N) GPU tensor with R = ", R);
+    tp_ = taylor->data_ptr<float>();
+  }
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * Ho * Wo * N}, g.options());
-  TP_CHECK_HIP(tp_conv_gen2(g.data_ptr<float>(), wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)N,
+  TP_CHECK_HIP(tp_conv_gen4(g.data_ptr<float>(), wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)N,
                             (int)ks, (int)stride, (int)pad, transposed ? 1 : 0, (int)Ho, (int)Wo, (int)cfg, (int)sp,
                             nullptr, nullptr, 0, rp, (int)res_stride, mp, nullptr, out.data_ptr<float>(),
-                            sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                            sp > 1 ? ws.data_ptr<float>() : nullptr, nullptr, tp_, (int)tay_mode, cur_stream()));
   return out;
 }
+
+int64_t conv_gen_tay_slots(int64_t cfg, int64_t HWo) { return tp_conv_gen_tay_slots((int)cfg, (int)HWo); }
 
 // Weight gradient: g (B, Ho, Wo, Cout) and x (B, H, W, Cin) NHWC -> dW (Cout, Kpad) with column
 // k = (kh, kw, ci) (Kpad = ks*ks*Cin rounded up to 32; padded columns are zero).
@@ -890,7 +911,8 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_gen_stats(Tensor x, Tensor w, Tensor? shift, int ks, int stride, int pad, int cfg) -> (Tensor, Tensor)");
   m.def("wino_wgrad(Tensor g, Tensor x, int cfg, int splits, Tensor(a!) out) -> ()");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
-        "int Ho, int Wo, bool transposed, int cfg, int splits) -> Tensor");
+        "int Ho, int Wo, bool transposed, int cfg, int splits, Tensor(a!)? taylor=None, int tay_mode=0) -> Tensor");
+  m.def("conv_gen_tay_slots(int cfg, int HWo) -> int", &conv_gen_tay_slots);
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits, Tensor(a!)? apoz=None, float slope=0.0) -> (Tensor, Tensor)");

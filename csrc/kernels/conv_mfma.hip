@@ -41,6 +41,8 @@ enum Epi : int {
   EPI_FWD_POOL = 1,  // + 2x2 max-pool: pooled value + argmax byte
   EPI_BWD = 2,       // dgrad epilogue: Taylor partial of the consumer's activation, masked/scaled grad
   EPI_PARTIAL = 3,   // raw split-K partial slab (epilogue applied by conv_epilogue)
+  EPI_FWD_TAY = 4,   // GEN 1x1 data gradient: EPI_FWD's LDS epilogue + Taylor partials (tay_part); a
+                     // separate instantiation so the partials' registers never burden EPI_FWD
 };
 
 struct ConvArgs {
@@ -81,7 +83,14 @@ struct ConvArgs {
                             // broadcast over row blocks: Shapley prefix-delta GEMM)
   double* bnpart;           // GEN EPI_FWD LDS epilogue, no split: per M tile the column sums and sums of
                             // squares of the stored outputs, [m_tile][2][N] (training BN statistics)
+  float* tay_part;          // GEN EPI_FWD LDS epilogue with a mask (data gradient), no split: Taylor
+                            // partials -(v * mask) (tay_mode 1: |v|) per (image, column) of every M
+                            // tile, slot r = m_tile - first tile of the image: [R][B][N], one writer each
 };
+
+// Taylor slots R of the GEN epilogue partials for tile height bm: the M tiles an image can touch
+__host__ __device__ constexpr int gen_tay_slots(int bm, int HWo) { return (HWo + bm - 2) / bm + 1; }
+constexpr int GEN_TAY_IMG = 4;  // images per tile the epilogue partials support (host-checked)
 
 // GEN 3 output row m -> (image, oh, ow). Parity order makes each stride-2 phase class one
 // contiguous range of B*Ho*Wo/4 rows: all but the (at most 3) boundary tiles see ONE class and
@@ -492,7 +501,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
 
   // ---- GEN forward / partial epilogue: transpose through LDS, float4 rows ---------------
   // (memory-bound 1x1 convs: scalar per-lane stores + residual loads ran at ~2 TB/s)
-  if constexpr (GEN != 0 && (EPI == EPI_FWD || EPI == EPI_PARTIAL)) {
+  if constexpr (GEN != 0 && (EPI == EPI_FWD || EPI == EPI_FWD_TAY || EPI == EPI_PARTIAL)) {
    if (p.epi_lds) {
     constexpr int LDT = BN + 4;
     constexpr int CB_IMG = 8;  // images per block whose counts are reduced in LDS
@@ -500,7 +509,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     float* ts = smem;  // the main loop ended with a barrier
     float* cb = smem + BM * LDT;  // APoZ counts [image in block][column]
     const int b_first = m0 / p.HWo;
-    const bool cb_lds = EPI == EPI_FWD && p.apoz && (min(m0 + BM, p.M) - 1) / p.HWo - b_first < CB_IMG;
+    const bool cb_lds = (EPI == EPI_FWD || EPI == EPI_FWD_TAY) && p.apoz && (min(m0 + BM, p.M) - 1) / p.HWo - b_first < CB_IMG;
     if (cb_lds)
       for (int t = tid; t < CB_IMG * BN; t += T::NT) cb[t] = 0.f;
 #pragma unroll
@@ -517,13 +526,17 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     const int n = n0 + c4 * 4;
     const bool ncol_ok = n < p.N;
     float4 sc4 = make_float4(1.f, 1.f, 1.f, 1.f), sh4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == EPI_FWD) {
+    if constexpr (EPI == EPI_FWD || EPI == EPI_FWD_TAY) {
       if (ncol_ok && p.scale) sc4 = *reinterpret_cast<const float4*>(p.scale + n);
       if (ncol_ok && p.shift) sh4 = *reinterpret_cast<const float4*>(p.shift + n);
     }
     int cur_b = -1;
     float4 cnt = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 bs = make_float4(0.f, 0.f, 0.f, 0.f), bq = bs;  // bnpart: this thread's column-quad sums
+    constexpr int NTQ = EPI == EPI_FWD_TAY ? GEN_TAY_IMG : 1;
+    float4 tq[NTQ];  // tay_part: this thread's column-quad partial per image slot of the tile
+#pragma unroll
+    for (int i = 0; i < NTQ; ++i) tq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     // rows are visited in passes of RSTEP; the residual / mask quads of PF passes are loaded
     // together first (PF global loads in flight per thread instead of one round trip per row)
     constexpr int RSTEP = T::NT / C4, RPT = BM / RSTEP, PF = RPT < 4 ? RPT : 4;
@@ -583,6 +596,25 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           v.w = nan_act(v.w, p.slope);
         }
         *reinterpret_cast<float4*>(p.out + o) = v;
+        if constexpr (EPI == EPI_FWD_TAY) {
+          if (p.tay_part) {  // slot by image (static selects: no dynamic register indexing)
+            const int sl = m / p.HWo - b_first;
+            float4 t;
+            if (p.tay_mode) {
+              t = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
+            } else {
+              t = make_float4(-(v.x * mq[u].x), -(v.y * mq[u].y), -(v.z * mq[u].z), -(v.w * mq[u].w));
+            }
+#pragma unroll
+            for (int i = 0; i < NTQ; ++i)
+              if (sl == i) {
+                tq[i].x += t.x;
+                tq[i].y += t.y;
+                tq[i].z += t.z;
+                tq[i].w += t.w;
+              }
+          }
+        }
         if (p.bnpart) {
           bs.x += v.x;
           bs.y += v.y;
@@ -614,7 +646,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
       }
       }
     }
-    if constexpr (EPI == EPI_FWD) {
+    if constexpr (EPI == EPI_FWD || EPI == EPI_FWD_TAY) {
       if (p.apoz && cur_b >= 0) {
         float* ap = cb_lds ? cb + (cur_b - b_first) * BN + c4 * 4 : p.apoz + (long long)cur_b * p.N + n;
         if (cnt.x > 0.f) atomicAdd(ap, cnt.x);
@@ -642,6 +674,25 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
 #pragma unroll 4
           for (int r = 0; r < RSTEP; ++r) acc += (double)red[(which * RSTEP + r) * BN + col];
           if (n0 + col < p.N) p.bnpart[((long long)(m0 / BM) * 2 + which) * p.N + n0 + col] = acc;
+        }
+      }
+      if (EPI == EPI_FWD_TAY && p.tay_part) {  // fold the RSTEP row lanes per (image slot, column), fixed order
+        static_assert(GEN_TAY_IMG * RSTEP * BN <= BM * LDT, "Taylor partial staging must fit in the tile");
+        __syncthreads();  // the tile in ts (and any bnpart staging) is no longer read
+        float* red = ts;  // [slot][RSTEP][BN]
+#pragma unroll
+        for (int i = 0; i < NTQ; ++i) *reinterpret_cast<float4*>(red + (i * RSTEP + row0) * BN + c4 * 4) = tq[i];
+        __syncthreads();
+        const int n_img = min((min(m0 + BM, p.M) - 1) / p.HWo - b_first + 1, NTQ);
+        const int B = p.M / p.HWo, R = gen_tay_slots(BM, p.HWo);
+        for (int t = tid; t < n_img * BN; t += T::NT) {
+          const int sl = t / BN, col = t - sl * BN;
+          float acc = 0.f;
+#pragma unroll 4
+          for (int r = 0; r < RSTEP; ++r) acc += red[(sl * RSTEP + r) * BN + col];
+          const int b = b_first + sl;
+          const int slot = m0 / BM - (b * p.HWo) / BM;
+          if (n0 + col < p.N && slot < R) p.tay_part[((long long)slot * B + b) * p.N + n0 + col] = acc;
         }
       }
     }
@@ -1415,13 +1466,39 @@ extern "C" int tp_conv_tile_m(int cfg) {
   }
 }
 
-// ``bnpart`` (nullable): [ceil(M / tile_m(cfg))][2][Cout] doubles receiving the per-tile column
-// sums / sums of squares of the output (training BatchNorm statistics); no split-K then.
+extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   double* bnpart, float* tay_part, int tay_mode, hipStream_t st);
+
+// Taylor partial slots of tp_conv_gen4's ``tay_part`` for tile config cfg at Ho*Wo output pixels
+// per image; 0 = the config cannot produce them (a tile would span more than GEN_TAY_IMG images).
+extern "C" int tp_conv_gen_tay_slots(int cfg, int HWo) {
+  if (cfg == 4) return 0;  // its 8-wave 128x128 EPI_FWD_TAY build spills 29 VGPRs (the others do not)
+  const int bm = tp_conv_tile_m(cfg);
+  if (HWo <= 0 || (bm - 1) / HWo + 1 > tp::GEN_TAY_IMG) return 0;
+  return tp::gen_tay_slots(bm, HWo);
+}
+
 extern "C" hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
                                    int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
                                    const float* scale, const float* shift, int relu, const float* res,
                                    int res_stride, const float* mask, float* apoz, float* out, float* ws,
                                    double* bnpart, hipStream_t st) {
+  return tp_conv_gen4(x, w, B, H, W, Cin, Cout, ks, stride, pad, transposed, Ho_t, Wo_t, cfg, splits, scale, shift,
+                      relu, res, res_stride, mask, apoz, out, ws, bnpart, nullptr, 0, st);
+}
+
+// ``bnpart`` (nullable): [ceil(M / tile_m(cfg))][2][Cout] doubles receiving the per-tile column
+// sums / sums of squares of the output (training BatchNorm statistics); no split-K then.
+// ``tay_part`` (nullable, needs ``mask``, no split-K, not transposed): [R][B][Cout] Taylor partials
+// (tp_conv_gen_tay_slots), every slot written or left as the caller zeroed it.
+extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   double* bnpart, float* tay_part, int tay_mode, hipStream_t st) {
   using namespace tp;
   const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
   if ((gen != 2 && Cin % 32 != 0) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
@@ -1474,6 +1551,14 @@ extern "C" hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H,
     if (splits > 1) return hipErrorInvalidValue;
     a.bnpart = bnpart;
   }
+  if (tay_part) {
+    if (splits > 1 || !mask || gen != 1 || cfg >= CFG_WS || tp_conv_gen_tay_slots(cfg, a.HWo) == 0)
+      return hipErrorInvalidValue;
+    a.tay_part = tay_part;
+    a.tay_mode = tay_mode;
+    a.epi_lds = 1;
+  }
+  if (a.tay_part) return gen_cfg<1, 1, EPI_FWD_TAY>(cfg, a, 1, st);
   if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);
   if (!ws) return hipErrorInvalidValue;
   ConvArgs b = a;

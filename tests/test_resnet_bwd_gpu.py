@@ -206,3 +206,35 @@ def test_resnet_engine_shapley_matches_fp64(cuda, prune):
         assert res[0].shape == res[1].shape == (6, mods[li].weight.shape[0])
         scale = np.abs(res[1]).max() + 1e-12
         assert np.abs(res[0] - res[1]).max() / scale < 2e-2, (li, np.abs(res[0] - res[1]).max(), scale)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6])
+@pytest.mark.parametrize("B,hw,C,N", [(4, 7, 128, 64), (3, 14, 64, 96), (2, 28, 32, 64), (2, 56, 64, 32)])
+@pytest.mark.parametrize("tay_mode", [0, 1])
+def test_conv_gen_bwd_taylor_partials(cuda, cfg, B, hw, C, N, tay_mode):
+    """1x1 dgrad with the Taylor / Sensitivity partials fused into the LDS epilogue (EPI_FWD_TAY):
+    the (R, B, N) slots sum to the fp64 reduction of the masked output, the output itself is
+    bit-identical to the same config without partials, and images spanning tiles get one slot
+    per tile (deterministic: no atomics)."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    R = T.conv_gen_tay_slots(cfg, hw * hw)
+    if R == 0:
+        pytest.skip("tile spans more than 4 images")
+    g = torch.Generator().manual_seed(cfg * 7 + hw + tay_mode)
+    wf = torch.randn(C, N, generator=g)  # forward 1x1 conv N -> C
+    gy = torch.randn(B, hw, hw, C, generator=g)
+    mask = torch.randn(B, hw, hw, N, generator=g).clamp_min(0)
+    ref = torch.einsum("bhwc,cn->bhwn", gy.double(), wf.double())
+    ref = torch.where(mask.double() > 0, ref, torch.zeros((), dtype=torch.float64))
+    tay_ref = ref.abs().sum((1, 2)) if tay_mode else (-(ref * mask.double())).sum((1, 2))
+    wt = wf.t().contiguous()
+    args = (gy.to(cuda), wt.to(cuda), None, 1, mask.to(cuda), 1, 1, 0, 0, 0, False, cfg, 1)
+    tay = torch.zeros(R, B, N, device=cuda)
+    out = T.conv_gen_bwd(*args, tay, tay_mode)
+    assert torch.equal(out, T.conv_gen_bwd(*args))
+    torch.testing.assert_close(out.cpu().double(), ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(tay.sum(0).cpu().double(), tay_ref, rtol=1e-4, atol=1e-3)
+    tay2 = torch.zeros_like(tay)
+    T.conv_gen_bwd(*args, tay2, tay_mode)
+    assert torch.equal(tay, tay2)  # deterministic

@@ -328,10 +328,11 @@ class ResNetEngine:
         """dL/d(input) of conv ``e`` from g = dL/d(conv output) (BN scale folded in), plus
         ``res``, masked by ``mask`` (the input's post-ReLU activation). ``low_res``: a strided
         1x1 conv's gradient at the output resolution (scattered by the consumer's res_stride).
-        Returns (gradient, Taylor slab or None): with ``taylor`` and a Winograd kernel chosen,
-        the dgrad epilogue also writes the per-(image, channel) partial sums of -(dL/da * a),
-        a = ``mask``, into an (R, B, C) slab (one writer per element: deterministic), which
-        saves the separate channel reduction's read of both tensors."""
+        Returns (gradient, Taylor slab or None): with ``taylor``, a Winograd 3x3 dgrad or a 1x1
+        dgrad (implicit GEMM, one K pass) also writes the per-(image, channel) partial sums of
+        -(dL/da * a), a = ``mask``, into an (R, B, C) slab from its epilogue (one writer per
+        element: deterministic), which saves the separate channel reduction's read of both
+        tensors."""
         e = self._bwd_operands(e)
         B, H, W, C = g.shape
         ks, s = e["ks"], e["stride"]
@@ -350,15 +351,25 @@ class ResNetEngine:
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
         key = ("rbwd", tuple(g.shape), N, ks, s, transposed, res is not None, res_stride, mask is not None)
 
+        # 1x1 dgrads with fused Taylor partials: one K pass, tiles spanning <= 4 images
+        gen_tay = taylor and ks == 1 and not transposed and mask is not None and res is None
+        if gen_tay:
+            cands = list(dict.fromkeys((c, 1) for c, _ in cands if c >= 0 and T.conv_gen_tay_slots(c, Ho * Wo) > 0))
+            key = key + ("tay",)
+            gen_tay = bool(cands)
+
         def run(cfg, sp, gg=g, rr=res, mm=mask, tay=None):
             if cfg in (WINO, WINO_LDS):
                 return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, tay, True, sp, cfg == WINO_LDS, 0)
             return T.conv_gen_bwd(gg, e["wt"], rr, res_stride, mm, ks, s if transposed else 1, pad, Ho, Wo,
-                                  transposed, cfg, sp)
+                                  transposed, cfg, sp, tay, 0)
 
-        cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands)
+        cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands if cands else None)
         if taylor and cfg in (WINO, WINO_LDS):
             tay = torch.zeros(taylor_slots(Ho, Wo), B, N, device=g.device)
+            return run(cfg, sp, tay=tay), tay
+        if gen_tay:
+            tay = torch.zeros(T.conv_gen_tay_slots(cfg, Ho * Wo), B, N, device=g.device)
             return run(cfg, sp, tay=tay), tay
         return run(cfg, sp), None
 
