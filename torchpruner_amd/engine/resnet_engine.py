@@ -324,15 +324,16 @@ class ResNetEngine:
             e["wt"] = w4.permute(3, 1, 2, 0).reshape(ci, ks * ks * co).contiguous()
         return e
 
-    def _dgrad(self, T, e, g, mask, res=None, res_stride=1, low_res=False, taylor=False):
+    def _dgrad(self, T, e, g, mask, res=None, res_stride=1, low_res=False, tay_mode=None):
         """dL/d(input) of conv ``e`` from g = dL/d(conv output) (BN scale folded in), plus
         ``res``, masked by ``mask`` (the input's post-ReLU activation). ``low_res``: a strided
         1x1 conv's gradient at the output resolution (scattered by the consumer's res_stride).
-        Returns (gradient, Taylor slab or None): with ``taylor``, a Winograd 3x3 dgrad or a 1x1
-        dgrad (implicit GEMM, one K pass) also writes the per-(image, channel) partial sums of
+        Returns (gradient, partial slab or None): with ``tay_mode`` 0, a Winograd 3x3 dgrad or a
+        1x1 dgrad (implicit GEMM, one K pass) also writes the per-(image, channel) partial sums of
         -(dL/da * a), a = ``mask``, into an (R, B, C) slab from its epilogue (one writer per
         element: deterministic), which saves the separate channel reduction's read of both
-        tensors."""
+        tensors; ``tay_mode`` 1 (Sensitivity): sums of |dL/da| of the masked gradient, 1x1 only
+        (the Winograd epilogue's |.| sees the unmasked gradient)."""
         e = self._bwd_operands(e)
         B, H, W, C = g.shape
         ks, s = e["ks"], e["stride"]
@@ -352,7 +353,7 @@ class ResNetEngine:
         key = ("rbwd", tuple(g.shape), N, ks, s, transposed, res is not None, res_stride, mask is not None)
 
         # 1x1 dgrads with fused Taylor partials: one K pass, tiles spanning <= 4 images
-        gen_tay = taylor and ks == 1 and not transposed and mask is not None and res is None
+        gen_tay = tay_mode is not None and ks == 1 and not transposed and mask is not None and res is None
         if gen_tay:
             cands = list(dict.fromkeys((c, 1) for c, _ in cands if c >= 0 and T.conv_gen_tay_slots(c, Ho * Wo) > 0))
             key = key + ("tay",)
@@ -362,10 +363,10 @@ class ResNetEngine:
             if cfg in (WINO, WINO_LDS):
                 return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, tay, True, sp, cfg == WINO_LDS, 0)
             return T.conv_gen_bwd(gg, e["wt"], rr, res_stride, mm, ks, s if transposed else 1, pad, Ho, Wo,
-                                  transposed, cfg, sp, tay, 0)
+                                  transposed, cfg, sp, tay, tay_mode or 0)
 
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands if cands else None)
-        if taylor and cfg in (WINO, WINO_LDS):
+        if tay_mode == 0 and cfg in (WINO, WINO_LDS):
             tay = torch.zeros(taylor_slots(Ho, Wo), B, N, device=g.device)
             return run(cfg, sp, tay=tay), tay
         if gen_tay:
@@ -402,9 +403,9 @@ class ResNetEngine:
             for ci in range(len(blk.convs) - 1, 0, -1):
                 a_prev = inner[ci - 1]
                 bn = blk.convs[ci - 1].bn
-                fuse = bn in want and mode in ("taylor", "taylor_signed")
-                g, tay = self._dgrad(T, e["convs"][ci], g, a_prev, taylor=fuse)  # dL/d(bn_{ci} output), masked
-                if tay is not None:  # Taylor partials from the Winograd dgrad epilogue
+                tm = ({"taylor": 0, "taylor_signed": 0, "sensitivity": 1}.get(mode) if bn in want else None)
+                g, tay = self._dgrad(T, e["convs"][ci], g, a_prev, tay_mode=tm)  # dL/d(bn_{ci} output), masked
+                if tay is not None:  # partials from the data-gradient epilogue
                     sums = tay.sum(0)
                     out[bn] = sums.abs_() if mode == "taylor" else sums
                 elif bn in want:
