@@ -777,6 +777,14 @@ class FusedChainEngine:
     # (profiles/bench/large_batch_graphs_vs_eager.txt), so the default stops at 1024.
     GRAPH_MAX_B = int(os.environ.get("TORCHPRUNER_GRAPH_MAX_B", "1024"))
 
+    def _bound_graph_cache(self, limit: int = 64):
+        """Bound the captured graphs (each holds a private memory pool). Replays of the graphs
+        being dropped may still run on the pipeline's streams, and dropping a graph returns its
+        pool to the allocator: wait for the device first (rare: only past ``limit`` entries)."""
+        if len(self._graphs) > limit:
+            torch.cuda.synchronize()
+            self._graphs.clear()
+
     def graphs_enabled(self, B: int, pipelined: bool = False) -> bool:
         mode = os.environ.get("TORCHPRUNER_GRAPHS", "auto")
         if mode == "all":
@@ -805,6 +813,7 @@ class FusedChainEngine:
                id(arena))
         g = self._graphs.get(key)
         if g is not None and (g["P"] is not P or g["arena"] is not arena):
+            torch.cuda.synchronize()  # its replays must finish before the stale graph (and pool) goes
             g = None
         if g is None:
             seen = self._graphs.get(("seen",) + key)
@@ -818,8 +827,7 @@ class FusedChainEngine:
             with torch.cuda.graph(graph, stream=side):
                 self.taylor(sx, sy, want, arena, mode)
             torch.cuda.current_stream(x.device).wait_stream(side)
-            if len(self._graphs) > 64:  # bound the graphs' private memory pools
-                self._graphs.clear()
+            self._bound_graph_cache()
             g = self._graphs[key] = {"graph": graph, "x": sx, "y": sy, "P": P, "arena": arena}
         g["x"].copy_(x)
         g["y"].copy_(y)
@@ -834,6 +842,7 @@ class FusedChainEngine:
         key = ("sv_static", k, tuple(zk.shape), tuple(y.shape), str(zk.device))
         st = self._graphs.get(key)
         if st is None:
+            self._bound_graph_cache()
             st = self._graphs[key] = {"z": torch.empty_like(zk), "y": torch.empty_like(y), "rank": None,
                                       "graphs": {}, "seen": {}, "k": k}
         st["z"].copy_(zk)
@@ -849,6 +858,8 @@ class FusedChainEngine:
         shallow layers were host-bound (profiles/bench/host_bound_probe_paths.txt)."""
         P = self._pack()
         if st["rank"] is None or st["rank"].shape != rank_padded.shape:
+            if st["graphs"]:
+                torch.cuda.synchronize()
             st["rank"] = torch.empty_like(rank_padded)
             st["graphs"].clear()
         torch.sub(rank_padded, p_first, out=st["rank"])
@@ -861,6 +872,7 @@ class FusedChainEngine:
 
         g = st["graphs"].get(cnt)
         if g is not None and g["P"] is not P:
+            torch.cuda.synchronize()  # its replays must finish before the stale graph (and pool) goes
             g = None
         if g is None:
             if st["seen"].get(cnt) is not P:  # first use of this chunk size: eager (autotunes, allocates)
@@ -887,6 +899,7 @@ class FusedChainEngine:
         key = ("apoz", tuple(x.shape), x.dtype, str(x.device), blocks, slot, self.bf16)
         g = self._graphs.get(key)
         if g is not None and g["P"] is not P:
+            torch.cuda.synchronize()  # its replays must finish before the stale graph (and pool) goes
             g = None
 
         def run(xx):
@@ -905,8 +918,7 @@ class FusedChainEngine:
             with torch.cuda.graph(graph, stream=side):
                 bufs = run(sx)
             torch.cuda.current_stream(x.device).wait_stream(side)
-            if len(self._graphs) > 64:
-                self._graphs.clear()
+            self._bound_graph_cache()
             g = self._graphs[key] = {"graph": graph, "x": sx, "P": P, "bufs": bufs}
         g["x"].copy_(x)
         g["graph"].replay()
