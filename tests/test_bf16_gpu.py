@@ -109,3 +109,33 @@ def test_bf16_engine_taylor_ranks_match_fp32(cuda):
         rho = spearmanr(a, b).correlation
         assert rho >= 0.99, (k, rho)
         assert np.abs(a - b).max() / np.abs(b).max() < 5e-2, k
+
+
+def test_shapley_fp32_after_bf16_on_one_engine(cuda):
+    """A bf16 Shapley run must not leave captured graphs / static buffers that a later fp32 run on
+    the same engine replays: fp32 after bf16 == a fresh fp32 run, bit for bit."""
+    from torchpruner_amd import ShapleyAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import invalidate
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(2)
+    model = prunable_vgg16().to(cuda).eval()
+    module = [m for m in model.features if isinstance(m, torch.nn.Conv2d)][8]
+    x = torch.randn(24, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (24,), device=cuda)
+
+    def run(dtype):
+        np.random.seed(4)
+        m = ShapleyAttributionMetric(model, DeviceLoader(x, y, 8), F.cross_entropy, cuda, sv_samples=2,
+                                     compute_dtype=dtype)
+        out = m.run(module, find_best_evaluation_module=True)
+        assert m.last_path["path"] == "fused", m.last_path
+        return out
+
+    invalidate(model)
+    fresh = run(None)
+    invalidate(model)
+    bf = run(torch.bfloat16)
+    after = run(None)
+    np.testing.assert_array_equal(after, fresh)
+    assert not np.array_equal(bf, fresh)  # the bf16 run really used bf16 operands

@@ -1,0 +1,27 @@
+"""The native extension carries the hash of the sources it was built from, and the loader refuses
+a binary that does not match the tree (an mtime-only rebuild check could keep
+a stale _C.so)."""
+import pytest
+
+from torchpruner_amd import _build
+from torchpruner_amd.ops import _native
+
+
+def test_source_hash_is_content_based(tmp_path, monkeypatch):
+    h = _build.source_hash()
+    assert len(h) == 16
+    # flags are part of the hash (an experiment build with extra flags is a different binary)
+    monkeypatch.setenv("TORCHPRUNER_HIPFLAGS", "-DTP_SOMETHING")
+    assert _build.source_hash() != h
+    monkeypatch.delenv("TORCHPRUNER_HIPFLAGS")
+    assert _build.source_hash() == h
+
+
+def test_loader_refuses_a_stale_extension(monkeypatch):
+    if not _build.OUT.exists():
+        pytest.skip("extension not built")
+    assert _build.stamped_hash() == _build.source_hash(), "in-tree _C.so is stale: run __graft_entry__.build()"
+    _native._check_stamp()  # matches: no error
+    monkeypatch.setattr(_build, "source_hash", lambda: "0" * 16)
+    with pytest.raises(RuntimeError, match="stale native extension"):
+        _native._check_stamp()

@@ -95,21 +95,27 @@ def test_pruned_vgg_engine_shapley_and_ablation(cuda, layer):
     y = torch.randint(0, 10, (8,), device=cuda)
     m64 = copy.deepcopy(model).double().cpu()
     p64 = [m for m in m64.features if isinstance(m, torch.nn.Conv2d)] + [m64.classifier[1], m64.classifier[4]]
+    from torchpruner_amd.engine.fused_chain import TUNER
     res = []
     for backend, mdl, mod, d, xx, yy in (("hip", model, module, cuda, x, y), ("torch", model, module, cuda, x, y),
                                          ("torch", m64, p64[layer], "cpu", x.double().cpu(), y.cpu())):
         os.environ["TORCHPRUNER_BACKEND"] = backend
         try:
             np.random.seed(5)
-            res.append(ShapleyAttributionMetric(mdl, DeviceLoader(xx, yy, 4), F.cross_entropy, d,
-                                                sv_samples=2).run(mod, find_best_evaluation_module=True))
+            with TUNER.fixed():  # pinned kernel choices: the fused numbers are the same on any box
+                res.append(ShapleyAttributionMetric(mdl, DeviceLoader(xx, yy, 4), F.cross_entropy, d,
+                                                    sv_samples=2).run(mod, find_best_evaluation_module=True))
         finally:
             del os.environ["TORCHPRUNER_BACKEND"]
     assert res[0].shape == (module.weight.shape[0],)
-    # single-unit deltas of a random-init net sit near fp32 loss rounding: both fp32 paths
-    # must be in the same error class w.r.t. the fp64 oracle
+    # single-unit deltas of a random-init net sit near fp32 loss rounding: bound the error in fp32
+    # ulps of the mean loss (forward-only values: no dependence on another library's algorithm)
+    with torch.no_grad():
+        lbar = float(F.cross_entropy(m64(x.double().cpu()), y.cpu()))
     err_fused, err_generic = np.abs(res[0] - res[2]).max(), np.abs(res[1] - res[2]).max()
-    assert err_fused <= 3 * err_generic + 1e-6, (err_fused, err_generic)
+    ulps = err_fused / (np.finfo(np.float32).eps * lbar)
+    print(f"pruned layer {layer}: fused_err={err_fused:.2e} ({ulps:.0f} ulps) miopen_err={err_generic:.2e}")
+    assert ulps < 100, (err_fused, err_generic, lbar)
     ev = find_best_module_for_attributions(model, module)
     ranking = np.random.RandomState(0).permutation(module.weight.shape[0])
     l_hip, a_hip = ablation_curve(model, ev, ranking, x, y)

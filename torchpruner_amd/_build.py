@@ -18,7 +18,10 @@ implicit cuDNN/cuBLAS/ATen kernels its hooks trigger.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -65,6 +68,7 @@ FILE_FLAGS = {"wino4": ["-fno-slp-vectorize"]}
 
 
 def _needs_rebuild(src: Path, obj: Path, deps: list[Path]) -> bool:
+    """mtime check (host-sanitizer build only; the extension itself rebuilds by content hash)."""
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
@@ -83,44 +87,101 @@ def _run(cmd, verbose):
     return r
 
 
+# ---------------------------------------------------------------- content hashes
+# The extension is rebuilt from what the sources SAY, not from file times: an object is recompiled
+# when the hash of its source + headers + (path-free) flags differs from the one recorded when it
+# was built (build/native/manifest.json), and the hash of the whole source set is stamped into
+# _C.so as the string ``TPAMD_SRC_HASH=<hex>``. ops.load() refuses a _C.so whose stamp does not
+# match the tree it runs from (a stale binary after a checkout or a copy that refreshed mtimes
+# unevenly would otherwise load silently).
+STAMP_RE = re.compile(rb"TPAMD_SRC_HASH=([0-9a-f]{16})")
+
+
+def _flag_sig(stem: str, binding: bool) -> str:
+    import torch
+    flags = [f for f in _common_flags() if not f.startswith("-I")] + FILE_FLAGS.get(stem, [])
+    extra = f"torch={torch.__version__}" if binding else ""
+    return " ".join(flags) + "|" + extra
+
+
+def _digest(paths, sig: str) -> str:
+    h = hashlib.sha256(sig.encode())
+    for p in paths:
+        h.update(p.relative_to(ROOT).as_posix().encode() + b"\0")
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def _sources():
+    return (sorted((CSRC / "include").glob("*.h")), sorted((CSRC / "kernels").glob("*.hip")),
+            sorted(CSRC.glob("*.cpp")))
+
+
+def source_hash() -> str:
+    """Hash of every source, header and flag that goes into ``_C.so``."""
+    headers, kernels, bindings = _sources()
+    per = [_digest([s] + headers, _flag_sig(s.stem, False)) for s in kernels] + \
+          [_digest([b] + headers, _flag_sig(b.stem, True)) for b in bindings]
+    return hashlib.sha256("".join(per).encode()).hexdigest()[:16]
+
+
+def stamped_hash(path: Path = OUT):
+    """The source hash stamped into a built extension (None when absent)."""
+    if not path.exists():
+        return None
+    m = STAMP_RE.search(path.read_bytes())
+    return m.group(1).decode() if m else None
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
     """Compile all HIP kernels + torch bindings into ``torchpruner_amd/_C.so``."""
     inc, lib, abi = _torch_paths()
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
-    headers = sorted((CSRC / "include").glob("*.h"))
-    kernels = sorted((CSRC / "kernels").glob("*.hip"))
-    bindings = sorted(CSRC.glob("*.cpp"))
+    headers, kernels, bindings = _sources()
+    man_path = BUILD_DIR / "manifest.json"
+    try:
+        manifest = json.loads(man_path.read_text()) if man_path.exists() and not force else {}
+    except ValueError:
+        manifest = {}
 
     jobs_list = []
     objs = []
-    for src in kernels:
+    new_manifest = {}
+    for src, is_binding in [(k, False) for k in kernels] + [(b, True) for b in bindings]:
         obj = BUILD_DIR / (src.stem + ".o")
         objs.append(obj)
-        if force or _needs_rebuild(src, obj, headers):
-            cmd = [HIPCC, *_common_flags(), *FILE_FLAGS.get(src.stem, []), f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-c",
-                   src, "-o", obj]
-            jobs_list.append(cmd)
-    for binding in bindings:
-        bobj = BUILD_DIR / (binding.stem + ".o")
-        objs.append(bobj)
-        if force or _needs_rebuild(binding, bobj, headers):
-            cmd = [HIPCC, *_common_flags(), f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-                   "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
-                   *[f"-I{p}" for p in inc], "-c", binding, "-o", bobj]
+        dig = _digest([src] + headers, _flag_sig(src.stem, is_binding))
+        new_manifest[obj.name] = dig
+        if force or not obj.exists() or manifest.get(obj.name) != dig:
+            if is_binding:
+                cmd = [HIPCC, *_common_flags(), f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+                       "-D__HIP_PLATFORM_AMD__=1", *[f"-I{p}" for p in inc], "-c", src, "-o", obj]
+            else:
+                cmd = [HIPCC, *_common_flags(), *FILE_FLAGS.get(src.stem, []), f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                       "-c", src, "-o", obj]
             jobs_list.append(cmd)
 
     n = jobs or min(8, os.cpu_count() or 4)
     if jobs_list:
         with ThreadPoolExecutor(max_workers=n) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
+    man_path.write_text(json.dumps(new_manifest, indent=1, sort_keys=True))
 
-    if force or jobs_list or not OUT.exists() or any(o.stat().st_mtime > OUT.stat().st_mtime for o in objs):
+    want = source_hash()
+    if force or jobs_list or stamped_hash() != want:
+        stamp_src = BUILD_DIR / "src_stamp.cpp"
+        stamp_src.write_text("// generated by torchpruner_amd/_build.py: hash of the sources of this _C.so\n"
+                             f'extern "C" __attribute__((used, visibility("default"))) const char tp_src_stamp[] = '
+                             f'"TPAMD_SRC_HASH={want}";\n')
+        stamp_obj = BUILD_DIR / "src_stamp.o"
+        _run([HIPCC, "-fPIC", "-O1", "-x", "c++", "-c", stamp_src, "-o", stamp_obj], verbose)
         tmp = OUT.with_suffix(".so.tmp")
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs,
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, stamp_obj,
                f"-L{lib}", f"-Wl,-rpath,{lib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip",
                "-lamdhip64", "-o", tmp]
         _run(cmd, verbose)
         os.replace(tmp, OUT)
+    assert stamped_hash() == want, "source stamp missing from the linked extension"
     return OUT
 
 

@@ -23,6 +23,7 @@ NumPy array — re-designed for MI355X:
 from __future__ import annotations
 
 import contextlib
+import itertools
 import logging
 import math
 import os
@@ -159,6 +160,7 @@ class _AttributionMetric(ABC):
         self.compute_dtype = compute_dtype
         self._ckpt = None
         self._run_accs = None
+        self._peeked = None  # (first batch, live iterator) taken by _first_input_shape
         # path transparency (new): which execution path served the last run() and, when the
         # generic hook path ran, why the native engines were rejected
         self.last_path = None
@@ -294,11 +296,29 @@ class _AttributionMetric(ABC):
         world, _ = self._world()
         return world > 1 and (self.shard_data is None or self.shard_data)
 
-    def _batches(self):
-        """Yield ``(global_batch_index, x, y)`` on ``self.device`` for this rank's batches."""
+    def _source(self):
+        """This rank's ``(global_batch_index, x, y)`` batches, straight from the data generator."""
         world, rank = self._world()
-        it = pdist.ShardedBatches(self.data_gen, rank, world) if self._sharding() else \
+        return pdist.ShardedBatches(self.data_gen, rank, world) if self._sharding() else \
             ((i, x, y) for i, (x, y) in enumerate(self.data_gen))
+
+    def _peek_source(self):
+        """The batch iterator the coming pass will consume (``_first_input_shape`` peeks it)."""
+        return self._source()
+
+    def _iter_source(self, factory):
+        """The peeked iterator (its first batch replayed) if the engine selection took one, else
+        ``factory()``: the data generator is iterated once per pass."""
+        peeked, self._peeked = getattr(self, "_peeked", None), None
+        if peeked is not None:
+            return itertools.chain([peeked[0]], peeked[1])
+        return factory()
+
+    def _batches(self):
+        """Yield ``(global_batch_index, x, y)`` on ``self.device`` for this rank's batches. A
+        batch the engine selection peeked at (``_first_input_shape``) is replayed first, from the
+        same iterator: the data generator is iterated once per pass, as by the reference."""
+        it = self._iter_source(self._source)
         ck = self._ckpt
         if ck is not None:
             it = ((i, x, y) for i, x, y in it if i not in ck.done)  # processed before an interruption
@@ -327,6 +347,7 @@ class _AttributionMetric(ABC):
             self._ckpt.restore(accs)
 
     def _end_run(self):
+        self._peeked = None  # a peeked batch belongs to this run's pass only
         if self._ckpt is not None:
             self._ckpt.save(self._run_accs)
         self._ckpt = None
@@ -487,20 +508,30 @@ class _AttributionMetric(ABC):
         return res
 
     def _first_input_shape(self):
-        """Shape of the data generator's first input batch, or None when it cannot be peeked at
-        without consuming it (one-shot iterators)."""
-        dg = self.data_gen
-        try:
+        """Shape of this rank's first input batch, or None. In-memory loaders (DeviceLoader,
+        per-rank ShardLoader) are indexed without iterating. Anything else is iterated ONCE, here:
+        the first batch and the live iterator are kept for the pass that follows (``_batches``),
+        so a DataLoader is not iterated twice (a second iterator would draw its shuffle seed and
+        start its workers again, shifting the RNG stream the reference's single pass sees) and a
+        one-shot iterable loses nothing."""
+        peeked = getattr(self, "_peeked", None)
+        if peeked is None:
+            dg = self.data_gen
+            x = None
             if getattr(dg, "local_only", False):  # a per-rank ShardLoader
                 first = next(iter(dg.batches.values()), None)
+                x = first[0] if first else None
+            elif hasattr(dg, "_batch") and hasattr(dg, "x"):  # DeviceLoader: resident tensors
+                x = dg._batch(0)[0] if len(dg) else None
             else:
-                it = iter(dg)
-                if it is dg:
-                    return None
+                it = iter(self._peek_source())
                 first = next(it, None)
-        except Exception:
-            return None
-        x = first[0] if isinstance(first, (tuple, list)) and first else None
+                if first is None:
+                    return None
+                self._peeked = peeked = (first, it)
+            if peeked is None:
+                return tuple(x.shape) if isinstance(x, torch.Tensor) else None
+        x = peeked[0][1]
         return tuple(x.shape) if isinstance(x, torch.Tensor) else None
 
     def _resnet_grad_pass(self, eng, eval_modules, accs, mode):

@@ -58,6 +58,19 @@ class ShapleyAttributionMetric(_AttributionMetric):
     def run(self, module, sv_samples=None, **kwargs):
         module = super().run(module, **kwargs)
         sv_samples = sv_samples if sv_samples is not None else self.samples
+        try:
+            return self._run(module, sv_samples)
+        finally:
+            self._peeked = None  # a batch peeked by the engine selection belongs to this run only
+
+    def _all_batches(self):
+        """Every batch with its global index (the prefix-split and single-rank passes)."""
+        return ((i, x, y) for i, (x, y) in enumerate(self.data_gen))
+
+    def _peek_source(self):
+        return self._source() if self._work_split() == "batches" else self._all_batches()
+
+    def _run(self, module, sv_samples):
         why = []
         fused = self._fused_prepare(module, why)
         path = "fused" if fused is not None else None
@@ -162,7 +175,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
         perm_ts = rank_ts = None
         segs = None
         batches = self._batches() if split == "batches" else \
-            ((i, _to(x, self.device), _to(y, self.device)) for i, (x, y) in enumerate(self.data_gen))
+            ((i, _to(x, self.device), _to(y, self.device)) for i, x, y in self._iter_source(self._all_batches))
         with torch.no_grad():
             for bidx, x, y in batches:
                 n, B, per_sample, base_loss, evaluate = prepare(x, y)
@@ -173,8 +186,11 @@ class ShapleyAttributionMetric(_AttributionMetric):
                 K = self._prefix_chunk(B, per_sample)
                 if segs is None or segs[0] != K:
                     segs = (K, self._segments(S, n, split == "prefixes", K))
-                # deltas are summed unscaled (fp64 sums of fp32 loss differences: exact, so any
-                # rank split / collective order gives the same bits) and divided by S at the end
+                # deltas are summed unscaled and divided by S at the end. fp64 sums of fp32 loss
+                # differences are exact while the exponent span of the terms plus log2(count)
+                # stays within fp64's 53 bits, which holds in practice (fp32 losses of one run
+                # span far less): then any rank split / collective order gives the same bits
+                # (tests/test_distributed.py checks world sizes 1-8 on a wide loss range)
                 if stats:
                     if sv_col is None:
                         sv_col = torch.zeros(n, dtype=torch.float64, device=base_loss.device)

@@ -21,6 +21,10 @@ def invalidate(model) -> bool:
     hit = False
     for cache in (fused_chain._ENGINES, resnet_engine._ENGINES):
         if model in cache:
+            if torch.cuda.is_available() and torch.cuda.is_initialized():
+                # replays of the engine's captured graphs may still run on pipeline streams, and
+                # dropping a graph returns its private pool to the allocator (as _bound_graph_cache)
+                torch.cuda.synchronize()
             del cache[model]
             hit = True
     return hit

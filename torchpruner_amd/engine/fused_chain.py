@@ -154,6 +154,10 @@ class Autotuner:
     def __init__(self):
         self.cache = {}
         self.enabled = os.environ.get("TORCHPRUNER_AUTOTUNE", "1") != "0"
+        self.policy = None
+        # bumped whenever a fixed()/pinned() context swaps the choice cache: captured HIP graphs
+        # bake in the kernels chosen when they were captured, so their keys include it
+        self.gen = 0
 
     @contextlib.contextmanager
     def fixed(self):
@@ -161,12 +165,28 @@ class Autotuner:
         picks the same configs, so results are bit-reproducible across processes (accuracy
         protocols, teacher training). Timing-based choices can differ between runs on a busy
         GPU, and different split-K / tile configs round differently."""
-        saved = (self.cache, self.enabled)
-        self.cache, self.enabled = {}, False
+        saved = (self.cache, self.enabled, self.policy)
+        self.cache, self.enabled, self.policy = {}, False, None
+        self.gen += 1
         try:
             yield self
         finally:
-            self.cache, self.enabled = saved
+            self.cache, self.enabled, self.policy = saved
+            self.gen += 1
+
+    @contextlib.contextmanager
+    def pinned(self, policy):
+        """Kernel choices made by ``policy(key, candidates, M, N, K) -> (cfg, splits)`` (None: the
+        untuned pick) with a private cache, never by timing: numerics tests pin one kernel family
+        at a time (:func:`family_policy`), so what they measure cannot depend on the box."""
+        saved = (self.cache, self.enabled, self.policy)
+        self.cache, self.enabled, self.policy = {}, False, policy
+        self.gen += 1
+        try:
+            yield self
+        finally:
+            self.cache, self.enabled, self.policy = saved
+            self.gen += 1
 
     def candidates(self, M, N, K, wino=None, wino_only=False):
         """``wino``: (P tiles, C) when the Winograd kernel applies to this conv; ``wino_only``
@@ -196,6 +216,11 @@ class Autotuner:
         hit = self.cache.get(key)
         if hit is not None:
             return hit
+        if self.policy is not None:
+            lst = cands if cands is not None else self.candidates(M, N, K, wino, wino_only and wino is not None)
+            res = self.policy(key, lst, M, N, K) or lst[0]
+            self.cache[key] = res
+            return res
         if not self.enabled or torch.cuda.is_current_stream_capturing():
             if cands is not None:
                 res = cands[0]
@@ -810,7 +835,7 @@ class FusedChainEngine:
         P = self._pack()
         # one graph per score arena: the stream pipeline replays slot k's graph into slot k's arena
         key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device), self.bf16,
-               id(arena))
+               id(arena), TUNER.gen)
         g = self._graphs.get(key)
         if g is not None and (g["P"] is not P or g["arena"] is not arena):
             torch.cuda.synchronize()  # its replays must finish before the stale graph (and pool) goes
@@ -839,7 +864,7 @@ class FusedChainEngine:
         """Static device buffers of a Shapley prefix evaluation of block ``k``'s output (one
         batch): the activation, the labels and the shifted rank vector that the captured graphs
         of :meth:`shapley_eval` read. Copies this batch in (two launches per batch)."""
-        key = ("sv_static", k, tuple(zk.shape), tuple(y.shape), str(zk.device))
+        key = ("sv_static", k, tuple(zk.shape), tuple(y.shape), str(zk.device), self.bf16, TUNER.gen)
         st = self._graphs.get(key)
         if st is None:
             self._bound_graph_cache()
@@ -896,7 +921,7 @@ class FusedChainEngine:
         as for :meth:`taylor_graphed`."""
         P = self._pack()
         blocks = tuple(sorted(blocks))
-        key = ("apoz", tuple(x.shape), x.dtype, str(x.device), blocks, slot, self.bf16)
+        key = ("apoz", tuple(x.shape), x.dtype, str(x.device), blocks, slot, self.bf16, TUNER.gen)
         g = self._graphs.get(key)
         if g is not None and g["P"] is not P:
             torch.cuda.synchronize()  # its replays must finish before the stale graph (and pool) goes
@@ -1017,6 +1042,40 @@ class FusedChainEngine:
                                    cands=cands)
             g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp, sc4, tm)
         return res
+
+
+KERNEL_FAMILIES = ("wino4", "wino2", "wino2_direct", "igemm")
+
+
+def family_policy(family: str, split: str = "min"):
+    """A :meth:`Autotuner.pinned` policy that runs every layer it can on one kernel family:
+    ``wino4`` F(4x4,3x3), ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
+    F(2x2) with direct patch loads, ``igemm`` the implicit GEMM (dense 2x2 GEMM, VALU first
+    layer). ``split``: the fewest ("min") or most ("max") channel splits of that family. Layers
+    the family does not cover keep the untuned pick."""
+    eng = FusedChainEngine
+
+    def member(c):
+        k = c[0]
+        if family == "wino4":
+            return k == WINO4
+        if family == "wino2":
+            return k in (WINO_LDS, WINO_UNP)
+        if family == "wino2_direct":
+            return k == WINO
+        if family == "igemm":
+            return 0 <= k <= 6 or eng.DENSE <= k < CFG_BF16 or k == eng.FIRST_DIRECT
+        raise ValueError(f"unknown kernel family {family!r}")
+
+    def policy(key, cands, M, N, K):
+        hit = [c for c in cands if member(c)]
+        if not hit and family == "igemm" and key[0] == "bwd":
+            return _pick_cfg(M, N, K)  # dgrad lists hold the Winograd kinds only
+        if not hit:
+            return None
+        return (min if split == "min" else max)(hit, key=lambda c: c[1])
+
+    return policy
 
 
 def logits_grad(logits: torch.Tensor, y: torch.Tensor, criterion=None) -> torch.Tensor:

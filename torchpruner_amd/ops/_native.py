@@ -38,11 +38,24 @@ def load() -> bool:
         if not _LIB.exists():
             raise FileNotFoundError(
                 f"{_LIB} not built; run `python -m torchpruner_amd._build` (or __graft_entry__.build())")
+        _check_stamp()
         torch.ops.load_library(str(_LIB))
         _loaded = True
     except Exception as e:  # pragma: no cover - exercised on boxes without the build
         _error = e
     return _loaded
+
+
+def _check_stamp():
+    """Refuse a ``_C.so`` built from other sources than the tree it is loaded from (the build
+    stamps the hash of every source, header and flag into it, _build.source_hash)."""
+    from .. import _build
+    if not (_build.CSRC / "kernels").is_dir():  # installed without sources: nothing to compare
+        return
+    want, got = _build.source_hash(), _build.stamped_hash(_LIB)
+    if got != want:
+        raise RuntimeError(f"stale native extension {_LIB}: built from sources {got}, this tree is {want}; "
+                           "rebuild with `python -m torchpruner_amd._build` (or __graft_entry__.build())")
 
 
 def available() -> bool:

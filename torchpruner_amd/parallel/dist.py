@@ -182,8 +182,9 @@ def state_digest(model: torch.nn.Module) -> str:
     import hashlib
     h = hashlib.sha256()
     for k, t in model.state_dict().items():
-        h.update(k.encode())
-        h.update(t.detach().cpu().contiguous().numpy().tobytes())
+        h.update(k.encode() + str(t.dtype).encode())
+        # raw bytes, dtype-agnostic (NumPy has no bfloat16)
+        h.update(t.detach().cpu().contiguous().reshape(-1).view(torch.uint8).numpy().tobytes())
     return h.hexdigest()[:16]
 
 
