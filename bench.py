@@ -38,6 +38,12 @@ Other BASELINE configs in the same run (all ranks, sharded like the headline):
 * ``shapley_vgg_img_evals_s``: config #4, Shapley sv_samples=5 over 1000 images (B=100, the
   nbVGG setup) at conv layers 0 / 6 / 12, downstream image-evaluations per second.
 
+* ``resnet50_finetune_img_s``: config #5, the ResNet-50 training step of the prune -> finetune loop
+  (224 px, B=128 per GPU, native kernels, PrunableDDP + SGD momentum, bucketed gradient
+  all-reduce over RCCL) timed after one data-parallel Taylor prune of every prunable bottleneck
+  conv + DDP rewrap; ``resnet50_prune_finetune``: one prune -> finetune round, Taylor vs Random,
+  from one teacher (``bench/resnet_finetune.py``).
+
 Accuracy (untimed; ``bench/prune_quality.py``, rank 0 after the process group is torn down):
 the teacher is pruned for real — ``Pruner.prune_model`` through ``get_vgg_pruning_graph`` on
 every conv, 50% of the filters, in 4 increments per layer with a few SGD steps between
@@ -84,6 +90,13 @@ def parse():
                     help="accuracy protocol over seeds seed..seed+K-1 (each its own teacher); top-1 figures "
                          "are means over the seeds, per-seed values are listed")
     ap.add_argument("--teacher-steps", type=int, default=None)
+    ap.add_argument("--extras", default="generic,bf16,b100,resnet,shapley,finetune,quality5",
+                    help="comma-separated extras to run (with --no-extras: none)")
+    ap.add_argument("--finetune-steps", type=int, default=10)
+    ap.add_argument("--finetune-batch", type=int, default=128)
+    ap.add_argument("--finetune-res", type=int, default=224)
+    ap.add_argument("--q5-res", type=int, default=112, help="config #5 quality round: image size")
+    ap.add_argument("--q5-max-steps", type=int, default=800, help="config #5 quality round: teacher step cap")
     return ap.parse_args()
 
 
@@ -268,24 +281,54 @@ def run(args) -> int:
 
 
 def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
-    """Same-algorithm library baseline + BASELINE configs #3 / #4 (all ranks, sharded)."""
-    import numpy as np
-    import torch
-    import torch.nn.functional as F
-
-    from torchpruner_amd import (APoZAttributionMetric, ShapleyAttributionMetric, TaylorAttributionMetric,
-                                 get_resnet_pruning_graph)
-    from torchpruner_amd.data import DeviceLoader, ShardLoader, StreamLoader
-    from torchpruner_amd.models import resnet50
-    from torchpruner_amd.parallel import dist as pdist
+    """Same-algorithm library baseline + BASELINE configs #3 / #4 / #5 (all ranks, sharded)."""
+    from torchpruner_amd.data import ShardLoader
 
     out = {}
-    B = args.batch
+    want = set(args.extras.split(","))
 
     def loader(n, seed, bs):
         return ShardLoader.build(lambda i: task.sample(bs, seed * 1_000_003 + i), n * world, bs, rank, world)
 
     # 1. the same one-pass run_many on the generic module/hook path, MIOpen/hipBLASLt convolutions
+    if "generic" in want:
+        out.update(_generic(args, model, convs, dev, world, timed_run, log, value, loader))
+    if "bf16" in want:
+        out.update(_bf16(args, model, convs, dev, world, timed_run, log, value, loader))
+    if "b100" in want:
+        out.update(_b100(args, model, convs, dev, world, timed_run, log, loader))
+    if "resnet" in want:
+        out.update(_resnet(args, dev, world, timed_run, log))
+    if "shapley" in want:
+        out.update(_shapley(args, model, task, convs, dev, world, log))
+    if "finetune" in want or "quality5" in want:
+        from torchpruner_amd.bench import resnet_finetune as rf
+        if "finetune" in want:
+            t0 = time.perf_counter()
+            r = rf.finetune_throughput(dev, world, rank, steps=args.finetune_steps, batch=args.finetune_batch,
+                                       res=args.finetune_res, seed=args.seed)
+            out.update(r)
+            log(f"[bench] config #5 ResNet-50 finetune step after a 20% prune + DDP rewrap, B={args.finetune_batch}: "
+                f"{r['resnet50_finetune_img_s']:.0f} img/s (dense {r['resnet50_train_dense_img_s']:.0f}) "
+                f"({time.perf_counter() - t0:.1f}s)")
+        if "quality5" in want:
+            t0 = time.perf_counter()
+            q = rf.prune_finetune_quality(dev, world, rank, seed=args.seed,
+                                          cfg={"res": args.q5_res, "teacher_max_steps": args.q5_max_steps})
+            out["resnet50_prune_finetune"] = q
+            log(f"[bench] config #5 one prune->finetune round (20%): teacher {q['teacher_top1']:.3f}; after prune "
+                f"Taylor {q['taylor_after_prune']:.3f} / Random {q['random_after_prune']:.3f}; after finetune Taylor "
+                f"{q['taylor_after_finetune']:.3f} / Random {q['random_after_finetune']:.3f} "
+                f"({time.perf_counter() - t0:.1f}s)")
+    return out
+
+
+def _generic(args, model, convs, dev, world, timed_run, log, value, loader):
+    import torch.nn.functional as F
+
+    from torchpruner_amd import TaylorAttributionMetric
+    out = {}
+    B = args.batch
     t0 = time.perf_counter()
     with _env(TORCHPRUNER_ENGINES="0", TORCHPRUNER_GENERIC_NATIVE="0"):
         TaylorAttributionMetric(model, loader(1, args.seed + 11, B), F.cross_entropy, dev).run_many(
@@ -299,7 +342,16 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
     out["engine_vs_generic_same_algorithm"] = round(value / generic, 2)
     log(f"[bench] generic path (MIOpen/hipBLASLt, same one-pass run_many): {generic:.0f} img/s -> engine "
         f"x{value / generic:.2f} ({time.perf_counter() - t0:.1f}s)")
+    return out
 
+
+def _bf16(args, model, convs, dev, world, timed_run, log, value, loader):
+    import torch
+    import torch.nn.functional as F
+
+    from torchpruner_amd import TaylorAttributionMetric
+    out = {}
+    B = args.batch
     # 1b. opt-in bf16 operands on the same engine (never the headline): throughput, and per-layer
     # rank agreement of the bf16 scores with the exact fp32 ones on the same batches
     t0 = time.perf_counter()
@@ -320,7 +372,14 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
                                            "score accumulators", "spearman_per_layer": [round(r, 5) for r in rho]}
     log(f"[bench] opt-in bf16 engine: {out['vgg_taylor_bf16_img_s']:.0f} img/s (x{out['bf16_vs_fp32_engine']} "
         f"fp32), min per-layer Spearman vs fp32 {min(rho):.4f} ({time.perf_counter() - t0:.1f}s)")
+    return out
 
+
+def _b100(args, model, convs, dev, world, timed_run, log, loader):
+    import torch.nn.functional as F
+
+    from torchpruner_amd import TaylorAttributionMetric
+    out = {}
     # 1c. the same fp32 Taylor run_many at the reference's attribution batch B=100 (nbVGG:193-196):
     # small batches run four in flight, each replaying a captured HIP graph of its step
     t0 = time.perf_counter()
@@ -335,7 +394,18 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
                           "pipeline": "4 batches in flight on 4 HIP streams, per-slot HIP-graph replay"}
     log(f"[bench] B=100 (reference attribution batch): {out['vgg_taylor_b100_img_s']:.0f} img/s "
         f"({time.perf_counter() - t0:.1f}s)")
+    return out
 
+
+def _resnet(args, dev, world, timed_run, log):
+    import torch
+    import torch.nn.functional as F
+
+    from torchpruner_amd import APoZAttributionMetric, TaylorAttributionMetric, get_resnet_pruning_graph
+    from torchpruner_amd.data import StreamLoader
+    from torchpruner_amd.models import resnet50
+    from torchpruner_amd.parallel import dist as pdist
+    out = {}
     # 2. config #3: ResNet-50, ImageNet shape, B=256 per GPU, every prunable bottleneck conv
     t0 = time.perf_counter()
     torch.manual_seed(0)
@@ -358,7 +428,18 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
     log(f"[bench] ResNet-50 B={rb}: APoZ {out['resnet50_apoz_img_s']:.0f} img/s, Taylor "
         f"{out['resnet50_taylor_img_s']:.0f} img/s ({time.perf_counter() - t0:.1f}s)")
     del rn
+    return out
 
+
+def _shapley(args, model, task, convs, dev, world, log):
+    import numpy as np
+    import torch
+    import torch.nn.functional as F
+
+    from torchpruner_amd import ShapleyAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.parallel import dist as pdist
+    out = {}
     # 3. config #4: Shapley sv_samples=5, 1000 images at B=100 (nbVGG:185-196), layers 0 / 6 / 12
     t0 = time.perf_counter()
     xs, ys = task.sample(1000, args.seed + 21)

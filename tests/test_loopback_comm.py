@@ -171,6 +171,7 @@ def test_shapley_work_split_modes():
         return m._work_split()
 
     assert run_loopback(3, body) == ["batches"] * 3
+    assert run_loopback(4, body) == ["hybrid"] * 4  # 6 = 4 whole + 2 prefix-split
     assert run_loopback(8, body) == ["prefixes"] * 8
     assert ShapleyAttributionMetric(model, dl, F.cross_entropy, torch.device("cpu"))._work_split() is None
 
@@ -198,3 +199,37 @@ def test_pruner_lower_level_api_syncs_indices():
     # rank 0's choices: out rows {0, 5} removed, then input column 0
     ref = w0[[1, 2, 3, 4]][:, [1, 2, 3]]
     assert torch.equal(outs[0][0], ref)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("reduction", ["mean", "none"])
+def test_shapley_balanced_sharding_bit_exact(world, reduction):
+    """10 batches on 8 ranks: whole batches for the first 8, the last 2
+    prefix-split on the single-rank chunk grid. Scores are bit-identical to one rank at every
+    world size, and the prefix work per rank is balanced (max / mean <= 1.1). The losses span a
+    wide range (a few near-zero, most large) to exercise the fp64 sums of fp32 deltas."""
+    torch.manual_seed(0)
+    model = with_forward_partial(nn.Sequential(nn.Linear(6, 48), nn.ReLU(), nn.Linear(48, 4))).eval()
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(40, 6, generator=g) * torch.logspace(-3, 2, 40).view(40, 1)
+    y = torch.randint(0, 4, (40,), generator=g)
+    dl = DeviceLoader(x, y, 4)  # 10 batches
+
+    def body(comm):
+        if comm is None or comm.rank == 0:
+            np.random.seed(9)
+        m = ShapleyAttributionMetric(model, dl, F.cross_entropy, torch.device("cpu"), sv_samples=3, prefix_batch=3,
+                                     reduction=reduction, group=comm)
+        return m.run(model[0]), m.last_work, m._work_split()
+
+    ref, ref_work, _ = body(None)
+    outs = run_loopback(world, body) if world > 1 else [body(None)]
+    for sv, _, split in outs:
+        np.testing.assert_array_equal(sv, ref)
+        if world == 8:
+            assert split == "hybrid"
+    evals = np.array([w["prefix_evals"] for _, w, _ in outs], dtype=float)
+    if world > 1:
+        assert evals.max() / evals.mean() <= 1.1, evals
+        # nothing but the boundary evaluations of the split ranges is redone
+        assert evals.sum() <= ref_work["prefix_evals"] * 1.25, (evals.sum(), ref_work)

@@ -68,7 +68,7 @@ class ShapleyAttributionMetric(_AttributionMetric):
         return ((i, x, y) for i, (x, y) in enumerate(self.data_gen))
 
     def _peek_source(self):
-        return self._source() if self._work_split() == "batches" else self._all_batches()
+        return self._source() if self._work_split() == "batches" else self._all_batches()  # hybrid: all
 
     def _run(self, module, sv_samples):
         why = []
@@ -128,6 +128,9 @@ class ShapleyAttributionMetric(_AttributionMetric):
         its own upstream forward and every prefix (scales for deep layers, where the upstream
         forward dominates); ``"prefixes"`` — every rank sees every batch and evaluates a
         contiguous range of the S*n prefixes (when there are fewer batches than ranks);
+        ``"hybrid"`` — the first floor(nb/world)*world batches go whole, round-robin, and the
+        nb % world remaining ones are prefix-split (10 batches on 8 ranks: 1 whole batch each +
+        1/8 of the prefixes of the last 2, instead of 2 ranks with 2 batches and 6 with 1);
         ``None`` — single rank / sharding disabled."""
         world, _ = self._world()
         if world == 1 or self.shard_data is False:
@@ -140,7 +143,9 @@ class ShapleyAttributionMetric(_AttributionMetric):
             nb = len(self.data_gen)
         except TypeError:
             return "prefixes"
-        return "batches" if nb >= world else "prefixes"
+        if nb < world:
+            return "prefixes"
+        return "batches" if nb % world == 0 else "hybrid"
 
     @staticmethod
     def _rank_of(perm, device):
@@ -150,63 +155,94 @@ class ShapleyAttributionMetric(_AttributionMetric):
         return r.to(device)
 
     def _accumulate_permutation(self, perm_t, rank_t, p_lo, p_hi, base_loss, evaluate, K, S, sink):
-        """Evaluate prefixes p_lo..p_hi of one permutation and add their deltas to ``sink``."""
+        """Evaluate prefixes p_lo..p_hi of one permutation and add their deltas to ``sink``.
+        Returns the number of prefix image-evaluations made (work accounting)."""
         B = base_loss.shape[0]
+        evals = 0
         # a range that starts inside the permutation takes its boundary loss L_{p_lo-1} from the
         # previous full chunk (the same stacked evaluation the single-rank run makes)
-        prev = base_loss if p_lo == 1 else evaluate(rank_t, max(1, p_lo - K), min(K, p_lo - 1))[-1]
+        if p_lo == 1:
+            prev = base_loss
+        else:
+            cnt0 = min(K, p_lo - 1)
+            prev = evaluate(rank_t, max(1, p_lo - K), cnt0)[-1]
+            evals += cnt0 * B
         cur = p_lo
         while cur <= p_hi:
             cnt = min(K, p_hi - cur + 1)
             Ls = evaluate(rank_t, cur, cnt)  # (cnt, B)
+            evals += cnt * B
             L = torch.cat([prev.view(1, B), Ls], 0).float().contiguous()
             sink(L, perm_t, cur - 1)
             prev = Ls[-1]
             cur += cnt
+        return evals
 
     def _run_batches(self, module, S, prepare):
-        """Shared driver. ``prepare(x, y)`` -> (n, B, per_sample, base_loss, evaluate)."""
+        """Shared driver. ``prepare(x, y)`` -> (n, B, per_sample, base_loss, evaluate).
+
+        Batches are "owned" (processed whole by this rank: its share of ``"batches"`` /
+        ``"hybrid"``, every batch on one rank) or "replicated" (seen by every rank, each
+        evaluating its contiguous share of the prefixes: ``"prefixes"``, the hybrid remainder).
+        Owned contributions are summed across ranks with their sample counts; replicated ones
+        are partial sums of one result whose count every rank already knows."""
         stats = self.reduction in ("mean", "sum")
         split = self._work_split()
+        world, rank = self._world()
+        nb_whole = None
+        if split == "hybrid":
+            nb_whole = (len(self.data_gen) // world) * world
         sv_col = None
-        slabs = []
-        count = 0
+        slabs_own, slabs_rep = [], []
+        count_own = count_rep = 0
         perms = None
         perm_ts = rank_ts = None
-        segs = None
-        batches = self._batches() if split == "batches" else \
-            ((i, _to(x, self.device), _to(y, self.device)) for i, x, y in self._iter_source(self._all_batches))
+        segs = {}
+        work = {"prefix_evals": 0, "upstream_batches": 0}
+        if split == "batches":
+            batches = self._batches()
+        else:
+            batches = ((i, _to(x, self.device), _to(y, self.device)) for i, x, y in self._iter_source(self._all_batches))
         with torch.no_grad():
             for bidx, x, y in batches:
+                replicated = split == "prefixes" or (split == "hybrid" and bidx >= nb_whole)
+                if split == "hybrid" and not replicated and bidx % world != rank:
+                    continue  # another rank's whole batch
                 n, B, per_sample, base_loss, evaluate = prepare(x, y)
+                work["upstream_batches"] += 1
                 if perms is None:
                     perms = self._permutations(n, S)  # drawn on rank 0, broadcast (R3)
                     perm_ts = [torch.as_tensor(p, dtype=torch.int32).to(base_loss.device) for p in perms]
                     rank_ts = [self._rank_of(p, base_loss.device) for p in perms]
                 K = self._prefix_chunk(B, per_sample)
-                if segs is None or segs[0] != K:
-                    segs = (K, self._segments(S, n, split == "prefixes", K))
+                if (K, replicated) not in segs:
+                    segs[(K, replicated)] = self._segments(S, n, replicated, K)
                 # deltas are summed unscaled and divided by S at the end. fp64 sums of fp32 loss
                 # differences are exact while the exponent span of the terms plus log2(count)
                 # stays within fp64's 53 bits, which holds in practice (fp32 losses of one run
                 # span far less): then any rank split / collective order gives the same bits
-                # (tests/test_distributed.py checks world sizes 1-8 on a wide loss range)
+                # (tests/test_loopback_comm.py checks world sizes 1-8)
                 if stats:
                     if sv_col is None:
                         sv_col = torch.zeros(n, dtype=torch.float64, device=base_loss.device)
                     sink = lambda L, pt, k0: ops.shapley_column(L, pt, sv_col, k0, 1.0)
                 else:
                     slab = torch.zeros(B, n, dtype=torch.float64, device=base_loss.device)
-                    slabs.append((bidx, slab))
+                    (slabs_rep if replicated else slabs_own).append((bidx, slab))
                     sink = lambda L, pt, k0, slab=slab: ops.shapley_scatter(L, pt, slab, 0, k0, 1.0)
                 with trace_range("tp.shapley.prefixes"):
-                    for j, p_lo, p_hi in segs[1]:
-                        self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi, base_loss, evaluate, K, S,
-                                                     sink)
-                count += B
-        if split == "batches" and perms is None:
+                    for j, p_lo, p_hi in segs[(K, replicated)]:
+                        work["prefix_evals"] += self._accumulate_permutation(perm_ts[j], rank_ts[j], p_lo, p_hi,
+                                                                             base_loss, evaluate, K, S, sink)
+                if replicated:
+                    count_rep += B
+                else:
+                    count_own += B
+        self.last_work = work
+        if split in ("batches", "hybrid") and perms is None:
             self._permutations(0, S)  # a rank without batches still joins the permutation broadcast (R3)
         if stats:
+            count = count_own + count_rep
             if split is not None:
                 with trace_range("tp.collective"):
                     # ranks agree on n even if one saw no batch; one (n + 1,) fp64 all-reduce (R4)
@@ -214,23 +250,28 @@ class ShapleyAttributionMetric(_AttributionMetric):
                     buf = torch.zeros(n + 1, dtype=torch.float64, device=self.device)
                     if sv_col is not None:
                         buf[:n] = sv_col
-                    buf[n] = float(count) if split == "batches" else 0.0
+                    buf[n] = float(count_own)
                     pdist.all_reduce_sum_(buf, self.group)
                     sv_col = buf[:n]
-                    if split == "batches":
-                        count = float(buf[n].item())
+                    count = float(buf[n].item()) + count_rep
             if sv_col is None:
                 return np.zeros(0)
             total = sv_col.cpu().numpy() / max(S, 1)
             return total / max(count, 1) if self.reduction == "mean" else total
-        if split == "batches":
+        parts = []
+        if split in ("batches", "hybrid"):
             with trace_range("tp.collective"):
-                sv = pdist.gather_ordered_rows(slabs, self.group)  # global batch order (R2)
-        else:
-            sv = torch.cat([t for _, t in slabs], 0) if slabs else torch.zeros(0, 0, dtype=torch.float64)
-            if split == "prefixes":
+                parts.append(pdist.gather_ordered_rows(slabs_own, self.group))  # global batch order (R2)
+        elif slabs_own:
+            parts.append(torch.cat([t for _, t in sorted(slabs_own, key=lambda s: s[0])], 0))
+        if split in ("prefixes", "hybrid") or slabs_rep:
+            rep = torch.cat([t for _, t in slabs_rep], 0) if slabs_rep else torch.zeros(0, 0, dtype=torch.float64)
+            if split is not None and rep.numel():
                 with trace_range("tp.collective"):
-                    pdist.all_reduce_sum_(sv, self.group)
+                    pdist.all_reduce_sum_(rep, self.group)
+            parts.append(rep)  # the replicated batches are the last ones (hybrid remainder)
+        parts = [p for p in parts if p.numel()]
+        sv = torch.cat([p.to(parts[0].device) for p in parts], 0) if parts else torch.zeros(0, 0, dtype=torch.float64)
         return self.aggregate_over_samples(sv.cpu().numpy() / max(S, 1))
 
     # ------------------------------------------------------------------ native path
