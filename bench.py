@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--generic-steps", type=int, default=2)
     ap.add_argument("--resnet-steps", type=int, default=8)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--quality-seeds", type=int, default=3,
+    ap.add_argument("--quality-seeds", type=int, default=5,
                     help="accuracy protocol over seeds seed..seed+K-1 (each its own teacher); top-1 figures "
                          "are means over the seeds, per-seed values are listed")
     ap.add_argument("--teacher-steps", type=int, default=None)
@@ -516,9 +516,12 @@ def accuracy(args, model, task, convs, scores, cfg, dev, log):
         runs.append(pq.run_protocol(s, dev, **cfg))  # its own teacher, task and held-out set
     mean = {k: float(np.mean([r[k] for r in runs])) for k in ("top1_before", "top1_pruned_taylor",
                                                              "top1_pruned_random")}
+    std = {k: float(np.std([r[k] for r in runs])) for k in ("top1_before", "top1_pruned_taylor",
+                                                           "top1_pruned_random")}
     ret = {m: float(np.mean([r[f"top1_pruned_{m}"] / max(r["top1_before"], 1e-9) for r in runs]))
            for m in ("taylor", "random")}
     pruned = {m: mean[f"top1_pruned_{m}"] for m in ("taylor", "random")}
+    diff = np.array([r["top1_pruned_taylor"] - r["top1_pruned_random"] for r in runs])
     out = {
         "top1_retained_at_50pct": round(ret["taylor"], 4),
         "top1_before": round(mean["top1_before"], 4),
@@ -528,12 +531,23 @@ def accuracy(args, model, task, convs, scores, cfg, dev, log):
         "quality_seeds": [r["seed"] for r in runs],
         "top1_pruned_50pct_taylor_per_seed": [round(r["top1_pruned_taylor"], 4) for r in runs],
         "top1_pruned_50pct_random_per_seed": [round(r["top1_pruned_random"], 4) for r in runs],
+        "top1_before_per_seed": [round(r["top1_before"], 4) for r in runs],
+        "top1_mean_std": {"before": [round(mean["top1_before"], 4), round(std["top1_before"], 4)],
+                          "taylor": [round(mean["top1_pruned_taylor"], 4), round(std["top1_pruned_taylor"], 4)],
+                          "random": [round(mean["top1_pruned_random"], 4), round(std["top1_pruned_random"], 4)]},
+        "taylor_minus_random": {"per_seed": [round(float(d), 4) for d in diff], "mean": round(float(diff.mean()), 4),
+                                "std": round(float(diff.std(ddof=1)) if len(diff) > 1 else 0.0, 4),
+                                "taylor_wins": int((diff > 0).sum()), "seeds": int(len(diff)),
+                                "kernel_choices": "TUNER.fixed() (untimed heuristic configs: bit-reproducible)"},
         "params_before_after": [sum(p.numel() for p in model.parameters()), params],
         "prune_protocol": {k: cfg[k] for k in ("frac", "increments", "ft_steps", "final_ft_steps", "recal_batches",
                                                "score_imgs", "val_imgs", "ft_lr", "noise", "teacher_wd")},
         "top1_layerwise_mask_50pct_taylor": round(lw_t, 4),
         "top1_layerwise_mask_50pct_random": round(lw_r, 4),
     }
+    log(f"[bench] Taylor - Random per seed {out['taylor_minus_random']['per_seed']}: mean "
+        f"{out['taylor_minus_random']['mean']:+.4f} +- {out['taylor_minus_random']['std']:.4f}, Taylor wins "
+        f"{out['taylor_minus_random']['taylor_wins']}/{len(diff)}")
     log(f"[bench] seeds {out['quality_seeds']}: mean top-1 before {mean['top1_before']:.4f}; 50% of every conv "
         f"pruned (iterative, {cfg['increments']} increments/layer, {cfg['ft_steps']} SGD steps each, "
         f"+{cfg['final_ft_steps']}): Taylor {pruned['taylor']:.4f}, Random {pruned['random']:.4f}; layerwise mask "

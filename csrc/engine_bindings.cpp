@@ -90,10 +90,10 @@ hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* per
 hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
 int tp_wino4_u_img();
 int tp_wino4_ok(int H, int W, int C, int K);
-int tp_wino4_lds_bytes(int S);
+int tp_wino4_lds_bytes(int S, int variant);
 hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act, float* taylor,
-                         float* apoz, int tay_mode, int splits, float* ws, hipStream_t st);
+                         float* apoz, int tay_mode, int splits, float* ws, int variant, hipStream_t st);
 }
 
 namespace {
@@ -452,7 +452,8 @@ void need_u4(const at::Tensor& u, int64_t C, int64_t K) {
 std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at::Tensor& u,
                                                   const c10::optional<at::Tensor>& scale,
                                                   const c10::optional<at::Tensor>& shift, bool relu, bool pool,
-                                                  const c10::optional<at::Tensor>& apoz, int64_t splits) {
+                                                  const c10::optional<at::Tensor>& apoz, int64_t splits,
+                                                  int64_t variant) {
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
   need_u4(u, C, K);
@@ -480,14 +481,14 @@ std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at:
   TP_CHECK_HIP(tp_conv_wino4(x.data_ptr<float>(), u.data_ptr<float>(), (int)B, (int)H, (int)C, (int)K,
                              pool ? EPI_FWD_POOL : EPI_FWD, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
                              pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap, 0, (int)sp,
-                             sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                             sp > 1 ? ws.data_ptr<float>() : nullptr, (int)variant, cur_stream()));
   return {out, am};
 }
 
 // F(4x4) dgrad with the conv_wino_dgrad epilogue contract (no unpooling: pass the unpooled grad)
 at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at::Tensor& act,
                             const c10::optional<at::Tensor>& bn_scale, const c10::optional<at::Tensor>& taylor,
-                            bool want_out, int64_t tay_mode, int64_t splits) {
+                            bool want_out, int64_t tay_mode, int64_t splits, int64_t variant) {
   need(g, "g", 4);
   need(act, "act", 4);
   const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
@@ -515,7 +516,7 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
   TP_CHECK_HIP(tp_conv_wino4(g.data_ptr<float>(), ut.data_ptr<float>(), (int)B, (int)H, (int)Cout, (int)Cin, EPI_BWD,
                              sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(),
                              tay, nullptr, (int)tay_mode, (int)sp, sp > 1 ? ws.data_ptr<float>() : nullptr,
-                             cur_stream()));
+                             (int)variant, cur_stream()));
   return out;
 }
 
@@ -892,7 +893,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("wino_lds_bytes() -> int", []() -> int64_t { return tp_wino_lds_bytes(); });
-  m.def("wino4_lds_bytes(int S) -> int", [](int64_t S) -> int64_t { return tp_wino4_lds_bytes((int)S); });
+  m.def("wino4_lds_bytes(int S, int variant=0) -> int",
+        [](int64_t S, int64_t variant) -> int64_t { return tp_wino4_lds_bytes((int)S, (int)variant); });
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
   m.def("maxpool2_nhwc(Tensor x) -> (Tensor, Tensor)");
   m.def("maxpool_nhwc(Tensor x, int k, int s, int pad) -> Tensor");
@@ -928,9 +930,9 @@ void register_engine_ops_def(torch::Library& m) {
         "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True, int tay_mode=0) -> Tensor");
   m.def("wino4_weights(Tensor w, bool flip_t, int K=0, int C=0) -> Tensor");
   m.def("conv_wino4_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, "
-        "Tensor(a!)? apoz=None, int splits=1) -> (Tensor, Tensor)");
+        "Tensor(a!)? apoz=None, int splits=1, int variant=0) -> (Tensor, Tensor)");
   m.def("conv_wino4_dgrad(Tensor g, Tensor ut, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, bool want_out, "
-        "int tay_mode=0, int splits=1) -> Tensor");
+        "int tay_mode=0, int splits=1, int variant=0) -> Tensor");
 }
 
 void register_engine_ops_impl(torch::Library& m) {

@@ -159,17 +159,19 @@ __device__ __forceinline__ void output_transform(const float (&m)[36], float (&y
         y[4 * r + 2], y[4 * r + 3]);
 }
 
-// Epilogue of a block of NW waves = NW/2 groups of 16 tiles x 2 output halves of 16 channels:
-// outputs staged in LDS per half of 32 tiles (ya: channels 0-15, yb: 16-31), then coalesced
-// 128-B traffic; ``part`` receives per-(tile, channel) partial sums (TB x 32 floats).
-template <int EPI, int S, int NW>
-__device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[NPT], int t0, int k0, float* ya, float* yb,
+// Epilogue of a block of NW waves holding PPW (16-tile group, 16-channel half) accumulator sets
+// each: TB = 8 * NW * PPW tiles x 32 output channels. Virtual wave v = wave + NW * pp owns group
+// v % (TB/16) and half v / (TB/16) (PPW = 1: MODE 2/3; PPW = 2: the wide kernel, one wave = one
+// group x both halves). Outputs are staged in LDS per half of 32 tiles (ya: channels 0-15, yb:
+// 16-31), then coalesced 128-B traffic; ``part`` receives per-(tile, channel) partial sums
+// (TB x 32 floats).
+template <int EPI, int S, int NW, int PPW = 1>
+__device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], int t0, int k0, float* ya, float* yb,
                                          float* part) {
   constexpr int TPR = S / 4, TI = TPR * TPR;
-  constexpr int GROUPS = NW / 2, TB = 16 * GROUPS, HALVES = TB / 32, TPW = 32 / NW;  // tiles per wave (phase 2)
+  constexpr int GROUPS = NW * PPW / 2, TB = 16 * GROUPS, HALVES = TB / 32, TPW = 32 / NW;  // tiles per wave (phase 2)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int grp = wave % GROUPS, nh = wave / GROUPS;
   const bool want_part = EPI == BWD ? p.taylor != nullptr : p.apoz != nullptr;
   const int c4 = lane & 7;
   const int k = k0 + 4 * c4;
@@ -181,18 +183,22 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[NPT], int t
 #pragma unroll
   for (int hf = 0; hf < HALVES; ++hf) {
     // ---- phase 1: output transform; park this half's 32 tiles x 16 px x (16 + 16) ch -------
-    if (grp / 2 == hf) {
-      float* ybuf = nh ? yb : ya;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int tl = (grp & 1) * 16 + 4 * g + r;
-        float m[36], y[16];
+    for (int pp = 0; pp < PPW; ++pp) {
+      const int vw = wave + NW * pp, grp = vw % GROUPS, nh = vw / GROUPS;
+      if (grp / 2 == hf) {
+        float* ybuf = nh ? yb : ya;
 #pragma unroll
-        for (int x = 0; x < NPT; ++x) m[x] = acc[x][r];
-        output_transform(m, y);
-        float* dst = ybuf + tl * TPL + j;
+        for (int r = 0; r < 4; ++r) {
+          const int tl = (grp & 1) * 16 + 4 * g + r;
+          float m[36], y[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) dst[q * 16] = y[q];
+          for (int x = 0; x < NPT; ++x) m[x] = acc[pp][x][r];
+          output_transform(m, y);
+          float* dst = ybuf + tl * TPL + j;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) dst[q * 16] = y[q];
+        }
       }
     }
     __syncthreads();
@@ -522,7 +528,7 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
       if (t == 1234.5f) p.out[0] = t;
       return;
     }
-    epilogue<EPI, S, 4>(p, acc, t0, k0, us0, xs0, pts);
+    epilogue<EPI, S, 4>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us0, xs0, pts);
     return;
   }
   float a0[36], a1[36], b0v[36], b1v[36];
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
     if (t == 1234.5f) p.out[0] = t;  // keeps the main loop alive
     return;
   }
-  epilogue<EPI, S, 4>(p, acc, t0, k0, us0, us1, xs0);
+  epilogue<EPI, S, 4>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us0, us1, xs0);
 }
 
 
@@ -793,8 +799,251 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
     if (t == 1234.5f) p.out[0] = t;
     return;
   }
-  if constexpr (XDBL) epilogue<EPI, S, 8>(p, acc, t0, k0, xs0, xs1, us);
-  else epilogue<EPI, S, 4>(p, acc, t0, k0, us, xs0, xs1);
+  if constexpr (XDBL) epilogue<EPI, S, 8>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, xs0, xs1, us);
+  else epilogue<EPI, S, 4>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us, xs0, xs1);
+}
+
+// WIDE: one block of 4 waves per CU (one wave per SIMD) = 64 tiles x 32 output channels; wave w
+// owns the 16 tiles of group w x BOTH 16-channel halves (72 accumulator tiles, 288 registers).
+//
+// Why: fp32 VALU work does not hide under fp32 MFMAs on gfx950 (profiles/wino4/
+// microbench_mfma_valu_lds.txt), so the input transform's cost per MFMA is what bounds the MODE 2/3
+// kernels (MFMA util 0.37-0.6). There, a wave multiplies each transformed patch by 16 output
+// channels and the two waves of a 16-tile group transform the same patches. Here each patch is
+// transformed once per block and feeds 32 channels: half the transform VALU and half the LDS-DMA
+// bytes per MFMA (the 36-KB U image of a chunk serves 64 tiles instead of 32). The price is one
+// wave per SIMD (no second block to run during a barrier), so the DMA runs well ahead: X is
+// double-buffered (1.5 chunks of lead), U in parity halves (each issued half a chunk ahead).
+// Same U images (layout 1), same staged X geometry (GeoT<S, 64>) and epilogues as MODE 2.
+// 288 accumulator registers do not fit the 256 AGPRs: with builtins the compiler shuffles them
+// between AGPRs, VGPRs and scratch inside the MFMA loop (261 v_accvgpr moves + scratch per chunk,
+// measured in the .s). So the MFMAs are inline asm with the accumulators pinned by constraint:
+// points 0-31 ("a": 256 AGPRs) and points 32-35 ("v": 32 VGPRs). hipcc pads no hazard inside an
+// asm string (cdna_hip_programming.md §5.7): each group opens with s_nop 1 (a VALU-written A/B
+// operand, or the zeroed accumulators, -> MFMA), consecutive MFMAs on one accumulator take it
+// whole as C (no wait states), and the loop ends with s_nop 15 before the epilogue reads them.
+#define W4W_AGPR_POINTS 32
+#define W4W_MFMA4(C, c0, c1, c2, c3, a0, a1, w0, w1)                                                  \
+  asm volatile("s_nop 1\n\t"                                                                         \
+               "v_mfma_f32_16x16x4_f32 %0, %4, %6, %0\n\t"                                           \
+               "v_mfma_f32_16x16x4_f32 %1, %4, %8, %1\n\t"                                           \
+               "v_mfma_f32_16x16x4_f32 %2, %5, %7, %2\n\t"                                           \
+               "v_mfma_f32_16x16x4_f32 %3, %5, %9, %3"                                               \
+               : "+" C(c0), "+" C(c1), "+" C(c2), "+" C(c3)                                           \
+               : "v"(a0), "v"(a1), "v"(w0.x), "v"(w0.y), "v"(w1.x), "v"(w1.y))
+
+template <int EPI, int S>
+__global__ __launch_bounds__(256, 1) void wino4_wide(Args p) {
+  constexpr int NW = 4, TB = 64;
+  using G = GeoT<S, TB>;
+  constexpr int TPR = S / 4, TI = TPR * TPR;
+  constexpr int PL = G::NI * G::IP;
+  constexpr int NXI = (2 * PL + 63) / 64;  // X DMA wave-instructions (64 16-B slots each)
+  constexpr int KX = (NXI + NW - 1) / NW;
+  constexpr int XN = (NXI > 34 ? NXI : 34) * 256;  // >= 32 * TPL floats (an epilogue half)
+  __shared__ __attribute__((aligned(16))) float us[U_IMG];
+  __shared__ __attribute__((aligned(16))) float xs0[XN];
+  __shared__ __attribute__((aligned(16))) float xs1[XN];
+  static_assert(32 * TPL <= XN && TB * TK <= U_IMG, "epilogue buffers");
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const int n_k = p.K / TK;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = tile % n_k, k0 = kb * TK;
+  const int blk_p = tile / n_k;
+  const int t0 = blk_p * TB;
+  const int b0 = t0 / TI;
+
+  const i32x4v urs = raw_rsrc(p.u, (unsigned)((long long)(p.C / 8) * n_k * U_IMG * 4));
+  const i32x4v xrs = raw_rsrc(p.x, (unsigned)(p.x_elems * 4));
+
+  const int tib = wave * 16 + j;
+  const int il = tib / TI, ti = tib - il * TI, tr = ti / TPR, tc = ti - tr * TPR;
+  const int sbase = S == 4 ? il * G::IP : il * G::IP + 4 * tr * G::RWP + (G::PAD ? 5 : 4) * tc;
+  const int poff = ((g >> 1) * PL + sbase) * 4 + (g & 1) * 2;  // plane g/2, channels 2g, 2g+1
+
+  // X DMA sources, 16 bits per instruction (pixel index in the block's images, plane, valid)
+  unsigned xcode[(KX + 1) / 2];
+#pragma unroll
+  for (int i = 0; i < (KX + 1) / 2; ++i) xcode[i] = 0u;
+#pragma unroll
+  for (int i = 0; i < KX; ++i) {
+    const int slot = (wave + NW * i) * 64 + lane;
+    const int h = slot / PL, s = slot - h * PL;
+    const int im = s / G::IP, rem = s - im * G::IP;
+    int xx, yy;
+    bool ok;
+    if constexpr (S == 4) {
+      yy = rem / 4;
+      xx = rem - yy * 4;
+      ok = rem < 16;
+    } else {
+      const int row = rem / G::RWP, colp = rem - row * G::RWP;
+      int w5 = 0;
+      if constexpr (G::PAD) {
+        const int blk5 = colp / 5;
+        w5 = colp - blk5 * 5;
+        xx = 4 * blk5 + w5 - 1;
+      } else {
+        xx = colp - 1;
+      }
+      yy = row - 1;
+      ok = w5 != 4 && row < G::RH && xx >= 0 && xx < S && yy >= 0 && yy < S;
+    }
+    ok = ok && h < 2 && im < G::NI && b0 + im < p.B;
+    const unsigned code = ok ? (unsigned)((im * S + yy) * S + xx) | ((unsigned)h << 11) | 0x1000u : 0u;
+    xcode[i >> 1] |= code << (16 * (i & 1));
+  }
+  static_assert(G::NI * S * S <= 2048, "X pixel code");
+  const unsigned xbase = (unsigned)b0 * S * S * (unsigned)p.C * 4u;
+  const unsigned lane16 = (unsigned)lane * 16u;
+  const unsigned c4 = (unsigned)p.C * 4u;
+
+  auto stage_u = [&](int c0, int hf) {  // U half hf (18 point pairs) of chunk c0/8
+    if (p.dbg & 1) return;
+    const unsigned ub = (unsigned)(((c0 >> 3) * n_k + kb) * U_IMG) * 4u;
+#pragma unroll
+    for (int i = 0; i < (18 + NW - 1) / NW; ++i) {
+      const int pt = wave + NW * i;
+      if (pt < 18) {
+        const int q = hf * 18 + pt;
+        dma16_asm(urs, lds_addr(us + q * 256), lane16, ub + (unsigned)q * 1024u);
+      }
+    }
+  };
+  auto stage_x = [&](int c0, float* xd) {
+    if (p.dbg & 2) return;
+#pragma unroll
+    for (int i = 0; i < KX; ++i)
+      if (wave + NW * i < NXI) {
+        const unsigned code = xcode[i >> 1] >> (16 * (i & 1));
+        const unsigned off = (code & 0x1000u) ? xbase + (code & 0x7ffu) * c4 + ((code >> 7) & 16u) : OOB;
+        dma16_asm(xrs, lds_addr(xd + (wave + NW * i) * 256), off, (unsigned)c0 * 4u);
+      }
+  };
+
+  const int nc_all = p.C / 8, cps = (nc_all + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c_lo = (int)blockIdx.y * cps, nc = min(nc_all, c_lo + cps);
+  f32x4 acc[2][NPT];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int x = 0; x < NPT; ++x) acc[h][x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* ul = us + j * 8 + 2 * (g ^ ((j >> 3) << 1));  // + nh * 128 + (e * 18 + pair) * 256
+  // U DMAs per wave per half: waves 0, 1 issue 5, waves 2, 3 issue 4 (18 point pairs over 4 waves)
+  const int nu = (18 - wave + NW - 1) / NW;
+  const int nx = (NXI - wave + NW - 1) / NW;  // this wave's X DMAs per chunk
+  // wait until at most the ``keep`` youngest of this wave's DMAs are in flight (vmcnt is in-order)
+  auto wait_keep = [&](int keep) {
+    switch (keep) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+      case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+      case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+      case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+      case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+      case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+      case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+      case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+      case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+      case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+      case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+      case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  };
+
+  // DMA order per wave: [X(c_lo)] [X(c_lo+1)] U0(c_lo) | per chunk c: U1(c) ... U0(c+1) X(c+2)
+  // Top of chunk c (in flight, youngest last): U0(c) is followed by nothing at c = c_lo except
+  // itself; later X(c+1) was issued after U0(c) (same mid-chunk batch: U0(c) then X(c+1)), so
+  // U0(c) + X(c) landed <=> at most this wave's X(c+1) DMAs are still in flight.
+  stage_x(8 * c_lo, xs0);
+  stage_u(8 * c_lo, 0);
+  if (c_lo + 1 < nc) stage_x(8 * (c_lo + 1), xs1);
+  for (int c = c_lo; c < nc; ++c) {
+    float* xb = ((c - c_lo) & 1) ? xs1 : xs0;  // X(c)
+    // c_lo: issued X(c), U0(c), X(c+1): keep X(c+1). c > c_lo: ... U0(c), X(c+1): keep X(c+1).
+    wait_keep(c + 1 < nc ? nx : 0);
+    lds_barrier();  // U0(c), X(c) visible; every wave is done with U1(c-1)
+    stage_u(8 * c, 1);
+    f2v v[36];
+    {
+      const float* p0 = xb + poff;
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          f2v d = {0.f, 0.f};
+          if constexpr (S == 4) {
+            if (r >= 1 && r <= 4 && q >= 1 && q <= 4) d = *reinterpret_cast<const f2v*>(p0 + ((r - 1) * 4 + (q - 1)) * 4);
+          } else {
+            d = *reinterpret_cast<const f2v*>(p0 + (r * G::RWP + q + (G::PAD && q >= 4 ? 1 : 0)) * 4);
+          }
+          v[r * 6 + q] = d;
+          __builtin_amdgcn_sched_barrier(0);  // one ds_read_b64 each (no ds_read2 merging)
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) bt6p(v[q], v[6 + q], v[12 + q], v[18 + q], v[24 + q], v[30 + q]);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) bt6p(v[6 * r], v[6 * r + 1], v[6 * r + 2], v[6 * r + 3], v[6 * r + 4], v[6 * r + 5]);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (e == 1) {
+        // U1(c) landed: in flight after it is nothing this chunk (X(c+1) was issued before it)
+        wait_keep(0);
+        lds_barrier();  // U1(c) visible; every wave is done with U0(c) and with its X(c) patch
+        if (c + 1 < nc) stage_u(8 * (c + 1), 0);
+        if (c + 2 < nc) stage_x(8 * (c + 2), xb);
+      }
+      const float* ue = ul + e * 18 * 256;
+      float2 wq[2][2];  // [pair parity][channel half]
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          wq[s2][h] = *reinterpret_cast<const float2*>(ue + s2 * 256 + h * 128);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+      for (int i = 0; i < 18; ++i) {
+        const float2 w0 = wq[i & 1][0], w1 = wq[i & 1][1];
+        if (i + 2 < 18) {
+          wq[i & 1][0] = *reinterpret_cast<const float2*>(ue + (i + 2) * 256);
+          __builtin_amdgcn_sched_barrier(0);
+          wq[i & 1][1] = *reinterpret_cast<const float2*>(ue + (i + 2) * 256 + 128);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const int x = 2 * i;
+        const float a0 = e ? v[x].y : v[x].x, a1 = e ? v[x + 1].y : v[x + 1].x;
+        if (x < W4W_AGPR_POINTS) W4W_MFMA4("a", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
+        else W4W_MFMA4("v", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  (void)nu;
+  // the last MFMA's results -> the epilogue's reads: 12 wait states for an 8-pass XDL op
+  asm volatile("s_nop 15\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (p.dbg & 16) {
+    float t = 0.f;
+#pragma unroll
+    for (int x = 0; x < NPT; ++x) t += acc[0][x][0] + acc[1][x][0];
+    if (t == 1234.5f) p.out[0] = t;
+    return;
+  }
+  epilogue<EPI, S, 4, 2>(p, acc, t0, k0, xs0, xs1, us);
 }
 
 // U = G g G^T into the LDS images: layout 0 (MODE 0/1): word ((x*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + e
@@ -876,16 +1125,20 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
                                               uint8_t* out_argmax, const float* act, float* taylor,
                                               float* apoz, int tay_mode, hipStream_t st);
 
+// variant 0: the TP_W4_MODE kernel (default MODE 3); variant 1: the WIDE kernel (64-tile blocks,
+// one wave per SIMD, each wave 16 tiles x 32 outputs).
 extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi,
                                     const float* scale, const float* shift, int relu, float* out, uint8_t* out_argmax,
                                     const float* act, float* taylor, float* apoz, int tay_mode, int splits,
-                                    float* ws, hipStream_t st) {
+                                    float* ws, int variant, hipStream_t st) {
   using namespace tp::w4;
   if (!tp_wino4_ok(S, S, C, K) || B <= 0) return hipErrorInvalidValue;
   const int nc = C / 8;
   splits = std::max(1, std::min(splits, nc));
   splits = (nc + (nc + splits - 1) / splits - 1) / ((nc + splits - 1) / splits);  // no empty split
-  if (splits > 1 && (kernel_mode() < 2 || !ws)) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 1) return hipErrorInvalidValue;
+  const bool wide = variant == 1;
+  if (splits > 1 && ((!wide && kernel_mode() < 2) || !ws)) return hipErrorInvalidValue;
   if (epi < 0 || epi > 2 || (epi == BWD && !act) || (epi != BWD && !out) || (epi == FWD_POOL && !out_argmax))
     return hipErrorInvalidValue;
   Args a{};
@@ -916,8 +1169,8 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
     return v;
   }();
   a.dbg = dbg;
-  const int mode = kernel_mode();
-  const int tb = mode == 2 ? 64 : TILES;  // MODE 3: 32-tile blocks
+  const int mode = wide ? 4 : kernel_mode();
+  const int tb = mode == 2 || mode == 4 ? 64 : TILES;  // MODE 3: 32-tile blocks
   const int n_p = (a.P + tb - 1) / tb, n_k = K / TK;
   const dim3 grid(n_p * n_k, splits);
   if (splits > 1) {
@@ -934,7 +1187,8 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
     if (b.slab * splits >= (1ll << 31)) return hipErrorInvalidValue;
 #define TP_W4P(SS)                                                                      \
   do {                                                                                  \
-    if (mode == 2) wino4_m2<PARTIAL, SS, 8><<<grid, 512, 0, st>>>(b);                   \
+    if (mode == 4) wino4_wide<PARTIAL, SS><<<grid, 256, 0, st>>>(b);                    \
+    else if (mode == 2) wino4_m2<PARTIAL, SS, 8><<<grid, 512, 0, st>>>(b);              \
     else wino4_m2<PARTIAL, SS, 4><<<grid, 256, 0, st>>>(b);                             \
   } while (0)
     if (S == 32) TP_W4P(32);
@@ -950,7 +1204,8 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   }
 #define TP_W4(E, SS)                                              \
   do {                                                            \
-    if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a);   \
+    if (mode == 4) wino4_wide<E, SS><<<grid, 256, 0, st>>>(a);    \
+    else if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a); \
     else if (mode == 3) wino4_m2<E, SS, 4><<<grid, 256, 0, st>>>(a); \
     else if (mode == 1) wino4_f4x3<E, SS, 1><<<grid, 256, 0, st>>>(a); \
     else wino4_f4x3<E, SS, 0><<<grid, 256, 0, st>>>(a);          \
@@ -971,12 +1226,13 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 }
 
 // static LDS bytes of a wino4 instantiation (occupancy / budget guard)
-extern "C" int tp_wino4_lds_bytes(int S) {
+extern "C" int tp_wino4_lds_bytes(int S, int variant) {
   using namespace tp::w4;
-  const int m = kernel_mode();
+  const int m = variant == 1 ? 4 : kernel_mode();
   const void* f = nullptr;
 #define TP_W4F(SS)                                                                            \
-  f = m == 2 ? (const void*)wino4_m2<BWD, SS, 8>                                              \
+  f = m == 4 ? (const void*)wino4_wide<BWD, SS>                                               \
+             : m == 2 ? (const void*)wino4_m2<BWD, SS, 8>                                     \
              : m == 3 ? (const void*)wino4_m2<BWD, SS, 4> : (const void*)wino4_f4x3<BWD, SS, 0>
   if (S == 32) TP_W4F(32);
   else if (S == 16) TP_W4F(16);

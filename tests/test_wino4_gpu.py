@@ -25,7 +25,8 @@ def _fwd_ref(x, w, sc, sh):
 
 
 @pytest.mark.parametrize("S,C,K,B", SHAPES)
-def test_wino4_forward(cuda, S, C, K, B):
+@pytest.mark.parametrize("variant", [0, 1])  # 1: the wide kernel (64-tile blocks, 32 outputs per wave)
+def test_wino4_forward(cuda, S, C, K, B, variant):
     T = _ops()
     g = torch.Generator(device=cuda).manual_seed(S * 1000 + C + K)
     x = torch.randn(B, S, S, C, device=cuda, generator=g)
@@ -34,7 +35,7 @@ def test_wino4_forward(cuda, S, C, K, B):
     sh = torch.randn(K, device=cuda, generator=g) * 0.1
     u = T.wino4_weights(w, False, 0, 0)
     apoz = torch.zeros(B, K, device=cuda)
-    y, _ = T.conv_wino4_fwd(x, u, sc, sh, True, False, apoz)
+    y, _ = T.conv_wino4_fwd(x, u, sc, sh, True, False, apoz, 1, variant)
     ref = _fwd_ref(x, w, sc, sh)
     err = ((y.double() - ref).abs().max() / ref.abs().max()).item()
     assert err < 2e-5, err
@@ -42,7 +43,7 @@ def test_wino4_forward(cuda, S, C, K, B):
     assert (apoz - cnt).abs().max().item() <= max(2.0, 1e-3 * S * S), (apoz - cnt).abs().max()
     # pooled epilogue
     apoz2 = torch.zeros(B, K, device=cuda)
-    yp, am = T.conv_wino4_fwd(x, u, sc, sh, True, True, apoz2)
+    yp, am = T.conv_wino4_fwd(x, u, sc, sh, True, True, apoz2, 1, variant)
     r4 = ref.permute(0, 3, 1, 2)
     pooled, idx = F.max_pool2d(r4, 2, return_indices=True)
     errp = ((yp.double() - pooled.permute(0, 2, 3, 1)).abs().max() / pooled.abs().max()).item()
@@ -61,7 +62,8 @@ def test_wino4_forward(cuda, S, C, K, B):
 
 @pytest.mark.parametrize("S,C,K,B", SHAPES)
 @pytest.mark.parametrize("mode", [0, 1])
-def test_wino4_dgrad(cuda, S, C, K, B, mode):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino4_dgrad(cuda, S, C, K, B, mode, variant):
     """dgrad of conv(Cin=K -> Cout=C): g (B,S,S,C) -> dL/dact (B,S,S,K) with the W_BWD epilogue."""
     T = _ops()
     Cout, Cin = C, K
@@ -73,7 +75,7 @@ def test_wino4_dgrad(cuda, S, C, K, B, mode):
     ut = T.wino4_weights(w, True, 0, 0)
     R = 2
     tay = torch.zeros(R, B, Cin, device=cuda)
-    out = T.conv_wino4_dgrad(go, ut, act, sc, tay, True, mode)
+    out = T.conv_wino4_dgrad(go, ut, act, sc, tay, True, mode, 1, variant)
     dx = torch.nn.grad.conv2d_input((B, Cin, S, S), w.double(), go.double().permute(0, 3, 1, 2), padding=1)
     dx = dx.permute(0, 2, 3, 1)
     ref_out = torch.where(act.double() > 0, dx * sc.double(), torch.zeros((), dtype=torch.float64, device=cuda))
@@ -84,7 +86,7 @@ def test_wino4_dgrad(cuda, S, C, K, B, mode):
     got_t = tay.double().sum(0)
     errt = ((got_t - ref_t).abs().max() / ref_t.abs().max()).item()
     assert errt < 2e-5, errt
-    if S != 32:
+    if S != 32 or variant == 1:
         assert tay[1].abs().max().item() == 0.0  # whole images per block: slot 0 only
 
 
@@ -93,11 +95,13 @@ def test_wino4_deterministic_and_lds_budget(cuda):
     x = torch.randn(7, 16, 16, 64, device=cuda)
     w = torch.randn(128, 64, 3, 3, device=cuda) * 0.05
     u = T.wino4_weights(w, False, 0, 0)
-    a1, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None)
-    a2, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None)
-    assert torch.equal(a1, a2)
+    for variant in (0, 1):
+        a1, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None, 1, variant)
+        a2, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None, 1, variant)
+        assert torch.equal(a1, a2)
     for S in (4, 8, 16, 32):
         assert 0 < T.wino4_lds_bytes(S) <= 160 * 1024
+        assert 0 < T.wino4_lds_bytes(S, 1) <= 160 * 1024
 
 
 def test_wino4_rejects_bad_shapes(cuda):
@@ -112,7 +116,8 @@ def test_wino4_rejects_bad_shapes(cuda):
 
 @pytest.mark.parametrize("S,C,K,B", [(32, 64, 64, 3), (16, 128, 96, 2), (8, 256, 64, 5), (4, 512, 64, 7)])
 @pytest.mark.parametrize("splits", [2, 4])
-def test_wino4_split_k(cuda, S, C, K, B, splits):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wino4_split_k(cuda, S, C, K, B, splits, variant):
     """Channel split-K (raw slabs + the deterministic combine) == one K pass, all epilogues."""
     T = _ops()
     import os
@@ -127,8 +132,8 @@ def test_wino4_split_k(cuda, S, C, K, B, splits):
     for pool in (False, True):
         a1 = torch.zeros(B, K, device=cuda)
         a2 = torch.zeros(B, K, device=cuda)
-        y1, m1 = T.conv_wino4_fwd(x, u, sc, sh, True, pool, a1, 1)
-        y2, m2 = T.conv_wino4_fwd(x, u, sc, sh, True, pool, a2, splits)
+        y1, m1 = T.conv_wino4_fwd(x, u, sc, sh, True, pool, a1, 1, variant)
+        y2, m2 = T.conv_wino4_fwd(x, u, sc, sh, True, pool, a2, splits, variant)
         assert ((y1 - y2).abs().max() / y1.abs().max()).item() < 1e-4
         assert (a1 - a2).abs().max().item() <= 2.0
         if pool:
@@ -144,10 +149,10 @@ def test_wino4_split_k(cuda, S, C, K, B, splits):
     scp = torch.rand(K, device=cuda, generator=g) + 0.5
     ut = T.wino4_weights(wd, True, 0, 0)
     t1, t2 = torch.zeros(2, B, K, device=cuda), torch.zeros(2, B, K, device=cuda)
-    o1 = T.conv_wino4_dgrad(go, ut, act, scp, t1, True, 0, 1)
-    o2 = T.conv_wino4_dgrad(go, ut, act, scp, t2, True, 0, splits)
+    o1 = T.conv_wino4_dgrad(go, ut, act, scp, t1, True, 0, 1, variant)
+    o2 = T.conv_wino4_dgrad(go, ut, act, scp, t2, True, 0, splits, variant)
     assert ((o1 - o2).abs().max() / o1.abs().max()).item() < 1e-4  # summation order only
     s1, s2 = t1.double().sum(0), t2.double().sum(0)
     assert ((s1 - s2).abs().max() / s1.abs().max()).item() < 1e-4
-    o3 = T.conv_wino4_dgrad(go, ut, act, scp, None, True, 0, splits)
+    o3 = T.conv_wino4_dgrad(go, ut, act, scp, None, True, 0, splits, variant)
     assert torch.equal(o2, o3)  # deterministic combine

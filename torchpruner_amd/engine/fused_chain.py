@@ -49,6 +49,7 @@ WINO_LDS = -2  # the same with the block input region staged through LDS
 WINO_UNP = -3  # dgrad of a pooled layer: explicit vectorised unpool, then the staged kernel on the
                # dense full-resolution gradient (vs rebuilding it from pooled cells per chunk)
 WINO4 = -4  # Winograd F(4x4,3x3) kernel (wino4.hip): square 4/8/16/32-pixel maps, 1.78x fewer MFMAs
+WINO4W = -5  # the same transform, WIDE kernel: 64-tile blocks, one wave per SIMD, 32 outputs per wave
 CFG_BF16 = 256  # tile-config flag of conv_igemm: bf16 operands / fp32 accumulation (opt-in, compute_dtype)
 _BF16_CFGS = (0, 2, 3)  # the implicit-GEMM tiles built with bf16 variants (conv_mfma.hip launch_any)
             # than F(2x2); dgrads of pooled layers take the explicit unpool first
@@ -104,14 +105,23 @@ _W4_SPLITS = os.environ.get("TORCHPRUNER_W4_SPLITS", "1") != "0"
 _TUNER_LOG = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") != "0"  # print every timed kernel choice
 
 
+_W4_WIDE = os.environ.get("TORCHPRUNER_W4_WIDE", "1") != "0"
+
+
 def _wino4_cands(B, H, W, K, C):
     """F(4x4) candidates: one K pass, plus channel-chunk split-K (raw slabs + the shared
-    deterministic combine) when the tile grid alone cannot fill the chip (small batches)."""
-    blocks = math.ceil(B * (H // 4) * (W // 4) / 32) * (K // 32)
-    sp, chunks = 1, C // 8
-    while _W4_SPLITS and blocks * sp < 2 * _CU and sp * 2 <= chunks // 4 and sp < 16:
-        sp *= 2
-    return [(WINO4, 1)] + ([(WINO4, sp)] if sp > 1 else []) + ([(WINO4, sp // 2)] if sp > 2 else [])
+    deterministic combine) when the tile grid alone cannot fill the chip (small batches); for
+    both kernels (MODE 3: 32-tile blocks, two per CU; WIDE: 64-tile blocks, one per CU)."""
+    out = []
+    for kind, tb, per_cu in ((WINO4, 32, 2), (WINO4W, 64, 1)):
+        if kind == WINO4W and not _W4_WIDE:
+            continue
+        blocks = math.ceil(B * (H // 4) * (W // 4) / tb) * (K // 32)
+        sp, chunks = 1, C // 8
+        while _W4_SPLITS and blocks * sp < per_cu * _CU and sp * 2 <= chunks // 4 and sp < 16:
+            sp *= 2
+        out += [(kind, 1)] + ([(kind, sp)] if sp > 1 else []) + ([(kind, sp // 2)] if sp > 2 else [])
+    return out
 
 
 def _wino_splits(P, K, C):
@@ -547,8 +557,9 @@ class FusedChainEngine:
         """``apoz``: (B, N) buffer that receives the counts of positive (pre-pool) outputs."""
         if cfg >= CFG_BF16:
             return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp, apoz)
-        if cfg == WINO4:
-            return T.conv_wino4_fwd(h, self._u4(e), e["scale"], e["shift"], True, e["pool"], apoz, sp)
+        if cfg in (WINO4, WINO4W):
+            return T.conv_wino4_fwd(h, self._u4(e), e["scale"], e["shift"], True, e["pool"], apoz, sp,
+                                    1 if cfg == WINO4W else 0)
         if cfg in (WINO, WINO_LDS):
             return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS, apoz)
         if cfg >= self.DENSE:
@@ -588,10 +599,11 @@ class FusedChainEngine:
         """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
         if cfg >= CFG_BF16:
             return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp, tay_mode=tm)
-        if cfg == WINO4:
+        if cfg in (WINO4, WINO4W):
             if am is not None:
                 g = T.unpool2_nhwc(g, am)
-            return T.conv_wino4_dgrad(g, self._u4(e, True), act, sc, taylor, want_out, tm, sp)
+            return T.conv_wino4_dgrad(g, self._u4(e, True), act, sc, taylor, want_out, tm, sp,
+                                      1 if cfg == WINO4W else 0)
         if cfg == WINO_UNP:
             return T.conv_wino_dgrad(T.unpool2_nhwc(g, am), None, e["ut"], act, sc, taylor, want_out, sp, True,
                                      tay_mode=tm)
@@ -1044,12 +1056,12 @@ class FusedChainEngine:
         return res
 
 
-KERNEL_FAMILIES = ("wino4", "wino2", "wino2_direct", "igemm")
+KERNEL_FAMILIES = ("wino4", "wino4w", "wino2", "wino2_direct", "igemm")
 
 
 def family_policy(family: str, split: str = "min"):
     """A :meth:`Autotuner.pinned` policy that runs every layer it can on one kernel family:
-    ``wino4`` F(4x4,3x3), ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
+    ``wino4`` F(4x4,3x3), ``wino4w`` its wide kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
     F(2x2) with direct patch loads, ``igemm`` the implicit GEMM (dense 2x2 GEMM, VALU first
     layer). ``split``: the fewest ("min") or most ("max") channel splits of that family. Layers
     the family does not cover keep the untuned pick."""
@@ -1059,6 +1071,8 @@ def family_policy(family: str, split: str = "min"):
         k = c[0]
         if family == "wino4":
             return k == WINO4
+        if family == "wino4w":
+            return k == WINO4W
         if family == "wino2":
             return k in (WINO_LDS, WINO_UNP)
         if family == "wino2_direct":
