@@ -65,6 +65,13 @@ __device__ __forceinline__ float nan_max(float a, float b) {
   return (a > b || a != a) ? a : b;
 }
 __device__ __forceinline__ float nan_relu(float x) { return (x > 0.f || x != x) ? x : 0.f; }
+
+// Per-element score partial of a data-gradient epilogue (g = dL/da, a = the activation):
+// tay_mode 0 Taylor -(g * a); 1 Sensitivity |g|; 2 Sensitivity of a ReLU-masked gradient
+// |g| where a > 0 (the evaluation module is the BN before the ReLU: ResNet bn1 / bn2).
+__device__ __forceinline__ float tay_term(int mode, float g, float a) {
+  return mode == 1 ? fabsf(g) : mode == 2 ? (a > 0.f ? fabsf(g) : 0.f) : -(g * a);
+}
 // NaN-propagating ReLU (slope 0) / LeakyReLU (slope > 0): NaN passes through (pruner NaN probe)
 __device__ __forceinline__ float nan_act(float x, float slope) {
   return (x > 0.f || x != x) ? x : (slope != 0.f ? x * slope : 0.f);

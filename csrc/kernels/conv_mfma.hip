@@ -75,7 +75,7 @@ struct ConvArgs {
   const float* mask;        // [M][N] activation: out = mask > 0 ? v : 0 (ReLU backward), nullable
   int res_stride;           // res is (B, ceil(Ho/s), ceil(Wo/s), N) added at pixels with oh, ow % s == 0
                             // (gradient of a strided 1x1 downsample conv scattered back), 1 = dense
-  int tay_mode;             // EPI_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
+  int tay_mode;             // EPI_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|, 2 |g| where a > 0
   int parity;               // GEN 3: rows ordered (oh%2, ow%2, b, oh/2, ow/2) so a tile sees few taps
   float slope;              // activation: 0 = ReLU, > 0 = LeakyReLU negative slope (fwd relu flag /
                             // EPI_BWD mask of the consumer activation)
@@ -757,7 +757,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
                   cur_b = b;
                   tsum = 0.f;
                 }
-                tsum += p.tay_mode ? fabsf(gval) : -(gval * a);
+                tsum += tay_term(p.tay_mode, gval, a);
               }
               if (p.out) p.out[o] = act_grad(a, gval * sc, p.slope);
             }
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(256) void conv_epilogue(ConvArgs p, const float* __
         float v = 0.f;
         for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
         const float a = p.act[o];
-        tsum += p.tay_mode ? fabsf(v) : -(v * a);
+        tsum += tay_term(p.tay_mode, v, a);
         if (p.out) p.out[o] = act_grad(a, v * sc, p.slope);
       }
       if (p.taylor) p.taylor[tay_index(p, b, n)] += tsum;
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(1024) void conv_epilogue_bwd_img(ConvArgs p, const 
       float v = 0.f;
       for (int s = 0; s < splits; ++s) v += slabs[s * MN + o];
       const float a = p.act[o];
-      tsum += p.tay_mode ? fabsf(v) : -(v * a);
+      tsum += tay_term(p.tay_mode, v, a);
       if (p.out) p.out[o] = act_grad(a, v * sc, p.slope);
     }
   }

@@ -201,6 +201,24 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
         }
       }
     }
+    // data gradient: this lane's phase-2 activations, issued before the barrier that ends phase 1
+    // (the accumulators are dead, so the registers are free): their global-memory latency runs
+    // while the block's other waves finish their output transforms, not inside phase 2
+    f32x4 apre[EPI == BWD ? TPW : 1][2];
+    if constexpr (EPI == BWD) {
+      const int qq = lane >> 3;
+#pragma unroll
+      for (int tt = 0; tt < TPW; ++tt) {
+        const int pt = t0 + hf * 32 + wave * TPW + tt;
+        const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int q = qq + 8 * h2;
+          const long long pix = ((long long)b * S + 4 * tr + (q >> 2)) * S + 4 * tc + (q & 3);
+          apre[tt][h2] = pt < p.P ? *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
     __syncthreads();
     // ---- phase 2: coalesced traffic; 8 lanes cover one pixel's 32 channels (128 B) ----------
     if constexpr (EPI == FWD_POOL) {
@@ -246,7 +264,7 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
       }
     } else {
       const int qq = lane >> 3;  // pixels qq and qq + 8 of the tile
-#pragma unroll 2
+#pragma unroll
       for (int tt = 0; tt < TPW; ++tt) {
         const int tl = wave * TPW + tt;
         const int tb = hf * 32 + tl;
@@ -276,9 +294,9 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
               }
               *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
             } else {  // BWD
-              const f32x4 a = *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k);
+              const f32x4 a = apre[EPI == BWD ? tt : 0][h2];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) sum[e] += p.tay_mode ? fabsf(yv[e]) : -(yv[e] * a[e]);
+              for (int e = 0; e < 4; ++e) sum[e] += tay_term(p.tay_mode, yv[e], a[e]);
               if (p.out) {
                 f32x4 v;
 #pragma unroll
@@ -612,8 +630,23 @@ __device__ __forceinline__ void bt6p(f2v& a0, f2v& a1, f2v& a2, f2v& a3, f2v& a4
   a5 = o5;
 }
 
-template <int EPI, int S, int NW>
+// SPREAD (NW = 4, variant 2): U0(c+1) is issued one 1-KB piece per two MFMA steps over the first
+// half of the parity-1 steps instead of in a burst at the mid-chunk barrier, where the burst
+// stalled the issuing wave on the TA address FIFO (SQ_VMEM_TA_ADDR_FIFO_FULL) while its MFMAs
+// waited; the MFMAs are inline asm with the accumulators pinned to VGPRs, so the branches around
+// the pieces cannot make the register allocator copy them (what defeated this schedule with
+// builtins). (Spreading X(c+1) over the parity-0 steps as well spilled ~25 VGPRs in the loop: the
+// whole transformed patch is still live there.)
+#define W4_MFMA2(NOP, c0, c1, a0, a1, w)                                                            \
+  asm volatile(NOP                                                                                  \
+               "v_mfma_f32_16x16x4_f32 %0, %2, %4, %0\n\t"                                         \
+               "v_mfma_f32_16x16x4_f32 %1, %3, %5, %1"                                             \
+               : "+v"(c0), "+v"(c1)                                                                 \
+               : "v"(a0), "v"(a1), "v"(w.x), "v"(w.y))
+
+template <int EPI, int S, int NW, bool SPREAD = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
+  static_assert(!SPREAD || NW == 4, "SPREAD is the 4-wave (two blocks per CU) schedule");
   constexpr int TB = 8 * NW, NG = NW / 2;  // tiles per block, 16-tile groups
   constexpr bool XDBL = NW == 8;           // X double-buffered (one block per CU)
   using G = GeoT<S, TB>;
@@ -707,6 +740,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
         dma16_asm(xrs, lds_addr(xd + (wave + NW * i) * 256), off, (unsigned)c0 * 4u);
       }
   };
+  auto stage_u_piece = [&](int c0, int hf, int i) {  // piece i of stage_u
+    if (p.dbg & 1) return;
+    const int pt = wave + NW * i;
+    if (pt < 18) {
+      const unsigned ub = (unsigned)(((c0 >> 3) * n_k + kb) * U_IMG) * 4u;
+      const int q = hf * 18 + pt;
+      dma16_asm(urs, lds_addr(us + q * 256), lane16, ub + (unsigned)q * 1024u);
+    }
+  };
 
   // split-K over channel chunks: blockIdx.y owns chunks [c_lo, c_hi) (host: no empty split)
   const int nc_all = p.C / 8, cps = (nc_all + (int)gridDim.y - 1) / (int)gridDim.y;
@@ -768,7 +810,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
         if (!XDBL && c + 1 < nc) wait_but_x();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
-        if (c + 1 < nc) stage_u(8 * (c + 1), 0);
+        if (!SPREAD && c + 1 < nc) stage_u(8 * (c + 1), 0);
         if (XDBL && c + 2 < nc) stage_x(8 * (c + 2), xb);
       }
       const float* ue = ul + e * 18 * 256;
@@ -784,12 +826,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
           __builtin_amdgcn_sched_barrier(0);
         }
         const int x = 2 * i;
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(e ? v[x].y : v[x].x, w.x, acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(e ? v[x + 1].y : v[x + 1].x, w.y, acc[x + 1], 0, 0, 0);
+        if constexpr (SPREAD) {
+          const float a0 = e ? v[x].y : v[x].x, a1 = e ? v[x + 1].y : v[x + 1].x;
+          if (i == 0) W4_MFMA2("s_nop 1\n\t", acc[x], acc[x + 1], a0, a1, w);
+          else W4_MFMA2("", acc[x], acc[x + 1], a0, a1, w);
+          if (e == 1 && c + 1 < nc && (i & 1) == 0 && i / 2 < (18 + NW - 1) / NW)
+            stage_u_piece(8 * (c + 1), 0, i / 2);  // U0(c+1), one piece per two parity-1 steps
+        } else {
+          acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(e ? v[x].y : v[x].x, w.x, acc[x], 0, 0, 0);
+          acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(e ? v[x + 1].y : v[x + 1].x, w.y, acc[x + 1], 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
+  if constexpr (SPREAD) asm volatile("s_nop 15" ::: "memory");  // inline-asm MFMA results -> epilogue reads
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (p.dbg & 16) {
@@ -819,12 +870,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
 // between AGPRs, VGPRs and scratch inside the MFMA loop (261 v_accvgpr moves + scratch per chunk,
 // measured in the .s). So the MFMAs are inline asm with the accumulators pinned by constraint:
 // points 0-31 ("a": 256 AGPRs) and points 32-35 ("v": 32 VGPRs). hipcc pads no hazard inside an
-// asm string (cdna_hip_programming.md §5.7): each group opens with s_nop 1 (a VALU-written A/B
-// operand, or the zeroed accumulators, -> MFMA), consecutive MFMAs on one accumulator take it
-// whole as C (no wait states), and the loop ends with s_nop 15 before the epilogue reads them.
+// asm string (cdna_hip_programming.md §5.7): the first group of each parity opens with s_nop 1 (a
+// VALU-written A operand, or the zeroed accumulators, -> MFMA), consecutive MFMAs on one
+// accumulator take it whole as C (no wait states), and the loop ends with s_nop 15 before the
+// epilogue reads them.
 #define W4W_AGPR_POINTS 32
-#define W4W_MFMA4(C, c0, c1, c2, c3, a0, a1, w0, w1)                                                  \
-  asm volatile("s_nop 1\n\t"                                                                         \
+#define W4W_MFMA4(C, NOP, c0, c1, c2, c3, a0, a1, w0, w1)                                             \
+  asm volatile(NOP                                                                                    \
                "v_mfma_f32_16x16x4_f32 %0, %4, %6, %0\n\t"                                           \
                "v_mfma_f32_16x16x4_f32 %1, %4, %8, %1\n\t"                                           \
                "v_mfma_f32_16x16x4_f32 %2, %5, %7, %2\n\t"                                           \
@@ -1026,8 +1078,11 @@ __global__ __launch_bounds__(256, 1) void wino4_wide(Args p) {
         }
         const int x = 2 * i;
         const float a0 = e ? v[x].y : v[x].x, a1 = e ? v[x + 1].y : v[x + 1].x;
-        if (x < W4W_AGPR_POINTS) W4W_MFMA4("a", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
-        else W4W_MFMA4("v", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
+        // the first group of a parity follows the transform / DMA-issue VALU code: 2 wait states;
+        // later groups follow only the B-operand ds_reads and their s_waitcnt (checked in the .s)
+        if (i == 0) W4W_MFMA4("a", "s_nop 1\n\t", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
+        else if (x < W4W_AGPR_POINTS) W4W_MFMA4("a", "", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
+        else W4W_MFMA4("v", "", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -1136,7 +1191,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   const int nc = C / 8;
   splits = std::max(1, std::min(splits, nc));
   splits = (nc + (nc + splits - 1) / splits - 1) / ((nc + splits - 1) / splits);  // no empty split
-  if (variant < 0 || variant > 1) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 2) return hipErrorInvalidValue;
   const bool wide = variant == 1;
   if (splits > 1 && ((!wide && kernel_mode() < 2) || !ws)) return hipErrorInvalidValue;
   if (epi < 0 || epi > 2 || (epi == BWD && !act) || (epi != BWD && !out) || (epi == FWD_POOL && !out_argmax))
@@ -1169,7 +1224,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
     return v;
   }();
   a.dbg = dbg;
-  const int mode = wide ? 4 : kernel_mode();
+  const int mode = wide ? 4 : variant == 2 ? 5 : kernel_mode();  // 5: MODE 3 with SPREAD DMA
   const int tb = mode == 2 || mode == 4 ? 64 : TILES;  // MODE 3: 32-tile blocks
   const int n_p = (a.P + tb - 1) / tb, n_k = K / TK;
   const dim3 grid(n_p * n_k, splits);
@@ -1188,6 +1243,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 #define TP_W4P(SS)                                                                      \
   do {                                                                                  \
     if (mode == 4) wino4_wide<PARTIAL, SS><<<grid, 256, 0, st>>>(b);                    \
+    else if (mode == 5) wino4_m2<PARTIAL, SS, 4, true><<<grid, 256, 0, st>>>(b);        \
     else if (mode == 2) wino4_m2<PARTIAL, SS, 8><<<grid, 512, 0, st>>>(b);              \
     else wino4_m2<PARTIAL, SS, 4><<<grid, 256, 0, st>>>(b);                             \
   } while (0)
@@ -1205,6 +1261,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 #define TP_W4(E, SS)                                              \
   do {                                                            \
     if (mode == 4) wino4_wide<E, SS><<<grid, 256, 0, st>>>(a);    \
+    else if (mode == 5) wino4_m2<E, SS, 4, true><<<grid, 256, 0, st>>>(a); \
     else if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a); \
     else if (mode == 3) wino4_m2<E, SS, 4><<<grid, 256, 0, st>>>(a); \
     else if (mode == 1) wino4_f4x3<E, SS, 1><<<grid, 256, 0, st>>>(a); \
@@ -1228,7 +1285,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 // static LDS bytes of a wino4 instantiation (occupancy / budget guard)
 extern "C" int tp_wino4_lds_bytes(int S, int variant) {
   using namespace tp::w4;
-  const int m = variant == 1 ? 4 : kernel_mode();
+  const int m = variant == 1 ? 4 : variant == 2 ? 3 : kernel_mode();
   const void* f = nullptr;
 #define TP_W4F(SS)                                                                            \
   f = m == 4 ? (const void*)wino4_wide<BWD, SS>                                               \

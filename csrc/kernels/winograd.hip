@@ -79,7 +79,7 @@ struct WinoArgs {
   FastDiv fd_timg, fd_w2, fd_ip, fd_rw;  // T_img = (H/2)(W/2), W/2, IP, RW
   float* apoz;              // W_FWD: [B][K] counts of positive outputs (exact integers), nullable
   int dbg;                  // experiment switches (TP_WINO_DBG): 1 no epilogue, 2 no restaging, 4 no transform
-  int tay_mode;             // W_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|
+  int tay_mode;             // W_BWD partials: 0 Taylor -(g*a), 1 Sensitivity |g|, 2 |g| where a > 0
 };
 
 // Phase-attribution switches for profiling experiments only: they skip barriers / stores and
@@ -294,8 +294,8 @@ phase2:
         // act: prefetched into LDS by the last chunk's DMA (slot tid + 256 i), else global
         const float4 a = al0 ? *reinterpret_cast<const float4*>((i < 4 ? al0 : al1) + ((i & 3) * 256 + tid) * 4)
                              : *reinterpret_cast<const float4*>(p.act + pix * p.K + k);
-        tq[i] = p.tay_mode ? make_float4(fabsf(y.x), fabsf(y.y), fabsf(y.z), fabsf(y.w))
-                           : make_float4(-(y.x * a.x), -(y.y * a.y), -(y.z * a.z), -(y.w * a.w));
+        tq[i] = make_float4(tay_term(p.tay_mode, y.x, a.x), tay_term(p.tay_mode, y.y, a.y),
+                            tay_term(p.tay_mode, y.z, a.z), tay_term(p.tay_mode, y.w, a.w));
         if (p.out) {
           float4 v;
           v.x = a.x > 0.f ? y.x * sc4.x : 0.f;

@@ -332,8 +332,8 @@ class ResNetEngine:
         1x1 dgrad (implicit GEMM, one K pass) also writes the per-(image, channel) partial sums of
         -(dL/da * a), a = ``mask``, into an (R, B, C) slab from its epilogue (one writer per
         element: deterministic), which saves the separate channel reduction's read of both
-        tensors; ``tay_mode`` 1 (Sensitivity): sums of |dL/da| of the masked gradient, 1x1 only
-        (the Winograd epilogue's |.| sees the unmasked gradient)."""
+        tensors; ``tay_mode`` 1 (Sensitivity): sums of |dL/da| of the masked gradient (the
+        Winograd epilogue masks it by a > 0 itself: its tay_mode 2)."""
         e = self._bwd_operands(e)
         B, H, W, C = g.shape
         ks, s = e["ks"], e["stride"]
@@ -360,13 +360,14 @@ class ResNetEngine:
             gen_tay = bool(cands)
 
         def run(cfg, sp, gg=g, rr=res, mm=mask, tay=None):
-            if cfg in (WINO, WINO_LDS):
-                return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, tay, True, sp, cfg == WINO_LDS, 0)
+            if cfg in (WINO, WINO_LDS):  # Sensitivity of the BN before the ReLU: |g| where a > 0 (mode 2)
+                return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, tay, True, sp, cfg == WINO_LDS,
+                                         2 if tay_mode == 1 else 0)
             return T.conv_gen_bwd(gg, e["wt"], rr, res_stride, mm, ks, s if transposed else 1, pad, Ho, Wo,
                                   transposed, cfg, sp, tay, tay_mode or 0)
 
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands if cands else None)
-        if tay_mode == 0 and cfg in (WINO, WINO_LDS):
+        if tay_mode is not None and cfg in (WINO, WINO_LDS):
             tay = torch.zeros(taylor_slots(Ho, Wo), B, N, device=g.device)
             return run(cfg, sp, tay=tay), tay
         if gen_tay:
