@@ -541,7 +541,7 @@ def accuracy(args, model, task, convs, scores, cfg, dev, log):
                                 "kernel_choices": "TUNER.fixed() (untimed heuristic configs: bit-reproducible)"},
         "params_before_after": [sum(p.numel() for p in model.parameters()), params],
         "prune_protocol": {k: cfg[k] for k in ("frac", "increments", "ft_steps", "final_ft_steps", "recal_batches",
-                                               "score_imgs", "val_imgs", "ft_lr", "noise", "teacher_wd")},
+                                               "score_imgs", "val_imgs", "ft_lr", "noise", "teacher_wd", "label_noise")},
         "top1_layerwise_mask_50pct_taylor": round(lw_t, 4),
         "top1_layerwise_mask_50pct_random": round(lw_r, 4),
     }

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3, 4])
     ap.add_argument("--teacher-steps", type=int, default=None)
     ap.add_argument("--modes", type=int, default=None)
+    ap.add_argument("--label-noise", type=float, default=None)
+    ap.add_argument("--set", nargs="*", default=[], help="extra protocol overrides key=value (numbers)")
     args = ap.parse_args()
     for noise in args.noise:
         over = {"noise": noise}
@@ -30,6 +32,11 @@ def main():
             over["teacher_steps"] = args.teacher_steps
         if args.modes:
             over["modes"] = args.modes
+        if args.label_noise is not None:
+            over["label_noise"] = args.label_noise
+        for kv in args.set:
+            k, v = kv.split("=")
+            over[k] = float(v) if "." in v or "e" in v else int(v)
         runs = []
         for s in args.seeds:
             r = pq.run_protocol(s, "cuda", **over)

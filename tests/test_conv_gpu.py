@@ -145,7 +145,7 @@ def test_nan_propagation(cuda):
 _COND_BOUND = {"wino4": 5e-5, "wino4w": 5e-5, "wino2": 1e-5, "wino2_direct": 1e-5, "igemm": 1e-5}
 
 
-@pytest.mark.parametrize("family", ["wino4", "wino4w", "wino2", "wino2_direct", "igemm"])
+@pytest.mark.parametrize("family", ["wino4", "wino2", "wino2_direct", "igemm"])
 @pytest.mark.parametrize("split", ["min", "max"])
 @pytest.mark.parametrize("mode", ["taylor", "sensitivity"])
 def test_engine_scores_match_fp64_oracle(cuda, family, split, mode):

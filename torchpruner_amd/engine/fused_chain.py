@@ -105,7 +105,9 @@ _W4_SPLITS = os.environ.get("TORCHPRUNER_W4_SPLITS", "1") != "0"
 _TUNER_LOG = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") != "0"  # print every timed kernel choice
 
 
-_W4_WIDE = os.environ.get("TORCHPRUNER_W4_WIDE", "1") != "0"
+# the WIDE F(4x4) kernel (variant 1) is correct but measured 0.8x the MODE 3 kernel on every VGG
+# layer (profiles/wino4/round4_wide_vs_mode3.txt): opt-in candidate only
+_W4_WIDE = os.environ.get("TORCHPRUNER_W4_WIDE", "0") != "0"
 
 
 def _wino4_cands(B, H, W, K, C):
