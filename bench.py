@@ -224,8 +224,9 @@ def run(args) -> int:
         "vs_baseline": None,
         "dtype": "fp32",
         "data": f"synthetic (CIFAR-10-shaped prototype-mixture task, {cfg['modes']} modes/class, noise "
-                f"{cfg['noise']}; random-init VGG16-BN trained {cfg['teacher_steps']} steps, untimed); each rank's "
-                "batches are generated in HBM before timing (no host->device copy in the timed region)",
+                f"{cfg['noise']}, {cfg['label_noise']:.0%} label noise; random-init VGG16-BN trained "
+                f"{cfg['teacher_steps']} steps, untimed); each rank's batches are generated in HBM before timing "
+                "(no host->device copy in the timed region)",
         "config": {
             "model": "VGG16-BN (CIFAR-10, reference classifier)",
             "global_batch": B * world,

@@ -849,7 +849,7 @@ class FusedChainEngine:
         P = self._pack()
         # one graph per score arena: the stream pipeline replays slot k's graph into slot k's arena
         key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device), self.bf16,
-               id(arena), TUNER.gen)
+               TUNER.gen, id(arena))
         g = self._graphs.get(key)
         if g is not None and (g["P"] is not P or g["arena"] is not arena):
             torch.cuda.synchronize()  # its replays must finish before the stale graph (and pool) goes
