@@ -108,8 +108,8 @@ def finetune_throughput(dev, world, rank, steps=10, warmup=3, batch=128, res=224
 # teacher: early stop at val top-1 >= 0.85 (checked every 25 steps); 8% label noise caps it at ~0.92
 # (as bench/prune_quality.py), so it cannot saturate at 1.0 even when the task is learnt quickly
 QUALITY = dict(res=112, classes=20, modes=8, noise=2.5, label_noise=0.08, batch=64, teacher_target=0.85,
-               teacher_max_steps=800, check_every=25, frac=0.2, ft_steps=15, recal_batches=8, val_batches=8,
-               score_batches=4, lr=0.01)
+               teacher_max_steps=800, check_every=25, frac=0.2, ft_steps=60, recal_batches=8, val_batches=8,
+               score_batches=4, lr=0.01, ft_lr=0.002)
 
 
 def prune_finetune_quality(dev, world, rank, seed=0, cfg=None):
@@ -147,7 +147,7 @@ def prune_finetune_quality(dev, world, rank, seed=0, cfg=None):
         model.load_state_dict(state)
         enable_native_convs(model)
         wrapper = PrunableDDP(model, device=dev)
-        opt = torch.optim.SGD(model.parameters(), lr=cfg["lr"], momentum=0.9, weight_decay=1e-4)
+        opt = torch.optim.SGD(model.parameters(), lr=cfg["ft_lr"], momentum=0.9, weight_decay=1e-4)
         pruner = Pruner(model, shape, dev, optimizer=opt)
         model.eval()
         graph = get_resnet_pruning_graph(model)
@@ -173,6 +173,6 @@ def prune_finetune_quality(dev, world, rank, seed=0, cfg=None):
         disable_native_convs([m for m in model.modules() if "forward" in m.__dict__])
         del model, wrapper, opt, pruner
     res["config"] = {k: cfg[k] for k in ("res", "classes", "modes", "noise", "label_noise", "batch", "frac",
-                                         "ft_steps", "recal_batches", "teacher_target")}
+                                         "ft_steps", "lr", "ft_lr", "recal_batches", "teacher_target")}
     res["note"] = "finetune batches are per GPU (weak scaling): the finetuned top-1 depends on the rank count"
     return res
