@@ -53,6 +53,7 @@ hipError_t tp_conv_first_direct(const float* x, const float* w, const float* sca
                                 int B, int Cin, int H, int W, int Cout, int relu, hipStream_t st);
 int tp_wino_taylor_slots(int H, int W);
 int tp_wino_lds_bytes();
+int tp_wino_staged_ok(int H, int W, int unpool);
 hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C, int H, int W, int Cp, hipStream_t st);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
@@ -60,6 +61,7 @@ hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u,
                         int tay_mode, hipStream_t st);
 hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st);
 hipError_t tp_wino_weights2(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
+hipError_t tp_wino_weights_bf16(const float* w, void* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
 hipError_t tp_pack_conv_weight(const float* w, float* out, int O, int I, int KS, int rows, int cols, int cpad, int mode,
                                hipStream_t st);
 long long tp_wino_wgrad_ws_elems(int B, int H, int W, int Cin, int Cout, int splits);
@@ -261,7 +263,8 @@ at::Tensor conv_first(const at::Tensor& x, const at::Tensor& w, const at::Tensor
 
 // Winograd U images of a 3x3 weight: w (K, C, 3, 3) -> (C/8, K/32, 4096); flip_t: the data-gradient
 // operand of the forward weight w (Cout = K', Cin = C', 3, 3) -> images of (C', K') with rotated taps.
-at::Tensor wino_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C) {
+// bf16: the bf16 images of the BF kernels (same shape, dtype bfloat16; opt-in compute_dtype).
+at::Tensor wino_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C, bool bf16) {
   need(w, "w", 4);
   TORCH_CHECK(w.size(2) == 3 && w.size(3) == 3, "w must be (.., .., 3, 3)");
   // K, C: the padded GEMM sizes (0 = the weight's own); the source may be narrower (zero padding)
@@ -271,9 +274,13 @@ at::Tensor wino_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C) 
   TORCH_CHECK(flip_t ? (w.size(0) <= C && w.size(1) <= K) : (w.size(0) <= K && w.size(1) <= C),
               "weight wider than the padded GEMM");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(w.device());
-  auto u = at::empty({C / 8, K / 32, 4096}, w.options());
-  TP_CHECK_HIP(tp_wino_weights2(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
-                                (int)w.size(0), (int)w.size(1), cur_stream()));
+  auto u = at::empty({C / 8, K / 32, 4096}, w.options().dtype(bf16 ? at::kBFloat16 : at::kFloat));
+  if (bf16)
+    TP_CHECK_HIP(tp_wino_weights_bf16(w.data_ptr<float>(), u.data_ptr(), (int)K, (int)C, flip_t ? 1 : 0,
+                                      (int)w.size(0), (int)w.size(1), cur_stream()));
+  else
+    TP_CHECK_HIP(tp_wino_weights2(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
+                                  (int)w.size(0), (int)w.size(1), cur_stream()));
   return u;
 }
 
@@ -338,11 +345,15 @@ int64_t wino_splits(int64_t splits, int64_t C) {
   return (chunks + per - 1) / per;
 }
 
-void need_u(const at::Tensor& u, int64_t C, int64_t K) {
-  need(u, "u", 3);
+// fp32 images, or bf16 ones (the BF kernels; staged input modes only): returns the staged-flag bit
+int need_u(const at::Tensor& u, int64_t C, int64_t K) {
+  TORCH_CHECK(u.is_cuda() && u.is_contiguous() && u.dim() == 3 &&
+                  (u.scalar_type() == at::kFloat || u.scalar_type() == at::kBFloat16),
+              "u must be a contiguous float32 or bfloat16 GPU tensor (C/8, K/32, 4096)");
   TORCH_CHECK(C % 8 == 0 && K % 32 == 0 && u.size(0) == C / 8 && u.size(1) == K / 32 && u.size(2) == 4096,
               "u must be the Winograd U images (C/8, K/32, 4096) = (", C / 8, ", ", K / 32, ", 4096), got ",
               u.sizes());
+  return u.scalar_type() == at::kBFloat16 ? 2 : 0;
 }
 
 // Winograd F(2x2,3x3) forward: x (B,H,W,C) NHWC, u (16, C, K) from winograd_weights().
@@ -352,7 +363,8 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
                                                  int64_t splits, bool staged, const c10::optional<at::Tensor>& apoz) {
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
-  need_u(u, C, K);
+  const int ubf = need_u(u, C, K);
+  TORCH_CHECK(!ubf || staged, "bf16 U images need the staged kernels");
   TORCH_CHECK(!pool || (H % 2 == 0 && W % 2 == 0), "Winograd with pooling needs even H, W");
   TORCH_CHECK(C % 8 == 0 && K % 32 == 0, "Winograd needs C % 8 == 0 and K % 32 == 0");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
@@ -374,8 +386,9 @@ std::tuple<at::Tensor, at::Tensor> conv_wino_fwd(const at::Tensor& x, const at::
                     apoz->numel() == B * K, "apoz must be a contiguous float32 (B, K) tensor");
     ap = apoz->data_ptr<float>();
   }
-  TP_CHECK_HIP(tp_conv_wino(x.data_ptr<float>(), nullptr, u.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)K,
-                            0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, staged ? 1 : 0, sc, sh, relu ? 1 : 0,
+  TP_CHECK_HIP(tp_conv_wino(x.data_ptr<float>(), nullptr, static_cast<const float*>(u.data_ptr()), (int)B, (int)H,
+                            (int)W, (int)C, (int)K, 0, pool ? EPI_FWD_POOL : EPI_FWD, (int)sp, (staged ? 1 : 0) | ubf,
+                            sc, sh, relu ? 1 : 0,
                             out.data_ptr<float>(),
                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap,
                             sp > 1 ? ws.data_ptr<float>() : nullptr, 0, cur_stream()));
@@ -392,7 +405,8 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
   need(act, "act", 4);
   const bool unpool = g_argmax.has_value() && g_argmax->defined();
   const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
-  need_u(ut, Cout, Cin);
+  const int ubf = need_u(ut, Cout, Cin);
+  TORCH_CHECK(!ubf || staged, "bf16 U images need the staged kernels");
   if (unpool) {
     TORCH_CHECK(g.size(1) * 2 == H && g.size(2) * 2 == W, "pooled grad shape mismatch");
     TORCH_CHECK(g_argmax->scalar_type() == at::kByte && g_argmax->sizes() == g.sizes() && g_argmax->is_contiguous(),
@@ -420,8 +434,8 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
   TP_CHECK_HIP(tp_conv_wino(g.data_ptr<float>(), unpool ? g_argmax->data_ptr<uint8_t>() : nullptr,
-                            ut.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cout, (int)Cin, unpool ? 1 : 0, EPI_BWD,
-                            (int)sp, staged ? 1 : 0, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
+                            static_cast<const float*>(ut.data_ptr()), (int)B, (int)H, (int)W, (int)Cout, (int)Cin,
+                            unpool ? 1 : 0, EPI_BWD, (int)sp, (staged ? 1 : 0) | ubf, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
                             act.data_ptr<float>(), tay, nullptr, sp > 1 ? ws.data_ptr<float>() : nullptr,
                             (int)tay_mode, cur_stream()));
   return out;
@@ -893,6 +907,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
 void register_engine_ops_def(torch::Library& m) {
   m.def("wino_taylor_slots(int H, int W) -> int", &wino_taylor_slots);
   m.def("wino_lds_bytes() -> int", []() -> int64_t { return tp_wino_lds_bytes(); });
+  m.def("wino_staged_ok(int H, int W, bool unpool) -> bool",
+        [](int64_t H, int64_t W, bool unpool) -> bool { return tp_wino_staged_ok((int)H, (int)W, unpool ? 1 : 0) != 0; });
   m.def("wino4_lds_bytes(int S, int variant=0) -> int",
         [](int64_t S, int64_t variant) -> int64_t { return tp_wino4_lds_bytes((int)S, (int)variant); });
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
@@ -921,7 +937,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_dgrad(Tensor g, Tensor? g_argmax, Tensor wt, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, "
         "bool want_out, int ks, int cfg, int splits, int tay_group=0, int tay_mode=0, float slope=0.0) -> Tensor");
   m.def("conv_first(Tensor x, Tensor w, Tensor scale, Tensor shift, bool relu, Tensor? wt=None) -> Tensor");
-  m.def("wino_weights(Tensor w, bool flip_t, int K=0, int C=0) -> Tensor");
+  m.def("wino_weights(Tensor w, bool flip_t, int K=0, int C=0, bool bf16=False) -> Tensor");
   m.def("prefix_tri_operands(Tensor z, Tensor w, Tensor perm, int p0, int cnt, int Kc) -> (Tensor, Tensor)");
   m.def("prefix_delta(Tensor T, Tensor wsub, Tensor neg_one, Tensor y0, bool relu, float slope, int cfg) -> Tensor");
   m.def("conv_wino_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, int splits, "

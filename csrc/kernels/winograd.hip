@@ -38,6 +38,14 @@
 namespace tp {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> two bf16 (round to nearest even, v_cvt_pk_bf16_f32) in one dword, .x in the low half
+__device__ __forceinline__ unsigned bf16x2_of(const f32x2 v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
 __device__ f32x2 buf_load_f32x2(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2f32");
 __device__ unsigned short buf_load_u16(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i16");
 
@@ -353,7 +361,12 @@ phase2:
   }
 }
 
-template <int EPI, int XMODE>
+// BF (opt-in, compute_dtype=bfloat16; staged input modes): U images in bf16 (half the bytes of
+// DMA) and the products on v_mfma_f32_16x16x16_bf16 with fp32 accumulation. A lane's V pair
+// (channels 2g, 2g+1, transformed in fp32) is rounded to bf16 and zero-padded to the MFMA's 4
+// k-values, so one bf16 MFMA replaces the two fp32 MFMAs of (e = 0, 1) per output half;
+// staging, transforms and epilogues are the fp32 kernel's.
+template <int EPI, int XMODE, int BF = 0>
 __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   constexpr bool STAGED = XMODE == X_STAGED || XMODE == X_STAGED_UNPOOL || XMODE == X_SPAN;
   constexpr bool UNPOOL = XMODE == X_UNPOOL;
@@ -379,7 +392,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   constexpr unsigned OOB = 0x80000000u;
 
   const __amdgpu_buffer_rsrc_t urs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, (int)(16u * p.C * p.K * 4u), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, (int)(16u * p.C * p.K * (BF ? 2u : 4u)), 0x00020000);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0,
                                                                         (int)(p.x_elems * 4), 0x00020000);
   const i32x4 xr = make_rsrc(p.x, (unsigned)(p.x_elems * 4));
@@ -540,9 +553,10 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
 
   // ---- staging (LDS-DMA): U image of chunk c0 (+ the input region when STAGED) ---------
   auto stage = [&](int c0, float* ud, float* xd) {
-    const unsigned ubase = (unsigned)(((c0 / W_CH) * n_k + kb) * W_UIMG) * 4u;
+    const unsigned ubase = (unsigned)(((c0 / W_CH) * n_k + kb) * W_UIMG) * (BF ? 2u : 4u);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ubase);
+    for (int i = 0; i < (BF ? 2 : 4); ++i)
+      dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ubase);
     if constexpr (XMODE == X_STAGED || XMODE == X_SPAN) {
 #pragma unroll
       for (int i = 0; i < MAX_ROUNDS; ++i)
@@ -684,6 +698,39 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
         }
       }
     }
+    if constexpr (BF) {
+      // bf16 image: dword (x*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + n = channels (2g, 2g+1) of output j + 16n
+      const unsigned* ulb = reinterpret_cast<const unsigned*>(ub) + uoff;
+      constexpr int AHEAD = 4;
+      u32x2 wq[AHEAD];
+#pragma unroll
+      for (int s = 0; s < AHEAD; ++s) wq[s] = *reinterpret_cast<const u32x2*>(ulb + s * 128);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const u32x2 w2 = wq[x % AHEAD];
+        if (x + AHEAD < 16) wq[x % AHEAD] = *reinterpret_cast<const u32x2*>(ulb + (x + AHEAD) * 128);
+        u32x2 av;
+        if constexpr (BF == 2) {
+          // V = hi + lo: hi = V truncated to bf16 (exact), lo = bf16(V - hi) in the MFMA's padding
+          // k-slots against the same U pair: ~16 mantissa bits of V at no extra MFMA
+          const unsigned u0 = __builtin_bit_cast(unsigned, v[x].x), u1 = __builtin_bit_cast(unsigned, v[x].y);
+          const f32x2 hf = {__builtin_bit_cast(float, u0 & 0xffff0000u), __builtin_bit_cast(float, u1 & 0xffff0000u)};
+          av = u32x2{__builtin_amdgcn_perm(u1, u0, 0x07060302u), bf16x2_of(v[x] - hf)};
+        } else {
+          av = u32x2{bf16x2_of(v[x]), 0u};
+        }
+        const s16x4 a = __builtin_bit_cast(s16x4, av);
+        acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, __builtin_bit_cast(s16x4, u32x2{w2.x, w2.x}),
+                                                             acc[x][0], 0, 0, 0);
+        acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, __builtin_bit_cast(s16x4, u32x2{w2.y, w2.y}),
+                                                             acc[x][1], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __syncthreads();
+      return;
+    }
     const float* ul = ub + uoff;
     constexpr int AHEAD = 4;
     float2 wq[AHEAD];
@@ -762,6 +809,44 @@ __global__ __launch_bounds__(256) void wino_weight_transform(const float* __rest
         }
     }
     u[t] = (float)acc;
+  }
+}
+
+// bf16 U images (the BF kernels): dword (xi*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + n of image (cb, kb)
+// holds bf16(U[xi][c][k]) for c = 8cb + 2g (low half) and c + 1 (high half), k = 32kb + j + 16n.
+__global__ __launch_bounds__(256) void wino_weight_transform_bf16(const float* __restrict__ w, unsigned* __restrict__ u,
+                                                                  int K, int C, int flip_t, int S0, int S1) {
+  constexpr int DW = W_UIMG / 2;
+  const long long total = (long long)(C / 8) * (K / 32) * DW;
+  const double G[4][3] = {{1.0, 0.0, 0.0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0.0, 0.0, 1.0}};
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int word = (int)(t % DW);
+    const long long img = t / DW;
+    const int kb = (int)(img % (K / 32)), cb = (int)(img / (K / 32));
+    const int n = word & 1, gs = (word >> 1) & 3, j = (word >> 3) & 15, xi = word >> 7;
+    const int g = gs ^ ((j >> 3) << 1);
+    const int k = 32 * kb + j + 16 * n;
+    const int i = xi >> 2, jj = xi & 3;
+    f32x2 pair;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int c = 8 * cb + 2 * g + e;
+      const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
+      double acc = 0.0;
+      if (r0 < S0 && r1 < S1) {
+        const float* src = w + ((long long)r0 * S1 + r1) * 9;
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+          for (int b = 0; b < 3; ++b) {
+            const int tap = flip_t ? (2 - a) * 3 + (2 - b) : a * 3 + b;
+            acc += G[i][a] * (double)src[tap] * G[jj][b];
+          }
+      }
+      pair[e] = (float)acc;
+    }
+    u[t] = bf16x2_of(pair);
   }
 }
 
@@ -957,7 +1042,8 @@ static SpanGeom span_geometry(int H, int W) {
 // Winograd conv: same operand/epilogue contract as tp_conv_igemm (3x3, stride 1, pad 1),
 // ``u`` = U images from winograd_weights(). epi: 0 fwd, 1 fwd+pool, 2 bwd (dgrad epilogue).
 // H, W even, C % 8 == 0, K % 32 == 0. splits > 1 -> partial slabs in ``ws`` + combine.
-// staged: 1 = LDS-staged input region when the shape allows it (else direct loads).
+// staged: bit 0 = LDS-staged input region when the shape allows it (else direct loads); bit 1 =
+// ``u`` holds bf16 images (tp_wino_weights_bf16) for the BF kernels — staged input modes only.
 extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B, int H, int W, int K, int epi,
                                               const float* scale, const float* shift, int relu, float* out,
                                               uint8_t* out_argmax, const float* act, float* taylor,
@@ -975,6 +1061,17 @@ extern "C" hipError_t tp_wino_weights2(const float* w, float* u, int K, int C, i
   const long long total = (long long)(C / 8) * (K / 32) * tp::W_UIMG;
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
   tp::wino_weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1);
+  return hipGetLastError();
+}
+
+// the bf16 images of the BF kernels: u = (C/8, K/32, 4096) bf16 (2048 dwords per image)
+extern "C" hipError_t tp_wino_weights_bf16(const float* w, void* u, int K, int C, int flip_t, int S0, int S1,
+                                           hipStream_t st) {
+  if (K % 32 || C % 8 || K <= 0 || C <= 0 || S0 <= 0 || S1 <= 0) return hipErrorInvalidValue;
+  if (flip_t ? (S0 > C || S1 > K) : (S0 > K || S1 > C)) return hipErrorInvalidValue;
+  const long long total = (long long)(C / 8) * (K / 32) * (tp::W_UIMG / 2);
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
+  tp::wino_weight_transform_bf16<<<grid, 256, 0, st>>>(w, static_cast<unsigned*>(u), K, C, flip_t, S0, S1);
   return hipGetLastError();
 }
 
@@ -1018,6 +1115,8 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   // odd H / W: a partial last tile row / column, direct loads only (no pooling / unpooling)
   const bool odd = (H & 1) || (W & 1);
   if ((odd && (unpool || epi == W_FWD_POOL)) || C % 8 != 0 || K % 32 != 0) return hipErrorInvalidValue;
+  const bool bf = (staged & 2) != 0;
+  staged &= 1;
   if (odd) staged = 0;
   WinoArgs a{};
   a.x = x;
@@ -1093,9 +1192,19 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
     a.pooled_m = epi == W_FWD_POOL ? 1 : 0;
     e_launch = W_PARTIAL;
   }
+  if (bf && xmode != X_STAGED && xmode != X_SPAN && xmode != X_STAGED_UNPOOL) return hipErrorInvalidValue;
+  static const bool bf_split = getenv("TP_WINO_BF_PLAIN") == nullptr;  // experiment: 1 = V rounded once
 #define TP_W(E)                                                                                 \
   do {                                                                                          \
-    if (xmode == X_STAGED) wino_f2x3<E, X_STAGED><<<grid, 256, 0, st>>>(a);                    \
+    if (bf && bf_split) {                                                                       \
+      if (xmode == X_STAGED) wino_f2x3<E, X_STAGED, 2><<<grid, 256, 0, st>>>(a);               \
+      else if (xmode == X_SPAN) wino_f2x3<E, X_SPAN, 2><<<grid, 256, 0, st>>>(a);              \
+      else wino_f2x3<E, X_STAGED_UNPOOL, 2><<<grid, 256, 0, st>>>(a);                          \
+    } else if (bf) {                                                                            \
+      if (xmode == X_STAGED) wino_f2x3<E, X_STAGED, 1><<<grid, 256, 0, st>>>(a);               \
+      else if (xmode == X_SPAN) wino_f2x3<E, X_SPAN, 1><<<grid, 256, 0, st>>>(a);              \
+      else wino_f2x3<E, X_STAGED_UNPOOL, 1><<<grid, 256, 0, st>>>(a);                          \
+    } else if (xmode == X_STAGED) wino_f2x3<E, X_STAGED><<<grid, 256, 0, st>>>(a);             \
     else if (xmode == X_SPAN) wino_f2x3<E, X_SPAN><<<grid, 256, 0, st>>>(a);                   \
     else if (xmode == X_STAGED_UNPOOL) wino_f2x3<E, X_STAGED_UNPOOL><<<grid, 256, 0, st>>>(a);  \
     else if (xmode == X_UNPOOL) wino_f2x3<E, X_UNPOOL><<<grid, 256, 0, st>>>(a);               \

@@ -6,7 +6,7 @@ import sys
 
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sys.argv[1:]:
-    for path in glob.glob(f):
+    for path in glob.glob(f, recursive=True):
         per = collections.defaultdict(float)
         for r in csv.DictReader(open(path)):
             per[(r["Dispatch_Id"], r["Kernel_Name"], r["Counter_Name"])] += float(r["Counter_Value"])

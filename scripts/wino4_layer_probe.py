@@ -1,5 +1,7 @@
-"""One F(4x4) layer (default S=8, C=K=256, B=2048, forward) launched a few times: a target for
-rocprofv3 PMC passes. python scripts/wino4_layer_probe.py [--S 8 --C 256 --K 256 --variant 0 --dgrad]"""
+"""One Winograd layer (default S=8, C=K=256, B=2048, forward) launched a few times: a target for
+rocprofv3 PMC passes. --kind wino4 (F(4x4) fp32), wino2 (F(2x2) staged fp32) or wino2bf (F(2x2)
+staged, bf16 U images + bf16 MFMA).
+python scripts/wino4_layer_probe.py [--S 8 --C 256 --K 256 --variant 0 --kind wino4]"""
 import argparse
 import os
 import sys
@@ -17,6 +19,7 @@ def main():
     ap.add_argument("--B", type=int, default=2048)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--kind", default="wino4", choices=["wino4", "wino2", "wino2bf"])
     args = ap.parse_args()
     from torchpruner_amd import ops
     T = ops.require()
@@ -25,9 +28,14 @@ def main():
     x = torch.randn(B, S, S, C, device=dev)
     w = torch.randn(K, C, 3, 3, device=dev) * 0.05
     sc, sh = torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev) * 0.1
-    u4 = T.wino4_weights(w, False, 0, 0)
+    if args.kind == "wino4":
+        u4 = T.wino4_weights(w, False, 0, 0)
+        run = lambda: T.conv_wino4_fwd(x, u4, sc, sh, True, False, None, 1, args.variant)  # noqa: E731
+    else:
+        u2 = T.wino_weights(w, False, K, C, args.kind == "wino2bf")
+        run = lambda: T.conv_wino_fwd(x, u2, sc, sh, True, False, 1, True)  # noqa: E731
     for _ in range(args.iters):
-        T.conv_wino4_fwd(x, u4, sc, sh, True, False, None, 1, args.variant)
+        run()
     torch.cuda.synchronize()
     print("done", flush=True)
 

@@ -50,6 +50,9 @@ WINO_UNP = -3  # dgrad of a pooled layer: explicit vectorised unpool, then the s
                # dense full-resolution gradient (vs rebuilding it from pooled cells per chunk)
 WINO4 = -4  # Winograd F(4x4,3x3) kernel (wino4.hip): square 4/8/16/32-pixel maps, 1.78x fewer MFMAs
 WINO4W = -5  # the same transform, WIDE kernel: 64-tile blocks, one wave per SIMD, 32 outputs per wave
+WINO_BF = -6  # bf16 operands (compute_dtype=bfloat16): the staged F(2x2) kernel with bf16 U images and
+              # v_mfma_f32_16x16x16_bf16 (winograd.hip BF); fp32 transforms, accumulation and epilogues
+WINO_BF_UNP = -7  # its dgrad of a pooled layer after an explicit unpool (as WINO_UNP)
 CFG_BF16 = 256  # tile-config flag of conv_igemm: bf16 operands / fp32 accumulation (opt-in, compute_dtype)
 _BF16_CFGS = (0, 2, 3)  # the implicit-GEMM tiles built with bf16 variants (conv_mfma.hip launch_any)
             # than F(2x2); dgrads of pooled layers take the explicit unpool first
@@ -555,8 +558,32 @@ class FusedChainEngine:
             e["dense"] = d
         return d
 
+    @staticmethod
+    def _ubf(e, dgrad=False):
+        """bf16 F(2x2) U images (the WINO_BF kernels) of the entry's weight, built on first use."""
+        key = "utb" if dgrad else "ub"
+        u = e.get(key)
+        if u is None:
+            u = e[key] = ops.require().wino_weights(e["w4d"], dgrad, 0, 0, True)
+        return u
+
+    @staticmethod
+    def _wino_bf_cands(T, B, H, W, N, C, pooled_grad=False):
+        """bf16 Winograd candidates ([0] = the untuned pick) when the staged kernels cover the
+        map (the BF kernels exist for the staged input modes only)."""
+        if not T.wino_staged_ok(H, W, False):
+            return []
+        sp = _wino_splits(B * (H // 2) * (W // 2), N, C)
+        sps = sorted({sp, max(1, sp // 2), 1}, reverse=True)
+        kinds = [WINO_BF]
+        if pooled_grad:
+            kinds = ([WINO_BF] if T.wino_staged_ok(H, W, True) else []) + [WINO_BF_UNP]
+        return [(k, s_) for k in kinds for s_ in sps]
+
     def _conv_run(self, T, e, h, cfg, sp, apoz=None):
         """``apoz``: (B, N) buffer that receives the counts of positive (pre-pool) outputs."""
+        if cfg == WINO_BF:
+            return T.conv_wino_fwd(h, self._ubf(e), e["scale"], e["shift"], True, e["pool"], sp, True, apoz)
         if cfg >= CFG_BF16:
             return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp, apoz)
         if cfg in (WINO4, WINO4W):
@@ -583,6 +610,8 @@ class FusedChainEngine:
         cands = None
         if self.bf16 and C % 32 == 0:
             cands = self._bf16_cands(M, N, K)
+            if wino is not None:
+                cands = self._wino_bf_cands(T, B, H, W, N, C) + cands
         elif H == 2 and W == 2 and C % 32 == 0:
             cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * N, 4 * C)] + \
                 TUNER.candidates(M, N, K, wino)
@@ -599,6 +628,10 @@ class FusedChainEngine:
 
     def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0):
         """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
+        if cfg in (WINO_BF, WINO_BF_UNP):
+            if cfg == WINO_BF_UNP:
+                g, am = T.unpool2_nhwc(g, am), None
+            return T.conv_wino_dgrad(g, am, self._ubf(e, True), act, sc, taylor, want_out, sp, True, tay_mode=tm)
         if cfg >= CFG_BF16:
             return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp, tay_mode=tm)
         if cfg in (WINO4, WINO4W):
@@ -1028,6 +1061,8 @@ class FusedChainEngine:
             sc4, cands = None, None
             if self.bf16 and Cg % 32 == 0:
                 cands = self._bf16_cands(M, Cin, e["wt"].shape[1])
+                if wino is not None:
+                    cands = self._wino_bf_cands(T, B, H, W, Cin, Cg, am is not None) + cands
             elif H == 2 and W == 2 and Cg % 32 == 0 and Cin % 32 == 0:
                 pe = P["convs"][ci - 1]
                 sc4 = pe.get("scale4")
