@@ -87,7 +87,7 @@ def test_bf16_engine_taylor_ranks_match_fp32(cuda):
 
     from torchpruner_amd import TaylorAttributionMetric
     from torchpruner_amd.data import DeviceLoader
-    from torchpruner_amd.engine.fused_chain import CFG_BF16, TUNER
+    from torchpruner_amd.engine.fused_chain import CFG_BF16, TUNER, WINO_BF, WINO_BF_UNP
     from torchpruner_amd.models import prunable_vgg16
     torch.manual_seed(0)
     model = prunable_vgg16().to(cuda).eval()
@@ -103,12 +103,47 @@ def test_bf16_engine_taylor_ranks_match_fp32(cuda):
     mb = TaylorAttributionMetric(model, dl, F.cross_entropy, cuda, compute_dtype=torch.bfloat16)
     bf = mb.run_many(convs, True)
     assert mb.last_path["path"] == "fused", mb.last_path
-    assert any(isinstance(v, tuple) and v[0] >= CFG_BF16 for v in TUNER.cache.values())
+    assert any(isinstance(v, tuple) and (v[0] >= CFG_BF16 or v[0] in (WINO_BF, WINO_BF_UNP))
+               for v in TUNER.cache.values())
     for k, (a, b) in enumerate(zip(bf, fp)):
         assert np.isfinite(a).all()
         rho = spearmanr(a, b).correlation
         assert rho >= 0.99, (k, rho)
         assert np.abs(a - b).max() / np.abs(b).max() < 5e-2, k
+
+
+@pytest.mark.parametrize("family", ["wino2_bf16", "igemm"])
+def test_bf16_engine_family_pinned(cuda, family):
+    """Each bf16 kernel family pinned in turn (bf16 F(2x2) Winograd with hi/lo V, bf16 implicit
+    GEMM) gives Taylor scores that rank like the fp32 ones; the pinned family really ran."""
+    from scipy.stats import spearmanr
+
+    from torchpruner_amd import TaylorAttributionMetric
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine import invalidate
+    from torchpruner_amd.engine.fused_chain import CFG_BF16, TUNER, WINO_BF, WINO_BF_UNP, family_policy
+    from torchpruner_amd.models import prunable_vgg16
+    torch.manual_seed(1)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    x = torch.randn(128, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (128,), device=cuda)
+    fp = TaylorAttributionMetric(model, DeviceLoader(x, y, 64), F.cross_entropy, cuda).run_many(convs, True)
+    invalidate(model)
+    with TUNER.pinned(family_policy(family)):
+        mb = TaylorAttributionMetric(model, DeviceLoader(x, y, 64), F.cross_entropy, cuda,
+                                     compute_dtype=torch.bfloat16)
+        bf = mb.run_many(convs, True)
+        kinds = {v[0] for v in TUNER.cache.values() if isinstance(v, tuple)}
+    invalidate(model)
+    assert mb.last_path["path"] == "fused", mb.last_path
+    if family == "wino2_bf16":
+        assert kinds & {WINO_BF, WINO_BF_UNP}, kinds
+    else:
+        assert any(k >= CFG_BF16 for k in kinds) and not kinds & {WINO_BF, WINO_BF_UNP}, kinds
+    for k, (a, b) in enumerate(zip(bf, fp)):
+        assert np.isfinite(a).all()
+        assert spearmanr(a, b).correlation >= 0.99, k
 
 
 def test_shapley_fp32_after_bf16_on_one_engine(cuda):

@@ -1,0 +1,43 @@
+"""Coalesced small loader batches on the fused engine (attributions/base.py COALESCE_PIXELS): k
+consecutive equal-shape batches run as one engine launch with each loader batch's 1/B loss
+scaling, so the Taylor / Sensitivity scores equal the batch-by-batch ones (up to the rounding of
+different kernel choices); leftover and odd-shaped batches run alone."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _loader(x, y, sizes):
+    out, o = [], 0
+    for s in sizes:
+        out.append((x[o:o + s], y[o:o + s]))
+        o += s
+    return out
+
+
+@pytest.mark.parametrize("metric", ["taylor", "sensitivity"])
+def test_coalesced_batches_match_batch_by_batch(cuda, monkeypatch, metric):
+    from torchpruner_amd import SensitivityAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.engine.fused_chain import TUNER
+    from torchpruner_amd.models import prunable_vgg16
+    cls = TaylorAttributionMetric if metric == "taylor" else SensitivityAttributionMetric
+    torch.manual_seed(0)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    sizes = [100] * 12 + [37]  # two groups of 5, two leftovers, an odd last batch
+    x = torch.randn(sum(sizes), 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (sum(sizes),), device=cuda)
+    with TUNER.fixed():
+        monkeypatch.setenv("TORCHPRUNER_COALESCE", "0")
+        ref_m = cls(model, _loader(x, y, sizes), F.cross_entropy, cuda)
+        ref = ref_m.run_many(convs, True)
+        assert ref_m.last_coalesce == 1
+        monkeypatch.setenv("TORCHPRUNER_COALESCE", "1")
+        m = cls(model, _loader(x, y, sizes), F.cross_entropy, cuda)
+        got = m.run_many(convs, True)
+        assert m.last_path["path"] == "fused" and m.last_coalesce == 5, (m.last_path, m.last_coalesce)
+    for k, (a, b) in enumerate(zip(got, ref)):
+        np.testing.assert_allclose(a, b, rtol=2e-4, atol=1e-6 * np.abs(b).max(), err_msg=str(k))

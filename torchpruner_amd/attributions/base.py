@@ -432,10 +432,24 @@ class _AttributionMetric(ABC):
                 h.remove()
             self.restore_deterministic()
 
+    # Small loader batches on the fused engine are coalesced: COALESCE_PIXELS input pixels per
+    # engine launch (B=100 at 32x32 -> 5 loader batches = 500 images per launch). In eval mode every
+    # sample's forward / backward is independent of the others in its batch and the fused
+    # cross-entropy keeps each loader batch's 1/B loss scaling, so every per-sample score is the one
+    # its own batch gives (up to kernel-choice rounding); scores are folded per sample, |.| included.
+    # TORCHPRUNER_COALESCE=0 turns it off.
+    COALESCE_PIXELS = 1 << 19
+
+    def _coalesce_factor(self, x) -> int:
+        if os.environ.get("TORCHPRUNER_COALESCE", "1") == "0" or not x.is_cuda:
+            return 1
+        return max(1, self.COALESCE_PIXELS // max(1, x.shape[0] * math.prod(x.shape[2:])))
+
     def _fused_grad_pass(self, engine, blocks, accs, mode, take_abs):
         """Gradient metrics on the fused VGG-chain engine: per batch ONE fused forward +
         input-gradient backward writes every block's per-sample partials (``mode`` taylor /
-        sensitivity), and ONE fold launch turns all layers' sums into fp64 accumulators."""
+        sensitivity), and ONE fold launch turns all layers' sums into fp64 accumulators. Small
+        batches are coalesced (see COALESCE_PIXELS) and pipelined over HIP streams."""
         from ..engine.fused_chain import engine_criterion
         owner = {}
         for k, b in enumerate(blocks):
@@ -444,15 +458,17 @@ class _AttributionMetric(ABC):
         stats = accs[0].mode == "stats"
         crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
         pipe = _BatchPipeline(engine, graph_replay=True) if stats and self._ckpt is None and crit is None else None
-        for i, x, y in self._batches():
+        self.last_coalesce = 1
+
+        def run_batch(i, x, y, loss_batch=None):
             B = x.shape[0]
 
             def launch(slot, x=x, y=y):
                 arena = engine.score_arena(x.shape[0], uniq, x.device, tuple(x.shape[2:]), slot=slot)
                 if engine.graphs_enabled(x.shape[0], pipelined=True):  # host-bound otherwise
-                    engine.taylor_graphed(x, y, set(uniq), arena, mode=mode, warm=True)
+                    engine.taylor_graphed(x, y, set(uniq), arena, mode=mode, warm=True, loss_batch=loss_batch)
                 else:
-                    engine.taylor(x, y, set(uniq), arena, mode=mode)
+                    engine.taylor(x, y, set(uniq), arena, mode=mode, loss_batch=loss_batch)
                 return arena
 
             def fold(arena, dev=x.device):
@@ -462,14 +478,14 @@ class _AttributionMetric(ABC):
             if pipe is not None and pipe.take(x, y, launch, fold):
                 for b in uniq:
                     accs[owner[b]].count += B
-                continue
+                return
             if stats:
                 arena = engine.score_arena(B, uniq, x.device, tuple(x.shape[2:]))
                 with trace_range("tp.forward_backward"):
                     if engine.graphs_enabled(B):  # small batches are launch-bound: replay a HIP graph
-                        engine.taylor_graphed(x, y, set(uniq), arena, mode=mode, criterion=crit)
+                        engine.taylor_graphed(x, y, set(uniq), arena, mode=mode, criterion=crit, loss_batch=loss_batch)
                     else:
-                        engine.taylor(x, y, set(uniq), arena, mode=mode, criterion=crit)
+                        engine.taylor(x, y, set(uniq), arena, mode=mode, criterion=crit, loss_batch=loss_batch)
                 sums = [accs[owner[b]].ensure_sum(arena[b].shape[-1], x.device, engine.real_width(b)) for b in uniq]
                 with trace_range("tp.fold"):
                     ops.score_fold_([arena[b] for b in uniq], sums, take_abs, 2)
@@ -480,6 +496,30 @@ class _AttributionMetric(ABC):
                 ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), take_abs, 1)
                 for b in uniq:
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
+
+        group, k = [], 1
+        for i, x, y in self._batches():
+            if pipe is None:
+                run_batch(i, x, y)
+                continue
+            if group and (x.shape != group[0][1].shape or y.shape != group[0][2].shape):
+                for g in group:  # a batch of another shape (the last one): no partial groups
+                    run_batch(*g)
+                group = []
+            if not group:
+                k = self._coalesce_factor(x)
+            group.append((i, x, y))
+            if len(group) < k:
+                continue
+            if k == 1:
+                run_batch(i, x, y)
+            else:
+                self.last_coalesce = k
+                run_batch(group[0][0], torch.cat([g[1] for g in group]), torch.cat([g[2] for g in group]),
+                          loss_batch=x.shape[0])
+            group = []
+        for g in group:
+            run_batch(*g)
         if pipe is not None:
             pipe.join()
         return [accs[owner[b]] for b in blocks]

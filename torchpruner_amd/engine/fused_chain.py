@@ -866,7 +866,7 @@ class FusedChainEngine:
         return mode == "1" and B <= self.GRAPH_MAX_B
 
     def taylor_graphed(self, x: torch.Tensor, y: torch.Tensor, want: set, arena: dict, mode="taylor",
-                       criterion=None, warm: bool = False):
+                       criterion=None, warm: bool = False, loss_batch: Optional[int] = None):
         """``taylor()`` replayed from a captured HIP graph: the ~40 launches of one fused
         forward + input-gradient backward become one graph launch, which is what small,
         launch-bound batches need. One graph per (input shapes, blocks, mode, score arena,
@@ -878,11 +878,11 @@ class FusedChainEngine:
         this shape eagerly already (kernels tuned, operands packed): capture on the first call
         (the stream pipeline's first batch of a shape runs alone, eagerly)."""
         if criterion is not None:  # a user criterion runs through autograd: eager launches
-            return self.taylor(x, y, want, arena, mode, criterion)
+            return self.taylor(x, y, want, arena, mode, criterion, loss_batch)
         P = self._pack()
         # one graph per score arena: the stream pipeline replays slot k's graph into slot k's arena
         key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, tuple(sorted(want)), mode, str(x.device), self.bf16,
-               TUNER.gen, id(arena))
+               loss_batch, TUNER.gen, id(arena))
         g = self._graphs.get(key)
         if g is not None and (g["P"] is not P or g["arena"] is not arena):
             torch.cuda.synchronize()  # its replays must finish before the stale graph (and pool) goes
@@ -891,13 +891,13 @@ class FusedChainEngine:
             seen = self._graphs.get(("seen",) + key)
             if not warm and (seen is None or seen[0] is not P or seen[1] is not arena):
                 self._graphs[("seen",) + key] = (P, arena)
-                return self.taylor(x, y, want, arena, mode)
+                return self.taylor(x, y, want, arena, mode, loss_batch=loss_batch)
             sx, sy = x.clone(), y.clone()
             graph = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(x.device)
             side.wait_stream(torch.cuda.current_stream(x.device))
             with torch.cuda.graph(graph, stream=side):
-                self.taylor(sx, sy, want, arena, mode)
+                self.taylor(sx, sy, want, arena, mode, loss_batch=loss_batch)
             torch.cuda.current_stream(x.device).wait_stream(side)
             self._bound_graph_cache()
             g = self._graphs[key] = {"graph": graph, "x": sx, "y": sy, "P": P, "arena": arena}
@@ -997,7 +997,7 @@ class FusedChainEngine:
         return g["bufs"]
 
     def taylor(self, x: torch.Tensor, y: torch.Tensor, want: Optional[set] = None, arena=None, mode="taylor",
-               criterion=None):
+               criterion=None, loss_batch: Optional[int] = None):
         """One fused forward+backward (``criterion``: see :func:`logits_grad`); returns {block index: per-sample signed Taylor sums
         sum_hw -(dL/da * a)} (``mode="sensitivity"``: sum_hw |dL/da|) for every requested block
         (conv blocks first, then linear blocks; the final linear has none) as (R, B, C) partial
@@ -1014,7 +1014,7 @@ class FusedChainEngine:
                      for b, sh in self._arena_shapes(x.shape[0], want, x.shape[2], x.shape[3]).items()}
         logits, saved = self.forward(x)
         B = logits.shape[0]
-        g = logits_grad(logits, y, criterion)
+        g = logits_grad(logits, y, criterion, loss_batch)
         lin_acts = saved["lin_acts"]
         acts = saved["acts"]
         res = {}
@@ -1093,15 +1093,16 @@ class FusedChainEngine:
         return res
 
 
-KERNEL_FAMILIES = ("wino4", "wino4w", "wino2", "wino2_direct", "igemm")
+KERNEL_FAMILIES = ("wino4", "wino4w", "wino2", "wino2_direct", "igemm", "wino2_bf16")
 
 
 def family_policy(family: str, split: str = "min"):
     """A :meth:`Autotuner.pinned` policy that runs every layer it can on one kernel family:
     ``wino4`` F(4x4,3x3), ``wino4w`` its wide kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
     F(2x2) with direct patch loads, ``igemm`` the implicit GEMM (dense 2x2 GEMM, VALU first
-    layer). ``split``: the fewest ("min") or most ("max") channel splits of that family. Layers
-    the family does not cover keep the untuned pick."""
+    layer; with bf16 operands the bf16 implicit GEMM), ``wino2_bf16`` the bf16 F(2x2) kernels
+    (compute_dtype=bfloat16 only). ``split``: the fewest ("min") or most ("max") channel splits of
+    that family. Layers the family does not cover keep the untuned pick."""
     eng = FusedChainEngine
 
     def member(c):
@@ -1115,7 +1116,9 @@ def family_policy(family: str, split: str = "min"):
         if family == "wino2_direct":
             return k == WINO
         if family == "igemm":
-            return 0 <= k <= 6 or eng.DENSE <= k < CFG_BF16 or k == eng.FIRST_DIRECT
+            return 0 <= k <= 6 or eng.DENSE <= k or k == eng.FIRST_DIRECT
+        if family == "wino2_bf16":
+            return k in (WINO_BF, WINO_BF_UNP)
         raise ValueError(f"unknown kernel family {family!r}")
 
     def policy(key, cands, M, N, K):
@@ -1129,13 +1132,16 @@ def family_policy(family: str, split: str = "min"):
     return policy
 
 
-def logits_grad(logits: torch.Tensor, y: torch.Tensor, criterion=None) -> torch.Tensor:
+def logits_grad(logits: torch.Tensor, y: torch.Tensor, criterion=None, loss_batch: Optional[int] = None) -> torch.Tensor:
     """dL/dlogits of the batch loss the engines back-propagate: the fused HIP log-softmax + NLL
     kernel for mean cross-entropy (``criterion=None``), else autograd through the user's
     criterion on the (detached) logits, with its default reduction — exactly the gradient the
-    reference's ``criterion(out, y).backward()`` feeds into the network (attributions.py:64-68)."""
+    reference's ``criterion(out, y).backward()`` feeds into the network (attributions.py:64-68).
+    ``loss_batch``: the mean is over batches of this size (coalesced loader batches, cross-entropy
+    only): every sample's gradient is what its own loader batch's backward gives it."""
     if criterion is None:
-        return ops.cross_entropy(logits, y, 1.0 / logits.shape[0], True)[1]
+        return ops.cross_entropy(logits, y, 1.0 / (loss_batch or logits.shape[0]), True)[1]
+    assert loss_batch is None or loss_batch == logits.shape[0], "coalesced batches need the fused cross-entropy"
     lg = logits.detach().requires_grad_(True)
     with torch.enable_grad():
         loss = criterion(lg, y)
