@@ -445,6 +445,35 @@ class _AttributionMetric(ABC):
             return 1
         return max(1, self.COALESCE_PIXELS // max(1, x.shape[0] * math.prod(x.shape[2:])))
 
+    def _coalesced_batches(self, on: bool):
+        """``(global_batch_index, x, y, loss_batch)`` over this rank's batches; with ``on``, runs of
+        k equal-shape batches come concatenated (``loss_batch`` = the loader batch size, the
+        group's first index), leftovers and odd shapes alone (``loss_batch`` None)."""
+        self.last_coalesce = 1
+        if not on:
+            for i, x, y in self._batches():
+                yield i, x, y, None
+            return
+        group, k = [], 1
+        for i, x, y in self._batches():
+            if group and (x.shape != group[0][1].shape or y.shape != group[0][2].shape):
+                for g in group:  # a batch of another shape (the last one): no partial groups
+                    yield g + (None,)
+                group = []
+            if not group:
+                k = self._coalesce_factor(x)
+            group.append((i, x, y))
+            if len(group) < k:
+                continue
+            if k == 1:
+                yield i, x, y, None
+            else:
+                self.last_coalesce = k
+                yield group[0][0], torch.cat([g[1] for g in group]), torch.cat([g[2] for g in group]), x.shape[0]
+            group = []
+        for g in group:
+            yield g + (None,)
+
     def _fused_grad_pass(self, engine, blocks, accs, mode, take_abs):
         """Gradient metrics on the fused VGG-chain engine: per batch ONE fused forward +
         input-gradient backward writes every block's per-sample partials (``mode`` taylor /
@@ -458,7 +487,6 @@ class _AttributionMetric(ABC):
         stats = accs[0].mode == "stats"
         crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
         pipe = _BatchPipeline(engine, graph_replay=True) if stats and self._ckpt is None and crit is None else None
-        self.last_coalesce = 1
 
         def run_batch(i, x, y, loss_batch=None):
             B = x.shape[0]
@@ -497,29 +525,8 @@ class _AttributionMetric(ABC):
                 for b in uniq:
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
 
-        group, k = [], 1
-        for i, x, y in self._batches():
-            if pipe is None:
-                run_batch(i, x, y)
-                continue
-            if group and (x.shape != group[0][1].shape or y.shape != group[0][2].shape):
-                for g in group:  # a batch of another shape (the last one): no partial groups
-                    run_batch(*g)
-                group = []
-            if not group:
-                k = self._coalesce_factor(x)
-            group.append((i, x, y))
-            if len(group) < k:
-                continue
-            if k == 1:
-                run_batch(i, x, y)
-            else:
-                self.last_coalesce = k
-                run_batch(group[0][0], torch.cat([g[1] for g in group]), torch.cat([g[2] for g in group]),
-                          loss_batch=x.shape[0])
-            group = []
-        for g in group:
-            run_batch(*g)
+        for i, x, y, lb in self._coalesced_batches(pipe is not None):
+            run_batch(i, x, y, lb)
         if pipe is not None:
             pipe.join()
         return [accs[owner[b]] for b in blocks]

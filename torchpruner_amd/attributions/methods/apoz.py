@@ -52,7 +52,8 @@ class APoZAttributionMetric(_AttributionMetric):
         stats = accs[0].mode == "stats"
         pipe = _BatchPipeline(engine, graph_replay=True) if stats and self._ckpt is None else None
         with torch.no_grad():
-            for i, x, _y in self._batches():
+            # small batches coalesced into one launch (per-sample counts: no loss involved)
+            for i, x, _y, _lb in self._coalesced_batches(pipe is not None):
                 B = x.shape[0]
 
                 def launch(slot, x=x):
