@@ -1,7 +1,7 @@
-"""Coalesced small loader batches (Taylor, Sensitivity, APoZ) on the fused engine (attributions/base.py COALESCE_PIXELS): k
+"""Coalesced small loader batches on the fused engine (attributions/base.py COALESCE_PIXELS): k
 consecutive equal-shape batches run as one engine launch with each loader batch's 1/B loss
-scaling, so the Taylor / Sensitivity scores equal the batch-by-batch ones (up to the rounding of
-different kernel choices); leftover and odd-shaped batches run alone."""
+scaling, so the Taylor / Sensitivity / APoZ scores equal the batch-by-batch ones (up to the
+rounding of different kernel choices); leftover and odd-shaped batches run alone."""
 import numpy as np
 import pytest
 import torch
