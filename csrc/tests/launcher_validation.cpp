@@ -79,6 +79,10 @@ int main() {
          hipErrorInvalidValue);  // odd H with unpooling
   EXPECT(tp_conv_wino(n, nullptr, n, 2, 8, 8, 12, 64, 0, 0, 1, 1, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
          hipErrorInvalidValue);  // C % 8
+  EXPECT(tp_conv_wino(n, nullptr, n, 2, 8, 8, 64, 64, 0, 0, 1, 2, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
+         hipErrorInvalidValue);  // bf16 U images (staged bit 1) without a staged input mode
+  EXPECT(tp_conv_wino(n, nullptr, n, 2, 7, 7, 64, 64, 0, 0, 1, 3, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
+         hipErrorInvalidValue);  // bf16 on an odd map (direct loads only)
   EXPECT(tp_bn_fwd_train(n, n, 16, 6, n, n, 1e-5f, 0.1f, n, n, n, n, n, n, nullptr, 0) == hipErrorInvalidValue);
   // warp-specialised 1x1 GEMM (conv_gen cfgs 16-18): Cin % 32, N % 4, stride, slope, variant, 2^31-byte bounds,
   // and the conv_gen entry's 1x1 / no-pad / dense-residual / no-bnpart gate
