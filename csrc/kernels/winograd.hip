@@ -368,12 +368,20 @@ phase2:
 // staging, transforms and epilogues are the fp32 kernel's. BF = 2 (TP_WINO_BF_SPLIT=1, measured
 // option): V carried as a bf16 hi + lo pair in the padding k-slots (~16 mantissa bits of V, only
 // U rounded); 18% slower, and on the trained headline teacher the scores rank the same.
+// BF = 3 (measured option TP_WINO_BF_K16=1; X_STAGED regions of <= 3 DMA rounds, C % 16 == 0):
+// 16-channel chunks — two 8-channel X images and two U images per stage — so a lane's MFMA
+// operand holds its two channel pairs (k = image 0 pair, image 1 pair) and every k-slot is used:
+// half the bf16 MFMAs (v_mfma_f32_16x16x16_bf16 costs as much as 16x16x32, ~16 cycles) and half
+// the barriers. Measured on the VGG16 layers: forward 0.5-19% faster on the 32/16-pixel maps,
+// the 32-pixel data gradient 28% slower, the engine unchanged (profiles/bf16/).
 // Measured and dropped: a 3-deep LDS-DMA ring for these kernels (DMA latency is not what bounds
 // them: fwd 1.0x, dgrad 0.94x without the act prefetch it displaced).
 template <int EPI, int XMODE, int BF = 0>
 __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   constexpr bool STAGED = XMODE == X_STAGED || XMODE == X_STAGED_UNPOOL || XMODE == X_SPAN;
   constexpr bool UNPOOL = XMODE == X_UNPOOL;
+  static_assert(BF != 3 || XMODE == X_STAGED, "16-channel bf16 chunks: staged regions only");
+  constexpr int CHK = BF == 3 ? 2 * W_CH : W_CH;  // input channels per stage
   // separate objects per buffer so the compiler's LDS-DMA alias tracking can tell them apart.
   // The staged modes use exactly 80 KB: two blocks per CU (160 KB). ANY extra __shared__ byte
   // halves the occupancy (tests/test_conv_gpu.py::test_wino_lds_budget guards this).
@@ -561,7 +569,19 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
 #pragma unroll
     for (int i = 0; i < (BF ? 2 : 4); ++i)
       dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ubase);
-    if constexpr (XMODE == X_STAGED || XMODE == X_SPAN) {
+    if constexpr (BF == 3) {  // second 8-channel half: U image of chunk c0/8 + 1, X image at + rounds
+      const unsigned ubase1 = (unsigned)((((c0 / W_CH) + 1) * n_k + kb) * W_UIMG) * 2u;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        dma16(urs, ud + W_UIMG / 2 + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ubase1);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i < p.rounds) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i < p.rounds)
+          dma16(xrs, xd + p.rounds * 1024 + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)(c0 + W_CH) * 4u);
+    } else if constexpr (XMODE == X_STAGED || XMODE == X_SPAN) {
 #pragma unroll
       for (int i = 0; i < MAX_ROUNDS; ++i)
         if (i < p.rounds) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
@@ -613,26 +633,27 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
   float* epi_y1 = us1;
   float* epi_a0 = nullptr;
   float* epi_a1 = nullptr;
-  unsigned act_src[STAGED && EPI == W_BWD ? 8 : 1];
   const __amdgpu_buffer_rsrc_t acts = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.act, (short)0, (STAGED && EPI == W_BWD) ? (int)((long long)p.B * p.H * p.W * p.K * 4) : 0, 0x00020000);
-  if constexpr (STAGED && EPI == W_BWD) {
-    const int t0 = blk_p * 64;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int slot = i * 256 + tid;
-      const int pl = slot >> 3, c4 = slot & 7;
-      const int tl = pl >> 2, q = pl & 3;
-      const int pt = t0 + tl;
-      unsigned off = 0x80000000u;
-      if (pt < p.P && k0 + 4 * c4 < p.K) {
-        const int bb = p.fd_timg.div(pt), rr = pt - bb * T_img;
-        const int r2 = p.fd_w2.div(rr);
-        const int oh = 2 * r2 + (q >> 1), ow = 2 * (rr - r2 * W2) + (q & 1);
-        off = (unsigned)(((((long long)bb * p.H + oh) * p.W + ow) * p.K + k0 + 4 * c4) * 4);
-      }
-      act_src[i] = off;
+  // DMA source offset of this thread's act slot in round i (slot = 8*pixel + c4: phase 2's order)
+  auto act_off = [&](int i) -> unsigned {
+    const int slot = i * 256 + tid;
+    const int pl = slot >> 3, c4 = slot & 7;
+    const int tl = pl >> 2, q = pl & 3;
+    const int pt = blk_p * 64 + tl;
+    unsigned off = 0x80000000u;
+    if (pt < p.P && k0 + 4 * c4 < p.K) {
+      const int bb = p.fd_timg.div(pt), rr = pt - bb * T_img;
+      const int r2 = p.fd_w2.div(rr);
+      const int oh = 2 * r2 + (q >> 1), ow = 2 * (rr - r2 * W2) + (q & 1);
+      off = (unsigned)(((((long long)bb * p.H + oh) * p.W + ow) * p.K + k0 + 4 * c4) * 4);
     }
+    return off;
+  };
+  unsigned act_src[STAGED && EPI == W_BWD && BF != 3 ? 8 : 1];
+  if constexpr (STAGED && EPI == W_BWD && BF != 3) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) act_src[i] = act_off(i);
   }
 
   // bf16 products of one chunk: U image ub (bf16), this lane's transformed pair v[16]
@@ -668,6 +689,64 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_s_setprio(0);
+  };
+
+  // BF == 3: one 16-channel stage. Each half's patch is read and transformed in turn and rounded
+  // to bf16 right away (16 dwords per half), then every point's two halves feed one MFMA per
+  // output half against U images 0 / 1
+  auto compute16 = [&](int c0, const float* ub, const float* xb, float* ud_next, float* xd_next, bool more) {
+    unsigned ah[2][16];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x2 d[16], v[16];
+      const char* xh = reinterpret_cast<const char*>(xb) + h * p.rounds * 4096;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) d[t] = *reinterpret_cast<const f32x2*>(xh + poff[t]);
+      input_transform2(d, v);
+#pragma unroll
+      for (int x = 0; x < 16; ++x) ah[h][x] = bf16x2_of(v[x]);
+      __builtin_amdgcn_sched_barrier(0);  // half 1's patch loads after half 0 is packed: 32 fewer live VGPRs
+    }
+    if (more) stage(c0 + CHK, ud_next, xd_next);
+    if constexpr (EPI == W_BWD) {
+      if (!more) {  // as compute(): the act tile lands under the last stage's MFMAs
+        epi_y0 = const_cast<float*>(ub);
+        epi_y1 = const_cast<float*>(xb);
+        epi_a0 = ud_next;
+        epi_a1 = xd_next;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // offsets computed here, once: no registers held over the loop
+          float* dst = (i < 4 ? ud_next : xd_next) + ((i & 3) * 256 + wave * 64) * 4;
+          dma16(acts, dst, act_off(i), 0u);
+        }
+      }
+    }
+    const unsigned* ul0 = reinterpret_cast<const unsigned*>(ub) + uoff;
+    const unsigned* ul1 = ul0 + W_UIMG / 2;
+    constexpr int AHEAD = 2;
+    u32x2 w0[AHEAD], w1[AHEAD];
+#pragma unroll
+    for (int s_ = 0; s_ < AHEAD; ++s_) {
+      w0[s_] = *reinterpret_cast<const u32x2*>(ul0 + s_ * 128);
+      w1[s_] = *reinterpret_cast<const u32x2*>(ul1 + s_ * 128);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+      const u32x2 a0 = w0[x % AHEAD], a1 = w1[x % AHEAD];
+      if (x + AHEAD < 16) {
+        w0[x % AHEAD] = *reinterpret_cast<const u32x2*>(ul0 + (x + AHEAD) * 128);
+        w1[x % AHEAD] = *reinterpret_cast<const u32x2*>(ul1 + (x + AHEAD) * 128);
+      }
+      const s16x4 a = __builtin_bit_cast(s16x4, u32x2{ah[0][x], ah[1][x]});
+      acc[x][0] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, __builtin_bit_cast(s16x4, u32x2{a0.x, a1.x}),
+                                                           acc[x][0], 0, 0, 0);
+      acc[x][1] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, __builtin_bit_cast(s16x4, u32x2{a0.y, a1.y}),
+                                                           acc[x][1], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __syncthreads();
   };
 
   auto compute = [&](int c0, const float* ub, const float* xb, float* ud_next, float* xd_next, bool more) {
@@ -770,9 +849,16 @@ __global__ __launch_bounds__(256, 2) void wino_f2x3(WinoArgs p) {
     if constexpr (!STAGED) issue_x(c_begin);
     stage(c_begin, us0, xs0);
     __syncthreads();
+    if constexpr (BF == 3) {
+      for (int c0 = c_begin; c0 < c_end; c0 += 2 * CHK) {
+        compute16(c0, us0, xs0, us1, xs1, c0 + CHK < c_end);
+        if (c0 + CHK < c_end) compute16(c0 + CHK, us1, xs1, us0, xs0, c0 + 2 * CHK < c_end);
+      }
+    } else {
     for (int c0 = c_begin; c0 < c_end; c0 += 2 * W_CH) {
       compute(c0, us0, xs0, us1, xs1, c0 + W_CH < c_end);
       if (c0 + W_CH < c_end) compute(c0 + W_CH, us1, xs1, us0, xs0, c0 + 2 * W_CH < c_end);
+    }
     }
   }
   if WDBG(p, 1) {
@@ -1206,9 +1292,24 @@ extern "C" hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, cons
   }
   if (bf && xmode != X_STAGED && xmode != X_SPAN && xmode != X_STAGED_UNPOOL) return hipErrorInvalidValue;
   static const bool bf_split = getenv("TP_WINO_BF_SPLIT") != nullptr;  // measured option: V as bf16 hi + lo
+  static const bool k16_ok = getenv("TP_WINO_BF_K16") != nullptr;  // measured option: 16-channel bf16 chunks
+  const bool k16 = bf && !bf_split && k16_ok && xmode == X_STAGED && a.rounds <= 3 && C % 16 == 0;
+  if (k16) {  // 16-channel stages: the channel split granule is 16
+    const int c16 = C / 16;
+    int sp16 = std::max(1, std::min(splits, c16));
+    a.c_per_split = ((c16 + sp16 - 1) / sp16) * 16;
+    splits = (C + a.c_per_split - 1) / a.c_per_split;
+    grid.y = splits;
+    if (splits == 1 && e_launch == W_PARTIAL) {  // the 16-channel granule left one split: no slabs
+      a.out = out;
+      e_launch = epi;
+    }
+  }
 #define TP_W(E)                                                                                 \
   do {                                                                                          \
-    if (bf && bf_split) {                                                                       \
+    if (k16) {                                                                                  \
+      wino_f2x3<E, X_STAGED, 3><<<grid, 256, 0, st>>>(a);                                       \
+    } else if (bf && bf_split) {                                                                \
       if (xmode == X_STAGED) wino_f2x3<E, X_STAGED, 2><<<grid, 256, 0, st>>>(a);               \
       else if (xmode == X_SPAN) wino_f2x3<E, X_SPAN, 2><<<grid, 256, 0, st>>>(a);              \
       else wino_f2x3<E, X_STAGED_UNPOOL, 2><<<grid, 256, 0, st>>>(a);                          \
