@@ -147,3 +147,19 @@ def test_wino_bf16_rejects_direct_mode(cuda):
     ubf = T.wino_weights(torch.randn(32, 32, 3, 3, device=cuda), False, 32, 32, True)
     with pytest.raises(RuntimeError):
         T.conv_wino_fwd(x, ubf, None, None, True, False, 1, False)
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("variant", ["TP_WINO_BF_K16", "TP_WINO_BF_SPLIT"])
+def test_wino_bf16_measured_options_match_emulation(cuda, variant):
+    """The launcher reads the option switches once per process, so each option runs the
+    emulation check (scripts/wino_bf16_diag.py: 4 VGG shapes, forward) in a child process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **{variant: "1"})
+    p = subprocess.run([sys.executable, os.path.join(root, "scripts", "wino_bf16_diag.py")], env=env, cwd=root,
+                       capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    rels = [float(ln.split(" rel ")[1].split()[0]) for ln in p.stdout.splitlines() if " rel " in ln]
+    assert len(rels) == 4 and max(rels) < 2e-5, p.stdout
