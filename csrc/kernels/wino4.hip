@@ -148,6 +148,31 @@ __device__ __forceinline__ void at6(const float m0, const float m1, const float 
   y3 = fmaf(8.f, d, b) + m5;
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// at6 on two accumulator rows at once (v_pk_add_f32 / v_pk_fma_f32): rows r, r+1 of an f32x4
+// accumulator are an aligned register pair, so the epilogue's output transform costs half the
+// VALU instructions; same operations and rounding as at6
+__device__ __forceinline__ void at6p(const f2v m0, const f2v m1, const f2v m2, const f2v m3, const f2v m4,
+                                     const f2v m5, f2v& y0, f2v& y1, f2v& y2, f2v& y3) {
+  const f2v a = m1 + m2, b = m1 - m2, c = m3 + m4, d = m3 - m4;
+  y0 = m0 + a + c;
+  y1 = 2.f * d + b;
+  y2 = 4.f * c + a;
+  y3 = 8.f * d + b + m5;
+}
+
+__device__ __forceinline__ void output_transform2(const f2v (&m)[36], f2v (&y)[16]) {
+  f2v t[24];
+#pragma unroll
+  for (int c = 0; c < 6; ++c)
+    at6p(m[c], m[6 + c], m[12 + c], m[18 + c], m[24 + c], m[30 + c], t[c], t[6 + c], t[12 + c], t[18 + c]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    at6p(t[6 * r], t[6 * r + 1], t[6 * r + 2], t[6 * r + 3], t[6 * r + 4], t[6 * r + 5], y[4 * r], y[4 * r + 1],
+         y[4 * r + 2], y[4 * r + 3]);
+}
+
 __device__ __forceinline__ void output_transform(const float (&m)[36], float (&y)[16]) {
   float t[24];  // 4 x 6
 #pragma unroll
@@ -189,15 +214,18 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
       if (grp / 2 == hf) {
         float* ybuf = nh ? yb : ya;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4; r += 2) {  // tiles r, r + 1 of this lane: packed pairs
           const int tl = (grp & 1) * 16 + 4 * g + r;
-          float m[36], y[16];
+          f2v m[36], y[16];
 #pragma unroll
-          for (int x = 0; x < NPT; ++x) m[x] = acc[pp][x][r];
-          output_transform(m, y);
+          for (int x = 0; x < NPT; ++x) m[x] = f2v{acc[pp][x][r], acc[pp][x][r + 1]};
+          output_transform2(m, y);
           float* dst = ybuf + tl * TPL + j;
 #pragma unroll
-          for (int q = 0; q < 16; ++q) dst[q * 16] = y[q];
+          for (int q = 0; q < 16; ++q) {
+            dst[q * 16] = y[q].x;
+            dst[TPL + q * 16] = y[q].y;
+          }
         }
       }
     }

@@ -141,6 +141,22 @@ __device__ __forceinline__ void output_transform(const float m[16], float y[4]) 
   }
 }
 
+// output_transform on two accumulator rows at once (v_pk_add_f32): rows r, r+1 of an f32x4
+// accumulator are an aligned register pair; same operations and order as output_transform
+__device__ __forceinline__ void output_transform2(const f32x2 m[16], f32x2 y[4]) {
+  f32x2 t[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t[0 * 4 + j] = m[0 * 4 + j] + m[1 * 4 + j] + m[2 * 4 + j];
+    t[1 * 4 + j] = m[1 * 4 + j] - m[2 * 4 + j] - m[3 * 4 + j];
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    y[a * 2 + 0] = t[a * 4 + 0] + t[a * 4 + 1] + t[a * 4 + 2];
+    y[a * 2 + 1] = t[a * 4 + 1] - t[a * 4 + 2] - t[a * 4 + 3];
+  }
+}
+
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // one 16-B-per-lane LDS-DMA: lane l's 16 bytes land at lds_base + 16*l
@@ -196,12 +212,17 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int tl = tl_base + r;
-      float m[16], y[4];
+    for (int r2 = 0; r2 < 4; r2 += 2) {  // tiles r2, r2 + 1: one packed output transform
+      f32x2 m2[16], y2[4];
 #pragma unroll
-      for (int x = 0; x < 16; ++x) m[x] = acc[x][n][r];
-      output_transform(m, y);
+      for (int x = 0; x < 16; ++x) m2[x] = f32x2{acc[x][n][r2], acc[x][n][r2 + 1]};
+      output_transform2(m2, y2);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+      const int tl = tl_base + r2 + h;
+      float y[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[q] = h ? y2[q].y : y2[q].x;
       if constexpr (EPI == W_FWD_POOL) {
         float best = 0.f;
         int arg = 0, cnt = 0;
@@ -221,6 +242,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& p, f32x4 (&acc)[16
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q) yb[ybuf_row(tl, q) * 16 + j] = y[q];
+      }
       }
     }
   }
