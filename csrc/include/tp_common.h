@@ -69,6 +69,23 @@ __device__ __forceinline__ float nan_relu(float x) { return (x > 0.f || x != x) 
 // Per-element score partial of a data-gradient epilogue (g = dL/da, a = the activation):
 // tay_mode 0 Taylor -(g * a); 1 Sensitivity |g|; 2 Sensitivity of a ReLU-masked gradient
 // |g| where a > 0 (the evaluation module is the BN before the ReLU: ResNet bn1 / bn2).
+// v + v[lane ^ 8] / ^ 16 / ^ 32 without the LDS: DPP row_ror:8 (xor 8 inside a 16-lane row) and
+// gfx950's v_permlane16_swap / v_permlane32_swap (the two swapped halves summed); each lane gets
+// the same float sum as `v + __shfl_xor(v, m)` (one add of the same two values), bit for bit
+__device__ __forceinline__ float xsum8(float v) {
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float xsum16(float v) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  return __builtin_bit_cast(float, (unsigned)s[0]) + __builtin_bit_cast(float, (unsigned)s[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  return __builtin_bit_cast(float, (unsigned)s[0]) + __builtin_bit_cast(float, (unsigned)s[1]);
+}
+
 __device__ __forceinline__ float tay_term(int mode, float g, float a) {
   return mode == 1 ? fabsf(g) : mode == 2 ? (a > 0.f ? fabsf(g) : 0.f) : -(g * a);
 }

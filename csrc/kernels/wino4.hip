@@ -284,8 +284,7 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
         if (want_part) {  // per-(tile, channel) count over the 4 pooled pixels (lanes ^8, ^16)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            cnt[e] += __shfl_xor(cnt[e], 8);
-            cnt[e] += __shfl_xor(cnt[e], 16);
+            cnt[e] = xsum16(xsum8(cnt[e]));
           }
           if (pp == 0) *reinterpret_cast<f32x4*>(part + tb * TK + 4 * c4) = cnt;
         }
@@ -337,9 +336,7 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
         if (want_part) {  // per-(tile, channel) sum over the 16 pixels: lanes ^8, ^16, ^32 (fixed order)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            sum[e] += __shfl_xor(sum[e], 8);
-            sum[e] += __shfl_xor(sum[e], 16);
-            sum[e] += __shfl_xor(sum[e], 32);
+            sum[e] = xsum32(xsum16(xsum8(sum[e])));
           }
           if (qq == 0) *reinterpret_cast<f32x4*>(part + tb * TK + 4 * c4) = sum;
         }

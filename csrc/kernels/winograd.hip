@@ -344,14 +344,10 @@ phase2:
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float4 t = tq[i];
-        t.x += __shfl_xor(t.x, 8);
-        t.y += __shfl_xor(t.y, 8);
-        t.z += __shfl_xor(t.z, 8);
-        t.w += __shfl_xor(t.w, 8);
-        t.x += __shfl_xor(t.x, 16);
-        t.y += __shfl_xor(t.y, 16);
-        t.z += __shfl_xor(t.z, 16);
-        t.w += __shfl_xor(t.w, 16);
+        t.x = xsum16(xsum8(t.x));
+        t.y = xsum16(xsum8(t.y));
+        t.z = xsum16(xsum8(t.z));
+        t.w = xsum16(xsum8(t.w));
         tq[i] = t;
       }
       __syncthreads();  // everyone is done reading yb0/yb1
