@@ -77,7 +77,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 2048)),
                     help="images per GPU per step (HBM-sized: small-spatial layers need >= 2k images to "
-                         "fill 256 CUs)")
+                         "fill 256 CUs; 4096 / 8192 measure 1-3%% more, but the MIOpen comparison extra "
+                         "then re-tunes for a minute)")
     ap.add_argument("--no-baseline", action="store_true", help="skip the reference-semantics eager timing")
     ap.add_argument("--baseline-batches", type=int, default=2)
     ap.add_argument("--no-prune", action="store_true", help="skip the (untimed) accuracy protocol")

@@ -46,3 +46,25 @@ def test_coalesced_batches_match_batch_by_batch(cuda, monkeypatch, metric):
         # Taylor: per-sample sums with cancellation, so a unit's mean can move by ~1e-4 relative
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-5 * np.abs(b).max(), err_msg=str(k))
         assert np.median(np.abs(a - b) / (np.abs(b) + 1e-30)) < 1e-4, k
+
+
+@pytest.mark.parametrize("metric", ["taylor", "apoz"])
+def test_oversized_batch_runs_in_slices(cuda, monkeypatch, metric):
+    """A batch over the engine's max_batch (32-bit buffer descriptors) runs in slices with the
+    whole batch's loss scaling: same scores as one launch (forced small limit here)."""
+    from torchpruner_amd import APoZAttributionMetric, TaylorAttributionMetric
+    from torchpruner_amd.engine.fused_chain import TUNER, FusedChainEngine
+    from torchpruner_amd.models import prunable_vgg16
+    cls = TaylorAttributionMetric if metric == "taylor" else APoZAttributionMetric
+    torch.manual_seed(3)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    x = torch.randn(300, 3, 32, 32, device=cuda)
+    y = torch.randint(0, 10, (300,), device=cuda)
+    monkeypatch.setenv("TORCHPRUNER_COALESCE", "0")
+    with TUNER.fixed():
+        ref = cls(model, _loader(x, y, [150, 150]), F.cross_entropy, cuda).run_many(convs, True)
+        monkeypatch.setattr(FusedChainEngine, "max_batch", lambda self, hw: 64)
+        got = cls(model, _loader(x, y, [150, 150]), F.cross_entropy, cuda).run_many(convs, True)
+    for k, (a, b) in enumerate(zip(got, ref)):
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-5 * np.abs(b).max(), err_msg=str(k))

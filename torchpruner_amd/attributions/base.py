@@ -445,11 +445,24 @@ class _AttributionMetric(ABC):
             return 1
         return max(1, self.COALESCE_PIXELS // max(1, x.shape[0] * math.prod(x.shape[2:])))
 
-    def _coalesced_batches(self, on: bool):
+    def _coalesced_batches(self, on: bool, max_batch=None):
         """``(global_batch_index, x, y, loss_batch)`` over this rank's batches; with ``on``, runs of
         k equal-shape batches come concatenated (``loss_batch`` = the loader batch size, the
-        group's first index), leftovers and odd shapes alone (``loss_batch`` None)."""
+        group's first index), leftovers and odd shapes alone (``loss_batch`` None).
+        ``max_batch(x) -> int``: a batch larger than that is run in slices (every slice with the
+        whole batch's loss scaling): the kernels' buffer descriptors address < 2^31 bytes."""
         self.last_coalesce = 1
+        for i, x, y, lb in self._coalesced_groups(on):
+            mb = max_batch(x) if max_batch is not None else x.shape[0]
+            if x.shape[0] <= mb:
+                yield i, x, y, lb
+                continue
+            n = -(-x.shape[0] // mb)
+            step = -(-x.shape[0] // n)  # equal slices (one shape to tune, no 1-image tail)
+            for s in range(0, x.shape[0], step):
+                yield i, x[s:s + step], y[s:s + step], lb or x.shape[0]
+
+    def _coalesced_groups(self, on: bool):
         if not on:
             for i, x, y in self._batches():
                 yield i, x, y, None
@@ -520,12 +533,13 @@ class _AttributionMetric(ABC):
                 for b in uniq:
                     accs[owner[b]].count += B
             else:
-                res = engine.taylor(x, y, set(uniq), mode=mode, criterion=crit)
+                res = engine.taylor(x, y, set(uniq), mode=mode, criterion=crit, loss_batch=loss_batch)
                 ops.score_fold_([res[b] for b in uniq], [None] * len(uniq), take_abs, 1)
                 for b in uniq:
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
 
-        for i, x, y, lb in self._coalesced_batches(pipe is not None):
+        big = (lambda x: engine.max_batch(tuple(x.shape[2:]))) if crit is None else None
+        for i, x, y, lb in self._coalesced_batches(pipe is not None, big):
             run_batch(i, x, y, lb)
         if pipe is not None:
             pipe.join()

@@ -53,7 +53,8 @@ class APoZAttributionMetric(_AttributionMetric):
         pipe = _BatchPipeline(engine, graph_replay=True) if stats and self._ckpt is None else None
         with torch.no_grad():
             # small batches coalesced into one launch (per-sample counts: no loss involved)
-            for i, x, _y, _lb in self._coalesced_batches(pipe is not None):
+            for i, x, _y, _lb in self._coalesced_batches(pipe is not None,
+                                                         lambda x: engine.max_batch(tuple(x.shape[2:]))):
                 B = x.shape[0]
 
                 def launch(slot, x=x):

@@ -794,6 +794,19 @@ class FusedChainEngine:
                 return H, W
         return 1, 1
 
+    def max_batch(self, hw) -> int:
+        """Largest batch whose activations stay inside the kernels' 32-bit buffer descriptors
+        (every tensor < 2^31 bytes): larger batches are run in slices (attributions/base.py)."""
+        H, W = hw
+        per = 4 * H * W * max(8, self.plan.convs[0].conv.in_channels) if self.plan.convs else 1
+        for blk in self.plan.convs:
+            per = max(per, 4 * H * W * blk.width)  # the conv output, before its pooling
+            if blk.pool is not None:
+                H, W = H // 2, W // 2
+        for blk in self.plan.linears:
+            per = max(per, 4 * blk.width)
+        return max(1, ((1 << 31) - 1) // per)
+
     def _arena_shapes(self, B, want, H0, W0):
         shapes = {}
         nconv = len(self.plan.convs)
