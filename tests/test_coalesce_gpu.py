@@ -68,3 +68,28 @@ def test_oversized_batch_runs_in_slices(cuda, monkeypatch, metric):
         got = cls(model, _loader(x, y, [150, 150]), F.cross_entropy, cuda).run_many(convs, True)
     for k, (a, b) in enumerate(zip(got, ref)):
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-5 * np.abs(b).max(), err_msg=str(k))
+
+
+@pytest.mark.parametrize("metric", ["taylor", "apoz"])
+def test_resnet_oversized_batch_runs_in_slices(cuda, monkeypatch, metric):
+    """The ResNet engine passes slice batches past ResNetEngine.max_batch the same way."""
+    from torchpruner_amd import APoZAttributionMetric, TaylorAttributionMetric, get_resnet_pruning_graph
+    from torchpruner_amd.engine.fused_chain import TUNER
+    from torchpruner_amd.engine.resnet_engine import ResNetEngine
+    from torchpruner_amd.models import resnet50
+    cls = TaylorAttributionMetric if metric == "taylor" else APoZAttributionMetric
+    torch.manual_seed(4)
+    model = resnet50(num_classes=10).to(cuda).eval().to(memory_format=torch.channels_last)
+    mods = [m for m, _ in get_resnet_pruning_graph(model)]
+    x = torch.randn(40, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (40,), device=cuda)
+    with TUNER.fixed():
+        m0 = cls(model, _loader(x, y, [20, 20]), F.cross_entropy, cuda)
+        ref = m0.run_many(mods, True)
+        assert m0.last_path["path"] == "resnet", m0.last_path
+        monkeypatch.setattr(ResNetEngine, "max_batch", lambda self, hw: 7)
+        m1 = cls(model, _loader(x, y, [20, 20]), F.cross_entropy, cuda)
+        got = m1.run_many(mods, True)
+        assert m1.last_path["path"] == "resnet", m1.last_path
+    for k, (a, b) in enumerate(zip(got, ref)):
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-5 * np.abs(b).max(), err_msg=str(k))

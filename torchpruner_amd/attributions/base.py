@@ -606,21 +606,23 @@ class _AttributionMetric(ABC):
         stats = accs[0].mode == "stats"
         crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
         pipe = _BatchPipeline(eng) if stats and self._ckpt is None and crit is None else None
+        # batches past the kernels' descriptor range run in slices (whole-batch loss scaling)
+        big = (lambda x: eng.max_batch(tuple(x.shape[2:]))) if crit is None else None
         with torch.no_grad():
-            for i, x, y in self._batches():
+            for i, x, y, lb in self._coalesced_batches(False, big):
                 def fold(res, dev=x.device):
                     slabs = [res[m] for m in uniq]
                     sums = [accs[first[m]].ensure_sum(res[m].shape[1], dev, m.num_features) for m in uniq]
                     for j in range(0, len(slabs), 16):
                         ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], False, 0)
 
-                if pipe is not None and pipe.take(x, y, lambda slot, x=x, y=y: eng.grad_scores(x, y, set(uniq), mode),
-                                                  fold):
+                if pipe is not None and pipe.take(x, y, lambda slot, x=x, y=y, lb=lb: eng.grad_scores(
+                        x, y, set(uniq), mode, loss_batch=lb), fold):
                     for m in uniq:
                         accs[first[m]].count += x.shape[0]
                     continue
                 with trace_range("tp.forward_backward"):
-                    res = eng.grad_scores(x, y, set(uniq), mode, crit)
+                    res = eng.grad_scores(x, y, set(uniq), mode, crit, loss_batch=lb)
                 if stats:
                     slabs = [res[m] for m in uniq]
                     sums = [accs[first[m]].ensure_sum(res[m].shape[1], x.device, m.num_features) for m in uniq]

@@ -101,7 +101,8 @@ class APoZAttributionMetric(_AttributionMetric):
             return bufs
 
         with torch.no_grad():
-            for i, x, _y in self._batches():
+            # batches past the kernels' descriptor range run in slices
+            for i, x, _y, _lb in self._coalesced_batches(False, lambda x: eng.max_batch(tuple(x.shape[2:]))):
                 B = x.shape[0]
 
                 def launch(slot, x=x):

@@ -107,6 +107,30 @@ class ResNetEngine:
         self._key = None
         self._packed = None
 
+    def max_batch(self, hw) -> int:
+        """Largest batch whose activations stay inside the kernels' 32-bit buffer descriptors
+        (every tensor < 2^31 bytes); attributions/base.py runs larger batches in slices."""
+        def out_hw(conv, H, W):
+            k, s_, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            return (H + 2 * pd - k) // s_ + 1, (W + 2 * pd - k) // s_ + 1
+
+        H, W = hw
+        per = 4 * H * W * 8  # the channel-padded NHWC input
+        H, W = out_hw(self.plan.stem.conv, H, W)
+        per = max(per, 4 * H * W * cpad(self.plan.stem.conv.out_channels))
+        mp = self.plan.maxpool
+        k, s_, pd = (mp.kernel_size if isinstance(mp.kernel_size, int) else mp.kernel_size[0],
+                     mp.stride if isinstance(mp.stride, int) else mp.stride[0],
+                     mp.padding if isinstance(mp.padding, int) else mp.padding[0])
+        H, W = (H + 2 * pd - k) // s_ + 1, (W + 2 * pd - k) // s_ + 1
+        for b in self.plan.blocks:
+            h, w = H, W
+            for c in b.convs:
+                h, w = out_hw(c.conv, h, w)
+                per = max(per, 4 * h * w * cpad(c.conv.out_channels))
+            H, W = h, w
+        return max(1, ((1 << 31) - 1) // per)
+
     def _all_convs(self):
         p = self.plan
         out = [p.stem]
@@ -375,7 +399,8 @@ class ResNetEngine:
             return run(cfg, sp, tay=tay), tay
         return run(cfg, sp), None
 
-    def grad_scores(self, x: torch.Tensor, y: torch.Tensor, want, mode: str, criterion=None):
+    def grad_scores(self, x: torch.Tensor, y: torch.Tensor, want, mode: str, criterion=None,
+                    loss_batch: Optional[int] = None):
         """One engine forward + input-gradient-only backward of the loss (mean cross-entropy on
         the fused kernel, or ``criterion`` through autograd on the logits); returns
         {BN module: (B, C_padded) per-sample ``ops.channel_reduce`` score} for the block BNs in
@@ -386,7 +411,7 @@ class ResNetEngine:
         logits, saved = self.forward(x, save=True)
         feat = saved.pop()
         B = logits.shape[0]
-        g_log = logits_grad(logits, y, criterion)
+        g_log = logits_grad(logits, y, criterion, loss_batch)
         g_feat = self._fc_bwd(T, P, g_log, feat)  # (B, C_last padded)
         y_last = saved[-1][2]
         HW = y_last.shape[1] * y_last.shape[2]
