@@ -1,4 +1,4 @@
-"""Coalesced small loader batches on the fused engine (attributions/base.py COALESCE_PIXELS): k
+"""Coalesced small loader batches on the fused engine (attributions/base.py COALESCE_ELEMS): k
 consecutive equal-shape batches run as one engine launch with each loader batch's 1/B loss
 scaling, so the Taylor / Sensitivity / APoZ scores equal the batch-by-batch ones (up to the
 rounding of different kernel choices); leftover and odd-shaped batches run alone."""
@@ -64,7 +64,7 @@ def test_oversized_batch_runs_in_slices(cuda, monkeypatch, metric):
     monkeypatch.setenv("TORCHPRUNER_COALESCE", "0")
     with TUNER.fixed():
         ref = cls(model, _loader(x, y, [150, 150]), F.cross_entropy, cuda).run_many(convs, True)
-        monkeypatch.setattr(FusedChainEngine, "max_batch", lambda self, hw: 64)
+        monkeypatch.setattr(FusedChainEngine, "max_batch", lambda self, shape: 64)
         got = cls(model, _loader(x, y, [150, 150]), F.cross_entropy, cuda).run_many(convs, True)
     for k, (a, b) in enumerate(zip(got, ref)):
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-5 * np.abs(b).max(), err_msg=str(k))
@@ -87,7 +87,7 @@ def test_resnet_oversized_batch_runs_in_slices(cuda, monkeypatch, metric):
         m0 = cls(model, _loader(x, y, [20, 20]), F.cross_entropy, cuda)
         ref = m0.run_many(mods, True)
         assert m0.last_path["path"] == "resnet", m0.last_path
-        monkeypatch.setattr(ResNetEngine, "max_batch", lambda self, hw: 7)
+        monkeypatch.setattr(ResNetEngine, "max_batch", lambda self, shape: 7)
         m1 = cls(model, _loader(x, y, [20, 20]), F.cross_entropy, cuda)
         got = m1.run_many(mods, True)
         assert m1.last_path["path"] == "resnet", m1.last_path

@@ -432,18 +432,18 @@ class _AttributionMetric(ABC):
                 h.remove()
             self.restore_deterministic()
 
-    # Small loader batches on the fused engine are coalesced: COALESCE_PIXELS input pixels per
-    # engine launch (B=100 at 32x32 -> 5 loader batches = 500 images per launch). In eval mode every
+    # Small loader batches on the fused engine are coalesced: ~COALESCE_ELEMS input elements per
+    # engine launch (B=100 at 3x32x32 -> 5 loader batches = 500 images per launch). In eval mode every
     # sample's forward / backward is independent of the others in its batch and the fused
     # cross-entropy keeps each loader batch's 1/B loss scaling, so every per-sample score is the one
     # its own batch gives (up to kernel-choice rounding); scores are folded per sample, |.| included.
     # TORCHPRUNER_COALESCE=0 turns it off.
-    COALESCE_PIXELS = 1 << 19
+    COALESCE_ELEMS = 3 << 19
 
     def _coalesce_factor(self, x) -> int:
         if os.environ.get("TORCHPRUNER_COALESCE", "1") == "0" or not x.is_cuda:
             return 1
-        return max(1, self.COALESCE_PIXELS // max(1, x.shape[0] * math.prod(x.shape[2:])))
+        return max(1, self.COALESCE_ELEMS // max(1, x.shape[0] * math.prod(x.shape[1:])))
 
     def _coalesced_batches(self, on: bool, max_batch=None):
         """``(global_batch_index, x, y, loss_batch)`` over this rank's batches; with ``on``, runs of
@@ -491,7 +491,7 @@ class _AttributionMetric(ABC):
         """Gradient metrics on the fused VGG-chain engine: per batch ONE fused forward +
         input-gradient backward writes every block's per-sample partials (``mode`` taylor /
         sensitivity), and ONE fold launch turns all layers' sums into fp64 accumulators. Small
-        batches are coalesced (see COALESCE_PIXELS) and pipelined over HIP streams."""
+        batches are coalesced (see COALESCE_ELEMS) and pipelined over HIP streams."""
         from ..engine.fused_chain import engine_criterion
         owner = {}
         for k, b in enumerate(blocks):
@@ -538,7 +538,7 @@ class _AttributionMetric(ABC):
                 for b in uniq:
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
 
-        big = (lambda x: engine.max_batch(tuple(x.shape[2:]))) if crit is None else None
+        big = (lambda x: engine.max_batch(tuple(x.shape[1:]))) if crit is None else None
         for i, x, y, lb in self._coalesced_batches(pipe is not None, big):
             run_batch(i, x, y, lb)
         if pipe is not None:
@@ -607,7 +607,7 @@ class _AttributionMetric(ABC):
         crit = engine_criterion(self.criterion, self.device)  # None: the fused cross-entropy kernel
         pipe = _BatchPipeline(eng) if stats and self._ckpt is None and crit is None else None
         # batches past the kernels' descriptor range run in slices (whole-batch loss scaling)
-        big = (lambda x: eng.max_batch(tuple(x.shape[2:]))) if crit is None else None
+        big = (lambda x: eng.max_batch(tuple(x.shape[1:]))) if crit is None else None
         with torch.no_grad():
             for i, x, y, lb in self._coalesced_batches(False, big):
                 def fold(res, dev=x.device):

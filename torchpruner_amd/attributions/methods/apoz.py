@@ -54,7 +54,7 @@ class APoZAttributionMetric(_AttributionMetric):
         with torch.no_grad():
             # small batches coalesced into one launch (per-sample counts: no loss involved)
             for i, x, _y, _lb in self._coalesced_batches(pipe is not None,
-                                                         lambda x: engine.max_batch(tuple(x.shape[2:]))):
+                                                         lambda x: engine.max_batch(tuple(x.shape[1:]))):
                 B = x.shape[0]
 
                 def launch(slot, x=x):
@@ -102,7 +102,7 @@ class APoZAttributionMetric(_AttributionMetric):
 
         with torch.no_grad():
             # batches past the kernels' descriptor range run in slices
-            for i, x, _y, _lb in self._coalesced_batches(False, lambda x: eng.max_batch(tuple(x.shape[2:]))):
+            for i, x, _y, _lb in self._coalesced_batches(False, lambda x: eng.max_batch(tuple(x.shape[1:]))):
                 B = x.shape[0]
 
                 def launch(slot, x=x):

@@ -794,15 +794,18 @@ class FusedChainEngine:
                 return H, W
         return 1, 1
 
-    def max_batch(self, hw) -> int:
+    def max_batch(self, sample_shape) -> int:
         """Largest batch whose activations stay inside the kernels' 32-bit buffer descriptors
-        (every tensor < 2^31 bytes): larger batches are run in slices (attributions/base.py)."""
-        H, W = hw
-        per = 4 * H * W * max(8, self.plan.convs[0].conv.in_channels) if self.plan.convs else 1
-        for blk in self.plan.convs:
-            per = max(per, 4 * H * W * blk.width)  # the conv output, before its pooling
-            if blk.pool is not None:
-                H, W = H // 2, W // 2
+        (every tensor < 2^31 bytes) for inputs of per-sample shape ``sample_shape`` ((C, H, W)
+        images or flat features); larger batches are run in slices (attributions/base.py)."""
+        shape = tuple(sample_shape)
+        per = 4 * 8 * max(1, math.prod(shape))  # the (channel-padded) input
+        if self.plan.convs and len(shape) == 3:
+            H, W = shape[1], shape[2]
+            for blk in self.plan.convs:
+                per = max(per, 4 * H * W * blk.width)  # the conv output, before its pooling
+                if blk.pool is not None:
+                    H, W = H // 2, W // 2
         for blk in self.plan.linears:
             per = max(per, 4 * blk.width)
         return max(1, ((1 << 31) - 1) // per)

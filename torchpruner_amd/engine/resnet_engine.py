@@ -107,14 +107,15 @@ class ResNetEngine:
         self._key = None
         self._packed = None
 
-    def max_batch(self, hw) -> int:
+    def max_batch(self, sample_shape) -> int:
         """Largest batch whose activations stay inside the kernels' 32-bit buffer descriptors
-        (every tensor < 2^31 bytes); attributions/base.py runs larger batches in slices."""
+        (every tensor < 2^31 bytes) for (C, H, W) inputs; attributions/base.py runs larger
+        batches in slices."""
         def out_hw(conv, H, W):
             k, s_, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
             return (H + 2 * pd - k) // s_ + 1, (W + 2 * pd - k) // s_ + 1
 
-        H, W = hw
+        H, W = tuple(sample_shape)[-2:]
         per = 4 * H * W * 8  # the channel-padded NHWC input
         H, W = out_hw(self.plan.stem.conv, H, W)
         per = max(per, 4 * H * W * cpad(self.plan.stem.conv.out_channels))
