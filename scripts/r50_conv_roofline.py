@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--ws", action="store_true", help="add the warp-specialised 1x1 GEMM cfgs (16-18)")
     ap.add_argument("--verbose", action="store_true", help="print every candidate's time")
+    ap.add_argument("--hw", type=int, default=None, help="only the convs on this input size")
     args = ap.parse_args()
     T = ops.require()
     dev = torch.device("cuda")
@@ -58,6 +59,8 @@ def main():
     print(f"{'cin':>5} {'cout':>5} {'k':>2} {'s':>2} {'hw':>4} {'n':>2} {'best':>24} {'us':>8} {'TF/s':>6} "
           f"{'TB/s':>6} {'roof%':>6}")
     for (cin, cout, ks, s, pad, H, W), n in conv_shapes(B).items():
+        if args.hw is not None and H != args.hw:
+            continue
         cin_p = 4 if (ks == 7 and cin <= 4) else cpad(cin)
         x = torch.randn(B, H, W, cin_p, device=dev)
         w = torch.randn(cout, cin_p, ks, ks, device=dev) * 0.05
@@ -71,11 +74,11 @@ def main():
         cands = [(c, sp) for c, sp in TUNER.candidates(M, cout, kk)]
         if args.ws and ks == 1:
             cands += [(16, 1), (17, 1), (18, 1)]
-        wino = ks == 3 and s == 1 and H % 2 == 0 and W % 2 == 0
+        wino = ks == 3 and s == 1  # odd H / W: partial last tile row / column (as the engine)
         if wino:
-            sp0 = _wino_splits(B * (H // 2) * (W // 2), cout, cin_p)
+            sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cout, cin_p)
             u = T.wino_weights(w, False)
-            cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
+            cands = [(k, sp) for sp in sorted({1, 2, 4, sp0}) for k in (WINO_LDS, WINO)] + cands
         results = []
         for cfg, sp in cands:
             def run():
