@@ -437,12 +437,15 @@ class _AttributionMetric(ABC):
     # sample's forward / backward is independent of the others in its batch and the fused
     # cross-entropy keeps each loader batch's 1/B loss scaling, so every per-sample score is the one
     # its own batch gives (up to kernel-choice rounding); scores are folded per sample, |.| included.
-    # TORCHPRUNER_COALESCE=0 turns it off.
+    # TORCHPRUNER_COALESCE=0 turns it off; =k (k >= 2) coalesces k loader batches per launch.
     COALESCE_ELEMS = 3 << 19
 
     def _coalesce_factor(self, x) -> int:
-        if os.environ.get("TORCHPRUNER_COALESCE", "1") == "0" or not x.is_cuda:
+        env = os.environ.get("TORCHPRUNER_COALESCE", "1")
+        if env == "0" or not x.is_cuda:
             return 1
+        if env.isdigit() and int(env) >= 2:
+            return int(env)
         return max(1, self.COALESCE_ELEMS // max(1, x.shape[0] * math.prod(x.shape[1:])))
 
     def _coalesced_batches(self, on: bool, max_batch=None):
