@@ -38,3 +38,14 @@ def test_shape_change_mid_group_flushes_in_order():
     m = _metric([4, 4, 6, 6, 6], k=3)
     out = list(m._coalesced_batches(True))
     assert [(i, x.shape[0], lb) for i, x, _, lb in out] == [(0, 4, None), (1, 4, None), (2, 18, 6)]
+
+
+def test_factor_from_env(monkeypatch):
+    class _X:  # stands for a CUDA batch (the factor is 1 for CPU tensors)
+        is_cuda, shape = True, (100, 3, 32, 32)
+
+    m = _metric([4], k=1)
+    del m._coalesce_factor  # the method, not the instance override
+    for env, want in (("0", 1), ("1", (3 << 19) // (100 * 3 * 32 * 32)), ("7", 7)):
+        monkeypatch.setenv("TORCHPRUNER_COALESCE", env)
+        assert m._coalesce_factor(_X()) == want, env
