@@ -10,5 +10,5 @@ tail -1 gpurun_out/smoke.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 --baseline > gpurun_out/bench_full.log 2>&1 || { tail -30 gpurun_out/bench_full.log; exit 1; }
 grep "\[bench\]" gpurun_out/bench_full.log; tail -1 gpurun_out/bench_full.log
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_bench -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-prune --train-steps 0 > $R/gpurun_out/prof_bench.log 2>&1 || { tail -30 $R/gpurun_out/prof_bench.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_bench -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-prune --teacher-steps 0 > $R/gpurun_out/prof_bench.log 2>&1 || { tail -30 $R/gpurun_out/prof_bench.log; exit 1; }
 echo done
