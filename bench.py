@@ -187,12 +187,16 @@ def run(args) -> int:
             dt = pdist.all_max_float(dt)
         return scores, dt
 
+    from torchpruner_amd.engine.fused_chain import TUNER, tuner_choices
+    phase = {}  # wall seconds per phase (rank 0's clock): an over-budget run can be attributed
+    t_run = time.perf_counter()
     cfg = dict(pq.DEFAULTS)
     if args.teacher_steps is not None:
         cfg["teacher_steps"] = args.teacher_steps
     t0 = time.perf_counter()
     model, task = pq.make_teacher(args.seed, dev, cfg)  # deterministic: identical on every rank ...
     sync = pdist.sync_module(model)  # ... checked (digests all-gathered) and made so (rank 0 broadcast)
+    phase["teacher"] = time.perf_counter() - t0
     log(f"[bench] teacher: {cfg['teacher_steps']} SGD steps in {time.perf_counter() - t0:.1f}s (untimed); "
         f"ranks agreed before broadcast: {sync['agreed_before']}")
     convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
@@ -202,12 +206,15 @@ def run(args) -> int:
         return ShardLoader.build(lambda i: task.sample(bs, seed * 1_000_003 + i), max(n_steps, 1) * world, bs,
                                  rank, world)
 
+    t0 = time.perf_counter()
     warm = TaylorAttributionMetric(model, loader(args.warmup, args.seed + 1), F.cross_entropy, dev)
     metric = TaylorAttributionMetric(model, loader(args.steps, args.seed + 2), F.cross_entropy, dev)
     timed_run(warm, convs)  # warmup (untimed): W steps + the collective
     scores, dt = timed_run(metric, convs)
     assert metric.last_path["path"] == "fused", metric.last_path
     del warm, metric
+    phase["headline"] = time.perf_counter() - t0
+    head_choices = tuner_choices()
     value = args.steps * B * world / dt
     log(f"[bench] {world} GPU(s) x {args.steps} steps x B={B}: {dt * 1e3:.1f} ms -> {value:.0f} img/s "
         f"(fused path, backend {backend_seen}, world {world_seen})")
@@ -241,10 +248,14 @@ def run(args) -> int:
         "launcher": "torchrun/external" if os.environ.get("TORCHELASTIC_RUN_ID") else
                     ("bench.py --gpus (self-spawned ranks)" if world > 1 else "single process"),
         "teacher_sync": {"agreed_before_broadcast": sync["agreed_before"], "digest": sync["digest"]},
+        "tuner_choices": {"headline": head_choices},
+        "phase_wall_s": phase,
     }
 
     if not args.no_extras:
-        result.update(extras(args, model, task, convs, dev, world, rank, timed_run, log, value))
+        result.update(extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase))
+        if "b100_tuner_choices" in result:
+            result["tuner_choices"]["b100"] = result.pop("b100_tuner_choices")
 
     if world > 1:  # everything below is single-rank: no rank may wait in a collective meanwhile
         pdist.barrier()
@@ -256,6 +267,7 @@ def run(args) -> int:
         from torchpruner_amd.bench.reference_semantics import reference_taylor_all
         from torchpruner_amd.data import DeviceLoader
         nb = args.baseline_batches
+        t_eager = time.perf_counter()
         xb, yb = task.sample(nb * B, args.seed + 5)
         try:
             with _env(TORCHPRUNER_BACKEND="torch"):
@@ -273,16 +285,21 @@ def run(args) -> int:
         result["vs_baseline"] = round((value / world) / eager, 2)
         result["vs_baseline_definition"] = ("per-GPU img/s / reference-semantics eager img/s on the same GPU "
                                             "(BASELINE.md: the reference publishes no number for this metric)")
+        phase["eager_reference"] = time.perf_counter() - t_eager
         log(f"[bench] reference-semantics eager: {eager:.0f} img/s per GPU -> vs_baseline {result['vs_baseline']}")
 
     if not args.no_prune:
+        t0 = time.perf_counter()
         result.update(accuracy(args, model, task, convs, scores, cfg, dev, log))
+        phase["accuracy"] = time.perf_counter() - t0
+    phase["total"] = time.perf_counter() - t_run
+    result["phase_wall_s"] = {k: round(v, 1) for k, v in phase.items()}
 
     print(json.dumps(result), flush=True)
     return 0
 
 
-def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
+def extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase):
     """Same-algorithm library baseline + BASELINE configs #3 / #4 / #5 (all ranks, sharded)."""
     from torchpruner_amd.data import ShardLoader
 
@@ -292,17 +309,22 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
     def loader(n, seed, bs):
         return ShardLoader.build(lambda i: task.sample(bs, seed * 1_000_003 + i), n * world, bs, rank, world)
 
+    def timed_phase(name, fn, *a):
+        t0 = time.perf_counter()
+        out.update(fn(*a))
+        phase[name] = time.perf_counter() - t0
+
     # 1. the same one-pass run_many on the generic module/hook path, MIOpen/hipBLASLt convolutions
     if "generic" in want:
-        out.update(_generic(args, model, convs, dev, world, timed_run, log, value, loader))
+        timed_phase("generic", _generic, args, model, convs, dev, world, timed_run, log, value, loader)
     if "bf16" in want:
-        out.update(_bf16(args, model, convs, dev, world, timed_run, log, value, loader))
+        timed_phase("bf16", _bf16, args, model, convs, dev, world, timed_run, log, value, loader)
     if "b100" in want:
-        out.update(_b100(args, model, convs, dev, world, timed_run, log, loader))
+        timed_phase("b100", _b100, args, model, task, convs, dev, world, rank, timed_run, log, loader)
     if "resnet" in want:
-        out.update(_resnet(args, dev, world, timed_run, log))
+        timed_phase("resnet", _resnet, args, dev, world, timed_run, log)
     if "shapley" in want:
-        out.update(_shapley(args, model, task, convs, dev, world, log))
+        timed_phase("shapley", _shapley, args, model, task, convs, dev, world, log)
     if "finetune" in want or "quality5" in want:
         from torchpruner_amd.bench import resnet_finetune as rf
         if "finetune" in want:
@@ -310,6 +332,7 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
             r = rf.finetune_throughput(dev, world, rank, steps=args.finetune_steps, batch=args.finetune_batch,
                                        res=args.finetune_res, seed=args.seed)
             out.update(r)
+            phase["finetune"] = time.perf_counter() - t0
             log(f"[bench] config #5 ResNet-50 finetune step after a 20% prune + DDP rewrap, B={args.finetune_batch}: "
                 f"{r['resnet50_finetune_img_s']:.0f} img/s (dense {r['resnet50_train_dense_img_s']:.0f}) "
                 f"({time.perf_counter() - t0:.1f}s)")
@@ -318,6 +341,7 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value):
             q = rf.prune_finetune_quality(dev, world, rank, seed=args.seed,
                                           cfg={"res": args.q5_res, "teacher_max_steps": args.q5_max_steps})
             out["resnet50_prune_finetune"] = q
+            phase["quality5"] = time.perf_counter() - t0
             log(f"[bench] config #5 one prune->finetune round (20%): teacher {q['teacher_top1']:.3f}; after prune "
                 f"Taylor {q['taylor_after_prune']:.3f} / Random {q['random_after_prune']:.3f}; after finetune Taylor "
                 f"{q['taylor_after_finetune']:.3f} / Random {q['random_after_finetune']:.3f} "
@@ -377,18 +401,22 @@ def _bf16(args, model, convs, dev, world, timed_run, log, value, loader):
     return out
 
 
-def _b100(args, model, convs, dev, world, timed_run, log, loader):
+def _b100(args, model, task, convs, dev, world, rank, timed_run, log, loader):
+    import torch
     import torch.nn.functional as F
 
     from torchpruner_amd import TaylorAttributionMetric
+    from torchpruner_amd.engine.fused_chain import TUNER, tuner_choices
     out = {}
     # 1c. the same fp32 Taylor run_many at the reference's attribution batch B=100 (nbVGG:193-196):
     # the engine coalesces 5 consecutive loader batches into one 500-image launch (each batch's
     # 1/B loss scaling kept: the same per-sample scores), pipelined over HIP streams with
-    # per-slot HIP-graph replay; also measured with one engine launch per loader batch
+    # per-slot HIP-graph replay; also measured with one engine launch per loader batch, and fed
+    # by the reference's own loader shape (host tensors, torch DataLoader, 1 worker, pinned memory)
     t0 = time.perf_counter()
     sb, s_steps = 100, 200
     res = {}
+    before = set(TUNER.cache)
     for coalesce in ("1", "0"):
         os.environ["TORCHPRUNER_COALESCE"] = coalesce
         try:
@@ -400,14 +428,38 @@ def _b100(args, model, convs, dev, world, timed_run, log, loader):
             os.environ.pop("TORCHPRUNER_COALESCE", None)
         assert sm.last_path["path"] == "fused", sm.last_path
         res[coalesce] = (round(s_steps * sb * world / sdt, 1), sm.last_coalesce)
+    out["b100_tuner_choices"] = tuner_choices({k: v for k, v in TUNER.cache.items() if k not in before})
+    # host loader: this rank's 200 batches as host tensors behind a reference-style DataLoader
+    # (experiments/models/cifar10.py:136-161: num_workers=1, pin_memory=True); run_many pins and
+    # copies each batch one ahead on a side HIP stream (data/prefetch.py) — H2D time included
+    xs, ys = [], []
+    for i in range(rank, s_steps * world, world):
+        x, y = task.sample(sb, (args.seed + 17) * 1_000_003 + i)
+        xs.append(x.cpu())
+        ys.append(y.cpu())
+    ds = torch.utils.data.TensorDataset(torch.cat(xs), torch.cat(ys))
+    del xs, ys
+    hl = torch.utils.data.DataLoader(ds, batch_size=sb, shuffle=False, num_workers=1, pin_memory=True)
+    TaylorAttributionMetric(model, torch.utils.data.DataLoader(torch.utils.data.Subset(ds, range(20 * sb)),
+                                                               batch_size=sb, num_workers=1, pin_memory=True),
+                            F.cross_entropy, dev).run_many(convs, find_best_evaluation_module=True)  # warm
+    hm = TaylorAttributionMetric(model, hl, F.cross_entropy, dev)
+    _, hdt = timed_run(hm, convs)
+    assert hm.last_path["path"] == "fused", hm.last_path
     out["vgg_taylor_b100_img_s"] = res["1"][0]
     out["vgg_taylor_b100_one_launch_per_batch_img_s"] = res["0"][0]
+    out["vgg_taylor_b100_host_loader_img_s"] = round(s_steps * sb * world / hdt, 1)
     out["b100_config"] = {"per_gpu_batch": sb, "steps": s_steps, "dtype": "fp32",
                           "coalesced_loader_batches_per_launch": res["1"][1],
                           "pipeline": "coalesced launches in flight on HIP streams, per-slot HIP-graph replay "
-                                      "(one launch per loader batch: 4 in flight)"}
+                                      "(one launch per loader batch: 4 in flight)",
+                          "host_loader": "torch DataLoader(TensorDataset of host fp32 tensors, batch_size=100, "
+                                         "num_workers=1, pin_memory=True) as experiments/models/cifar10.py:136-161; "
+                                         "run_many prefetches one batch ahead on a side stream (data/prefetch.py); "
+                                         f"coalescing {hm.last_coalesce}"}
     log(f"[bench] B=100 (reference attribution batch): {out['vgg_taylor_b100_img_s']:.0f} img/s with "
-        f"{res['1'][1]} loader batches per launch, {res['0'][0]:.0f} img/s one launch per batch "
+        f"{res['1'][1]} loader batches per launch, {res['0'][0]:.0f} img/s one launch per batch, "
+        f"{out['vgg_taylor_b100_host_loader_img_s']:.0f} img/s from a host DataLoader "
         f"({time.perf_counter() - t0:.1f}s)")
     return out
 

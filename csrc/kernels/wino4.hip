@@ -184,17 +184,98 @@ __device__ __forceinline__ void output_transform(const float (&m)[36], float (&y
         y[4 * r + 2], y[4 * r + 3]);
 }
 
+// Split-points epilogue, phase 1 (32-tile blocks of 4 waves): wave (grp = wave & 1, ph = wave >> 1)
+// holds rows 3ph..3ph+2 of the 6x6 transform-point grid (acc[nh * 18 + 6 rr + c]) for its 16
+// tiles x both 16-channel halves. Y = A^T M A is linear in M, so each wave forms the partial
+// output of its three rows; the ph = 0 waves write it into ya / yb, the ph = 1 waves add theirs
+// (fixed order: one add per output, deterministic). Partial column passes:
+//   ph 0 (rows 0-2): t0 = m0 + m1 + m2, t1 = t3 = m1 - m2, t2 = m1 + m2
+//   ph 1 (rows 3-5): t0 = s, t1 = 2d, t2 = 4s, t3 = 8d + m5   (s = m3 + m4, d = m3 - m4)
+// and for ph 1 the row pass runs on s, d, m5 once each (at6 is linear), the scalings folding
+// into the adds.
+__device__ __forceinline__ void at6row(const f2v* t, f2v& y0, f2v& y1, f2v& y2, f2v& y3) {
+  at6p(t[0], t[1], t[2], t[3], t[4], t[5], y0, y1, y2, y3);
+}
+
+// one wave's partial output (its three point rows) for tiles r, r + 1 of the lane: written
+// (ph 0) or added (ph 1) into the parked tile image
+template <int PH>
+__device__ __forceinline__ void sp_partial(const f32x4 (&acc)[NPT], int grp, int lane, float* ya, float* yb) {
+  const int j = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh) {
+    float* ybuf = nh ? yb : ya;
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {  // tiles r, r + 1 of this lane: packed pairs
+      const int tl = grp * 16 + 4 * g + r;
+      f2v m[18];
+#pragma unroll
+      for (int x = 0; x < 18; ++x) m[x] = f2v{acc[nh * 18 + x][r], acc[nh * 18 + x][r + 1]};
+      float* dst = ybuf + tl * TPL + j;
+      if constexpr (PH == 0) {
+        f2v t0[6], t1[6], t2[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const f2v a = m[6 + c] + m[12 + c];
+          t1[c] = m[6 + c] - m[12 + c];
+          t2[c] = a;
+          t0[c] = m[c] + a;
+        }
+        f2v y[12];
+        at6row(t0, y[0], y[1], y[2], y[3]);
+        at6row(t1, y[4], y[5], y[6], y[7]);
+        at6row(t2, y[8], y[9], y[10], y[11]);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const f2v v = y[q < 12 ? q : q - 8];  // output row 3 = row 1
+          dst[q * 16] = v.x;
+          dst[TPL + q * 16] = v.y;
+        }
+      } else {
+        f2v s[6], d[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          s[c] = m[c] + m[6 + c];
+          d[c] = m[c] - m[6 + c];
+        }
+        f2v ys[4], yd[4], y5[4];
+        at6row(s, ys[0], ys[1], ys[2], ys[3]);
+        at6row(d, yd[0], yd[1], yd[2], yd[3]);
+        at6row(m + 12, y5[0], y5[1], y5[2], y5[3]);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int row = q >> 2, col = q & 3;
+          f2v add;
+          if (row == 0) add = ys[col];
+          else if (row == 1) add = 2.f * yd[col];
+          else if (row == 2) add = 4.f * ys[col];
+          else add = 8.f * yd[col] + y5[col];
+          dst[q * 16] += add.x;
+          dst[TPL + q * 16] += add.y;
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void sp_phase1(const f32x4 (&acc)[NPT], int ph, int grp, int lane, float* ya, float* yb) {
+  if (ph == 0) sp_partial<0>(acc, grp, lane, ya, yb);
+  __syncthreads();  // ph 1 adds after every ph 0 write has landed
+  if (ph == 1) sp_partial<1>(acc, grp, lane, ya, yb);
+}
+
 // Epilogue of a block of NW waves holding PPW (16-tile group, 16-channel half) accumulator sets
 // each: TB = 8 * NW * PPW tiles x 32 output channels. Virtual wave v = wave + NW * pp owns group
 // v % (TB/16) and half v / (TB/16) (PPW = 1: MODE 2/3; PPW = 2: the wide kernel, one wave = one
 // group x both halves). Outputs are staged in LDS per half of 32 tiles (ya: channels 0-15, yb:
 // 16-31), then coalesced 128-B traffic; ``part`` receives per-(tile, channel) partial sums
-// (TB x 32 floats).
-template <int EPI, int S, int NW, int PPW = 1>
+// (TB x 32 floats). SPP: the split-points kernel (NW = 4, 32 tiles): phase 1 is sp_phase1.
+template <int EPI, int S, int NW, int PPW = 1, bool SPP = false>
 __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], int t0, int k0, float* ya, float* yb,
                                          float* part) {
   constexpr int TPR = S / 4, TI = TPR * TPR;
   constexpr int GROUPS = NW * PPW / 2, TB = 16 * GROUPS, HALVES = TB / 32, TPW = 32 / NW;  // tiles per wave (phase 2)
+  static_assert(!SPP || (NW == 4 && PPW == 1), "split-points epilogue: 32-tile blocks of 4 waves");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
   const bool want_part = EPI == BWD ? p.taylor != nullptr : p.apoz != nullptr;
@@ -208,8 +289,9 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
 #pragma unroll
   for (int hf = 0; hf < HALVES; ++hf) {
     // ---- phase 1: output transform; park this half's 32 tiles x 16 px x (16 + 16) ch -------
+    if constexpr (SPP) sp_phase1(acc[0], wave >> 1, wave & 1, lane, ya, yb);
 #pragma unroll
-    for (int pp = 0; pp < PPW; ++pp) {
+    for (int pp = 0; pp < (SPP ? 0 : PPW); ++pp) {
       const int vw = wave + NW * pp, grp = vw % GROUPS, nh = vw / GROUPS;
       if (grp / 2 == hf) {
         float* ybuf = nh ? yb : ya;
@@ -669,9 +751,115 @@ __device__ __forceinline__ void bt6p(f2v& a0, f2v& a1, f2v& a2, f2v& a3, f2v& a4
                : "+v"(c0), "+v"(c1)                                                                 \
                : "v"(a0), "v"(a1), "v"(w.x), "v"(w.y))
 
-template <int EPI, int S, int NW, bool SPREAD = false>
+// Split points (variant 3): the two waves of a 16-tile group each own three rows of the 6x6
+// transform-point grid (18 points) x all 32 output channels instead of all 36 points x 16
+// channels. The accumulators stay 36 tiles per wave, the MFMAs 72 per chunk, but each wave forms
+// only its half of V = B^T d B: the first (column) pass computes 3 of its 6 outputs, the second
+// runs on 3 rows — 72 packed VALU ops per chunk instead of 168 (the 12-op length-6 transform
+// below, vs 14). fp32 VALU does not co-issue with fp32 MFMAs on gfx950, so this is the lever.
+//   B^T rows: o0 = 4a0 - 5a2 + a4; o1/o2 = p +- q (p = a4 - 4a2, q = a3 - 4a1);
+//             o3/o4 = r +- 2s (r = a4 - a2, s = a3 - a1); o5 = 4a1 - 5a3 + a5
+__device__ __forceinline__ void bt6q(f2v& a0, f2v& a1, f2v& a2, f2v& a3, f2v& a4, f2v& a5) {
+  const f2v p = -4.f * a2 + a4, q = -4.f * a1 + a3, r = a4 - a2, s = a3 - a1;
+  const f2v o0 = 4.f * a0 + (-5.f * a2 + a4);
+  const f2v o5 = 4.f * a1 + (-5.f * a3 + a5);
+  a0 = o0;
+  a1 = p + q;
+  a2 = p - q;
+  a3 = 2.f * s + r;
+  a4 = -2.f * s + r;
+  a5 = o5;
+}
+
+// first (column) pass of one patch column for point half ph: rows 3ph..3ph+2 of V's column c
+template <int PH>
+__device__ __forceinline__ void sp_col(const f2v (&a)[6], f2v (&w)[18], int c) {
+  if constexpr (PH == 0) {
+    const f2v p = -4.f * a[2] + a[4], q = -4.f * a[1] + a[3];
+    w[c] = 4.f * a[0] + (-5.f * a[2] + a[4]);
+    w[6 + c] = p + q;
+    w[12 + c] = p - q;
+  } else {
+    const f2v r = a[4] - a[2], s = a[3] - a[1];
+    w[c] = 2.f * s + r;
+    w[6 + c] = -2.f * s + r;
+    w[12 + c] = 4.f * a[1] + (-5.f * a[3] + a[5]);
+  }
+}
+
+// w[6 rr + c] = V[3 ph + rr][c] of the lane's two channels. The patch is read column by column
+// (one ds_read_b64 each), one column ahead of its pass, so at most two raw columns are live
+// (24 VGPRs instead of the whole 72-register patch: no spills beside the 144 accumulators).
+template <int S, typename G, int PH>
+__device__ __forceinline__ void sp_read_transform(const float* p0, f2v (&w)[18]) {
+  f2v col[2][6];
+  auto rd = [&](int q, f2v (&d)[6]) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      f2v v = {0.f, 0.f};
+      if constexpr (S == 4) {
+        if (r >= 1 && r <= 4 && q >= 1 && q <= 4) v = *reinterpret_cast<const f2v*>(p0 + ((r - 1) * 4 + (q - 1)) * 4);
+      } else {
+        v = *reinterpret_cast<const f2v*>(p0 + (r * G::RWP + q + (G::PAD && q >= 4 ? 1 : 0)) * 4);
+      }
+      d[r] = v;
+      __builtin_amdgcn_sched_barrier(0);  // one ds_read_b64 each (no ds_read2 merging)
+    }
+  };
+  rd(0, col[0]);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    if (c + 1 < 6) rd(c + 1, col[(c + 1) & 1]);
+    sp_col<PH>(col[c & 1], w, c);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 3; ++rr) bt6q(w[6 * rr], w[6 * rr + 1], w[6 * rr + 2], w[6 * rr + 3], w[6 * rr + 4], w[6 * rr + 5]);
+}
+
+// the 72 MFMAs of one chunk for a split-points wave: per parity e (input channel 2g + e) 9 point
+// pairs x both channel halves; ``mid`` runs between the parities (U1 wait + barrier + next DMAs)
+template <typename Mid>
+__device__ __forceinline__ void sp_mfma_chunk(int c, int nc, const f2v (&w)[18], const float* ul, f32x4 (&acc)[NPT],
+                                              Mid mid, int ph) {
+  (void)c;
+  (void)nc;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    if (e == 1) mid();
+    const float* ue = ul + (e * 18 + 9 * ph) * 256;
+    float2 wq[2][2];  // [pair parity][channel half]
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        wq[s2][h] = *reinterpret_cast<const float2*>(ue + s2 * 256 + h * 128);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const float2 w0 = wq[i & 1][0], w1 = wq[i & 1][1];
+      if (i + 2 < 9) {
+        wq[i & 1][0] = *reinterpret_cast<const float2*>(ue + (i + 2) * 256);
+        __builtin_amdgcn_sched_barrier(0);
+        wq[i & 1][1] = *reinterpret_cast<const float2*>(ue + (i + 2) * 256 + 128);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int x = 2 * i;
+      const float a0 = e ? w[x].y : w[x].x, a1 = e ? w[x + 1].y : w[x + 1].x;
+      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, w0.x, acc[x], 0, 0, 0);
+      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, w0.y, acc[x + 1], 0, 0, 0);
+      acc[18 + x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, w1.x, acc[18 + x], 0, 0, 0);
+      acc[18 + x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, w1.y, acc[18 + x + 1], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <int EPI, int S, int NW, bool SPREAD = false, bool SPLITP = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   static_assert(!SPREAD || NW == 4, "SPREAD is the 4-wave (two blocks per CU) schedule");
+  static_assert(!SPLITP || (NW == 4 && !SPREAD), "split points: 4-wave blocks, burst DMA");
   constexpr int TB = 8 * NW, NG = NW / 2;  // tiles per block, 16-tile groups
   constexpr bool XDBL = NW == 8;           // X double-buffered (one block per CU)
   using G = GeoT<S, TB>;
@@ -781,7 +969,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   f32x4 acc[NPT];
 #pragma unroll
   for (int x = 0; x < NPT; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* ul = us + nh * 128 + j * 8 + 2 * (g ^ ((j >> 3) << 1));
+  // SPLITP: nh is the wave's point half (rows 3nh..3nh+2 of the 6x6 grid); it reads both channel halves
+  const float* ul = us + (SPLITP ? 0 : nh * 128) + j * 8 + 2 * (g ^ ((j >> 3) << 1));
   const bool full_x = (NXI - wave + NW - 1) / NW == KX;  // this wave issues KX (else KX - 1) X DMAs
   // Wait until at most this wave's X DMAs of one chunk (issued last) are in flight
   auto wait_but_x = [&]() {
@@ -801,6 +990,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     stage_u(8 * c, 1);
+    if constexpr (SPLITP) {
+      f2v w[18];
+      if (nh == 0) sp_read_transform<S, G, 0>(xb + poff, w);  // wave-uniform branch
+      else sp_read_transform<S, G, 1>(xb + poff, w);
+      lds_barrier();  // every wave has its patch: X(c+1) into the single buffer
+      if (c + 1 < nc) stage_x(8 * (c + 1), xs0);
+      sp_mfma_chunk(c, nc, w, ul, acc, [&]() {
+        if (c + 1 < nc) wait_but_x();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (c + 1 < nc) stage_u(8 * (c + 1), 0);
+      }, nh);
+      continue;
+    }
     f2v v[36];
     {
       const float* p0 = xb + poff;
@@ -876,7 +1079,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
     return;
   }
   if constexpr (XDBL) epilogue<EPI, S, 8>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, xs0, xs1, us);
-  else epilogue<EPI, S, 4>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us, xs0, xs1);
+  else epilogue<EPI, S, 4, 1, SPLITP>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us, xs0, xs1);
 }
 
 // WIDE: one block of 4 waves per CU (one wave per SIMD) = 64 tiles x 32 output channels; wave w
@@ -1206,7 +1409,8 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
                                               float* apoz, int tay_mode, hipStream_t st);
 
 // variant 0: the TP_W4_MODE kernel (default MODE 3); variant 1: the WIDE kernel (64-tile blocks,
-// one wave per SIMD, each wave 16 tiles x 32 outputs).
+// one wave per SIMD, each wave 16 tiles x 32 outputs); variant 2: MODE 3 with spread U DMA;
+// variant 3: MODE 3 with split points (each wave 18 points x 32 outputs, half the transform).
 extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi,
                                     const float* scale, const float* shift, int relu, float* out, uint8_t* out_argmax,
                                     const float* act, float* taylor, float* apoz, int tay_mode, int splits,
@@ -1216,9 +1420,9 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   const int nc = C / 8;
   splits = std::max(1, std::min(splits, nc));
   splits = (nc + (nc + splits - 1) / splits - 1) / ((nc + splits - 1) / splits);  // no empty split
-  if (variant < 0 || variant > 2) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 3) return hipErrorInvalidValue;
   const bool wide = variant == 1;
-  if (splits > 1 && ((!wide && kernel_mode() < 2) || !ws)) return hipErrorInvalidValue;
+  if (splits > 1 && ((variant == 0 && kernel_mode() < 2) || !ws)) return hipErrorInvalidValue;
   if (epi < 0 || epi > 2 || (epi == BWD && !act) || (epi != BWD && !out) || (epi == FWD_POOL && !out_argmax))
     return hipErrorInvalidValue;
   Args a{};
@@ -1249,7 +1453,8 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
     return v;
   }();
   a.dbg = dbg;
-  const int mode = wide ? 4 : variant == 2 ? 5 : kernel_mode();  // 5: MODE 3 with SPREAD DMA
+  // 5: MODE 3 with SPREAD DMA; 6: MODE 3 with split points
+  const int mode = wide ? 4 : variant == 2 ? 5 : variant == 3 ? 6 : kernel_mode();
   const int tb = mode == 2 || mode == 4 ? 64 : TILES;  // MODE 3: 32-tile blocks
   const int n_p = (a.P + tb - 1) / tb, n_k = K / TK;
   const dim3 grid(n_p * n_k, splits);
@@ -1268,6 +1473,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 #define TP_W4P(SS)                                                                      \
   do {                                                                                  \
     if (mode == 4) wino4_wide<PARTIAL, SS><<<grid, 256, 0, st>>>(b);                    \
+    else if (mode == 6) wino4_m2<PARTIAL, SS, 4, false, true><<<grid, 256, 0, st>>>(b); \
     else if (mode == 5) wino4_m2<PARTIAL, SS, 4, true><<<grid, 256, 0, st>>>(b);        \
     else if (mode == 2) wino4_m2<PARTIAL, SS, 8><<<grid, 512, 0, st>>>(b);              \
     else wino4_m2<PARTIAL, SS, 4><<<grid, 256, 0, st>>>(b);                             \
@@ -1286,6 +1492,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 #define TP_W4(E, SS)                                              \
   do {                                                            \
     if (mode == 4) wino4_wide<E, SS><<<grid, 256, 0, st>>>(a);    \
+    else if (mode == 6) wino4_m2<E, SS, 4, false, true><<<grid, 256, 0, st>>>(a); \
     else if (mode == 5) wino4_m2<E, SS, 4, true><<<grid, 256, 0, st>>>(a); \
     else if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a); \
     else if (mode == 3) wino4_m2<E, SS, 4><<<grid, 256, 0, st>>>(a); \
@@ -1310,7 +1517,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
 // static LDS bytes of a wino4 instantiation (occupancy / budget guard)
 extern "C" int tp_wino4_lds_bytes(int S, int variant) {
   using namespace tp::w4;
-  const int m = variant == 1 ? 4 : variant == 2 ? 3 : kernel_mode();
+  const int m = variant == 1 ? 4 : variant >= 2 ? 3 : kernel_mode();
   const void* f = nullptr;
 #define TP_W4F(SS)                                                                            \
   f = m == 4 ? (const void*)wino4_wide<BWD, SS>                                               \

@@ -1,7 +1,7 @@
 """Is the B=100 fused-engine step host-bound? Times the host side of every pipelined batch
 (``_BatchPipeline.take``: Python + kernel launches of one engine forward/backward and its fold)
 against the wall time of the whole run, for VGG16-BN Taylor at B=100 (random init, synthetic data).
-Usage: python scripts/b100_host_probe.py [--batch 100] [--steps 200]"""
+Usage: python scripts/probes/b100_host_probe.py [--batch 100] [--steps 200]"""
 import argparse
 import os
 import sys
@@ -10,7 +10,7 @@ import time
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from torchpruner_amd import TaylorAttributionMetric  # noqa: E402
 from torchpruner_amd.attributions import base  # noqa: E402

@@ -1,6 +1,6 @@
 """The opt-in bf16 VGG16 Taylor engine step at B=2048 (random-init weights, synthetic batches): a
 few tuned warm-up batches, then --steps timed batches; a target for rocprofv3 --kernel-trace
---stats (the step's per-kernel breakdown). python scripts/bf16_step_probe.py [--steps 5] [--fp32]"""
+--stats (the step's per-kernel breakdown). python scripts/probes/bf16_step_probe.py [--steps 5] [--fp32]"""
 import argparse
 import os
 import sys
@@ -9,7 +9,7 @@ import time
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

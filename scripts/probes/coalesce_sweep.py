@@ -1,6 +1,6 @@
 """B=100 VGG16 Taylor run_many (bench.py's vgg_taylor_b100_img_s setup: random-init weights,
 synthetic batches) at several coalescing factors (TORCHPRUNER_COALESCE=k loader batches per engine
-launch; 1 = the default element target). python scripts/coalesce_sweep.py [--factors 1,10,20]"""
+launch; 1 = the default element target). python scripts/probes/coalesce_sweep.py [--factors 1,10,20]"""
 import argparse
 import os
 import sys
@@ -9,7 +9,7 @@ import time
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

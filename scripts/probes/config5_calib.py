@@ -2,7 +2,7 @@
 
 Runs prune_finetune_quality for every combination of the given overrides and prints one JSON line
 per run (teacher top-1, Taylor / Random after prune and after finetune).
-Usage: python scripts/config5_calib.py --set lr=0.01,0.003 ft_steps=15,60 --seeds 0 1
+Usage: python scripts/probes/config5_calib.py --set lr=0.01,0.003 ft_steps=15,60 --seeds 0 1
 """
 import argparse
 import itertools
@@ -10,7 +10,7 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

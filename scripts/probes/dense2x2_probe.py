@@ -1,13 +1,13 @@
 """The VGG16 2x2-map layers as dense GEMMs (engine/fused_chain.py DENSE: B x 4C -> 4N, here
 2048 x 2048 x 2048 fp32): every implicit-GEMM tile config x split-K of the native kernel vs
-hipBLASLt (torch.mm). python scripts/dense2x2_probe.py [--m 2048] [--n 2048] [--k 2048]"""
+hipBLASLt (torch.mm). python scripts/probes/dense2x2_probe.py [--m 2048] [--n 2048] [--k 2048]"""
 import argparse
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from torchpruner_amd import ops  # noqa: E402
 from torchpruner_amd.engine.fused_chain import TUNER  # noqa: E402

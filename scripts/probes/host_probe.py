@@ -2,9 +2,9 @@
 finalisation (everything enqueued, nothing waited for) against the run's wall time. A ratio
 near 1 means the GPU waits for Python; well below 1 means the run is GPU-bound.
 
-    python scripts/host_probe.py shapley --layer 6      # VGG16 Shapley S=5, 1000 images, B=100
-    python scripts/host_probe.py taylor --batch 100     # VGG16 Taylor, 200 batches
-    python scripts/host_probe.py resnet-taylor --batch 256
+    python scripts/probes/host_probe.py shapley --layer 6      # VGG16 Shapley S=5, 1000 images, B=100
+    python scripts/probes/host_probe.py taylor --batch 100     # VGG16 Taylor, 200 batches
+    python scripts/probes/host_probe.py resnet-taylor --batch 256
 """
 import argparse
 import os
@@ -14,7 +14,7 @@ import time
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from torchpruner_amd import (APoZAttributionMetric, ShapleyAttributionMetric,  # noqa: E402
                              TaylorAttributionMetric)

@@ -3,7 +3,7 @@
 For every noise level, runs the full protocol (teacher -> Taylor- and Random-pruned copies) over
 several seeds and prints one JSON line per run plus a summary per noise level: teacher top-1
 mean, Taylor / Random top-1 mean +- std, the paired Taylor - Random difference and its sign
-count. Usage: python scripts/quality_calib.py --noise 3.5 4.0 --seeds 0 1 2 3 4 [--teacher-steps N]
+count. Usage: python scripts/probes/quality_calib.py --noise 3.5 4.0 --seeds 0 1 2 3 4 [--teacher-steps N]
 """
 import argparse
 import json
@@ -12,7 +12,7 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from torchpruner_amd.bench import prune_quality as pq  # noqa: E402
 

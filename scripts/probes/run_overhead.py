@@ -1,7 +1,7 @@
 """Per-run fixed cost of TaylorAttributionMetric.run_many on the fused VGG engine: times runs of
 1, 5 and 20 batches (B images each), fits t = a + b * n, and profiles the host side of one
 1-batch run (cProfile, top functions by cumulative time).
-Usage: python scripts/run_overhead.py [--batch 2048]"""
+Usage: python scripts/probes/run_overhead.py [--batch 2048]"""
 import argparse
 import cProfile
 import os
@@ -12,7 +12,7 @@ import time
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from torchpruner_amd import TaylorAttributionMetric  # noqa: E402
 from torchpruner_amd.data import DeviceLoader  # noqa: E402

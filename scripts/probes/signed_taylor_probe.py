@@ -6,7 +6,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from torchpruner_amd import TaylorAttributionMetric  # noqa: E402
 from torchpruner_amd.data import DeviceLoader  # noqa: E402
 from torchpruner_amd.models import prunable_vgg16  # noqa: E402

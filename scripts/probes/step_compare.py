@@ -1,5 +1,5 @@
 """Side-by-side per-dispatch durations of the last engine step of several rocprofv3 kernel traces
-(e.g. TP_WINO_DBG experiments): python scripts/step_compare.py dirA dirB ..."""
+(e.g. TP_WINO_DBG experiments): python scripts/probes/step_compare.py dirA dirB ..."""
 import csv
 import glob
 import re

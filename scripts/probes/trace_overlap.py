@@ -1,7 +1,7 @@
 """Kernel overlap in a rocprofv3 kernel trace: over the last ``frac`` of the trace's time span,
 the wall span, the summed kernel time, the union of kernel intervals (time with >= 1 kernel
 running) and the average number of kernels in flight; plus the per-kernel-name summed time.
-Usage: python scripts/trace_overlap.py <kernel_trace.csv> [frac=0.5] [top=15]"""
+Usage: python scripts/probes/trace_overlap.py <kernel_trace.csv> [frac=0.5] [top=15]"""
 import collections
 import csv
 import re

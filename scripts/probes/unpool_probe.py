@@ -1,12 +1,12 @@
 """Bandwidth of the argmax unpooling kernel (prune_ops.hip unpool2_nhwc_v4) at the VGG16/CIFAR
 pooled-layer shapes, B=2048 fp32: us per launch and GB/s (gradient + argmax read, full-size
-gradient written). python scripts/unpool_probe.py"""
+gradient written). python scripts/probes/unpool_probe.py"""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from torchpruner_amd import ops  # noqa: E402
 

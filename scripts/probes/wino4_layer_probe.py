@@ -1,14 +1,14 @@
 """One Winograd layer (default S=8, C=K=256, B=2048, forward) launched a few times: a target for
 rocprofv3 PMC passes. --kind wino4 (F(4x4) fp32), wino2 (F(2x2) staged fp32) or wino2bf (F(2x2)
 staged, bf16 U images + bf16 MFMA).
-python scripts/wino4_layer_probe.py [--S 8 --C 256 --K 256 --variant 0 --kind wino4]"""
+python scripts/probes/wino4_layer_probe.py [--S 8 --C 256 --K 256 --variant 0 --kind wino4]"""
 import argparse
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

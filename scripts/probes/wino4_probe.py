@@ -1,11 +1,11 @@
 """A few launches of the F(4x4) and F(2x2) forward kernels on one VGG16 layer shape, for PMC runs:
-``python scripts/wino4_probe.py S C K [B]``."""
+``python scripts/probes/wino4_probe.py S C K [B]``."""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from torchpruner_amd import ops  # noqa: E402
 
 T = ops.require()

@@ -3,7 +3,7 @@ vs the MODE 3 kernel (variant 0: 32-tile blocks, two blocks per CU) on the VGG16
 shapes: per-layer us for the forward (BN+ReLU, pooled where VGG pools) and the data gradient
 (Taylor partials), each at its best split count, plus the max relative difference of the two.
 
-    python scripts/wino4_wide_bench.py [--batch 2048] [--iters 10]
+    python scripts/probes/wino4_wide_bench.py [--batch 2048] [--iters 10]
 """
 import argparse
 import os
@@ -11,7 +11,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 LAYERS = [(32, 64, 64, True), (16, 64, 128, False), (16, 128, 128, True), (8, 128, 256, False),
           (8, 256, 256, False), (8, 256, 256, True), (4, 256, 512, False), (4, 512, 512, False),

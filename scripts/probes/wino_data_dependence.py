@@ -3,7 +3,7 @@
 Times the staged forward kernel (no epilogue work beyond the store) on one VGG16 layer shape with
 the same launch geometry and three inputs: dense N(0,1), ReLU'd N(0,1) (~50% zeros, like the
 forward's post-ReLU activations) and all zeros; and the dgrad kernel with dense vs sparse gradients.
-Usage: python scripts/wino_data_dependence.py [--batch 2048]
+Usage: python scripts/probes/wino_data_dependence.py [--batch 2048]
 """
 import argparse
 import os
@@ -11,7 +11,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from torchpruner_amd import ops  # noqa: E402
 from torchpruner_amd.engine.fused_chain import winograd_weights  # noqa: E402

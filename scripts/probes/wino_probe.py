@@ -4,7 +4,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from torchpruner_amd import ops  # noqa: E402
 from torchpruner_amd.engine.fused_chain import taylor_slots, winograd_weights  # noqa: E402
 

@@ -1,0 +1,114 @@
+"""F(4x4,3x3) kernel variants on the VGG16-CIFAR 3x3 conv shapes: per-layer us for the forward
+(BN+ReLU, pooled where VGG pools) and the data gradient (Taylor partials), each at its best split
+count, plus the max relative difference of every variant against the first one listed.
+
+    python scripts/wino4_variant_bench.py --variants 0 3 [--batch 2048 100] [--iters 10]
+
+variants (wino4.hip ``tp_conv_wino4``): 0 MODE 3 (32-tile blocks, two blocks per CU), 1 WIDE,
+2 MODE 3 + spread U DMA, 3 MODE 3 with split transform points.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+LAYERS = [(32, 64, 64, True), (16, 64, 128, False), (16, 128, 128, True), (8, 128, 256, False),
+          (8, 256, 256, False), (8, 256, 256, True), (4, 256, 512, False), (4, 512, 512, False),
+          (4, 512, 512, True)]
+TB = {0: (32, 2), 1: (64, 1), 2: (32, 2), 3: (32, 2)}
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def splits_for(B, S, K, C, tb, per_cu):
+    blocks = -(-B * (S // 4) ** 2 // tb) * (K // 32)
+    out, sp = [1], 1
+    while blocks * sp < per_cu * 256 and sp * 2 <= (C // 8) // 4 and sp < 16:
+        sp *= 2
+        out.append(sp)
+    return out
+
+
+def rel(a, b):
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, nargs="+", default=[2048, 100])
+    ap.add_argument("--variants", type=int, nargs="+", default=[0, 3])
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    from torchpruner_amd import ops
+    T = ops.require()
+    dev = torch.device("cuda")
+    V = args.variants
+    for B in args.batch:
+        tot = {(k, v): 0.0 for k in "fb" for v in V}
+        print(f"B={B}: per layer us at the best split, variants {V} (max rel diff vs variant {V[0]})", flush=True)
+        for S, C, K, pool in LAYERS:
+            g = torch.Generator(device=dev).manual_seed(S + C + K)
+            x = torch.randn(B, S, S, C, device=dev, generator=g)
+            w = torch.randn(K, C, 3, 3, device=dev, generator=g) * 0.05
+            sc, sh = torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev) * 0.1
+            u4 = T.wino4_weights(w, False, 0, 0)
+            gg = torch.randn(B, S, S, K, device=dev, generator=g)
+            act = torch.relu(torch.randn(B, S, S, C, device=dev, generator=g))
+            scp = torch.rand(C, device=dev) + 0.5
+            ut4 = T.wino4_weights(w, True, 0, 0)
+            tay = torch.zeros(4, B, C, device=dev)
+            res, outs = {}, {}
+            for v in V:
+                tb, per_cu = TB[v]
+                best = None
+                for sp in splits_for(B, S, K, C, tb, per_cu):
+                    t = timeit(lambda: T.conv_wino4_fwd(x, u4, sc, sh, True, pool, None, sp, v), args.iters)
+                    if best is None or t < best[0]:
+                        best = (t, sp)
+                res[("f", v)] = best
+                outs[("f", v)] = T.conv_wino4_fwd(x, u4, sc, sh, True, pool, None, 1, v)[0]
+                if C % 32 == 0:
+                    best = None
+                    for sp in splits_for(B, S, C, K, tb, per_cu):
+                        t = timeit(lambda: T.conv_wino4_dgrad(gg, ut4, act, scp, tay, True, 0, sp, v), args.iters)
+                        if best is None or t < best[0]:
+                            best = (t, sp)
+                    res[("b", v)] = best
+                    t1 = torch.zeros(4, B, C, device=dev)
+                    outs[("b", v)] = (T.conv_wino4_dgrad(gg, ut4, act, scp, t1, True, 0, 1, v), t1)
+                else:
+                    res[("b", v)] = (float("nan"), 0)
+            line = f"S={S:2d} C={C:3d} K={K:3d} pool={int(pool)} |"
+            for k, nm in (("f", "fwd"), ("b", "dgrad")):
+                line += f" {nm}"
+                for v in V:
+                    t, sp = res[(k, v)]
+                    line += f" {t:7.1f}(sp{sp})"
+                    if t == t:
+                        tot[(k, v)] += t
+                    if v != V[0] and (k, v) in outs:
+                        if k == "f":
+                            d = rel(outs[(k, v)], outs[(k, V[0])])
+                        else:
+                            d = max(rel(outs[(k, v)][0], outs[(k, V[0])][0]), rel(outs[(k, v)][1], outs[(k, V[0])][1]))
+                        line += f"[{d:.1e}]"
+                line += " |"
+            print(line, flush=True)
+        print("total " + " ".join(f"{k}{v}={tot[(k, v)]:.0f}" for k in "fb" for v in V), flush=True)
+
+
+if __name__ == "__main__":
+    main()

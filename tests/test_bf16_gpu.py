@@ -114,7 +114,8 @@ def test_bf16_engine_taylor_ranks_match_fp32(cuda):
 
 @pytest.mark.parametrize("family", ["wino2_bf16", "igemm"])
 def test_bf16_engine_family_pinned(cuda, family):
-    """Each bf16 kernel family pinned in turn (bf16 F(2x2) Winograd with hi/lo V, bf16 implicit
+    """Each bf16 kernel family pinned in turn (bf16 F(2x2) Winograd with plain bf16-rounded V — the
+    hi/lo split is the env-gated TP_WINO_BF_SPLIT path, not tested here — and the bf16 implicit
     GEMM) gives Taylor scores that rank like the fp32 ones; the pinned family really ran."""
     from scipy.stats import spearmanr
 

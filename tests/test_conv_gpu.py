@@ -142,7 +142,7 @@ def test_nan_propagation(cuda):
 # engine's own ReLU masks and pool argmaxes (engine/oracle.py), per pinned kernel family. Measured
 # on MI355X (profiles/numerics/taylor_oracle_per_family.txt): F(4x4) <= 1.2e-5 (its +-2 transform
 # points amplify rounding ~8x), F(2x2) / implicit GEMM <= 2.5e-6; the bounds leave ~4x headroom.
-_COND_BOUND = {"wino4": 5e-5, "wino4w": 5e-5, "wino2": 1e-5, "wino2_direct": 1e-5, "igemm": 1e-5}
+_COND_BOUND = {"wino4": 5e-5, "wino4_m3": 5e-5, "wino4w": 5e-5, "wino2": 1e-5, "wino2_direct": 1e-5, "igemm": 1e-5}
 
 
 @pytest.mark.parametrize("family", ["wino4", "wino2", "wino2_direct", "igemm"])
@@ -160,7 +160,7 @@ def test_engine_scores_match_fp64_oracle(cuda, family, split, mode):
     from torchpruner_amd.data import DeviceLoader
     from torchpruner_amd.engine import maybe_engine
     from torchpruner_amd.engine.fused_chain import TUNER, family_policy
-    from torchpruner_amd.engine.oracle import engine_scores_fp64
+    from torchpruner_amd.engine.oracle import engine_scores_fp64, flip_violations
     from torchpruner_amd.models import prunable_vgg16
     from torchpruner_amd.utils import find_best_module_for_attributions
     torch.manual_seed(0)
@@ -180,8 +180,13 @@ def test_engine_scores_match_fp64_oracle(cuda, family, split, mode):
             got = SensitivityAttributionMetric(model, DeviceLoader(x, y, B), F.cross_entropy, cuda,
                                                reduction="none").run_many(mods, True)
         cond, plain = {b: [] for b in idx}, {b: [] for b in idx}
+        flips, totals = {}, {}
         for i in range(0, x.shape[0], B):
-            c, _ = engine_scores_fp64(eng, x[i:i + B], y[i:i + B], conditioned=True, mode=mode)
+            tot = {}
+            c, fl = engine_scores_fp64(eng, x[i:i + B], y[i:i + B], conditioned=True, mode=mode, totals=tot)
+            for b in fl:
+                flips[b] = flips.get(b, 0) + fl[b]
+                totals[b] = totals.get(b, 0) + tot[b]
             p, _ = engine_scores_fp64(eng, x[i:i + B], y[i:i + B], conditioned=False, mode=mode)
             for b in idx:
                 cond[b].append(c[b])
@@ -195,6 +200,11 @@ def test_engine_scores_match_fp64_oracle(cuda, family, split, mode):
         print(f"{family}/{split} {mode} block {b}: cond {err:.2e} plain(|.| mean) {err_plain:.2e}")
         assert err < _COND_BOUND[family], (b, err)
         assert err_plain < 5e-3, (b, err_plain)
+    # decisions (ReLU masks, pool argmaxes) taken differently from fp64 given identical upstream
+    # decisions: rare rounding ties only — a systematic mis-decision near 0 fails here
+    # (tests/test_oracle.py::test_flip_bound_catches_a_wrong_relu_threshold)
+    print(f"{family}/{split} {mode} decision flips per block: {flips} of {totals}")
+    assert flip_violations(flips, totals) == {}, flip_violations(flips, totals)
 
 
 def test_engine_taylor_bit_reproducible(cuda):

@@ -107,3 +107,33 @@ def test_oracle_counts_and_replays_flipped_decisions():
     # plain fp64 follows its own decisions, so downstream of the flip it agrees with the engine
     assert flips[2] == 1 and sum(flips.values()) == 1 and flips2[2] == 1
     assert not torch.equal(cond[0], plain[0])  # upstream scores follow the engine's mask
+
+
+def test_flip_bound_catches_a_wrong_relu_threshold():
+    """Red on purpose: an engine whose ReLU decides ``x > 0.02`` instead of ``x > 0`` (a
+    systematic mis-decision near zero) still matches the mask-conditioned oracle exactly — the
+    tight check conditions on the engine's own decisions — but its flips break the per-block
+    bound (FLIP_RATE_BOUND of the block's decisions) that the GPU test and smoke() assert."""
+    from torchpruner_amd.engine.oracle import FLIP_RATE_BOUND, flip_violations
+    m = _model()
+    x = torch.randn(4, 3, 32, 32, dtype=torch.float64)
+    y = torch.randint(0, 10, (4,))
+    good = _TorchChain(m)
+    tot = {}
+    _, flips = engine_scores_fp64(good, x, y, conditioned=True, totals=tot)
+    assert set(tot) == set(flips) and all(v > 0 for v in tot.values())
+    assert flip_violations(flips, tot) == {}
+    bad = _TorchChain(m)
+    fwd = bad.forward
+
+    def thresholded(xx):
+        logits, saved = fwd(xx)
+        saved["acts"] = [(torch.where(h > 0.02, h, torch.zeros((), dtype=h.dtype)), am) for h, am in saved["acts"]]
+        return logits, saved
+
+    bad.forward = thresholded
+    tot2 = {}
+    _, flips2 = engine_scores_fp64(bad, x, y, conditioned=True, totals=tot2)
+    viol = flip_violations(flips2, tot2)
+    assert viol, flips2
+    assert all(f > FLIP_RATE_BOUND * n for f, n in viol.values())

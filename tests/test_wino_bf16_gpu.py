@@ -153,7 +153,7 @@ def test_wino_bf16_rejects_direct_mode(cuda):
 @pytest.mark.parametrize("variant", ["TP_WINO_BF_K16", "TP_WINO_BF_SPLIT"])
 def test_wino_bf16_measured_options_match_emulation(cuda, variant):
     """The launcher reads the option switches once per process, so each option runs the
-    emulation check (scripts/wino_bf16_diag.py: 4 VGG shapes, forward) in a child process."""
+    emulation check (scripts/probes/wino_bf16_diag.py: 4 VGG shapes, forward) in a child process."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -91,10 +91,13 @@ def _run(cmd, verbose):
 # The extension is rebuilt from what the sources SAY, not from file times: an object is recompiled
 # when the hash of its source + headers + (path-free) flags differs from the one recorded when it
 # was built (build/native/manifest.json), and the hash of the whole source set is stamped into
-# _C.so as the string ``TPAMD_SRC_HASH=<hex>``. ops.load() refuses a _C.so whose stamp does not
-# match the tree it runs from (a stale binary after a checkout or a copy that refreshed mtimes
-# unevenly would otherwise load silently).
+# _C.so as the string ``TPAMD_SRC_HASH=<hex>``, the hash of the build flags / torch version as
+# ``TPAMD_FLAG_HASH=<hex>``. ops.load() refuses a _C.so whose source stamp does not match the tree
+# it runs from (a stale binary after a checkout or a copy that refreshed mtimes unevenly would
+# otherwise load silently); a flag-stamp mismatch (an env var of the build shell such as
+# TORCHPRUNER_HIPFLAGS / PYTORCH_ROCM_ARCH that differs at load time) only warns.
 STAMP_RE = re.compile(rb"TPAMD_SRC_HASH=([0-9a-f]{16})")
+FLAG_STAMP_RE = re.compile(rb"TPAMD_FLAG_HASH=([0-9a-f]{16})")
 
 
 def _flag_sig(stem: str, binding: bool) -> str:
@@ -118,18 +121,25 @@ def _sources():
 
 
 def source_hash() -> str:
-    """Hash of every source, header and flag that goes into ``_C.so``."""
+    """Hash of every source and header that goes into ``_C.so`` (content only: independent of
+    the environment of the shell that loads it)."""
     headers, kernels, bindings = _sources()
-    per = [_digest([s] + headers, _flag_sig(s.stem, False)) for s in kernels] + \
-          [_digest([b] + headers, _flag_sig(b.stem, True)) for b in bindings]
+    per = [_digest([s] + headers, "") for s in kernels + bindings]
     return hashlib.sha256("".join(per).encode()).hexdigest()[:16]
 
 
-def stamped_hash(path: Path = OUT):
-    """The source hash stamped into a built extension (None when absent)."""
+def flag_hash() -> str:
+    """Hash of the per-file compile flags (env-dependent: arch, TORCHPRUNER_HIPFLAGS, torch)."""
+    _, kernels, bindings = _sources()
+    sig = [_flag_sig(s.stem, False) for s in kernels] + [_flag_sig(b.stem, True) for b in bindings]
+    return hashlib.sha256("\n".join(sig).encode()).hexdigest()[:16]
+
+
+def stamped_hash(path: Path = OUT, flags: bool = False):
+    """The source (``flags=True``: flag) hash stamped into a built extension (None when absent)."""
     if not path.exists():
         return None
-    m = STAMP_RE.search(path.read_bytes())
+    m = (FLAG_STAMP_RE if flags else STAMP_RE).search(path.read_bytes())
     return m.group(1).decode() if m else None
 
 
@@ -167,12 +177,14 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
     man_path.write_text(json.dumps(new_manifest, indent=1, sort_keys=True))
 
-    want = source_hash()
-    if force or jobs_list or stamped_hash() != want:
+    want, want_flags = source_hash(), flag_hash()
+    if force or jobs_list or stamped_hash() != want or stamped_hash(flags=True) != want_flags:
         stamp_src = BUILD_DIR / "src_stamp.cpp"
-        stamp_src.write_text("// generated by torchpruner_amd/_build.py: hash of the sources of this _C.so\n"
+        stamp_src.write_text("// generated by torchpruner_amd/_build.py: hashes of the sources / flags of this _C.so\n"
                              f'extern "C" __attribute__((used, visibility("default"))) const char tp_src_stamp[] = '
-                             f'"TPAMD_SRC_HASH={want}";\n')
+                             f'"TPAMD_SRC_HASH={want}";\n'
+                             f'extern "C" __attribute__((used, visibility("default"))) const char tp_flag_stamp[] = '
+                             f'"TPAMD_FLAG_HASH={want_flags}";\n')
         stamp_obj = BUILD_DIR / "src_stamp.o"
         _run([HIPCC, "-fPIC", "-O1", "-x", "c++", "-c", stamp_src, "-o", stamp_obj], verbose)
         tmp = OUT.with_suffix(".so.tmp")

@@ -566,10 +566,22 @@ class _AttributionMetric(ABC):
         if not self._engines_allowed() and not bf16:
             return _reject(why, f"compute_dtype={self.compute_dtype} runs the generic autocast path")
         res = maybe_engine(self.model, eval_modules, self.criterion, self.device, need_ce=need_ce, why=why,
-                           pre_act_ok=pre_act_ok, input_shape=self._first_input_shape())
+                           pre_act_ok=pre_act_ok, input_shape=self._agreed_input_shape())
         if res is not None:
             res[0].bf16 = bf16
         return res
+
+    def _agreed_input_shape(self):
+        """``_first_input_shape`` made rank-consistent under data-parallel sharding: a rank whose
+        shard is empty (fewer batches than ranks) peeks nothing, so every rank takes the first
+        non-empty rank's shape (one all_gather_object) and all ranks make the same fused / generic
+        decision (``last_path`` could otherwise differ across ranks)."""
+        shape = self._first_input_shape()
+        world, _ = self._world()
+        if world > 1 and self._sharding():
+            shapes = pdist.all_gather_object(shape, group=self.group)
+            shape = next((tuple(s_) for s_ in shapes if s_ is not None), None)
+        return shape
 
     def _first_input_shape(self):
         """Shape of this rank's first input batch, or None. In-memory loaders (DeviceLoader,

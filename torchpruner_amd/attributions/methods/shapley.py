@@ -202,7 +202,10 @@ class ShapleyAttributionMetric(_AttributionMetric):
         if split == "batches":
             batches = self._batches()
         else:
-            batches = ((i, _to(x, self.device), _to(y, self.device)) for i, x, y in self._iter_source(self._all_batches))
+            # hybrid: another rank's whole batch is skipped before its host->device copy
+            batches = ((i, _to(x, self.device), _to(y, self.device))
+                       for i, x, y in self._iter_source(self._all_batches)
+                       if not (split == "hybrid" and i < nb_whole and i % world != rank))
         with torch.no_grad():
             for bidx, x, y in batches:
                 replicated = split == "prefixes" or (split == "hybrid" and bidx >= nb_whole)

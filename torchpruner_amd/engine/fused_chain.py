@@ -53,6 +53,9 @@ WINO4W = -5  # the same transform, WIDE kernel: 64-tile blocks, one wave per SIM
 WINO_BF = -6  # bf16 operands (compute_dtype=bfloat16): the staged F(2x2) kernel with bf16 U images and
               # v_mfma_f32_16x16x16_bf16 (winograd.hip BF); fp32 transforms, accumulation and epilogues
 WINO_BF_UNP = -7  # its dgrad of a pooled layer after an explicit unpool (as WINO_UNP)
+WINO4S = -8  # F(4x4) MODE 3 with split transform points (wino4.hip variant 3): each wave of a 16-tile
+             # pair owns 18 of the 36 points x all 32 outputs, so each wave forms half of V = B^T d B
+             # (72 packed VALU ops per 72 MFMAs instead of 168): the default F(4x4) kernel
 CFG_BF16 = 256  # tile-config flag of conv_igemm: bf16 operands / fp32 accumulation (opt-in, compute_dtype)
 _BF16_CFGS = (0, 2, 3)  # the implicit-GEMM tiles built with bf16 variants (conv_mfma.hip launch_any)
             # than F(2x2); dgrads of pooled layers take the explicit unpool first
@@ -113,12 +116,16 @@ _TUNER_LOG = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") != "0"  # print every 
 _W4_WIDE = os.environ.get("TORCHPRUNER_W4_WIDE", "0") != "0"
 
 
+_W4_VARIANT = {WINO4: 0, WINO4W: 1, WINO4S: 3}
+
+
 def _wino4_cands(B, H, W, K, C):
     """F(4x4) candidates: one K pass, plus channel-chunk split-K (raw slabs + the shared
     deterministic combine) when the tile grid alone cannot fill the chip (small batches); for
-    both kernels (MODE 3: 32-tile blocks, two per CU; WIDE: 64-tile blocks, one per CU)."""
+    the split-points kernel (the untuned pick), MODE 3 (32-tile blocks, two per CU) and, opt-in,
+    WIDE (64-tile blocks, one per CU)."""
     out = []
-    for kind, tb, per_cu in ((WINO4, 32, 2), (WINO4W, 64, 1)):
+    for kind, tb, per_cu in ((WINO4S, 32, 2), (WINO4, 32, 2), (WINO4W, 64, 1)):
         if kind == WINO4W and not _W4_WIDE:
             continue
         blocks = math.ceil(B * (H // 4) * (W // 4) / tb) * (K // 32)
@@ -262,6 +269,36 @@ class Autotuner:
 
 
 TUNER = Autotuner()
+
+_KIND_NAMES = {WINO: "wino2_direct", WINO_LDS: "wino2", WINO_UNP: "wino2_unpool", WINO4: "wino4_m3", WINO4W: "wino4w",
+               WINO_BF: "wino2_bf16", WINO_BF_UNP: "wino2_bf16_unpool", WINO4S: "wino4", -10: "first_direct"}
+
+
+def kernel_name(cfg: int) -> str:
+    """Readable name of a tuner choice: a Winograd kind, ``igemm<tile>`` (``_TILES``), ``dense2x2``
+    igemm (2x2 layers as one dense GEMM), ``bf16`` igemm variants, or a persistent 1x1 GEMM."""
+    if cfg in _KIND_NAMES:
+        return _KIND_NAMES[cfg]
+    if cfg >= 100 and cfg < CFG_BF16:
+        bm, bn = _TILES.get(cfg - 100, (0, 0))
+        return f"dense2x2_igemm{bm}x{bn}"
+    if cfg >= CFG_BF16:
+        bm, bn = _TILES.get(cfg - CFG_BF16, (0, 0))
+        return f"igemm{bm}x{bn}_bf16"
+    if cfg in _TILES:
+        bm, bn = _TILES[cfg]
+        return f"igemm{bm}x{bn}" + ("_8w" if cfg >= 4 else "")
+    return f"cfg{cfg}"
+
+
+def tuner_choices(cache=None) -> dict:
+    """The autotuner's per-shape picks as ``{key: [kernel, splits]}`` (bench JSON ``tuner_choices``:
+    which kernel family / split each layer ran on this box, so box-to-box spread is diagnosable)."""
+    cache = TUNER.cache if cache is None else cache
+    out = {}
+    for key, (cfg, sp) in cache.items():
+        out["/".join(str(k).replace(" ", "") for k in key)] = [kernel_name(cfg), int(sp)]
+    return out
 
 
 def cpad(c: int, q: int = 32) -> int:
@@ -586,9 +623,9 @@ class FusedChainEngine:
             return T.conv_wino_fwd(h, self._ubf(e), e["scale"], e["shift"], True, e["pool"], sp, True, apoz)
         if cfg >= CFG_BF16:
             return T.conv_fwd(h, e["w"], e["scale"], e["shift"], True, e["pool"], 3, cfg, sp, apoz)
-        if cfg in (WINO4, WINO4W):
+        if cfg in _W4_VARIANT:
             return T.conv_wino4_fwd(h, self._u4(e), e["scale"], e["shift"], True, e["pool"], apoz, sp,
-                                    1 if cfg == WINO4W else 0)
+                                    _W4_VARIANT[cfg])
         if cfg in (WINO, WINO_LDS):
             return T.conv_wino_fwd(h, e["u"], e["scale"], e["shift"], True, e["pool"], sp, cfg == WINO_LDS, apoz)
         if cfg >= self.DENSE:
@@ -610,7 +647,7 @@ class FusedChainEngine:
         cands = None
         if self.bf16 and C % 32 == 0:
             cands = self._bf16_cands(M, N, K)
-            if wino is not None:
+            if wino is not None:  # [0] (the untuned / TUNER.fixed() pick): bf16 F(2x2), bf16-rounded V
                 cands = self._wino_bf_cands(T, B, H, W, N, C) + cands
         elif H == 2 and W == 2 and C % 32 == 0:
             cands = [(self.DENSE + c, s_) for c, s_ in TUNER.candidates(B, 4 * N, 4 * C)] + \
@@ -634,11 +671,11 @@ class FusedChainEngine:
             return T.conv_wino_dgrad(g, am, self._ubf(e, True), act, sc, taylor, want_out, sp, True, tay_mode=tm)
         if cfg >= CFG_BF16:
             return T.conv_dgrad(g, am, e["wt"], act, sc, taylor, want_out, 3, cfg, sp, tay_mode=tm)
-        if cfg in (WINO4, WINO4W):
+        if cfg in _W4_VARIANT:
             if am is not None:
                 g = T.unpool2_nhwc(g, am)
             return T.conv_wino4_dgrad(g, self._u4(e, True), act, sc, taylor, want_out, tm, sp,
-                                      1 if cfg == WINO4W else 0)
+                                      _W4_VARIANT[cfg])
         if cfg == WINO_UNP:
             return T.conv_wino_dgrad(T.unpool2_nhwc(g, am), None, e["ut"], act, sc, taylor, want_out, sp, True,
                                      tay_mode=tm)
@@ -859,7 +896,7 @@ class FusedChainEngine:
     # GPU-bound down to B=8 (profiles/hip_graphs_taylor_step.txt), but with two batches in flight
     # the GPU finishes a B=100 step (~55 launches) faster than Python enqueues it: the host spent
     # 0.77-0.99 ms per batch in the pipeline against 0.85-1.04 ms of wall
-    # (scripts/b100_host_probe.py), so the pipelined launches replay one graph per slot. Large
+    # (scripts/probes/b100_host_probe.py), so the pipelined launches replay one graph per slot. Large
     # batches are GPU-bound: replay trims ~1% at B=2048, but the graphs' multi-GB private pools
     # then slowed later small-batch work in the same process by 7-17%
     # (profiles/bench/large_batch_graphs_vs_eager.txt), so the default stops at 1024.
@@ -1109,12 +1146,12 @@ class FusedChainEngine:
         return res
 
 
-KERNEL_FAMILIES = ("wino4", "wino4w", "wino2", "wino2_direct", "igemm", "wino2_bf16")
+KERNEL_FAMILIES = ("wino4", "wino4_m3", "wino4w", "wino2", "wino2_direct", "igemm", "wino2_bf16")
 
 
 def family_policy(family: str, split: str = "min"):
     """A :meth:`Autotuner.pinned` policy that runs every layer it can on one kernel family:
-    ``wino4`` F(4x4,3x3), ``wino4w`` its wide kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
+    ``wino4`` F(4x4,3x3) (split-points kernel), ``wino4_m3`` its MODE 3 kernel, ``wino4w`` its wide kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
     F(2x2) with direct patch loads, ``igemm`` the implicit GEMM (dense 2x2 GEMM, VALU first
     layer; with bf16 operands the bf16 implicit GEMM), ``wino2_bf16`` the bf16 F(2x2) kernels
     (compute_dtype=bfloat16 only). ``split``: the fewest ("min") or most ("max") channel splits of
@@ -1124,6 +1161,8 @@ def family_policy(family: str, split: str = "min"):
     def member(c):
         k = c[0]
         if family == "wino4":
+            return k == WINO4S
+        if family == "wino4_m3":
             return k == WINO4
         if family == "wino4w":
             return k == WINO4W
@@ -1220,8 +1259,11 @@ def maybe_engine(model, eval_modules, criterion, device, need_ce=True, why=None,
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda":
         return _reject(why, f"device {dev} is not a GPU")
-    if ops.backend() == "torch" or not ops.available():
-        return _reject(why, "native extension disabled (TORCHPRUNER_BACKEND=torch) or not built")
+    if ops.backend() == "torch":
+        return _reject(why, "native extension disabled (TORCHPRUNER_BACKEND=torch)")
+    if not ops.available():
+        from ..ops import _native
+        return _reject(why, f"native extension failed to load: {_native.load_error()!r}")
     if not engines_enabled():
         return _reject(why, "fused engines disabled (TORCHPRUNER_ENGINES=0)")
     if model.training:

@@ -54,13 +54,26 @@ def _unpool(gp, q, H, W):
     return full.view(B, C, H // 2, W // 2, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H, W)
 
 
+FLIP_RATE_BOUND = 1e-5  # decision flips per block allowed against fp64, per decision (tests, smoke)
+
+
+def flip_violations(flips: dict, totals: dict, rate: float = FLIP_RATE_BOUND) -> dict:
+    """Blocks whose engine-vs-fp64 decision flips exceed ``rate`` of their decisions:
+    {block: (flips, decisions)}. A kernel that systematically mis-decides values near 0 (sign
+    of zero, denormal flush, ``>=`` for ``>``) passes the mask-conditioned score check — it
+    compares arithmetic given the engine's own decisions — but not this bound."""
+    return {b: (flips[b], totals[b]) for b in flips if flips[b] > rate * totals[b]}
+
+
 @torch.no_grad()
-def engine_scores_fp64(engine, x, y, conditioned=True, mode="taylor"):
+def engine_scores_fp64(engine, x, y, conditioned=True, mode="taylor", totals=None):
     """Per-sample scores {block: (B, C_real) fp64} of one batch: ``mode="taylor"`` the signed
     sum_hw -(dL/da * a), ``"sensitivity"`` sum_hw |dL/da| (a = the block activation's output),
     with L the batch-mean cross-entropy. Returns (scores, flips): ``flips[block]`` counts the
-    units whose ReLU mask or pool argmax differs between the engine and plain fp64 (both runs
-    are computed; ``conditioned`` picks which decisions the returned scores use)."""
+    units whose ReLU mask or pool argmax differs between the engine and fp64 given the same
+    upstream decisions (both are computed; ``conditioned`` picks which decisions the returned
+    scores use and feed downstream). ``totals`` (a dict, optional) receives each block's number
+    of decisions (units of its activation), the denominator of :func:`flip_violations`."""
     plan = engine.plan
     saved = engine.forward(x)[1]
     acts_f = saved["acts"]
@@ -84,19 +97,23 @@ def engine_scores_fp64(engine, x, y, conditioned=True, mode="taylor"):
             q_f = acts_f[i][1].permute(0, 3, 1, 2)[:, :c].long().cpu().contiguous()
             m_f = hf > 0
             flips[i] = int(((m_f != m_own) | ((q_f != q_own) & (m_f | m_own))).sum())
+            if totals is not None:
+                totals[i] = int(m_f.numel())
             q, m = (q_f, m_f) if conditioned else (q_own, m_own)
             act = torch.where(m, win.gather(-1, q.unsqueeze(-1)).squeeze(-1), torch.zeros((), dtype=pre.dtype))
         else:
             m_own = pre > 0
             m_f = hf > 0
             flips[i] = int((m_f != m_own).sum())
+            if totals is not None:
+                totals[i] = int(m_f.numel())
             q, m = None, (m_f if conditioned else m_own)
             act = torch.where(m, pre, torch.zeros((), dtype=pre.dtype))
         convs.append((act, q, m, scale, H, W))
         h = act
     nconv = len(plan.convs)
     lin_in = [h.reshape(B, -1) if nconv else x.double().cpu().reshape(B, -1)]
-    lmask = []
+    lmask = {}  # linear index -> ReLU mask (no entry: no activation, identity in the backward)
     for j, lb in enumerate(plan.linears):
         w = lb.linear.weight.detach().double().cpu()
         b = lb.linear.bias.detach().double().cpu() if lb.linear.bias is not None else 0.0
@@ -106,9 +123,11 @@ def engine_scores_fp64(engine, x, y, conditioned=True, mode="taylor"):
             m_f = lin_f[j + 1].reshape(B, -1)[:, :n].cpu() > 0
             m_own = z > 0
             flips[nconv + j] = int((m_f != m_own).sum())
+            if totals is not None:
+                totals[nconv + j] = int(m_f.numel())
             m = m_f if conditioned else m_own
             z = torch.where(m, z, z * lb.slope)
-            lmask.append(m)
+            lmask[j] = m
         lin_in.append(z)
     logits = lin_in[-1]
     g = (torch.softmax(logits, 1) - F.one_hot(y.cpu(), logits.shape[1]).double()) / B
@@ -123,7 +142,8 @@ def engine_scores_fp64(engine, x, y, conditioned=True, mode="taylor"):
         ga = g @ plan.linears[j].linear.weight.detach().double().cpu()
         if j > 0:
             scores[nconv + j - 1] = score(ga, lin_in[j])
-            g = torch.where(lmask[j - 1], ga, ga * plan.linears[j - 1].slope)
+            m = lmask.get(j - 1)
+            g = ga if m is None else torch.where(m, ga, ga * plan.linears[j - 1].slope)
         elif nconv:
             act = convs[-1][0]
             g_out = ga.view(act.shape)

@@ -48,7 +48,10 @@ def load() -> bool:
 
 def _check_stamp():
     """Refuse a ``_C.so`` built from other sources than the tree it is loaded from (the build
-    stamps the hash of every source, header and flag into it, _build.source_hash)."""
+    stamps the hash of every source and header into it, _build.source_hash). Build flags are
+    stamped separately (_build.flag_hash): they depend on the build shell's environment
+    (PYTORCH_ROCM_ARCH, TORCHPRUNER_HIPFLAGS), so a mismatch there only warns — a correct binary
+    must not be refused because the loading shell's env differs."""
     from .. import _build
     if not (_build.CSRC / "kernels").is_dir():  # installed without sources: nothing to compare
         return
@@ -56,6 +59,17 @@ def _check_stamp():
     if got != want:
         raise RuntimeError(f"stale native extension {_LIB}: built from sources {got}, this tree is {want}; "
                            "rebuild with `python -m torchpruner_amd._build` (or __graft_entry__.build())")
+    fwant, fgot = _build.flag_hash(), _build.stamped_hash(_LIB, flags=True)
+    if fgot != fwant:
+        import warnings
+        warnings.warn(f"native extension {_LIB} was built with other flags ({fgot}) than this environment "
+                      f"implies ({fwant}: PYTORCH_ROCM_ARCH / TORCHPRUNER_HIPFLAGS / torch version); loading it",
+                      RuntimeWarning, stacklevel=3)
+
+
+def load_error():
+    """Why the extension failed to load (None when loaded or not tried)."""
+    return _error
 
 
 def available() -> bool:

@@ -69,10 +69,14 @@ class Pruner:
             logger.warning("no cascading modules defined")
             cascading_modules = []
 
-        # 1. NaN-probe: nanify the pruned output channels, record NaN input channels downstream
+        # 1. NaN-probe: nanify the pruned output channels, record NaN input channels downstream.
+        # What the probe finds lives in a per-call context, not on the modules (the
+        # reference stashes _nan_indices / _activation_len on them, pruner.py:155-167, which is
+        # not reentrant: two pruners probing one module would overwrite each other's findings)
+        probe = _ProbeRun()
         handles = [module.register_forward_hook(self._nanify_hook(indices))]
         for next_module in cascading_modules:
-            handles.append(next_module.register_forward_hook(self._detect_nan_hook()))
+            handles.append(next_module.register_forward_hook(self._detect_nan_hook(probe)))
         try:
             self._run_forward()
         finally:
@@ -81,13 +85,10 @@ class Pruner:
 
         # 2. Prune every cascading module whose input saw NaNs (inputs), then the module (outputs)
         for next_module in cascading_modules:
-            if hasattr(next_module, "_nan_indices"):
-                idx = getattr(next_module, "_nan_indices")
-                length = getattr(next_module, "_activation_len", None)
-                self._prune_module(next_module, _as_index_array(idx), direction="in", original_len=length)
-                delattr(next_module, "_nan_indices")
-            if hasattr(next_module, "_activation_len"):
-                delattr(next_module, "_activation_len")
+            idx = probe.nan_indices.get(next_module)
+            if idx is not None:
+                self._prune_module(next_module, _as_index_array(idx), direction="in",
+                                   original_len=probe.activation_len.get(next_module))
         self._prune_module(module, indices, direction="out")
 
     def prune_module(self, module, indices, direction="out", original_len=None):
@@ -218,12 +219,18 @@ class Pruner:
         return _hook
 
     @staticmethod
-    def _detect_nan_hook():
-        """Forward hook recording which input channels of a module carry NaNs."""
+    def _detect_nan_hook(probe=None):
+        """Forward hook recording which input channels of a module carry NaNs: into ``probe``
+        (a :class:`_ProbeRun`, what prune_model uses), or — called without one, as the
+        reference's own tests do (test_pruner.py:77-120) — as ``_nan_indices`` /
+        ``_activation_len`` attributes of the module."""
 
         def _hook(module, input, __):
             x = input[0]
-            setattr(module, "_activation_len", float(x.shape[1]))
+            if probe is not None:
+                probe.activation_len[module] = float(x.shape[1])
+            else:
+                setattr(module, "_activation_len", float(x.shape[1]))
             if x.dim() >= 2 and x.is_contiguous() and x.dtype == torch.float32:
                 flags = ops.nan_channels(x)
             else:
@@ -233,7 +240,10 @@ class Pruner:
                 flags = torch.isnan(v.sum(0).flatten(0))
             indices = flags.nonzero().flatten(0).cpu().numpy()
             if len(indices) > 0:
-                setattr(module, "_nan_indices", indices)
+                if probe is not None:
+                    probe.nan_indices[module] = indices
+                else:
+                    setattr(module, "_nan_indices", indices)
 
         return _hook
 
@@ -254,6 +264,15 @@ class Pruner:
             self.model.train(was_training)
             torch.backends.cudnn.deterministic = d
             torch.backends.cudnn.benchmark = b
+
+
+class _ProbeRun:
+    """What one NaN probe found, per cascading module (keyed by module object): the NaN input
+    channels and the input width (for the Dropout rescale)."""
+
+    def __init__(self):
+        self.nan_indices = {}
+        self.activation_len = {}
 
 
 def _set_width(module, direction, n):
