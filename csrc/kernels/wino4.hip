@@ -201,6 +201,7 @@ __device__ __forceinline__ void at6row(const f2v* t, f2v& y0, f2v& y1, f2v& y2, 
 // (ph 0) or added (ph 1) into the parked tile image
 template <int PH>
 __device__ __forceinline__ void sp_partial(const f32x4 (&acc)[NPT], int grp, int lane, float* ya, float* yb) {
+  grp &= 1;  // tile group within the parked half of 32 tiles
   const int j = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int nh = 0; nh < 2; ++nh) {
@@ -258,10 +259,13 @@ __device__ __forceinline__ void sp_partial(const f32x4 (&acc)[NPT], int grp, int
   }
 }
 
-__device__ __forceinline__ void sp_phase1(const f32x4 (&acc)[NPT], int ph, int grp, int lane, float* ya, float* yb) {
-  if (ph == 0) sp_partial<0>(acc, grp, lane, ya, yb);
+// active: the wave's tile group lies in the half of 32 tiles being parked (8-wave blocks park
+// their 64 tiles in two halves)
+__device__ __forceinline__ void sp_phase1(const f32x4 (&acc)[NPT], int ph, int grp, int lane, float* ya, float* yb,
+                                          bool active) {
+  if (active && ph == 0) sp_partial<0>(acc, grp, lane, ya, yb);
   __syncthreads();  // ph 1 adds after every ph 0 write has landed
-  if (ph == 1) sp_partial<1>(acc, grp, lane, ya, yb);
+  if (active && ph == 1) sp_partial<1>(acc, grp, lane, ya, yb);
 }
 
 // Epilogue of a block of NW waves holding PPW (16-tile group, 16-channel half) accumulator sets
@@ -269,13 +273,13 @@ __device__ __forceinline__ void sp_phase1(const f32x4 (&acc)[NPT], int ph, int g
 // v % (TB/16) and half v / (TB/16) (PPW = 1: MODE 2/3; PPW = 2: the wide kernel, one wave = one
 // group x both halves). Outputs are staged in LDS per half of 32 tiles (ya: channels 0-15, yb:
 // 16-31), then coalesced 128-B traffic; ``part`` receives per-(tile, channel) partial sums
-// (TB x 32 floats). SPP: the split-points kernel (NW = 4, 32 tiles): phase 1 is sp_phase1.
+// (TB x 32 floats). SPP: the split-points kernels (NW = 4 / 8: 32 / 64 tiles): phase 1 is sp_phase1.
 template <int EPI, int S, int NW, int PPW = 1, bool SPP = false>
 __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], int t0, int k0, float* ya, float* yb,
                                          float* part) {
   constexpr int TPR = S / 4, TI = TPR * TPR;
   constexpr int GROUPS = NW * PPW / 2, TB = 16 * GROUPS, HALVES = TB / 32, TPW = 32 / NW;  // tiles per wave (phase 2)
-  static_assert(!SPP || (NW == 4 && PPW == 1), "split-points epilogue: 32-tile blocks of 4 waves");
+  static_assert(!SPP || PPW == 1, "split-points epilogue: one accumulator set per wave");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
   const bool want_part = EPI == BWD ? p.taylor != nullptr : p.apoz != nullptr;
@@ -289,7 +293,7 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
 #pragma unroll
   for (int hf = 0; hf < HALVES; ++hf) {
     // ---- phase 1: output transform; park this half's 32 tiles x 16 px x (16 + 16) ch -------
-    if constexpr (SPP) sp_phase1(acc[0], wave >> 1, wave & 1, lane, ya, yb);
+    if constexpr (SPP) sp_phase1(acc[0], wave / GROUPS, wave % GROUPS, lane, ya, yb, (wave % GROUPS) / 2 == hf);
 #pragma unroll
     for (int pp = 0; pp < (SPP ? 0 : PPW); ++pp) {
       const int vw = wave + NW * pp, grp = vw % GROUPS, nh = vw / GROUPS;
@@ -859,6 +863,7 @@ __device__ __forceinline__ void sp_mfma_chunk(int c, int nc, const f2v (&w)[18],
 template <int EPI, int S, int NW, bool SPREAD = false, bool SPLITP = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   static_assert(!SPREAD || NW == 4, "SPREAD is the 4-wave (two blocks per CU) schedule");
+  // (an 8-wave 64-tile split-points build measured 5-8% slower than the 4-wave one: not built)
   static_assert(!SPLITP || (NW == 4 && !SPREAD), "split points: 4-wave blocks, burst DMA");
   constexpr int TB = 8 * NW, NG = NW / 2;  // tiles per block, 16-tile groups
   constexpr bool XDBL = NW == 8;           // X double-buffered (one block per CU)
@@ -994,13 +999,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
       f2v w[18];
       if (nh == 0) sp_read_transform<S, G, 0>(xb + poff, w);  // wave-uniform branch
       else sp_read_transform<S, G, 1>(xb + poff, w);
-      lds_barrier();  // every wave has its patch: X(c+1) into the single buffer
-      if (c + 1 < nc) stage_x(8 * (c + 1), xs0);
+      if constexpr (!XDBL) {
+        lds_barrier();  // every wave has its patch: X(c+1) into the single buffer
+        if (c + 1 < nc) stage_x(8 * (c + 1), xs0);
+      }
       sp_mfma_chunk(c, nc, w, ul, acc, [&]() {
-        if (c + 1 < nc) wait_but_x();
+        if (!XDBL && c + 1 < nc) wait_but_x();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         if (c + 1 < nc) stage_u(8 * (c + 1), 0);
+        if (XDBL && c + 2 < nc) stage_x(8 * (c + 2), xb);
       }, nh);
       continue;
     }
