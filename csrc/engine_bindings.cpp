@@ -95,7 +95,8 @@ int tp_wino4_ok(int H, int W, int C, int K);
 int tp_wino4_lds_bytes(int S, int variant);
 hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act, float* taylor,
-                         float* apoz, int tay_mode, int splits, float* ws, int variant, hipStream_t st);
+                         float* apoz, int tay_mode, int splits, float* ws, int variant, hipStream_t st,
+                         const uint8_t* unpool_am);
 }
 
 namespace {
@@ -495,14 +496,17 @@ std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at:
   TP_CHECK_HIP(tp_conv_wino4(x.data_ptr<float>(), u.data_ptr<float>(), (int)B, (int)H, (int)C, (int)K,
                              pool ? EPI_FWD_POOL : EPI_FWD, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
                              pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap, 0, (int)sp,
-                             sp > 1 ? ws.data_ptr<float>() : nullptr, (int)variant, cur_stream()));
+                             sp > 1 ? ws.data_ptr<float>() : nullptr, (int)variant, cur_stream(), nullptr));
   return {out, am};
 }
 
-// F(4x4) dgrad with the conv_wino_dgrad epilogue contract (no unpooling: pass the unpooled grad)
+// F(4x4) dgrad with the conv_wino_dgrad epilogue contract (input: the unpooled grad). unpool_am
+// (B, H, W, Cin) uint8, with want_out and one K pass: the output is written unpooled through those
+// 2x2-pool argmax bytes at (B, 2H, 2W, Cin) — the operand of the previous layer's data gradient
 at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at::Tensor& act,
                             const c10::optional<at::Tensor>& bn_scale, const c10::optional<at::Tensor>& taylor,
-                            bool want_out, int64_t tay_mode, int64_t splits, int64_t variant) {
+                            bool want_out, int64_t tay_mode, int64_t splits, int64_t variant,
+                            const c10::optional<at::Tensor>& unpool_am) {
   need(g, "g", 4);
   need(act, "act", 4);
   const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
@@ -522,15 +526,24 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
     (void)R;
     tay = taylor->data_ptr<float>();
   }
-  at::Tensor out;
-  if (want_out) out = at::empty({B, H, W, Cin}, g.options());
   const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, Cout / 8));
+  const uint8_t* unp = nullptr;
+  if (unpool_am.has_value() && unpool_am->defined()) {
+    const auto& m = *unpool_am;
+    TORCH_CHECK(want_out && sp == 1, "fused unpooling needs want_out and one K pass (splits=1)");
+    TORCH_CHECK(m.is_cuda() && m.scalar_type() == at::kByte && m.is_contiguous() && m.dim() == 4 && m.size(0) == B &&
+                    m.size(1) == H && m.size(2) == W && m.size(3) == Cin,
+                "unpool_am must be contiguous uint8 (B, H, W, Cin) argmax bytes on the GPU");
+    unp = m.data_ptr<uint8_t>();
+  }
+  at::Tensor out;
+  if (want_out) out = unp ? at::empty({B, 2 * H, 2 * W, Cin}, g.options()) : at::empty({B, H, W, Cin}, g.options());
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
   TP_CHECK_HIP(tp_conv_wino4(g.data_ptr<float>(), ut.data_ptr<float>(), (int)B, (int)H, (int)Cout, (int)Cin, EPI_BWD,
                              sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(),
                              tay, nullptr, (int)tay_mode, (int)sp, sp > 1 ? ws.data_ptr<float>() : nullptr,
-                             (int)variant, cur_stream()));
+                             (int)variant, cur_stream(), unp));
   return out;
 }
 
@@ -948,7 +961,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_wino4_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, "
         "Tensor(a!)? apoz=None, int splits=1, int variant=0) -> (Tensor, Tensor)");
   m.def("conv_wino4_dgrad(Tensor g, Tensor ut, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, bool want_out, "
-        "int tay_mode=0, int splits=1, int variant=0) -> Tensor");
+        "int tay_mode=0, int splits=1, int variant=0, Tensor? unpool_am=None) -> Tensor");
 }
 
 void register_engine_ops_impl(torch::Library& m) {

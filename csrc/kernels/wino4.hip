@@ -89,6 +89,9 @@ struct Args {
   int pool_order;     // PARTIAL: rows in pooled order (b, y/2, x/2, y&1, x&1) for a pooled combine
   int dbg;            // phase-cost experiments only (TP_W4_DBG; results are WRONG when set): 1 no U DMA,
                       // 2 no X DMA, 16 no epilogue
+  const uint8_t* unp; // BWD with out: the argmax bytes (B,S,S,K) of the 2x2 pool that produced the
+                      // activation; ``out`` is then written unpooled at (B,2S,2S,K) (the consumer's
+                      // full-resolution operand: no separate unpooling pass)
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -188,7 +191,7 @@ __device__ __forceinline__ void output_transform(const float (&m)[36], float (&y
 // holds rows 3ph..3ph+2 of the 6x6 transform-point grid (acc[nh * 18 + 6 rr + c]) for its 16
 // tiles x both 16-channel halves. Y = A^T M A is linear in M, so each wave forms the partial
 // output of its three rows; the ph = 0 waves write it into ya / yb, the ph = 1 waves add theirs
-// (fixed order: one add per output, deterministic). Partial column passes:
+// with LDS float adds (fixed order: one add per output after the write, deterministic). Partial column passes:
 //   ph 0 (rows 0-2): t0 = m0 + m1 + m2, t1 = t3 = m1 - m2, t2 = m1 + m2
 //   ph 1 (rows 3-5): t0 = s, t1 = 2d, t2 = 4s, t3 = 8d + m5   (s = m3 + m4, d = m3 - m4)
 // and for ph 1 the row pass runs on s, d, m5 once each (at6 is linear), the scalings folding
@@ -251,8 +254,10 @@ __device__ __forceinline__ void sp_partial(const f32x4 (&acc)[NPT], int grp, int
           else if (row == 1) add = 2.f * yd[col];
           else if (row == 2) add = 4.f * ys[col];
           else add = 8.f * yd[col] + y5[col];
-          dst[q * 16] += add.x;
-          dst[TPL + q * 16] += add.y;
+          // one LDS add per output (ds_add_f32, no return) instead of a read-modify-write: each
+          // address receives exactly this one add after the ph 0 write, so the order is fixed
+          atomicAdd(dst + q * 16, add.x);
+          atomicAdd(dst + TPL + q * 16, add.y);
         }
       }
     }
@@ -414,7 +419,20 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
                 f32x4 v;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = a[e] > 0.f ? yv[e] * sc4[e] : 0.f;
-                *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+                if (p.unp) {  // the 2x2 window of this pooled pixel: v at its argmax, 0 elsewhere
+                  const unsigned am4 = *reinterpret_cast<const unsigned*>(p.unp + pix * p.K + k);
+                  const int yy = 4 * tr + (q >> 2), xx = 4 * tc + (q & 3);
+                  const long long o00 = (((long long)b * 2 * S + 2 * yy) * 2 * S + 2 * xx) * p.K + k;
+#pragma unroll
+                  for (int w = 0; w < 4; ++w) {
+                    f32x4 o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = ((am4 >> (8 * e)) & 0xffu) == (unsigned)w ? v[e] : 0.f;
+                    *reinterpret_cast<f32x4*>(p.out + o00 + ((long long)(w >> 1) * 2 * S + (w & 1)) * p.K) = o;
+                  }
+                } else {
+                  *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+                }
               }
             }
           }
@@ -1422,7 +1440,7 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
 extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi,
                                     const float* scale, const float* shift, int relu, float* out, uint8_t* out_argmax,
                                     const float* act, float* taylor, float* apoz, int tay_mode, int splits,
-                                    float* ws, int variant, hipStream_t st) {
+                                    float* ws, int variant, hipStream_t st, const uint8_t* unpool_am) {
   using namespace tp::w4;
   if (!tp_wino4_ok(S, S, C, K) || B <= 0) return hipErrorInvalidValue;
   const int nc = C / 8;
@@ -1432,6 +1450,10 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   const bool wide = variant == 1;
   if (splits > 1 && ((variant == 0 && kernel_mode() < 2) || !ws)) return hipErrorInvalidValue;
   if (epi < 0 || epi > 2 || (epi == BWD && !act) || (epi != BWD && !out) || (epi == FWD_POOL && !out_argmax))
+    return hipErrorInvalidValue;
+  // fused unpooling: the data gradient's full-resolution output, one K pass (the split-K combine
+  // writes pooled rows)
+  if (unpool_am && (epi != BWD || !out || splits > 1 || 2ll * B * 2 * S * 2 * S * K >= (1ll << 31)))
     return hipErrorInvalidValue;
   Args a{};
   a.x = x;
@@ -1454,6 +1476,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   a.taylor = epi == BWD ? taylor : nullptr;
   a.apoz = epi == BWD ? nullptr : apoz;
   a.tay_mode = tay_mode;
+  a.unp = unpool_am;
   static const int dbg = [] {
     const char* d = getenv("TP_W4_DBG");
     const int v = d ? atoi(d) : 0;

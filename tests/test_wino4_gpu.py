@@ -156,3 +156,29 @@ def test_wino4_split_k(cuda, S, C, K, B, splits, variant):
     assert ((s1 - s2).abs().max() / s1.abs().max()).item() < 1e-4
     o3 = T.conv_wino4_dgrad(go, ut, act, scp, None, True, 0, splits, variant)
     assert torch.equal(o2, o3)  # deterministic combine
+
+
+@pytest.mark.parametrize("S,C,K,B", [(16, 64, 128, 3), (8, 128, 256, 2), (4, 256, 512, 5), (8, 32, 64, 1)])
+@pytest.mark.parametrize("variant", [0, 3])
+def test_wino4_dgrad_fused_unpool(cuda, S, C, K, B, variant):
+    """The data gradient written unpooled through the previous block's 2x2-pool argmax bytes
+    (engine: no separate unpooling pass) == the pooled output followed by unpool2_nhwc, bit for
+    bit, with the Taylor partials unchanged."""
+    T = _ops()
+    Cout, Cin = C, K
+    g = torch.Generator(device=cuda).manual_seed(S + C + K + B)
+    go = torch.randn(B, S, S, Cout, device=cuda, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, device=cuda, generator=g) / (3 * Cin ** 0.5)
+    act = torch.relu(torch.randn(B, S, S, Cin, device=cuda, generator=g))
+    sc = torch.rand(Cin, device=cuda, generator=g) + 0.5
+    am = torch.randint(0, 4, (B, S, S, Cin), device=cuda, generator=g, dtype=torch.uint8)
+    ut = T.wino4_weights(w, True, 0, 0)
+    t1 = torch.zeros(2, B, Cin, device=cuda)
+    t2 = torch.zeros(2, B, Cin, device=cuda)
+    ref = T.unpool2_nhwc(T.conv_wino4_dgrad(go, ut, act, sc, t1, True, 0, 1, variant), am)
+    got = T.conv_wino4_dgrad(go, ut, act, sc, t2, True, 0, 1, variant, am)
+    assert got.shape == (B, 2 * S, 2 * S, Cin)
+    assert torch.equal(got, ref)
+    assert torch.equal(t1, t2)
+    with pytest.raises(RuntimeError):  # split-K combines pooled rows: the fused path is one K pass
+        T.conv_wino4_dgrad(go, ut, act, sc, None, True, 0, 2, variant, am)

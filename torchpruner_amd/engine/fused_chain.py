@@ -56,6 +56,9 @@ WINO_BF_UNP = -7  # its dgrad of a pooled layer after an explicit unpool (as WIN
 WINO4S = -8  # F(4x4) MODE 3 with split transform points (wino4.hip variant 3): each wave of a 16-tile
              # pair owns 18 of the 36 points x all 32 outputs, so each wave forms half of V = B^T d B
              # (72 packed VALU ops per 72 MFMAs instead of 168): the default F(4x4) kernel
+WINO4S_FU = -11  # its data gradient writing the output unpooled through the previous block's pool
+                 # argmax (one K pass): no separate unpooling pass for the next data gradient
+WINO4_FU = -12  # the same with the MODE 3 kernel
 CFG_BF16 = 256  # tile-config flag of conv_igemm: bf16 operands / fp32 accumulation (opt-in, compute_dtype)
 _BF16_CFGS = (0, 2, 3)  # the implicit-GEMM tiles built with bf16 variants (conv_mfma.hip launch_any)
             # than F(2x2); dgrads of pooled layers take the explicit unpool first
@@ -109,6 +112,8 @@ def _wino4_ok(H, W, C, K):
 
 _W4_SPLITS = os.environ.get("TORCHPRUNER_W4_SPLITS", "1") != "0"
 _TUNER_LOG = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") != "0"  # print every timed kernel choice
+_TUNE_ROUNDS = int(os.environ.get("TORCHPRUNER_TUNE_ROUNDS", "3"))
+_TUNE_MARGIN = float(os.environ.get("TORCHPRUNER_TUNE_MARGIN", "0.02"))
 
 
 # the WIDE F(4x4) kernel (variant 1) is correct but measured 0.8x the MODE 3 kernel on every VGG
@@ -116,7 +121,8 @@ _TUNER_LOG = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") != "0"  # print every 
 _W4_WIDE = os.environ.get("TORCHPRUNER_W4_WIDE", "0") != "0"
 
 
-_W4_VARIANT = {WINO4: 0, WINO4W: 1, WINO4S: 3}
+_W4_VARIANT = {WINO4: 0, WINO4W: 1, WINO4S: 3, WINO4S_FU: 3, WINO4_FU: 0}
+_W4_FUSED = (WINO4S_FU, WINO4_FU)
 
 
 def _wino4_cands(B, H, W, K, C):
@@ -250,18 +256,28 @@ class Autotuner:
                 res = (WINO_LDS, _wino_splits(wino[0], N, wino[1])) if wino is not None else _pick_cfg(M, N, K)
             self.cache[key] = res
             return res
-        best = None
-        for cand in (cands if cands is not None else self.candidates(M, N, K, wino, wino_only and wino is not None)):
-            run(*cand)  # warm
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(2):
-                run(*cand)
-            e1.record()
-            e1.synchronize()
-            t = e0.elapsed_time(e1)
-            if best is None or t < best[0]:
-                best = (t, cand)
+        # every candidate timed round-robin (warm launch, then the min over _TUNE_ROUNDS rounds of 2
+        # launches): back-to-back timings of configs within a few % of each other are dominated by
+        # clock (DVFS) drift, which made single-shot choices vary from box to box; and the untuned
+        # pick (lst[0], what TUNER.fixed() runs) is kept unless another is _TUNE_MARGIN faster
+        lst = list(cands if cands is not None else self.candidates(M, N, K, wino, wino_only and wino is not None))
+        times = {}
+        for r in range(_TUNE_ROUNDS):
+            for cand in lst:
+                if r == 0:
+                    run(*cand)  # warm
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(2):
+                    run(*cand)
+                e1.record()
+                e1.synchronize()
+                t = e0.elapsed_time(e1)
+                times[cand] = min(times.get(cand, t), t)
+        fast = min(lst, key=lambda c: times[c])
+        best = (times[fast], fast)
+        if times[lst[0]] <= times[fast] * (1.0 + _TUNE_MARGIN):
+            best = (times[lst[0]], lst[0])
         self.cache[key] = best[1]
         if _TUNER_LOG:
             print(f"[tuner] {key} -> {best[1]} ({best[0] / 2 * 1e3:.1f} us)", file=sys.stderr, flush=True)
@@ -271,7 +287,8 @@ class Autotuner:
 TUNER = Autotuner()
 
 _KIND_NAMES = {WINO: "wino2_direct", WINO_LDS: "wino2", WINO_UNP: "wino2_unpool", WINO4: "wino4_m3", WINO4W: "wino4w",
-               WINO_BF: "wino2_bf16", WINO_BF_UNP: "wino2_bf16_unpool", WINO4S: "wino4", -10: "first_direct"}
+               WINO_BF: "wino2_bf16", WINO_BF_UNP: "wino2_bf16_unpool", WINO4S: "wino4", -10: "first_direct",
+               WINO4S_FU: "wino4_fused_unpool", WINO4_FU: "wino4_m3_fused_unpool"}
 
 
 def kernel_name(cfg: int) -> str:
@@ -663,8 +680,12 @@ class FusedChainEngine:
         """bf16-operand implicit-GEMM candidates ([0] = the untuned pick)."""
         return [(CFG_BF16 + c, s_) for c, s_ in TUNER.candidates(M, N, K) if c in _BF16_CFGS]
 
-    def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0):
-        """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|."""
+    def _dgrad_run(self, T, e, g, am, act, sc, taylor, want_out, cfg, sp, sc4=None, tm=0, unp=None):
+        """``tm``: score partials the epilogue writes — 0 Taylor -(g*a), 1 Sensitivity |g|.
+        ``unp``: argmax bytes of the 2x2 pool that produced ``act``: an F(4x4) kernel in one K
+        pass then writes its output unpooled (full resolution, the previous layer's operand)."""
+        assert (unp is not None) == (cfg in _W4_FUSED) and (unp is None or (sp == 1 and want_out)), \
+            "fused unpooling: the F(4x4) *_FU kinds, splits=1, with an output"
         if cfg in (WINO_BF, WINO_BF_UNP):
             if cfg == WINO_BF_UNP:
                 g, am = T.unpool2_nhwc(g, am), None
@@ -675,7 +696,7 @@ class FusedChainEngine:
             if am is not None:
                 g = T.unpool2_nhwc(g, am)
             return T.conv_wino4_dgrad(g, self._u4(e, True), act, sc, taylor, want_out, tm, sp,
-                                      _W4_VARIANT[cfg])
+                                      _W4_VARIANT[cfg], unp)
         if cfg == WINO_UNP:
             return T.conv_wino_dgrad(T.unpool2_nhwc(g, am), None, e["ut"], act, sc, taylor, want_out, sp, True,
                                      tay_mode=tm)
@@ -1096,10 +1117,13 @@ class FusedChainEngine:
             g = T.conv_dgrad(g, None, e["wt"], act, bn_scale, taylor, want_out, 1, cfg, sp, tay_mode=tm, slope=slope)
         # conv stack: g is dL/d(pre-activation of conv nconv-1) * bn_scale, at the
         # (pooled, if pooled) output resolution of that block
+        unpooled = False  # the previous data gradient already wrote g at full resolution
         for ci in range(nconv - 1, 0, -1):
             e = P["convs"][ci]
             prev_act = acts[ci - 1][0]
             _, am = acts[ci]
+            if unpooled:
+                am = None
             taylor = None
             if (ci - 1) in want:
                 taylor = arena[ci - 1]
@@ -1136,22 +1160,37 @@ class FusedChainEngine:
                 cands = TUNER.candidates(M, Cin, e["wt"].shape[1], wino, True)
             if not self.bf16 and self.use_wino and _wino4_ok(H, W, Cg, Cin) and "w4d" in e and cands is not None:
                 cands = _wino4_cands(B, H, W, Cin, Cg) + cands  # [0] = the untuned pick
+            # the previous block pools: an F(4x4) data gradient in one K pass writes its output unpooled
+            # through that pool's argmax (no separate unpooling pass: its read of the pooled
+            # gradient and the second write are saved); other kernels hand the pooled gradient on
+            unp = acts[ci - 1][1] if need_out and not self.bf16 else None
+            if unp is not None and cands is not None and any(c[0] in (WINO4S, WINO4) for c in cands):
+                cands = cands + [(WINO4S_FU, 1), (WINO4_FU, 1)]  # timed against unfused + explicit unpool
+
+            def fuse(c, s_, unp=unp):
+                return unp if c in _W4_FUSED else None
+
+            def trial(c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4, unp=unp):
+                out = self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_, s4, unp=fuse(c, s_))
+                if unp is not None and c not in _W4_FUSED:
+                    T.unpool2_nhwc(out, unp)  # the unpooling pass the next data gradient then runs
+                return out
+
             cfg, sp = TUNER.choose(("bwd", tuple(g.shape), tuple(prev_act.shape), am is not None, wino is not None,
-                                    self.bf16),
-                                   M, Cin, e["wt"].shape[1],
-                                   lambda c, s_, e=e, gg=gg, am=am, pa=prev_act, sc=sc_prev, no=need_out, s4=sc4:
-                                   self._dgrad_run(T, e, gg, am, pa, sc, None, no, c, s_, s4), wino, wino_only=True,
-                                   cands=cands)
-            g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp, sc4, tm)
+                                    self.bf16, unp is not None),
+                                   M, Cin, e["wt"].shape[1], trial, wino, wino_only=True, cands=cands)
+            g = self._dgrad_run(T, e, g, am, prev_act, sc_prev, taylor, need_out, cfg, sp, sc4, tm, unp=fuse(cfg, sp))
+            unpooled = fuse(cfg, sp) is not None
         return res
 
 
-KERNEL_FAMILIES = ("wino4", "wino4_m3", "wino4w", "wino2", "wino2_direct", "igemm", "wino2_bf16")
+KERNEL_FAMILIES = ("wino4", "wino4_fused", "wino4_m3", "wino4w", "wino2", "wino2_direct", "igemm", "wino2_bf16")
 
 
 def family_policy(family: str, split: str = "min"):
     """A :meth:`Autotuner.pinned` policy that runs every layer it can on one kernel family:
-    ``wino4`` F(4x4,3x3) (split-points kernel), ``wino4_m3`` its MODE 3 kernel, ``wino4w`` its wide kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
+    ``wino4`` F(4x4,3x3) (split-points kernel), ``wino4_fused`` the same with the data gradients of
+    pooled blocks unpooling in their epilogue, ``wino4_m3`` its MODE 3 kernel, ``wino4w`` its wide kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
     F(2x2) with direct patch loads, ``igemm`` the implicit GEMM (dense 2x2 GEMM, VALU first
     layer; with bf16 operands the bf16 implicit GEMM), ``wino2_bf16`` the bf16 F(2x2) kernels
     (compute_dtype=bfloat16 only). ``split``: the fewest ("min") or most ("max") channel splits of
@@ -1162,6 +1201,8 @@ def family_policy(family: str, split: str = "min"):
         k = c[0]
         if family == "wino4":
             return k == WINO4S
+        if family == "wino4_fused":  # the split-points kernel, data gradients unpooling in their epilogue
+            return k in (WINO4S_FU, WINO4S)
         if family == "wino4_m3":
             return k == WINO4
         if family == "wino4w":
@@ -1182,6 +1223,8 @@ def family_policy(family: str, split: str = "min"):
             return _pick_cfg(M, N, K)  # dgrad lists hold the Winograd kinds only
         if not hit:
             return None
+        if family == "wino4_fused" and any(c[0] == WINO4S_FU for c in hit):
+            return (WINO4S_FU, 1)
         return (min if split == "min" else max)(hit, key=lambda c: c[1])
 
     return policy
