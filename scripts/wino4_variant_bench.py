@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[2048, 100])
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 3])
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--real", action="store_true", help="engine-like operands: post-ReLU forward inputs, "
+                                                        "half-zero (ReLU-masked) output gradients")
     ap.add_argument("--rounds", type=int, default=3, help="variants timed round-robin this many times (min kept): "
                                                          "DVFS drifts between back-to-back configs")
     args = ap.parse_args()
@@ -71,10 +73,14 @@ def main():
         for S, C, K, pool in LAYERS:
             g = torch.Generator(device=dev).manual_seed(S + C + K)
             x = torch.randn(B, S, S, C, device=dev, generator=g)
+            if args.real:
+                x = torch.relu(x)
             w = torch.randn(K, C, 3, 3, device=dev, generator=g) * 0.05
             sc, sh = torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev) * 0.1
             u4 = T.wino4_weights(w, False, 0, 0)
             gg = torch.randn(B, S, S, K, device=dev, generator=g)
+            if args.real:
+                gg = gg * (torch.rand(B, S, S, K, device=dev, generator=g) > 0.5)
             act = torch.relu(torch.randn(B, S, S, C, device=dev, generator=g))
             scp = torch.rand(C, device=dev) + 0.5
             ut4 = T.wino4_weights(w, True, 0, 0)

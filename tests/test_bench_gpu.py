@@ -31,6 +31,9 @@ def test_bench_self_launches_two_ranks(cuda):
     assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 128
     assert out["teacher_sync"]["agreed_before_broadcast"] is True  # deterministic native training
     assert out["value"] > 0
+    # diagnosability: per-phase wall seconds and the per-layer kernel choices of this box
+    assert {"teacher", "headline", "total"} <= set(out["phase_wall_s"])
+    assert out["tuner_choices"]["headline"], out["tuner_choices"]
 
 
 @pytest.mark.timeout(320)
@@ -54,6 +57,10 @@ def test_bench_config5_two_ranks(cuda):
     assert cfg["in_sync"] is True and cfg["loss_finite"] is True
     before, after = cfg["params_before_after"]
     assert after < before  # really pruned, DDP rebuilt on the new shapes
+    # iterative: two prune -> rewrap -> finetune rounds (momentum sliced twice), each timed
+    rounds = cfg["rounds"]
+    assert len(rounds) == 2 and all(r["img_s"] > 0 and r["in_sync"] for r in rounds)
+    assert before > rounds[0]["params"] > rounds[1]["params"] == after
     q = out["resnet50_prune_finetune"]
     assert q["teacher_agreed_before_broadcast"] is True  # identical deterministic teachers
     assert q["taylor_in_sync"] is True and q["random_in_sync"] is True

@@ -145,6 +145,50 @@ def iterative_prune(model, task, method, seed, cfg, log=None):
     return model
 
 
+ONESHOT_FRACS = (0.3, 0.5)
+ONESHOT_RECAL = 8  # BN re-estimation batches after a one-shot prune (no finetuning)
+
+
+def oneshot_prune(model, task, method, seed, cfg, frac):
+    """One-shot structured pruning without any finetuning (the reference's notebooks never
+    finetune after pruning, nbUNT:169-193 / nbVGG:1233-1285): every conv of the teacher is
+    scored ONCE (Taylor over ``score_imgs`` held-out images, one ``run_many`` over all convs, or
+    random scores), ``frac`` of each conv's lowest-scored filters are pruned for real
+    (``Pruner.prune_model`` + cascade), and only the BatchNorm running statistics are
+    re-estimated (``ONESHOT_RECAL`` batches). Measures the ranking itself: nothing retrains."""
+    dev = next(model.parameters()).device
+    graph = [(m, c) for m, c in get_vgg_pruning_graph(model) if isinstance(m, torch.nn.Conv2d)]
+    convs = [m for m, _ in graph]
+    if method == "taylor":
+        xs, ys = task.sample(cfg["score_imgs"], seed * 7 + 11)
+        model.eval()
+        with TUNER.fixed():
+            scores = TaylorAttributionMetric(model, DeviceLoader(xs, ys, 100), F.cross_entropy, dev,
+                                             shard_data=False).run_many(convs, find_best_evaluation_module=True)
+    else:
+        rng = np.random.RandomState(seed * 31 + int(frac * 100))
+        scores = [rng.random_sample(m.out_channels) for m in convs]
+    pruner = Pruner(model, (3, 32, 32), dev, sync_indices=False)
+    for (module, cascade), s in zip(graph, scores):  # out-channel indices are unchanged by earlier cuts
+        cut = int(len(s) * frac)
+        if cut > 0:
+            pruner.prune_model(module, np.argsort(s, kind="stable")[:cut], cascading_modules=cascade)
+    recalibrate(model, task, seed * 1000 + 777, dict(cfg, recal_batches=ONESHOT_RECAL))
+    model.zero_grad(set_to_none=True)
+    return model
+
+
+def oneshot_top1(teacher, task, seed, cfg, xv, yv):
+    """{"top1_pruned_{30,50}pct_oneshot_{taylor,random}": top-1} of one teacher."""
+    out = {}
+    for frac in ONESHOT_FRACS:
+        for method in ("taylor", "random"):
+            m = oneshot_prune(copy.deepcopy(teacher), task, method, seed, cfg, frac)
+            out[f"top1_pruned_{int(frac * 100)}pct_oneshot_{method}"] = top1(m, xv, yv)
+            del m
+    return out
+
+
 def weights_digest(model) -> str:
     h = hashlib.sha256()
     for t in model.state_dict().values():
@@ -160,6 +204,7 @@ def run_protocol(seed=0, device="cuda", log=None, **overrides):
     xv, yv = task.sample(cfg["val_imgs"], seed * 7 + 3)
     before = top1(teacher, xv, yv)
     out = {"seed": seed, "top1_before": before, "teacher_digest": weights_digest(teacher)}
+    out.update(oneshot_top1(teacher, task, seed, cfg, xv, yv))
     for method in ("taylor", "random"):
         m = iterative_prune(copy.deepcopy(teacher), task, method, seed, cfg, log=log)
         out[f"top1_pruned_{method}"] = top1(m, xv, yv)

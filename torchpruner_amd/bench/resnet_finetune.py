@@ -58,7 +58,7 @@ def _timed(fn, world):
 
 
 def finetune_throughput(dev, world, rank, steps=10, warmup=3, batch=128, res=224, frac=0.2, seed=0,
-                        score_batch=64):
+                        score_batch=64, rounds=2):
     torch.manual_seed(seed)
     model = resnet50().to(dev).to(memory_format=torch.channels_last)
     sync = pdist.sync_module(model)
@@ -75,30 +75,42 @@ def finetune_throughput(dev, world, rank, steps=10, warmup=3, batch=128, res=224
     train(wrapper, dev, F.cross_entropy, stream(2, seed + 1), opt, 0, log_every=0)  # momentum buffers exist
     _, dt_dense = _timed(lambda: train(wrapper, dev, F.cross_entropy, stream(steps, seed + 2), opt, 0, log_every=0),
                          world)
-    t0 = time.perf_counter()
-    model.eval()
-    graph = get_resnet_pruning_graph(model)
-    scores = TaylorAttributionMetric(model, stream(1, seed + 3, score_batch), F.cross_entropy, dev).run_many(
-        [m for m, _ in graph], find_best_evaluation_module=True)
-    _prune_all(model, pruner, scores, frac)
-    wrapper.rewrap()
-    t_prune = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    train(wrapper, dev, F.cross_entropy, stream(warmup, seed + 4), opt, 1, log_every=0)  # new shapes: tune
-    torch.cuda.synchronize()
-    t_warm = time.perf_counter() - t0
-    (loss, _), dt = _timed(lambda: train(wrapper, dev, F.cross_entropy, stream(steps, seed + 5), opt, 1,
-                                         log_every=0), world)
+    # the iterative loop (nbUNT:169-193 prunes layer after layer, then trains): ``rounds`` rounds
+    # of [data-parallel Taylor scores -> prune frac of every prunable conv (parameters, grads and
+    # momentum sliced, R5) -> DDP rewrap (R7) -> new-shape warm-up -> timed finetune segment]
+    per_round, t_prune, t_warm, tot_imgs, tot_dt, loss = [], [], [], 0, 0.0, float("nan")
+    for r in range(rounds):
+        t0 = time.perf_counter()
+        model.eval()
+        graph = get_resnet_pruning_graph(model)
+        scores = TaylorAttributionMetric(model, stream(1, seed + 3 + 10 * r, score_batch), F.cross_entropy,
+                                         dev).run_many([m for m, _ in graph], find_best_evaluation_module=True)
+        _prune_all(model, pruner, scores, frac)
+        wrapper.rewrap()
+        t_prune.append(round(time.perf_counter() - t0, 2))
+        t0 = time.perf_counter()
+        train(wrapper, dev, F.cross_entropy, stream(warmup, seed + 4 + 10 * r), opt, 1, log_every=0)  # new shapes
+        torch.cuda.synchronize()
+        t_warm.append(round(time.perf_counter() - t0, 2))
+        (loss, _), dt = _timed(lambda: train(wrapper, dev, F.cross_entropy, stream(steps, seed + 5 + 10 * r), opt,
+                                             1, log_every=0), world)
+        per_round.append({"round": r + 1, "img_s": round(steps * batch * world / dt, 1),
+                          "params": count_parameters(model), "in_sync": params_in_sync(model)})
+        tot_imgs += steps * batch * world
+        tot_dt += dt
+    dt = tot_dt / rounds
     out = {
-        "resnet50_finetune_img_s": round(steps * batch * world / dt, 1),
+        "resnet50_finetune_img_s": round(tot_imgs / tot_dt, 1),
         "resnet50_train_dense_img_s": round(steps * batch * world / dt_dense, 1),
         "resnet50_finetune_config": {
             "per_gpu_batch": batch, "image": list(shape), "steps": steps, "warmup": warmup, "dtype": "fp32",
-            "prune": f"{frac:.0%} of every prunable bottleneck conv (conv1/conv2), Taylor scores, one round",
+            "prune": f"{rounds} rounds, each {frac:.0%} of every prunable bottleneck conv (conv1/conv2) by Taylor "
+                     "scores, then DDP rewrap and a timed finetune segment; the value is over all rounds",
+            "rounds": per_round,
             "params_before_after": [params0, count_parameters(model)], "optimizer": "SGD momentum 0.9, wd 1e-4",
-            "ddp": f"PrunableDDP (bucket_cap_mb={wrapper.bucket_cap_mb}), rewrapped after the prune",
-            "kernels": "native training convs / BN (engine/train.py)", "prune_rewrap_s": round(t_prune, 2),
-            "new_shape_warmup_s": round(t_warm, 2), "in_sync": params_in_sync(model),
+            "ddp": f"PrunableDDP (bucket_cap_mb={wrapper.bucket_cap_mb}), rewrapped after every prune",
+            "kernels": "native training convs / BN (engine/train.py)", "prune_rewrap_s": t_prune,
+            "new_shape_warmup_s": t_warm, "in_sync": params_in_sync(model),
             "weights_agreed_before_broadcast": sync["agreed_before"], "loss_finite": bool(np.isfinite(loss))},
     }
     disable_native_convs([m for m in model.modules() if "forward" in m.__dict__])
