@@ -191,7 +191,7 @@ __device__ __forceinline__ void output_transform(const float (&m)[36], float (&y
 // holds rows 3ph..3ph+2 of the 6x6 transform-point grid (acc[nh * 18 + 6 rr + c]) for its 16
 // tiles x both 16-channel halves. Y = A^T M A is linear in M, so each wave forms the partial
 // output of its three rows; the ph = 0 waves write it into ya / yb, the ph = 1 waves add theirs
-// with LDS float adds (fixed order: one add per output after the write, deterministic). Partial column passes:
+// (read-modify-write; fixed order: one add per output after the write, deterministic). Partial column passes:
 //   ph 0 (rows 0-2): t0 = m0 + m1 + m2, t1 = t3 = m1 - m2, t2 = m1 + m2
 //   ph 1 (rows 3-5): t0 = s, t1 = 2d, t2 = 4s, t3 = 8d + m5   (s = m3 + m4, d = m3 - m4)
 // and for ph 1 the row pass runs on s, d, m5 once each (at6 is linear), the scalings folding
@@ -254,10 +254,11 @@ __device__ __forceinline__ void sp_partial(const f32x4 (&acc)[NPT], int grp, int
           else if (row == 1) add = 2.f * yd[col];
           else if (row == 2) add = 4.f * ys[col];
           else add = 8.f * yd[col] + y5[col];
-          // one LDS add per output (ds_add_f32, no return) instead of a read-modify-write: each
-          // address receives exactly this one add after the ph 0 write, so the order is fixed
-          atomicAdd(dst + q * 16, add.x);
-          atomicAdd(dst + TPL + q * 16, add.y);
+          // plain read-modify-write, one per output after the ph 0 write (fixed order). NOT an LDS
+          // float atomic: ds_add_f32 made this epilogue 5x slower on post-ReLU operands than on
+          // N(0,1) ones (data-dependent; profiles/wino4/split_points_r5.txt)
+          dst[q * 16] += add.x;
+          dst[TPL + q * 16] += add.y;
         }
       }
     }
