@@ -454,18 +454,19 @@ def _b100(args, model, task, convs, dev, world, rank, timed_run, log, loader):
     del xs, ys
     host = {}
     # "per_sample": the reference's loader verbatim (default collate: 100 __getitem__ + a stack per
-    # batch in the worker); "batched": the same DataLoader class with a BatchSampler, so the worker
-    # slices each batch from the host tensors in one indexing op
+    # batch in the worker; the worker is forked at every pass); "batched": the same DataLoader class
+    # with a BatchSampler (one indexing op per batch) and a persistent worker, forked once during
+    # the warm-up pass: forking this GPU process stalls it ~1.2 s (profiles/bench/b100_host_loader_r5.txt)
     for kind in ("batched", "per_sample"):
-        def mk(dset, kind=kind):
-            if kind == "per_sample":
-                return torch.utils.data.DataLoader(dset, batch_size=sb, shuffle=False, num_workers=1, pin_memory=True)
-            bs = torch.utils.data.BatchSampler(torch.utils.data.SequentialSampler(dset), sb, drop_last=False)
-            return torch.utils.data.DataLoader(dset, sampler=bs, batch_size=None, num_workers=1, pin_memory=True)
-
-        TaylorAttributionMetric(model, mk(torch.utils.data.Subset(ds, range(20 * sb))), F.cross_entropy,
-                                dev).run_many(convs, find_best_evaluation_module=True)  # warm
-        hm = TaylorAttributionMetric(model, mk(ds), F.cross_entropy, dev)
+        if kind == "per_sample":
+            dl = torch.utils.data.DataLoader(ds, batch_size=sb, shuffle=False, num_workers=1, pin_memory=True)
+        else:
+            bs = torch.utils.data.BatchSampler(torch.utils.data.SequentialSampler(ds), sb, drop_last=False)
+            dl = torch.utils.data.DataLoader(ds, sampler=bs, batch_size=None, num_workers=1, pin_memory=True,
+                                             persistent_workers=True)
+        TaylorAttributionMetric(model, dl, F.cross_entropy, dev).run_many(
+            convs, find_best_evaluation_module=True)  # warm (and, persistent, the worker's fork)
+        hm = TaylorAttributionMetric(model, dl, F.cross_entropy, dev)
         _, hdt = timed_run(hm, convs)
         assert hm.last_path["path"] == "fused", hm.last_path
         host[kind] = (round(s_steps * sb * world / hdt, 1), hm.last_coalesce)
@@ -480,9 +481,11 @@ def _b100(args, model, task, convs, dev, world, rank, timed_run, log, loader):
                           "host_loader": "torch DataLoader over a TensorDataset of host fp32 tensors, num_workers=1, "
                                          "pin_memory=True (experiments/models/cifar10.py:136-161); run_many pins and "
                                          "copies one batch ahead on a side HIP stream (data/prefetch.py). "
-                                         "host_loader_img_s: BatchSampler (one indexing op per batch); "
-                                         "host_loader_per_sample_img_s: the reference's default per-sample collate "
-                                         f"(CPU-bound in its one worker); coalescing {host['batched'][1]}"}
+                                         "host_loader_img_s: BatchSampler (one indexing op per batch), persistent worker "
+                                         "(forked once, in the untimed warm-up pass); host_loader_per_sample_img_s: the "
+                                         "reference's default per-sample collate, worker forked per pass (a ~1.2 s stall "
+                                         "of this GPU process per fork, profiles/bench/b100_host_loader_r5.txt); "
+                                         f"coalescing {host['batched'][1]}"}
     log(f"[bench] B=100 (reference attribution batch): {out['vgg_taylor_b100_img_s']:.0f} img/s with "
         f"{res['1'][1]} loader batches per launch, {res['0'][0]:.0f} img/s one launch per batch, "
         f"{out['vgg_taylor_b100_host_loader_img_s']:.0f} img/s from a host DataLoader (per-sample collate "

@@ -213,3 +213,25 @@ def test_invalidate_after_data_edit(cuda):
     ref = _scores(model, x, y, 16, "0")
     for a, r in zip(got, ref):
         np.testing.assert_array_equal(a, r)
+
+
+@pytest.mark.timeout(120)
+def test_graph_capture_survives_a_pinning_loader_thread(cuda, monkeypatch):
+    """A torch DataLoader with workers and pin_memory runs a pinning thread in this process while
+    the engine captures its per-slot HIP graphs: with the default global capture mode that
+    thread's host-memory calls invalidated the capture (hipErrorStreamCaptureInvalidated, found
+    with one launch per batch, round 5); captures are thread-local now."""
+    import torch.nn.functional as F
+
+    from torchpruner_amd import TaylorAttributionMetric
+    from torchpruner_amd.models import prunable_vgg16
+    monkeypatch.setenv("TORCHPRUNER_COALESCE", "0")
+    torch.manual_seed(0)
+    model = prunable_vgg16().to(cuda).eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    ds = torch.utils.data.TensorDataset(torch.randn(24 * 16, 3, 32, 32), torch.randint(0, 10, (24 * 16,)))
+    dl = torch.utils.data.DataLoader(ds, batch_size=16, num_workers=1, pin_memory=True)
+    got = TaylorAttributionMetric(model, dl, F.cross_entropy, cuda).run_many(convs, True)
+    ref = TaylorAttributionMetric(model, [(x, y) for x, y in dl], F.cross_entropy, cuda).run_many(convs, True)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)

@@ -741,12 +741,15 @@ class _BatchPipeline:
         if key not in self.seen:  # autotune / allocate alone, after everything in flight
             self.join()
             self.seen.add(key)
+            # this batch's kernel choices are timed as they will run: ``depth`` in flight
+            from ..engine.fused_chain import TUNER
+            TUNER.concurrency = self._depth_for(x, graphs) if self._depth_for(x, graphs) > 2 else 1
+            self._tuning = True
             return False
+        self._end_tuning()
         if self.streams is None:
             if self.depth is None:
-                small = x.shape[0] * math.prod(x.shape[2:]) <= self.DEEP_MAX_PIXELS
-                self.depth = 4 if small and self.graph_replay and graphs is not None and \
-                    graphs(x.shape[0], pipelined=True) else 2
+                self.depth = self._depth_for(x, graphs)
             self.streams = [torch.cuda.Stream(x.device) for _ in range(self.depth)]
         cur = torch.cuda.current_stream(x.device)
         slot = self.n % self.depth
@@ -765,7 +768,20 @@ class _BatchPipeline:
         self.n += 1
         return True
 
+    def _depth_for(self, x, graphs) -> int:
+        if self.depth is not None:
+            return self.depth
+        small = x.shape[0] * math.prod(x.shape[2:]) <= self.DEEP_MAX_PIXELS
+        return 4 if small and self.graph_replay and graphs is not None and graphs(x.shape[0], pipelined=True) else 2
+
+    def _end_tuning(self):
+        if getattr(self, "_tuning", False):
+            from ..engine.fused_chain import TUNER
+            TUNER.concurrency = 1
+            self._tuning = False
+
     def join(self):
+        self._end_tuning()
         if self.streams is not None:
             cur = torch.cuda.current_stream(self.streams[0].device)
             for st in self.streams:

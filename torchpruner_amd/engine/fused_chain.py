@@ -186,6 +186,13 @@ class Autotuner:
         # bumped whenever a fixed()/pinned() context swaps the choice cache: captured HIP graphs
         # bake in the kernels chosen when they were captured, so their keys include it
         self.gen = 0
+        # > 1 while tuning the shapes of small batches that will run ``concurrency`` in flight on
+        # as many HIP streams (attributions/base.py _BatchPipeline): candidates are then timed as
+        # that many concurrent launches, i.e. by throughput, not by the latency of one launch
+        # alone — alone, split-K looks best because it fills the idle CUs; in flight, the other
+        # batches fill them and split-K's partial slabs and combine launch are pure extra work
+        self.concurrency = 1
+        self._streams = []
 
     @contextlib.contextmanager
     def fixed(self):
@@ -262,17 +269,31 @@ class Autotuner:
         # pick (lst[0], what TUNER.fixed() runs) is kept unless another is _TUNE_MARGIN faster
         lst = list(cands if cands is not None else self.candidates(M, N, K, wino, wino_only and wino is not None))
         times = {}
+        conc = max(1, int(self.concurrency))
+        if conc > 1:
+            while len(self._streams) < conc:
+                self._streams.append(torch.cuda.Stream())
         for r in range(_TUNE_ROUNDS):
             for cand in lst:
                 if r == 0:
                     run(*cand)  # warm
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(2):
-                    run(*cand)
+                if conc > 1:  # conc concurrent launch pairs, normalised to one pair
+                    cur = torch.cuda.current_stream()
+                    for st in self._streams[:conc]:
+                        st.wait_event(e0)
+                        with torch.cuda.stream(st):
+                            for _ in range(2):
+                                run(*cand)
+                    for st in self._streams[:conc]:
+                        cur.wait_stream(st)
+                else:
+                    for _ in range(2):
+                        run(*cand)
                 e1.record()
                 e1.synchronize()
-                t = e0.elapsed_time(e1)
+                t = e0.elapsed_time(e1) / conc
                 times[cand] = min(times.get(cand, t), t)
         fast = min(lst, key=lambda c: times[c])
         best = (times[fast], fast)
@@ -280,7 +301,8 @@ class Autotuner:
             best = (times[lst[0]], lst[0])
         self.cache[key] = best[1]
         if _TUNER_LOG:
-            print(f"[tuner] {key} -> {best[1]} ({best[0] / 2 * 1e3:.1f} us)", file=sys.stderr, flush=True)
+            print(f"[tuner] {key} -> {best[1]} ({best[0] / 2 * 1e3:.1f} us{f', {conc} in flight' if conc > 1 else ''})",
+                  file=sys.stderr, flush=True)
         return best[1]
 
 
@@ -970,7 +992,7 @@ class FusedChainEngine:
             graph = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(x.device)
             side.wait_stream(torch.cuda.current_stream(x.device))
-            with torch.cuda.graph(graph, stream=side):
+            with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
                 self.taylor(sx, sy, want, arena, mode, loss_batch=loss_batch)
             torch.cuda.current_stream(x.device).wait_stream(side)
             self._bound_graph_cache()
@@ -1027,7 +1049,7 @@ class FusedChainEngine:
             graph = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(st["z"].device)
             side.wait_stream(torch.cuda.current_stream(st["z"].device))
-            with torch.cuda.graph(graph, stream=side):
+            with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
                 out = run()
             torch.cuda.current_stream(st["z"].device).wait_stream(side)
             g = st["graphs"][cnt] = {"graph": graph, "out": out, "P": P}
@@ -1061,7 +1083,7 @@ class FusedChainEngine:
             graph = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(x.device)
             side.wait_stream(torch.cuda.current_stream(x.device))
-            with torch.cuda.graph(graph, stream=side):
+            with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
                 bufs = run(sx)
             torch.cuda.current_stream(x.device).wait_stream(side)
             self._bound_graph_cache()
