@@ -361,7 +361,9 @@ def _generic(args, model, convs, dev, world, timed_run, log, value, loader):
     t0 = time.perf_counter()
     with _env(TORCHPRUNER_ENGINES="0", TORCHPRUNER_GENERIC_NATIVE="0"):
         def warm():  # MIOpen kernel selection / compilation (untimed, no collective: shard_data=False)
-            TaylorAttributionMetric(model, loader(1, args.seed + 11, B), F.cross_entropy, dev,
+            from torchpruner_amd.data import DeviceLoader
+            xw, yw = next(iter(loader(1, args.seed + 11, B).batches.values()))  # this rank's batch
+            TaylorAttributionMetric(model, DeviceLoader(xw, yw, B), F.cross_entropy, dev,
                                     shard_data=False).run_many(convs, find_best_evaluation_module=True)
 
         from torchpruner_amd.parallel import dist as pdist
