@@ -72,6 +72,7 @@ hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H, int W, int
                         const float* shift, int relu, const float* res, int res_stride, const float* mask,
                         float* apoz, float* out, float* ws, double* bnpart, hipStream_t st);
 int tp_conv_tile_m(int cfg);
+long long tp_conv_sk_ws_floats(int cfg, int ks, int transposed, int tay, int M, int N);
 hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
                         int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
                         const float* shift, int relu, const float* res, int res_stride, const float* mask,
@@ -551,6 +552,18 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
 
 int64_t wino_taylor_slots(int64_t H, int64_t W) { return tp_wino_taylor_slots((int)H, (int)W); }
 
+// Stream-K fixup workspace of a GEN conv launch whose cfg carries the stream-K flag (32): undefined
+// when the flag is absent or stream-K does not apply at this shape (the launcher then runs the
+// data-parallel grid).
+static constexpr int64_t kCfgSK = 32;
+static at::Tensor sk_workspace(int64_t cfg, int64_t ks, bool transposed, bool tay, int64_t M, int64_t N,
+                        const at::TensorOptions& o) {
+  if (cfg < 0 || !(cfg & kCfgSK)) return at::Tensor();
+  const long long n = tp_conv_sk_ws_floats((int)(cfg & ~kCfgSK), (int)ks, transposed ? 1 : 0, tay ? 1 : 0, (int)M,
+                                           (int)N);
+  return n > 0 ? at::empty({(int64_t)n}, o) : at::Tensor();
+}
+
 // General strided conv forward (ResNet): x NHWC (B,H,W,Cin) with Cin % 32 == 0 (ks 1 or 3) or
 // Cin == 4 (ks 7, padded stem input); w (Cout, K) with K = conv_gen_k(ks, Cin), k = (kh,kw,ci).
 // Epilogue: out = relu?(acc*scale + shift + res); apoz (B, Cout) += count(out > 0).
@@ -590,9 +603,16 @@ at::Tensor conv_gen(const at::Tensor& x, const at::Tensor& w, const c10::optiona
   sp = (kt + per - 1) / per;
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * Ho * Wo * Cout}, x.options());
+  int64_t cf = cfg;
+  if (sp == 1 && Cin != 4) {
+    ws = sk_workspace(cfg, ks, false, false, B * Ho * Wo, Cout, x.options());
+    if (!ws.defined()) cf = cfg & ~kCfgSK;
+  } else if (cfg >= 0) {
+    cf = cfg & ~kCfgSK;
+  }
   TP_CHECK_HIP(tp_conv_gen(x.data_ptr<float>(), w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin, (int)Cout,
-                           (int)ks, (int)stride, (int)pad, (int)cfg, (int)sp, sc, sh, relu ? 1 : 0, rp, ap,
-                           out.data_ptr<float>(), sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream()));
+                           (int)ks, (int)stride, (int)pad, (int)cf, (int)sp, sc, sh, relu ? 1 : 0, rp, ap,
+                           out.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr, cur_stream()));
   return out;
 }
 
@@ -717,14 +737,28 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
   }
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * Ho * Wo * N}, g.options());
+  int64_t cf = cfg;
+  if (sp == 1 && !transposed) {
+    ws = sk_workspace(cfg, ks, false, tp_ != nullptr, B * Ho * Wo, N, g.options());
+    if (!ws.defined()) cf = cfg & ~kCfgSK;
+  } else if (cfg >= 0) {
+    cf = cfg & ~kCfgSK;
+  }
   TP_CHECK_HIP(tp_conv_gen4(g.data_ptr<float>(), wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)N,
-                            (int)ks, (int)stride, (int)pad, transposed ? 1 : 0, (int)Ho, (int)Wo, (int)cfg, (int)sp,
+                            (int)ks, (int)stride, (int)pad, transposed ? 1 : 0, (int)Ho, (int)Wo, (int)cf, (int)sp,
                             nullptr, nullptr, 0, rp, (int)res_stride, mp, nullptr, out.data_ptr<float>(),
-                            sp > 1 ? ws.data_ptr<float>() : nullptr, nullptr, tp_, (int)tay_mode, cur_stream()));
+                            ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, tp_, (int)tay_mode,
+                            cur_stream()));
   return out;
 }
 
 int64_t conv_gen_tay_slots(int64_t cfg, int64_t HWo) { return tp_conv_gen_tay_slots((int)cfg, (int)HWo); }
+
+// Fixup-workspace floats of a stream-K GEN launch of tile config cfg at an M x N GEMM (0 = stream-K
+// does not apply; the launcher then runs the data-parallel grid).
+int64_t conv_sk_ws(int64_t cfg, int64_t ks, bool tay, int64_t M, int64_t N) {
+  return tp_conv_sk_ws_floats((int)(cfg & ~kCfgSK), (int)ks, 0, tay ? 1 : 0, (int)M, (int)N);
+}
 
 // Weight gradient: g (B, Ho, Wo, Cout) and x (B, H, W, Cin) NHWC -> dW (Cout, Kpad) with column
 // k = (kh, kw, ci) (Kpad = ks*ks*Cin rounded up to 32; padded columns are zero).
@@ -789,9 +823,12 @@ std::tuple<at::Tensor, at::Tensor> conv_gen_stats(const at::Tensor& x, const at:
   auto out = at::empty({B, Ho, Wo, Cout}, x.options());
   const int64_t M = B * Ho * Wo, tm = tp_conv_tile_m((int)cfg);
   auto part = at::empty({(M + tm - 1) / tm, 2, Cout}, x.options().dtype(at::kDouble));
+  at::Tensor ws = Cin != 4 ? sk_workspace(cfg, ks, false, false, M, Cout, x.options()) : at::Tensor();
+  const int64_t cf = ws.defined() || cfg < 0 ? cfg : cfg & ~kCfgSK;
   TP_CHECK_HIP(tp_conv_gen3(x.data_ptr<float>(), w.data_ptr<float>(), (int)B, (int)H, (int)W, (int)Cin, (int)Cout,
-                            (int)ks, (int)stride, (int)pad, 0, 0, 0, (int)cfg, 1, nullptr, sh, 0, nullptr, 1, nullptr,
-                            nullptr, out.data_ptr<float>(), nullptr, part.data_ptr<double>(), cur_stream()));
+                            (int)ks, (int)stride, (int)pad, 0, 0, 0, (int)cf, 1, nullptr, sh, 0, nullptr, 1, nullptr,
+                            nullptr, out.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr,
+                            part.data_ptr<double>(), cur_stream()));
   return {out, part};
 }
 
@@ -944,6 +981,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits, Tensor(a!)? taylor=None, int tay_mode=0) -> Tensor");
   m.def("conv_gen_tay_slots(int cfg, int HWo) -> int", &conv_gen_tay_slots);
+  m.def("conv_sk_ws(int cfg, int ks, bool tay, int M, int N) -> int", &conv_sk_ws);
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
         "int splits, Tensor(a!)? apoz=None, float slope=0.0) -> (Tensor, Tensor)");

@@ -33,6 +33,7 @@ __device__ __forceinline__ uint2 bf16x4_of(const f32x4 v) {
 }
 
 constexpr int CFG_BF16 = 256;  // tile-config flag: bf16 operands (conv_igemm BF), fp32 accumulation
+constexpr int CFG_SK = 32;     // tile-config flag: stream-K split of the tiles x k-slices space (GEN 1, one K pass)
 constexpr int CFG_WS = 16;     // cfgs 16..18: persistent warp-specialised 1x1 GEMM (gemm_ws.hip), 1x1 stride-s
                                // GEN 1 convs and their dgrads (no split-K, no bnpart, dense residual)
 
@@ -86,6 +87,14 @@ struct ConvArgs {
   float* tay_part;          // GEN EPI_FWD LDS epilogue with a mask (data gradient), no split: Taylor
                             // partials -(v * mask) (tay_mode 1: |v|) per (image, column) of every M
                             // tile, slot r = m_tile - first tile of the image: [R][B][N], one writer each
+  // stream-K (GEN 1, one K pass; see tp_conv_gen4): sk_blocks = P > 0 blocks share the tiles x
+  // k-slices iteration space in equal contiguous ranges; a tile cut by a range boundary f has its
+  // two raw partial accumulator sets in sk_ws[f][0 / 1] (BM * BN floats each) and gets its
+  // epilogue from the fixup launch (sk_fixup = 1, block f): slot 0 + slot 1 in that fixed order
+  int sk_blocks;
+  int sk_fixup;
+  long long sk_iters;
+  float* sk_ws;
 };
 
 // Taylor slots R of the GEN epilogue partials for tile height bm: the M tiles an image can touch
@@ -187,7 +196,8 @@ __device__ __forceinline__ float4 res_quad(const ConvArgs& p, long long pix, int
 // staged into LDS (rows of 32 bf16 = 16 dwords, padded to 20: 80-B rows keep the 16-B fragment
 // reads conflict-free), products on v_mfma_f32_32x32x16_bf16 with fp32 accumulation; loads,
 // epilogues and every output stay fp32. 16x the fp32 MFMA rate: the K slice is 2 MFMAs, not 16.
-template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI, int GEN = 0, bool BF = false>
+template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI, int GEN = 0, bool BF = false,
+          bool SK = false>
 __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, WM, WN) / 128) void conv_igemm(ConvArgs p) {
   using T = Tile<BM, BN, WM, WN>;
   constexpr int BK = T::BK, LDK = T::LDK;
@@ -198,19 +208,20 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   static_assert(!BF || GEN == 0, "bf16 operands: GEN 0 only");
   unsigned* smu = reinterpret_cast<unsigned*>(smem);
 
-  const int tid = threadIdx.x;
+  constexpr int SK_PART = 2, SK_FIX = 3;  // stream-K segment modes (0: the tile's whole K range)
+  constexpr int TILEF = BM * BN;          // floats of one partial accumulator set
+
+  // one output tile (or, stream-K, a K range of it); returns early for empty tiles. ``tid``: the
+  // stream-K loop passes an opaque copy of threadIdx.x so the lane-derived addressing is not
+  // hoisted out of the segment loop and kept live across it.
+  auto run_tile = [&](const int tid, const int tile, const int split, const int sk_kb, const int sk_ke,
+                      const int sk_mode, float* sk_slab) __attribute__((always_inline)) {
   const int lane = tid & 63, wave = tid >> 6;
   const int n_tiles = (p.N + BN - 1) / BN;
   const int m_tiles = (p.M + BM - 1) / BM;
-  // GEN 3 parity order puts the 4-, 2- and 1-tap phase classes in consecutive M ranges: the
-  // contiguous XCD remap would hand the two heaviest XCDs all 4-tap tiles and the last two all
-  // 1-tap tiles (max/mean work 4/2.25 -> the kernel ran ~1.7x long). Plain round-robin dispatch
-  // spreads every class over all XCDs; the A operand here is the small low-resolution gradient.
-  const int tile = (GEN == 3 && p.parity) ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (tile / n_tiles) * BM;
   const int n0 = (tile % n_tiles) * BN;
   if (m0 >= m_tiles * BM) return;
-  const int split = blockIdx.y;
   const int cin_tiles = p.Cin / BK;
   unsigned tmask = (1u << (KS * KS)) - 1u;  // GEN 3: taps any row of this tile can use
   if constexpr (GEN == 3) {
@@ -225,8 +236,8 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     }
   }
   const int kt_total = GEN == 3 ? __builtin_popcount(tmask) * cin_tiles : p.K / BK;
-  const int kt_begin = GEN == 3 ? 0 : split * p.k_tiles_per_split;
-  const int kt_end = GEN == 3 ? kt_total : min(kt_total, kt_begin + p.k_tiles_per_split);
+  const int kt_begin = sk_mode ? sk_kb : GEN == 3 ? 0 : split * p.k_tiles_per_split;
+  const int kt_end = sk_mode ? sk_ke : GEN == 3 ? kt_total : min(kt_total, kt_begin + p.k_tiles_per_split);
 
   // ---- per-thread A rows: loop-invariant offsets + a bitmask of in-bounds taps ----------
   // Loads go through buffer descriptors: an out-of-range offset returns zeros in hardware,
@@ -432,7 +443,19 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   const int wn0 = (wave % T::WAVES_N) * WN;
   const int li = lane & 31, lh = lane >> 5;
 
-  if (kt_begin < kt_end) {
+  if (sk_mode == SK_FIX) {  // stream-K fixup: the tile's two partial sets, slot 0 + slot 1 (fixed order)
+    const float* s0 = sk_slab + (size_t)wave * (T::TM * T::TN * 1024);
+    const float* s1 = s0 + TILEF;
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int o = ((i * T::TN + j) * 16 + r) * 64 + lane;
+          acc[i][j][r] = s0[o] + s1[o];
+        }
+  } else if (kt_begin < kt_end) {
     load_tile(kt_begin);
     store_tile(0);
     __syncthreads();
@@ -497,6 +520,16 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
       __syncthreads();
       buf ^= 1;
     }
+  }
+  if (sk_mode == SK_PART) {  // stream-K: this block's K range of the tile, raw, one 256-B row per store
+    float* d = sk_slab + (size_t)wave * (T::TM * T::TN * 1024);
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) d[((i * T::TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+    return;
   }
 
   // ---- GEN forward / partial epilogue: transpose through LDS, float4 rows ---------------
@@ -795,6 +828,54 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           if (p.apoz && cur_b >= 0 && cnt > 0.f) atomicAdd(p.apoz + (long long)cur_b * p.N + n, cnt);
         }
       }
+    }
+  }
+  };  // run_tile
+
+  // ---- which tiles this block runs. Default: one tile per block (grid.y = split-K slab).
+  // GEN 3 parity order puts the 4-, 2- and 1-tap phase classes in consecutive M ranges: the
+  // contiguous XCD remap would hand the two heaviest XCDs all 4-tap tiles and the last two all
+  // 1-tap tiles (max/mean work 4/2.25 -> the kernel ran ~1.7x long). Plain round-robin dispatch
+  // spreads every class over all XCDs; the A operand here is the small low-resolution gradient.
+  // Stream-K (GEN 1, one K pass): block b (XCD-contiguous) owns iterations [b I / P, (b+1) I / P)
+  // of the tiles x k-slices space, I / P >= k-slices per tile (host-checked), so a range boundary
+  // cuts at most one tile and every cut tile has exactly two contributors: the block before the
+  // boundary (slices from 0: slot 0) and the one after (through the last slice: slot 1).
+  // SK: a separate instantiation, so the segment loop (whose loop-invariant hoisting costs ~100
+  // VGPRs) never touches the data-parallel kernels
+  constexpr bool sk = GEN == 1 && SK;
+  const int KT = p.K / BK;
+  const long long I = p.sk_iters, P = p.sk_blocks > 0 ? p.sk_blocks : 1;
+  const int b = sk || !(GEN == 3 && p.parity) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  long long it = sk ? (long long)b * I / P : 0;
+  const long long hi = sk ? (long long)(b + 1) * I / P : 0;
+  if constexpr (!sk) {
+    run_tile(threadIdx.x, b, blockIdx.y, 0, 0, 0, nullptr);
+  } else {
+    for (int seg = 0;; ++seg) {
+      int tile, kb = 0, ke = 0, mode = 0;
+      float* slab = nullptr;
+      if (p.sk_fixup) {
+        if (seg || b == 0 || it % KT == 0) break;  // no tile cut at boundary b
+        tile = (int)(it / KT);
+        mode = SK_FIX;
+        slab = p.sk_ws + (size_t)b * 2 * TILEF;
+      } else {
+        if (it >= hi) break;
+        tile = (int)(it / KT);
+        kb = (int)(it % KT);
+        ke = (int)min((long long)KT, kb + (hi - it));
+        if (kb != 0 || ke != KT) {
+          mode = SK_PART;
+          slab = kb == 0 ? p.sk_ws + (size_t)(b + 1) * 2 * TILEF  // cut at the range's end
+                         : p.sk_ws + ((size_t)b * 2 + 1) * TILEF;  // cut at the range's start
+        }
+        it += ke - kb;
+      }
+      if (seg) __syncthreads();  // the previous segment's LDS reads are done
+      int tid = threadIdx.x;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid));
+      run_tile(tid, tile, 0, kb, ke, mode, slab);
     }
   }
 }
@@ -1345,12 +1426,71 @@ extern "C" hipError_t tp_nchw_to_nhwc_pad(const float* x, float* y, int B, int C
 // ReLU, optional APoZ counts of the output (exact integer counts per (image, channel)).
 // ---------------------------------------------------------------------------------------------
 namespace {
+// Stream-K geometry of a GEN kernel instantiation: P = co-resident blocks (CUs x occupancy), the
+// number of equal iteration ranges; applicable when the tile count is at least P and not a
+// multiple of it (otherwise data-parallel tiles are already balanced).
+template <int BM, int BN, int WM, int WN, int KS, int GEN, int EPI>
+int sk_blocks() {
+  static const int P = [] {
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, reinterpret_cast<const void*>(&tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN, false, true>),
+            tp::Tile<BM, BN, WM, WN>::NT, 0) != hipSuccess)
+      return 0;
+    return cus * nb;
+  }();
+  return P;
+}
+
+template <int BM, int BN, int WM, int WN, int KS, int GEN, int EPI>
+long long sk_ws_floats(int M, int N) {
+  const long long tiles = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if constexpr (GEN != 1) return 0;
+  const int P = sk_blocks<BM, BN, WM, WN, KS, GEN, EPI>();
+  if (P <= 0 || tiles < P || tiles % P == 0) return 0;
+  return (long long)P * 2 * BM * BN;
+}
+
 template <int BM, int BN, int WM, int WN, int KS, int GEN, int EPI>
 hipError_t launch_gen(const tp::ConvArgs& a, int splits, hipStream_t st) {
   const int m_tiles = (a.M + BM - 1) / BM, n_tiles = (a.N + BN - 1) / BN;
+  constexpr int NT = tp::Tile<BM, BN, WM, WN>::NT;
+  if constexpr (GEN == 1 && (EPI == tp::EPI_FWD || EPI == tp::EPI_FWD_TAY)) {
+  if (a.sk_blocks < 0) {  // stream-K requested (a.sk_ws sized by sk_ws_floats): balanced ranges, then the fixups
+    if (splits == 1 && a.sk_ws && sk_ws_floats<BM, BN, WM, WN, KS, GEN, EPI>(a.M, a.N) > 0) {
+      tp::ConvArgs b = a;
+      b.sk_blocks = sk_blocks<BM, BN, WM, WN, KS, GEN, EPI>();
+      b.sk_iters = (long long)m_tiles * n_tiles * (a.K / 32);
+      b.sk_fixup = 0;
+      tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN, false, true><<<b.sk_blocks, NT, 0, st>>>(b);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      b.sk_fixup = 1;
+      tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN, false, true><<<b.sk_blocks, NT, 0, st>>>(b);
+      return hipGetLastError();
+    }
+  }
+  }
   dim3 grid(m_tiles * n_tiles, splits);
-  tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN><<<grid, tp::Tile<BM, BN, WM, WN>::NT, 0, st>>>(a);
+  tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN><<<grid, NT, 0, st>>>(a);
   return hipGetLastError();
+}
+
+template <int KS, int EPI>
+long long sk_ws_cfg(int cfg, int M, int N) {
+  switch (cfg) {
+    case 0: return sk_ws_floats<128, 128, 64, 64, KS, 1, EPI>(M, N);
+    case 1: return sk_ws_floats<256, 64, 64, 64, KS, 1, EPI>(M, N);
+    case 2: return sk_ws_floats<64, 64, 32, 32, KS, 1, EPI>(M, N);
+    case 3: return sk_ws_floats<128, 64, 64, 32, KS, 1, EPI>(M, N);
+    case 4: return sk_ws_floats<128, 128, 64, 32, KS, 1, EPI>(M, N);
+    case 5: return sk_ws_floats<256, 64, 64, 32, KS, 1, EPI>(M, N);
+    case 6: return sk_ws_floats<128, 64, 32, 32, KS, 1, EPI>(M, N);
+  }
+  return 0;
 }
 
 template <int KS, int GEN, int EPI>
@@ -1386,6 +1526,17 @@ hipError_t gen_dispatch(int ks, int gen, int cfg, const tp::ConvArgs& a, int spl
 extern "C" hipError_t tp_gemm1x1_ws(const float* x, const float* w, int B, int H, int W, int Cin, int N, int stride,
                                     const float* scale, const float* shift, int relu, float slope, const float* res,
                                     const float* mask, float* apoz, float* out, int variant, hipStream_t st);
+
+// Workspace floats a stream-K GEN 1 launch of tile config ``cfg`` (without the CFG_SK flag) needs at
+// this GEMM shape (0: stream-K does not apply: transposed / strided-gather, 5x5, or the tiles are
+// fewer than the co-resident blocks or already a multiple of them). ``tay``: the data-gradient
+// Taylor-partials instantiation (EPI_FWD_TAY).
+extern "C" long long tp_conv_sk_ws_floats(int cfg, int ks, int transposed, int tay, int M, int N) {
+  if (transposed || cfg < 0 || cfg > 6) return 0;
+  if (ks == 1) return tay ? sk_ws_cfg<1, tp::EPI_FWD_TAY>(cfg, M, N) : sk_ws_cfg<1, tp::EPI_FWD>(cfg, M, N);
+  if (ks == 3 && !tay) return sk_ws_cfg<3, tp::EPI_FWD>(cfg, M, N);
+  return 0;
+}
 
 extern "C" int tp_conv_gen_k(int ks, int Cin) {
   return Cin == 4 ? (ks * ks * 4 + 31) / 32 * 32 : ks * ks * Cin;
@@ -1459,7 +1610,7 @@ extern "C" hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H,
 
 // M tile height of an implicit-GEMM tile config (the row count of a bnpart slab is ceil(M / it))
 extern "C" int tp_conv_tile_m(int cfg) {
-  switch (cfg) {
+  switch (cfg & ~tp::CFG_SK) {
     case 1: case 5: return 256;
     case 2: return 64;
     default: return 128;
@@ -1475,6 +1626,7 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
 // Taylor partial slots of tp_conv_gen4's ``tay_part`` for tile config cfg at Ho*Wo output pixels
 // per image; 0 = the config cannot produce them (a tile would span more than GEN_TAY_IMG images).
 extern "C" int tp_conv_gen_tay_slots(int cfg, int HWo) {
+  cfg &= ~tp::CFG_SK;
   if (cfg == 4) return 0;  // its 8-wave 128x128 EPI_FWD_TAY build spills 29 VGPRs (the others do not)
   const int bm = tp_conv_tile_m(cfg);
   if (HWo <= 0 || (bm - 1) / HWo + 1 > tp::GEN_TAY_IMG) return 0;
@@ -1502,6 +1654,11 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
   using namespace tp;
   const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
   if ((gen != 2 && Cin % 32 != 0) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
+  const bool sk = cfg >= 0 && (cfg & CFG_SK) && (cfg & ~CFG_SK) < CFG_WS;
+  if (sk) {  // stream-K: GEN 1, one K pass, ``ws`` = the fixup slots (tp_conv_sk_ws_floats)
+    cfg &= ~CFG_SK;
+    if (gen != 1 || splits > 1 || !ws || (ks != 1 && ks != 3)) return hipErrorInvalidValue;
+  }
   if (cfg >= CFG_WS && cfg < CFG_WS + 3) {  // persistent warp-specialised 1x1 kernel (gemm_ws.hip)
     if (gen != 1 || ks != 1 || pad != 0 || res_stride != 1 || bnpart) return hipErrorInvalidValue;
     return tp_gemm1x1_ws(x, w, B, H, W, Cin, Cout, stride, scale, shift, relu, 0.f, res, mask, apoz, out,
@@ -1557,6 +1714,10 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
     a.tay_part = tay_part;
     a.tay_mode = tay_mode;
     a.epi_lds = 1;
+  }
+  if (sk) {
+    a.sk_blocks = -1;
+    a.sk_ws = ws;
   }
   if (a.tay_part) return gen_cfg<1, 1, EPI_FWD_TAY>(cfg, a, 1, st);
   if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);

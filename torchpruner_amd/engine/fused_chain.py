@@ -59,6 +59,7 @@ WINO4S = -8  # F(4x4) MODE 3 with split transform points (wino4.hip variant 3): 
 WINO4S_FU = -11  # its data gradient writing the output unpooled through the previous block's pool
                  # argmax (one K pass): no separate unpooling pass for the next data gradient
 WINO4_FU = -12  # the same with the MODE 3 kernel
+CFG_SK = 32  # tile-config flag of the GEN implicit GEMM: stream-K (conv_mfma.hip launch_gen)
 CFG_BF16 = 256  # tile-config flag of conv_igemm: bf16 operands / fp32 accumulation (opt-in, compute_dtype)
 _BF16_CFGS = (0, 2, 3)  # the implicit-GEMM tiles built with bf16 variants (conv_mfma.hip launch_any)
             # than F(2x2); dgrads of pooled layers take the explicit unpool first
@@ -156,6 +157,19 @@ def _splits_for(M, N, K, bm, bn):
     while tiles * splits < 2 * _CU and splits * 2 <= kt // 4 and splits < 16:
         splits *= 2
     return splits
+
+
+def sk_candidates(T, cands, ks: int, M: int, N: int, tay: bool = False):
+    """Stream-K variants (cfg | CFG_SK, 1) of the GEN implicit-GEMM tile configs in ``cands``
+    where stream-K applies at this shape: the tiles x k-slices space is cut into one equal range per
+    co-resident block, so the last partial wave of output tiles (ResNet's 1x1 GEMMs at B=256 leave
+    up to ~40% of the CUs idle in it) is spread over the whole chip. The C++ side decides
+    applicability (T.conv_sk_ws: the fixup workspace, 0 = not applicable)."""
+    out = []
+    for c in dict.fromkeys(c for c, _ in cands if 0 <= c <= 6):
+        if T.conv_sk_ws(c, ks, tay, M, N) > 0:
+            out.append((c | CFG_SK, 1))
+    return out
 
 
 def _pick_cfg(M: int, N: int, K: int):
@@ -318,6 +332,8 @@ def kernel_name(cfg: int) -> str:
     igemm (2x2 layers as one dense GEMM), ``bf16`` igemm variants, or a persistent 1x1 GEMM."""
     if cfg in _KIND_NAMES:
         return _KIND_NAMES[cfg]
+    if CFG_SK <= cfg < CFG_SK + 7:
+        return kernel_name(cfg - CFG_SK) + "_streamk"
     if cfg >= 100 and cfg < CFG_BF16:
         bm, bn = _TILES.get(cfg - 100, (0, 0))
         return f"dense2x2_igemm{bm}x{bn}"

@@ -28,7 +28,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import TUNER, WINO, WINO_LDS, _wino_splits, cpad, logits_grad, taylor_slots, winograd_weights
+from .fused_chain import (TUNER, WINO, WINO_LDS, _wino_splits, cpad, logits_grad, sk_candidates, taylor_slots,
+                          winograd_weights)
 
 
 @dataclass
@@ -199,6 +200,8 @@ class ResNetEngine:
         Ho, Wo = (H + 2 * pd - ks) // s + 1, (W + 2 * pd - ks) // s + 1
         M, N, K = B * Ho * Wo, e["scale"].numel(), e["w"].shape[1]
         cands = TUNER.candidates(M, N, K)
+        if C != 4:
+            cands = cands + sk_candidates(T, cands, ks, M, N)
         if "u" in e and res is None:  # odd H / W: partial last tile row / column (direct loads)
             sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + ([(WINO_LDS, 1)] if sp0 > 1 else []) + cands
@@ -371,6 +374,7 @@ class ResNetEngine:
             cands = [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
         else:
             cands = TUNER.candidates(M, N, K)
+            cands = cands + sk_candidates(T, cands, ks, M, N, tay=False)
         wino_ok = "ut" in e and res is None and mask is not None
         if wino_ok:
             sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)

@@ -37,7 +37,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import _CU, TUNER, WINO, WINO_LDS, _wino_splits, cpad
+from .fused_chain import _CU, TUNER, WINO, WINO_LDS, _wino_splits, cpad, sk_candidates
 
 
 def _wino_ok(ks, stride, pad, H, W, cin, cout) -> bool:
@@ -128,6 +128,8 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
         return T.conv_gen(xh, cache["wk"], None, shift, False, None, None, ks, stride, pad, cfg, sp)
 
     cands = TUNER.candidates(M, cout_p, kk)
+    if cin_p != 4:
+        cands = cands + sk_candidates(T, cands, ks, M, cout_p)
     if wino:
         sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cout_p, cin_p)
         cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
@@ -184,6 +186,8 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
                               transposed, cfg, sp)
 
     cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
+    if not transposed:
+        cands = cands + sk_candidates(T, cands, ks, M, cin_p)
     if wino:
         cands = [(WINO_LDS, _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cin_p, cout_p)), (WINO, 1)] + cands
     key = ("tdgrad", tuple(g.shape), cin_p, ks, stride, pad, res is not None and res_stride)
