@@ -158,7 +158,7 @@ def test_wino_bf16_measured_options_match_emulation(cuda, variant):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, **{variant: "1"})
-    p = subprocess.run([sys.executable, os.path.join(root, "scripts", "wino_bf16_diag.py")], env=env, cwd=root,
+    p = subprocess.run([sys.executable, os.path.join(root, "scripts", "probes", "wino_bf16_diag.py")], env=env, cwd=root,
                        capture_output=True, text=True, timeout=180)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     rels = [float(ln.split(" rel ")[1].split()[0]) for ln in p.stdout.splitlines() if " rel " in ln]
