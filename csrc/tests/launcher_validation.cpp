@@ -14,6 +14,7 @@ int tp_wino_taylor_slots(int H, int W);
 int tp_wino_staged_ok(int H, int W, int unpool);
 void tp_wino_geometry(int H, int W, int unpool, int* out9);
 int tp_bn_groups(int P, int C);
+long long tp_conv_sk_ws_floats(int cfg, int ks, int transposed, int tay, int M, int N);
 hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
                         int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
                         const float* shift, int relu, const float* res, int res_stride, const float* mask,
@@ -96,6 +97,22 @@ int main() {
          hipErrorInvalidValue);  // cfg 16 is 1x1 only
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 17, 1, n, n, 0, n, 2, n, n, n, n, 0) ==
          hipErrorInvalidValue);  // strided residual
+  // stream-K (cfg | 32): GEN 1 only, one K pass, a fixup workspace, ks 1 / 3; no workspace is
+  // asked for where it cannot apply (transposed, 5x5, warp-specialised cfgs)
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 3, 2, 1, 1, 16, 16, 32, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // transposed
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 32, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // no workspace
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 32 + 2, 2, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // split-K and stream-K together
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 5, 1, 2, 0, 0, 0, 32, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // 5x5
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 4, 64, 7, 2, 3, 0, 0, 0, 32, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // 4-channel stem (GEN 2)
+  EXPECT(tp_conv_sk_ws_floats(0, 1, 1, 0, 1 << 20, 512) == 0);  // transposed
+  EXPECT(tp_conv_sk_ws_floats(0, 5, 0, 0, 1 << 20, 512) == 0);  // 5x5
+  EXPECT(tp_conv_sk_ws_floats(16, 1, 0, 0, 1 << 20, 512) == 0); // warp-specialised cfg
+  EXPECT(tp_conv_sk_ws_floats(0, 3, 0, 1, 1 << 20, 512) == 0);  // Taylor partials are 1x1 only
 
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
