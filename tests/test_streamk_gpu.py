@@ -123,3 +123,50 @@ def test_streamk_bn_statistics(cuda):
         yd = y.double().reshape(-1, cout)
         torch.testing.assert_close(part.sum(0)[0], yd.sum(0), rtol=1e-4, atol=1e-3)  # fp32 in-tile sums
         torch.testing.assert_close(part.sum(0)[1], (yd * yd).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("which", ["apoz", "taylor"])
+def test_resnet_engine_with_streamk_pinned(cuda, which):
+    """The ResNet engine with every conv that has a stream-K candidate pinned to it gives the scores
+    of the same engine pinned to the data-parallel tile configs (APoZ counts up to decisions within
+    rounding of 0; Taylor to fp32 rounding), and stream-K really ran."""
+    from torchpruner_amd import APoZAttributionMetric, TaylorAttributionMetric, get_resnet_pruning_graph
+    from torchpruner_amd.data import DeviceLoader
+    from torchpruner_amd.engine.fused_chain import CFG_SK, TUNER
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    import numpy as np
+    torch.manual_seed(3)
+    model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=10, width=32).to(cuda).eval()
+    for m in model.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_var.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.1, 0.1)
+    x = torch.randn(32, 3, 224, 224, device=cuda)
+    y = torch.randint(0, 10, (32,), device=cuda)
+    mods = [m for m, _ in get_resnet_pruning_graph(model)]
+    metric = {"apoz": APoZAttributionMetric, "taylor": TaylorAttributionMetric}[which]
+    used = []
+
+    def sk_policy(key, cands, M, N, K):
+        sk = [c for c in cands if 0 <= c[0] and c[0] & CFG_SK and c[0] < CFG_SK + 7]
+        if sk:
+            used.append(key)
+            return sk[0]
+        return None
+
+    def dp_policy(key, cands, M, N, K):
+        dp = [c for c in cands if 0 <= c[0] <= 6 and c[1] == 1]
+        return dp[0] if dp else None
+
+    out = {}
+    for name, pol in (("sk", sk_policy), ("dp", dp_policy)):
+        with TUNER.pinned(pol):
+            m = metric(model, DeviceLoader(x, y, 32), F.cross_entropy, cuda)
+            out[name] = m.run_many(mods, True)
+            assert m.last_path["path"] == "resnet", m.last_path
+    assert used, "no conv had a stream-K candidate"
+    for a, b in zip(out["sk"], out["dp"]):
+        if which == "apoz":
+            np.testing.assert_allclose(a, b, atol=0.5)
+        else:
+            np.testing.assert_allclose(a, b, rtol=2e-3, atol=2e-3 * float(np.abs(b).max()))
