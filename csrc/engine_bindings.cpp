@@ -93,6 +93,7 @@ hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* per
 hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
 int tp_wino4_u_img();
 int tp_wino4_ok(int H, int W, int C, int K);
+int tp_wino4_taylor_slots(int S);
 int tp_wino4_lds_bytes(int S, int variant);
 hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act, float* taylor,
@@ -473,7 +474,8 @@ std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at:
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
   need_u4(u, C, K);
-  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)C, (int)K), "F(4x4) Winograd needs square 4/8/16/32 maps, C % 8 == 0, "
+  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)C, (int)K), "F(4x4) Winograd needs square 4/8/16/32 (or, split-points "
+              "variant 3 without pooling, 56/28/14/7) maps, C % 8 == 0, "
               "K % 32 == 0; got ", x.sizes(), " K=", K);
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   const float* sc = opt_ptr(scale, K, "scale");
@@ -513,18 +515,16 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
   const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
   need_u4(ut, Cout, Cin);
   TORCH_CHECK(g.size(0) == B && g.size(1) == H && g.size(2) == W, "grad shape mismatch");
-  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)Cout, (int)Cin), "F(4x4) dgrad needs square 4/8/16/32 maps, "
+  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)Cout, (int)Cin), "F(4x4) dgrad needs square 4/8/16/32/56/28/14/7 maps, "
               "Cout % 8 == 0, Cin % 32 == 0");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
   const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
   float* tay = nullptr;
   if (taylor.has_value() && taylor->defined()) {
-    const int64_t R = std::max<int64_t>(tp_wino_taylor_slots((int)H, (int)W), 2);
+    const int64_t R = tp_wino4_taylor_slots((int)H);
     TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
-                    taylor->numel() % (B * Cin) == 0 && taylor->numel() >= (H == 32 ? 2 : 1) * B * Cin,
-                "taylor must be a contiguous float32 (R', B, Cin) GPU tensor with R' >= ", H == 32 ? 2 : 1,
-                " partial slots");
-    (void)R;
+                    taylor->numel() % (B * Cin) == 0 && taylor->numel() >= R * B * Cin,
+                "taylor must be a contiguous float32 (R', B, Cin) GPU tensor with R' >= ", R, " partial slots");
     tay = taylor->data_ptr<float>();
   }
   const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, Cout / 8));
@@ -959,6 +959,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("wino_lds_bytes() -> int", []() -> int64_t { return tp_wino_lds_bytes(); });
   m.def("wino_staged_ok(int H, int W, bool unpool) -> bool",
         [](int64_t H, int64_t W, bool unpool) -> bool { return tp_wino_staged_ok((int)H, (int)W, unpool ? 1 : 0) != 0; });
+  m.def("wino4_taylor_slots(int S) -> int", [](int64_t S) -> int64_t { return tp_wino4_taylor_slots((int)S); });
   m.def("wino4_lds_bytes(int S, int variant=0) -> int",
         [](int64_t S, int64_t variant) -> int64_t { return tp_wino4_lds_bytes((int)S, (int)variant); });
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");

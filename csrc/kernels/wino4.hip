@@ -70,6 +70,21 @@ template <int TB> struct GeoT<16, TB> { static constexpr int NI = TB / 16, RH = 
 template <int TB> struct GeoT<8, TB> { static constexpr int NI = TB / 4, RH = 10, RWP = 10, IP = 101, PAD = 0; };
 template <int TB> struct GeoT<4, TB> { static constexpr int NI = TB, RH = 4, RWP = 4, IP = 17, PAD = 0; };
 template <int S> constexpr int x_rounds() { return (2 * plane_slots<S>() + 255) / 256; }
+// Band geometry: square maps of any other size (ResNet's 56 / 28 / 14 / 7 pixels). Tile rows hold
+// TPR = ceil(S / 4) tiles (the last one partial when S % 4: its out-of-map pixels read zeros and
+// are not stored); a block takes BR whole tile rows counted across images (TBR <= 32 real tiles,
+// the other MFMA rows are padding); each tile row is staged on its own — 6 pixel rows with the
+// halo, columns x' = x + 1 in [0, 4 TPR + 1] with a pad slot after every 4 (col' = x' + x'/4) — so
+// a band that straddles two images needs no special case. R: Taylor partial slots per image (the
+// most bands one image's TPR tile rows can overlap; one writer per slot).
+template <int S> struct Band {
+  static constexpr bool ON = !(S == 4 || S == 8 || S == 16 || S == 32);
+  static constexpr int TPR = (S + 3) / 4, BR = 32 / TPR, TBR = BR * TPR;
+  static constexpr int W = 4 * TPR + 2, RWP = W + (W - 1) / 4, RH = 6 * BR;
+  static constexpr int NI = 1, IP = RH * RWP, PAD = 1;
+  static constexpr int R = (TPR + BR - 2) / BR + 1;
+  static_assert(!ON || (S >= 5 && BR >= 1), "band geometry: 5 <= S <= 128");
+};
 
 struct Args {
   const float* x;     // NHWC (B, S, S, C): the input (forward) or the output gradient (dgrad)
@@ -283,8 +298,12 @@ __device__ __forceinline__ void sp_phase1(const f32x4 (&acc)[NPT], int ph, int g
 template <int EPI, int S, int NW, int PPW = 1, bool SPP = false>
 __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], int t0, int k0, float* ya, float* yb,
                                          float* part) {
-  constexpr int TPR = S / 4, TI = TPR * TPR;
+  constexpr int TPR = (S + 3) / 4, TI = TPR * TPR;
   constexpr int GROUPS = NW * PPW / 2, TB = 16 * GROUPS, HALVES = TB / 32, TPW = 32 / NW;  // tiles per wave (phase 2)
+  constexpr bool BAND = Band<S>::ON;
+  constexpr int TBR = BAND ? Band<S>::TBR : TB;  // real tiles of the block (t0 = block * TBR)
+  constexpr bool PART_TILE = S % 4 != 0;         // the last tile of a row is partial
+  static_assert(!BAND || (EPI != FWD_POOL && NW == 4 && PPW == 1), "band geometry: no pooling, 4-wave blocks");
   static_assert(!SPP || PPW == 1, "split-points epilogue: one accumulator set per wave");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -329,13 +348,16 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
       const int qq = lane >> 3;
 #pragma unroll
       for (int tt = 0; tt < TPW; ++tt) {
-        const int pt = t0 + hf * 32 + wave * TPW + tt;
+        const int tbv = hf * 32 + wave * TPW + tt;
+        const int pt = t0 + tbv;
         const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
           const int q = qq + 8 * h2;
-          const long long pix = ((long long)b * S + 4 * tr + (q >> 2)) * S + 4 * tc + (q & 3);
-          apre[tt][h2] = pt < p.P ? *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const int yy = 4 * tr + (q >> 2), xx = 4 * tc + (q & 3);
+          const long long pix = ((long long)b * S + yy) * S + xx;
+          const bool ok = pt < p.P && tbv < TBR && (!PART_TILE || (yy < S && xx < S));
+          apre[tt][h2] = ok ? *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
@@ -389,11 +411,12 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
         const int tb = hf * 32 + tl;
         const int pt = t0 + tb;
         f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-        if (pt < p.P) {
+        if (pt < p.P && tb < TBR) {
           const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2) {
             const int q = qq + 8 * h2;
+            if (PART_TILE && (4 * tr + (q >> 2) >= S || 4 * tc + (q & 3) >= S)) continue;  // outside the map
             const f32x4 yv = *reinterpret_cast<const f32x4*>(ysrc + tl * TPL + q * 16);
             const long long pix = ((long long)b * S + 4 * tr + (q >> 2)) * S + 4 * tc + (q & 3);
             if constexpr (EPI == PARTIAL) {
@@ -450,6 +473,27 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
     __syncthreads();  // ya / yb are rewritten by the next half
   }
   if (!want_part) return;
+  if constexpr (BAND) {
+    // a band's tiles cover consecutive images (one writer per (slot, image, channel): slot = this
+    // block's index among the bands that overlap the image; APoZ counts are exact, added atomically)
+    const int b0 = t0 / TI, nimg = (t0 + TBR - 1) / TI - b0 + 1;
+    const int blk = t0 / TBR;
+    for (int t = tid; t < nimg * TK; t += 64 * NW) {
+      const int il = t / TK, kk = t - il * TK;
+      const int b = b0 + il;
+      if (b >= p.B) continue;
+      const int s0 = max(0, b * TI - t0), s1 = min(TBR, (b + 1) * TI - t0);
+      float s = 0.f;
+      for (int ti = s0; ti < s1; ++ti) s += part[ti * TK + kk];
+      if constexpr (EPI == BWD) {
+        const int slot = blk - (b * TPR) / Band<S>::BR;
+        p.taylor[((long long)slot * p.B + b) * p.K + k0 + kk] += s;
+      } else {
+        if (s > 0.f) atomicAdd(p.apoz + (long long)b * p.K + k0 + kk, s);
+      }
+    }
+    return;
+  }
   // ---- per-(image, channel) sums over the block's tiles of the image, fixed order ------------
   // Whole images per block: one writer per sum. A block of half an image (S = 32, 32 tiles):
   // Taylor partials go to slot (half) of the (R, B, K) slab (single writer per slot); APoZ counts
@@ -886,8 +930,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   static_assert(!SPLITP || (NW == 4 && !SPREAD), "split points: 4-wave blocks, burst DMA");
   constexpr int TB = 8 * NW, NG = NW / 2;  // tiles per block, 16-tile groups
   constexpr bool XDBL = NW == 8;           // X double-buffered (one block per CU)
-  using G = GeoT<S, TB>;
-  constexpr int TPR = S / 4, TI = TPR * TPR;
+  constexpr bool BAND = Band<S>::ON;
+  static_assert(!BAND || SPLITP, "band geometry: the split-points kernel");
+  using G = std::conditional_t<BAND, Band<S>, GeoT<S, TB>>;
+  constexpr int TPR = (S + 3) / 4, TI = TPR * TPR;
+  constexpr int TBR = BAND ? Band<S>::TBR : TB;  // real tiles per block
   constexpr int PL = G::NI * G::IP;
   constexpr int NXI = (2 * PL + 63) / 64;  // X DMA wave-instructions (64 16-B slots each)
   constexpr int KX = (NXI + NW - 1) / NW;
@@ -904,7 +951,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int kb = tile % n_k, k0 = kb * TK;
   const int blk_p = tile / n_k;
-  const int t0 = blk_p * TB;
+  const int t0 = blk_p * TBR;
   const int b0 = t0 / TI;
   const int grp = wave % NG, nh = wave / NG;
 
@@ -912,19 +959,39 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   const i32x4v xrs = raw_rsrc(p.x, (unsigned)(p.x_elems * 4));
 
   const int tib = grp * 16 + j;
-  const int il = tib / TI, ti = tib - il * TI, tr = ti / TPR, tc = ti - tr * TPR;
-  const int sbase = S == 4 ? il * G::IP : il * G::IP + 4 * tr * G::RWP + (G::PAD ? 5 : 4) * tc;
+  int sbase;
+  if constexpr (BAND) {
+    const int sl = tib < TBR ? tib : 0;  // padding MFMA rows read tile 0's patch (results dropped)
+    sbase = (sl / TPR) * 6 * G::RWP + 5 * (sl % TPR);
+  } else {
+    const int il = tib / TI, ti = tib - il * TI, tr = ti / TPR, tc = ti - tr * TPR;
+    sbase = S == 4 ? il * G::IP : il * G::IP + 4 * tr * G::RWP + (G::PAD ? 5 : 4) * tc;
+  }
   const int poff = ((g >> 1) * PL + sbase) * 4 + (g & 1) * 2;  // plane g/2, channels 2g, 2g+1
 
   // X DMA sources, 16 bits per instruction: pixel index relative to the block's first image (11
   // bits), plane (1), valid (1); the byte offset is rebuilt at issue (3 VALU) — half the registers
-  unsigned xcode[(KX + 1) / 2];
+  // (band geometry: 32-bit codes — valid bit 31, plane bit 30, pixel index from the block's first
+  // image in bits 0-29)
+  unsigned xcode[BAND ? KX : (KX + 1) / 2];
 #pragma unroll
-  for (int i = 0; i < (KX + 1) / 2; ++i) xcode[i] = 0u;
+  for (int i = 0; i < (BAND ? KX : (KX + 1) / 2); ++i) xcode[i] = 0u;
 #pragma unroll
   for (int i = 0; i < KX; ++i) {
     const int slot = (wave + NW * i) * 64 + lane;
     const int h = slot / PL, s = slot - h * PL;
+    if constexpr (BAND) {
+      const int row = s / G::RWP, colp = s - row * G::RWP;
+      const int bi = row / 6, rr = row - bi * 6;
+      const int blk5 = colp / 5, w5 = colp - blk5 * 5;
+      const int xx = 4 * blk5 + w5 - 1;
+      const int gr = blk_p * Band<S>::BR + bi;  // global tile row
+      const int b = gr / TPR, tr = gr - b * TPR;
+      const int yy = 4 * tr - 1 + rr;
+      const bool ok = h < 2 && bi < Band<S>::BR && w5 != 4 && xx >= 0 && xx < S && yy >= 0 && yy < S && b < p.B;
+      xcode[i] = ok ? 0x80000000u | ((unsigned)h << 30) | (unsigned)(((b - b0) * S + yy) * S + xx) : 0u;
+      continue;
+    }
     const int im = s / G::IP, rem = s - im * G::IP;
     int xx, yy;
     bool ok;
@@ -949,7 +1016,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
     const unsigned code = ok ? (unsigned)((im * S + yy) * S + xx) | ((unsigned)h << 11) | 0x1000u : 0u;
     xcode[i >> 1] |= code << (16 * (i & 1));
   }
-  static_assert(G::NI * S * S <= 2048, "X pixel code");
+  static_assert(BAND || G::NI * S * S <= 2048, "X pixel code");
   const unsigned xbase = (unsigned)b0 * S * S * (unsigned)p.C * 4u;
   const unsigned lane16 = (unsigned)lane * 16u;
   const unsigned c4 = (unsigned)p.C * 4u;
@@ -972,8 +1039,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
 #pragma unroll
     for (int i = 0; i < KX; ++i)
       if (wave + NW * i < NXI) {
-        const unsigned code = xcode[i >> 1] >> (16 * (i & 1));
-        const unsigned off = (code & 0x1000u) ? xbase + (code & 0x7ffu) * c4 + ((code >> 7) & 16u) : OOB;
+        unsigned off;
+        if constexpr (BAND) {
+          const unsigned code = xcode[i];
+          off = (code >> 31) ? xbase + (code & 0x3fffffffu) * c4 + ((code >> 26) & 16u) : OOB;
+        } else {
+          const unsigned code = xcode[i >> 1] >> (16 * (i & 1));
+          off = (code & 0x1000u) ? xbase + (code & 0x7ffu) * c4 + ((code >> 7) & 16u) : OOB;
+        }
         dma16_asm(xrs, lds_addr(xd + (wave + NW * i) * 256), off, (unsigned)c0 * 4u);
       }
   };
@@ -1420,8 +1493,25 @@ extern "C" hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, i
 
 extern "C" int tp_wino4_u_img() { return tp::w4::U_IMG; }
 
+// square map sizes served by the band geometry (split-points kernel only): ResNet's 3x3 stride-1 maps
+static bool wino4_band_size(int S) { return S == 56 || S == 28 || S == 14 || S == 7; }
+
 extern "C" int tp_wino4_ok(int H, int W, int C, int K) {
-  return H == W && (H == 4 || H == 8 || H == 16 || H == 32) && C % 8 == 0 && C >= 8 && K % 32 == 0 && K >= 32;
+  return H == W && (H == 4 || H == 8 || H == 16 || H == 32 || wino4_band_size(H)) && C % 8 == 0 && C >= 8 &&
+         K % 32 == 0 && K >= 32;
+}
+
+// Taylor partial slots (R of the (R, B, K) slab) a wino4 data gradient writes at S x S maps
+extern "C" int tp_wino4_taylor_slots(int S) {
+  using namespace tp::w4;
+  switch (S) {
+    case 56: return Band<56>::R;
+    case 28: return Band<28>::R;
+    case 14: return Band<14>::R;
+    case 7: return Band<7>::R;
+    case 32: return 2;
+    default: return 1;
+  }
 }
 
 // F(4x4,3x3) conv, S x S maps. epi: 0 fwd (BN affine + ReLU), 1 fwd + 2x2 max-pool (+ argmax),
@@ -1444,6 +1534,9 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
                                     float* ws, int variant, hipStream_t st, const uint8_t* unpool_am) {
   using namespace tp::w4;
   if (!tp_wino4_ok(S, S, C, K) || B <= 0) return hipErrorInvalidValue;
+  // band geometry (56 / 28 / 14 / 7-pixel maps): the split-points kernel, no pooling / unpooling
+  const bool band = wino4_band_size(S);
+  if (band && (variant != 3 || epi == FWD_POOL || unpool_am)) return hipErrorInvalidValue;
   const int nc = C / 8;
   splits = std::max(1, std::min(splits, nc));
   splits = (nc + (nc + splits - 1) / splits - 1) / ((nc + splits - 1) / splits);  // no empty split
@@ -1462,7 +1555,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   a.B = B;
   a.C = C;
   a.K = K;
-  const int tpr = S / 4;
+  const int tpr = (S + 3) / 4;
   a.P = B * tpr * tpr;
   a.x_elems = (long long)B * S * S * C;
   if (a.x_elems * 4 >= (1ll << 31) || (long long)(C / 8) * (K / 32) * U_IMG * 4 >= (1ll << 31))
@@ -1488,7 +1581,8 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   // 5: MODE 3 with SPREAD DMA; 6: MODE 3 with split points
   const int mode = wide ? 4 : variant == 2 ? 5 : variant == 3 ? 6 : kernel_mode();
   const int tb = mode == 2 || mode == 4 ? 64 : TILES;  // MODE 3: 32-tile blocks
-  const int n_p = (a.P + tb - 1) / tb, n_k = K / TK;
+  const int br = band ? 32 / tpr : 0;                  // band: whole tile rows per block
+  const int n_p = band ? (B * tpr + br - 1) / br : (a.P + tb - 1) / tb, n_k = K / TK;
   const dim3 grid(n_p * n_k, splits);
   if (splits > 1) {
     Args b = a;
@@ -1502,6 +1596,17 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
     b.slab = (long long)B * S * S * K;
     b.pool_order = epi == FWD_POOL;
     if (b.slab * splits >= (1ll << 31)) return hipErrorInvalidValue;
+    if (band) {
+      if (S == 56) wino4_m2<PARTIAL, 56, 4, false, true><<<grid, 256, 0, st>>>(b);
+      else if (S == 28) wino4_m2<PARTIAL, 28, 4, false, true><<<grid, 256, 0, st>>>(b);
+      else if (S == 14) wino4_m2<PARTIAL, 14, 4, false, true><<<grid, 256, 0, st>>>(b);
+      else wino4_m2<PARTIAL, 7, 4, false, true><<<grid, 256, 0, st>>>(b);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      return tp_conv_epilogue_slabs(ws, splits, B, S, S, K, epi, scale, epi == BWD ? nullptr : shift, relu, out,
+                                    out_argmax, act, epi == BWD ? taylor : nullptr, epi == BWD ? nullptr : apoz,
+                                    tay_mode, st);
+    }
 #define TP_W4P(SS)                                                                      \
   do {                                                                                  \
     if (mode == 4) wino4_wide<PARTIAL, SS><<<grid, 256, 0, st>>>(b);                    \
@@ -1538,6 +1643,19 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
     else if (S == 8) TP_W4(E, 8);   \
     else TP_W4(E, 4);               \
   } while (0)
+#define TP_W4B(E)                                                                \
+  do {                                                                           \
+    if (S == 56) wino4_m2<E, 56, 4, false, true><<<grid, 256, 0, st>>>(a);       \
+    else if (S == 28) wino4_m2<E, 28, 4, false, true><<<grid, 256, 0, st>>>(a);  \
+    else if (S == 14) wino4_m2<E, 14, 4, false, true><<<grid, 256, 0, st>>>(a);  \
+    else wino4_m2<E, 7, 4, false, true><<<grid, 256, 0, st>>>(a);                \
+  } while (0)
+  if (band) {
+    if (epi == FWD) TP_W4B(FWD);
+    else TP_W4B(BWD);
+    return hipGetLastError();
+  }
+#undef TP_W4B
   if (epi == FWD) TP_W4S(FWD);
   else if (epi == FWD_POOL) TP_W4S(FWD_POOL);
   else TP_W4S(BWD);
@@ -1551,6 +1669,15 @@ extern "C" int tp_wino4_lds_bytes(int S, int variant) {
   using namespace tp::w4;
   const int m = variant == 1 ? 4 : variant >= 2 ? 3 : kernel_mode();
   const void* f = nullptr;
+  if (wino4_band_size(S)) {
+    f = S == 56 ? (const void*)wino4_m2<BWD, 56, 4, false, true>
+        : S == 28 ? (const void*)wino4_m2<BWD, 28, 4, false, true>
+        : S == 14 ? (const void*)wino4_m2<BWD, 14, 4, false, true>
+                  : (const void*)wino4_m2<BWD, 7, 4, false, true>;
+    hipFuncAttributes at{};
+    if (hipFuncGetAttributes(&at, f) != hipSuccess) return -1;
+    return (int)at.sharedSizeBytes;
+  }
 #define TP_W4F(SS)                                                                            \
   f = m == 4 ? (const void*)wino4_wide<BWD, SS>                                               \
              : m == 2 ? (const void*)wino4_m2<BWD, SS, 8>                                     \

@@ -182,3 +182,82 @@ def test_wino4_dgrad_fused_unpool(cuda, S, C, K, B, variant):
     assert torch.equal(t1, t2)
     with pytest.raises(RuntimeError):  # split-K combines pooled rows: the fused path is one K pass
         T.conv_wino4_dgrad(go, ut, act, sc, None, True, 0, 2, variant, am)
+
+
+# band geometry (split-points kernel, variant 3): ResNet's 56/28/14/7-pixel maps — whole tile rows
+# per block counted across images (28-pixel bands straddle images), partial last tiles at 14 / 7
+BAND_SHAPES = [(56, 64, 64, 3), (28, 128, 128, 2), (14, 256, 256, 3), (7, 512, 64, 5), (28, 24, 32, 3),
+               (7, 64, 96, 37), (14, 32, 32, 1)]
+
+
+@pytest.mark.parametrize("S,C,K,B", BAND_SHAPES)
+def test_wino4_band_forward(cuda, S, C, K, B):
+    T = _ops()
+    g = torch.Generator(device=cuda).manual_seed(S * 1000 + C + K + B)
+    x = torch.randn(B, S, S, C, device=cuda, generator=g)
+    w = torch.randn(K, C, 3, 3, device=cuda, generator=g) / (3 * C ** 0.5)
+    sc = torch.rand(K, device=cuda, generator=g) + 0.5
+    sh = torch.randn(K, device=cuda, generator=g) * 0.1
+    u = T.wino4_weights(w, False, 0, 0)
+    apoz = torch.zeros(B, K, device=cuda)
+    y, _ = T.conv_wino4_fwd(x, u, sc, sh, True, False, apoz, 1, 3)
+    ref = _fwd_ref(x, w, sc, sh)
+    err = ((y.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-5, err
+    cnt = (ref > 0).sum((1, 2)).float()
+    assert (apoz - cnt).abs().max().item() <= max(2.0, 1e-3 * S * S), (apoz - cnt).abs().max()
+    # no pooling, and only the split-points kernel has the band geometry
+    with pytest.raises(RuntimeError):
+        T.conv_wino4_fwd(x, u, sc, sh, True, True, None, 1, 3)
+    with pytest.raises(RuntimeError):
+        T.conv_wino4_fwd(x, u, sc, sh, True, False, None, 1, 0)
+
+
+@pytest.mark.parametrize("S,C,K,B", BAND_SHAPES)
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_wino4_band_dgrad(cuda, S, C, K, B, mode):
+    """Band-geometry data gradient: masked output and the Taylor / Sensitivity / masked-|g| partials
+    over T.wino4_taylor_slots(S) slots (a band straddling two images writes one slot of each)."""
+    T = _ops()
+    Cout, Cin = C, K
+    gen = torch.Generator(device=cuda).manual_seed(S * 7 + C * 3 + K + mode)
+    w = torch.randn(Cout, Cin, 3, 3, device=cuda, generator=gen) / (3 * Cin ** 0.5)
+    go = torch.randn(B, S, S, Cout, device=cuda, generator=gen)
+    act = torch.relu(torch.randn(B, S, S, Cin, device=cuda, generator=gen))
+    sc = torch.rand(Cin, device=cuda, generator=gen) + 0.5
+    ut = T.wino4_weights(w, True, 0, 0)
+    R = T.wino4_taylor_slots(S)
+    assert R >= 1
+    tay = torch.zeros(R, B, Cin, device=cuda)
+    out = T.conv_wino4_dgrad(go, ut, act, sc, tay, True, mode, 1, 3)
+    dx = torch.nn.grad.conv2d_input((B, Cin, S, S), w.double(), go.double().permute(0, 3, 1, 2), padding=1)
+    dx = dx.permute(0, 2, 3, 1)
+    zero = torch.zeros((), dtype=torch.float64, device=cuda)
+    ref_out = torch.where(act.double() > 0, dx * sc.double(), zero)
+    err = ((out.double() - ref_out).abs().max() / ref_out.abs().max()).item()
+    assert err < 2e-5, err
+    part = {0: -(dx * act.double()), 1: dx.abs(), 2: torch.where(act.double() > 0, dx.abs(), zero)}[mode]
+    ref_t = part.sum((1, 2))
+    errt = ((tay.double().sum(0) - ref_t).abs().max() / ref_t.abs().max()).item()
+    assert errt < 2e-5, errt
+    # no output: the partials alone
+    tay2 = torch.zeros(R, B, Cin, device=cuda)
+    T.conv_wino4_dgrad(go, ut, act, sc, tay2, False, mode, 1, 3)
+    assert torch.equal(tay2, tay)
+
+
+@pytest.mark.parametrize("S,C,K,B", [(56, 64, 64, 2), (28, 128, 64, 3), (7, 512, 64, 4)])
+def test_wino4_band_split_k(cuda, S, C, K, B):
+    T = _ops()
+    g = torch.Generator(device=cuda).manual_seed(S + C + 11)
+    x = torch.randn(B, S, S, C, device=cuda, generator=g)
+    w = torch.randn(K, C, 3, 3, device=cuda, generator=g) / (3 * C ** 0.5)
+    sc = torch.rand(K, device=cuda, generator=g) + 0.5
+    sh = torch.randn(K, device=cuda, generator=g) * 0.1
+    u = T.wino4_weights(w, False, 0, 0)
+    a1, a2 = torch.zeros(B, K, device=cuda), torch.zeros(B, K, device=cuda)
+    y1, _ = T.conv_wino4_fwd(x, u, sc, sh, True, False, a1, 1, 3)
+    y2, _ = T.conv_wino4_fwd(x, u, sc, sh, True, False, a2, 2, 3)
+    assert ((y1 - y2).abs().max() / y1.abs().max()).item() < 1e-4
+    assert (a1 - a2).abs().max().item() <= 2.0
+    assert 0 < T.wino4_lds_bytes(S) <= 80 * 1024  # two blocks per CU

@@ -28,8 +28,28 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import (TUNER, WINO, WINO_LDS, _wino_splits, cpad, logits_grad, sk_candidates, taylor_slots,
-                          winograd_weights)
+from .fused_chain import (_CU, _W4_SPLITS, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, logits_grad,
+                          sk_candidates, taylor_slots, winograd_weights)
+
+_W4_SIZES = (56, 28, 14, 7, 32, 16, 8, 4)  # square maps of the F(4x4) kernel (band geometry for the first four)
+
+
+def wino4_cands(B: int, S: int, K: int, C: int):
+    """F(4x4,3x3) split-points candidates (WINO4S, channel splits) for a stride-1 pad-1 3x3 conv on
+    S x S maps (wino4.hip; ResNet's 56/28/14/7-pixel maps use its band geometry: whole 4-pixel tile
+    rows per block, counted across images); empty when the kernel does not apply."""
+    if S not in _W4_SIZES or C % 8 or K % 32:
+        return []
+    tpr = (S + 3) // 4
+    if S in (56, 28, 14, 7):
+        br = 32 // tpr
+        blocks = -(-B * tpr // br) * (K // 32)
+    else:
+        blocks = -(-B * tpr * tpr // 32) * (K // 32)
+    sp, chunks = 1, C // 8
+    while _W4_SPLITS and blocks * sp < 2 * _CU and sp * 2 <= chunks // 4 and sp < 16:
+        sp *= 2
+    return [(WINO4S, 1)] + ([(WINO4S, sp)] if sp > 1 else [])
 
 
 @dataclass
@@ -170,6 +190,7 @@ class ResNetEngine:
              "stride": c.conv.stride[0], "pad": c.conv.padding[0]}
         if e["ks"] == 3 and e["stride"] == 1 and w.shape[1] % 8 == 0 and w.shape[0] % 32 == 0:
             e["u"] = winograd_weights(w)  # stride-1 3x3: Winograd candidate
+            e["w4d"] = w.contiguous()     # F(4x4) U images built on first use (_u4)
         return e
 
     def _pack(self):
@@ -194,6 +215,15 @@ class ResNetEngine:
         return self._packed
 
     @staticmethod
+    def _u4(T, e, dgrad=False):
+        """F(4x4) U images of a stride-1 3x3 conv (forward, or the data gradient's flipped /
+        transposed operand with the BN scale folded in), cached in the packed entry."""
+        key = "ut4" if dgrad else "u4"
+        if key not in e:
+            e[key] = T.wino4_weights(e["w4t"] if dgrad else e["w4d"], dgrad, 0, 0)
+        return e[key]
+
+    @staticmethod
     def _conv(T, e, h, relu, res=None, apoz=None):
         B, H, W, C = h.shape
         ks, s, pd = e["ks"], e["stride"], e["pad"]
@@ -205,11 +235,15 @@ class ResNetEngine:
         if "u" in e and res is None:  # odd H / W: partial last tile row / column (direct loads)
             sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + ([(WINO_LDS, 1)] if sp0 > 1 else []) + cands
+            if H == W and pd == 1:
+                cands = cands + wino4_cands(B, H, N, C)
         key = ("gen", tuple(h.shape), N, ks, s, res is not None)
 
         def run(cfg, sp, hh=h, ap=None):
             if cfg in (WINO, WINO_LDS):
                 return T.conv_wino_fwd(hh, e["u"], e["scale"], e["shift"], relu, False, sp, cfg == WINO_LDS, ap)[0]
+            if cfg == WINO4S:
+                return T.conv_wino4_fwd(hh, ResNetEngine._u4(T, e), e["scale"], e["shift"], relu, False, ap, sp, 3)[0]
             return T.conv_gen(hh, e["w"], e["scale"], e["shift"], relu, res, ap, ks, s, pd, cfg, sp)
 
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands)
@@ -348,6 +382,7 @@ class ResNetEngine:
         elif e["stride"] == 1:  # stride-1 3x3 dgrad = conv of g with flipped taps
             e["wt"] = w4.flip(1, 2).permute(3, 1, 2, 0).reshape(ci, ks * ks * co).contiguous()
             e["ut"] = winograd_weights(w4.permute(0, 3, 1, 2).flip(2, 3).transpose(0, 1))
+            e["w4t"] = w4.permute(0, 3, 1, 2).contiguous()  # (co, ci, 3, 3): wino4_weights flips it
         else:  # strided: transposed gather kernel, natural tap order
             e["wt"] = w4.permute(3, 1, 2, 0).reshape(ci, ks * ks * co).contiguous()
         return e
@@ -379,6 +414,8 @@ class ResNetEngine:
         if wino_ok:
             sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
+            if H == W and e["pad"] == 1:
+                cands = cands + wino4_cands(B, H, N, C)
         key = ("rbwd", tuple(g.shape), N, ks, s, transposed, res is not None, res_stride, mask is not None)
 
         # 1x1 dgrads with fused Taylor partials: one K pass, tiles spanning <= 4 images
@@ -392,12 +429,18 @@ class ResNetEngine:
             if cfg in (WINO, WINO_LDS):  # Sensitivity of the BN before the ReLU: |g| where a > 0 (mode 2)
                 return T.conv_wino_dgrad(gg, None, e["ut"], mm, None, tay, True, sp, cfg == WINO_LDS,
                                          2 if tay_mode == 1 else 0)
+            if cfg == WINO4S:
+                return T.conv_wino4_dgrad(gg, ResNetEngine._u4(T, e, True), mm, None, tay, True,
+                                          2 if tay_mode == 1 else 0, sp, 3)
             return T.conv_gen_bwd(gg, e["wt"], rr, res_stride, mm, ks, s if transposed else 1, pad, Ho, Wo,
                                   transposed, cfg, sp, tay, tay_mode or 0)
 
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands if cands else None)
         if tay_mode is not None and cfg in (WINO, WINO_LDS):
             tay = torch.zeros(taylor_slots(Ho, Wo), B, N, device=g.device)
+            return run(cfg, sp, tay=tay), tay
+        if tay_mode is not None and cfg == WINO4S:
+            tay = torch.zeros(T.wino4_taylor_slots(Ho), B, N, device=g.device)
             return run(cfg, sp, tay=tay), tay
         if gen_tay:
             tay = torch.zeros(T.conv_gen_tay_slots(cfg, Ho * Wo), B, N, device=g.device)
