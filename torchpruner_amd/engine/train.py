@@ -37,7 +37,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .fused_chain import _CU, TUNER, WINO, WINO_LDS, _wino_splits, cpad, sk_candidates
+from .fused_chain import _CU, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, sk_candidates
+from .resnet_engine import wino4_cands
 
 
 def _wino_ok(ks, stride, pad, H, W, cin, cout) -> bool:
@@ -123,6 +124,10 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
             if "u" not in cache:
                 cache["u"] = T.wino_weights(w32, False, cout_p, cin_p)
             return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
+        if cfg == WINO4S:  # Winograd F(4x4,3x3): 4x fewer multiplies (band geometry on ResNet's maps)
+            if "u4" not in cache:
+                cache["u4"] = T.wino4_weights(w32, False, cout_p, cin_p)
+            return T.conv_wino4_fwd(xh, cache["u4"], None, shift, False, False, None, sp, 3)[0]
         if "wk" not in cache:  # [cout_p][(kh, kw, ci)] zero-padded GEMM operand
             cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
         return T.conv_gen(xh, cache["wk"], None, shift, False, None, None, ks, stride, pad, cfg, sp)
@@ -133,9 +138,11 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
     if wino:
         sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cout_p, cin_p)
         cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
+        if H == W:
+            cands = cands + wino4_cands(B, H, cout_p, cin_p)
     cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
     part = None
-    if stats and _EPI_STATS and cfg not in (WINO, WINO_LDS) and sp == 1:
+    if stats and _EPI_STATS and cfg not in (WINO, WINO_LDS, WINO4S) and sp == 1:
         if "wk" not in cache:
             cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
         y, part = T.conv_gen_stats(xh, cache["wk"], shift, ks, stride, pad, cfg)
@@ -180,6 +187,10 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
             if "ut" not in cache:
                 cache["ut"] = T.wino_weights(w32, True, cin_p, cout_p)
             return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
+        if cfg == WINO4S:
+            if "ut4" not in cache:
+                cache["ut4"] = T.wino4_weights(w32, True, cin_p, cout_p)
+            return T.conv_wino4_fwd(g, cache["ut4"], None, None, False, False, None, sp, 3)[0]
         if "wt" not in cache:  # [ci][(kh, kw, co)], flipped for stride 1
             cache["wt"] = T.pack_conv_weight(w32, cin_p, K, cout_p, 2 if transposed else 1)
         return T.conv_gen_bwd(g, cache["wt"], res, res_stride, None, ks, stride if transposed else 1, pad_b, H, W,
@@ -190,6 +201,8 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
         cands = cands + sk_candidates(T, cands, ks, M, cin_p)
     if wino:
         cands = [(WINO_LDS, _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cin_p, cout_p)), (WINO, 1)] + cands
+        if H == W:
+            cands = cands + wino4_cands(B, H, cin_p, cout_p)
     key = ("tdgrad", tuple(g.shape), cin_p, ks, stride, pad, res is not None and res_stride)
     cfg, sp = TUNER.choose(key, M, cin_p, K, run, cands=cands)
     return run(cfg, sp)
