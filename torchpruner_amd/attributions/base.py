@@ -708,7 +708,11 @@ class _BatchPipeline:
     buffer allocation, lazily packed operands). Two batches' activations are live at once, so it
     is off for inputs of >= 2^24 pixels per batch (B >= 16384 at 32x32, B >= 335 at 224x224;
     TORCHPRUNER_STREAMS_MAX_PIXELS overrides), with TORCHPRUNER_GRAPHS=1/all (one graph-replayed
-    batch at a time), and with TORCHPRUNER_STREAMS=0. ResNet-50 at B=256: APoZ +8%, Taylor +7%.
+    batch at a time), and with TORCHPRUNER_STREAMS=0. ResNet-50 at B=256: APoZ +8%, Taylor +7%
+    (round 4, F(2x2) 3x3 kernels); with the F(4x4) band kernels three batches in flight for
+    large images (>= 112 x 112: ~70 launches per step, many of them short 7/14-px layers) measured
+    +1-2% over two (APoZ 14.96k -> 15.08k, Taylor 7.72k -> 7.87k), while the 32x32 headline
+    keeps two (three: -0.6 to -1%).
     On the fused VGG/MLP engine a pipelined batch replays a HIP graph of its step per slot
     (FusedChainEngine.graphs_enabled), captured on the slot's first batch: with two batches in
     flight the B=100 step is host-bound otherwise."""
@@ -772,7 +776,9 @@ class _BatchPipeline:
         if self.depth is not None:
             return self.depth
         small = x.shape[0] * math.prod(x.shape[2:]) <= self.DEEP_MAX_PIXELS
-        return 4 if small and self.graph_replay and graphs is not None and graphs(x.shape[0], pipelined=True) else 2
+        if small and self.graph_replay and graphs is not None and graphs(x.shape[0], pipelined=True):
+            return 4
+        return 3 if x.dim() == 4 and x.shape[2] * x.shape[3] >= 112 * 112 else 2
 
     def _end_tuning(self):
         if getattr(self, "_tuning", False):
