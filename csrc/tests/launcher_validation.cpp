@@ -15,6 +15,12 @@ int tp_wino_staged_ok(int H, int W, int unpool);
 void tp_wino_geometry(int H, int W, int unpool, int* out9);
 int tp_bn_groups(int P, int C);
 long long tp_conv_sk_ws_floats(int cfg, int ks, int transposed, int tay, int M, int N);
+int tp_wino4_ok(int H, int W, int C, int K);
+int tp_wino4_taylor_slots(int S);
+hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
+                         const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act, float* taylor,
+                         float* apoz, int tay_mode, int splits, float* ws, int variant, hipStream_t st,
+                         const uint8_t* unpool_am);
 hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
                         int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
                         const float* shift, int relu, const float* res, int res_stride, const float* mask,
@@ -113,6 +119,18 @@ int main() {
   EXPECT(tp_conv_sk_ws_floats(0, 5, 0, 0, 1 << 20, 512) == 0);  // 5x5
   EXPECT(tp_conv_sk_ws_floats(16, 1, 0, 0, 1 << 20, 512) == 0); // warp-specialised cfg
   EXPECT(tp_conv_sk_ws_floats(0, 3, 0, 1, 1 << 20, 512) == 0);  // Taylor partials are 1x1 only
+  // F(4x4): VGG sizes and the band geometry's ResNet sizes; bands never pool / unpool and only the
+  // split-points kernel (variant 3) has them; Taylor slots per image = the most bands overlapping it
+  EXPECT(tp_wino4_ok(32, 32, 64, 64) && tp_wino4_ok(56, 56, 64, 64) && tp_wino4_ok(7, 7, 512, 512));
+  EXPECT(!tp_wino4_ok(12, 12, 64, 64) && !tp_wino4_ok(56, 28, 64, 64) && !tp_wino4_ok(56, 56, 64, 48));
+  EXPECT(tp_wino4_taylor_slots(56) == 8 && tp_wino4_taylor_slots(28) == 3 && tp_wino4_taylor_slots(14) == 2);
+  EXPECT(tp_wino4_taylor_slots(7) == 2 && tp_wino4_taylor_slots(32) == 2 && tp_wino4_taylor_slots(8) == 1);
+  EXPECT(tp_conv_wino4(n, n, 2, 56, 64, 64, 1, n, n, 1, n, nullptr, n, n, n, 0, 1, n, 3, 0, nullptr) ==
+         hipErrorInvalidValue);  // band + 2x2 pool
+  EXPECT(tp_conv_wino4(n, n, 2, 28, 64, 64, 0, n, n, 1, n, nullptr, n, n, n, 0, 1, n, 0, 0, nullptr) ==
+         hipErrorInvalidValue);  // band on the MODE 3 kernel
+  EXPECT(tp_conv_wino4(n, n, 2, 14, 64, 64, 2, n, n, 0, n, nullptr, n, n, n, 0, 1, n, 3, 0,
+                       reinterpret_cast<const uint8_t*>(n)) == hipErrorInvalidValue);  // dgrad without act
 
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
