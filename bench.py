@@ -85,7 +85,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the generic-path / ResNet-50 / Shapley figures")
     ap.add_argument("--generic-steps", type=int, default=2)
-    ap.add_argument("--resnet-steps", type=int, default=8)
+    ap.add_argument("--resnet-steps", type=int, default=16)
     ap.add_argument("--resnet-batch", type=int, default=256, help="config #3 images per GPU per step")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--quality-seeds", type=int, default=5,

@@ -624,25 +624,28 @@ class _AttributionMetric(ABC):
         # batches past the kernels' descriptor range run in slices (whole-batch loss scaling)
         big = (lambda x: eng.max_batch(tuple(x.shape[1:]))) if crit is None else None
         with torch.no_grad():
+            # stats: epilogue partial slabs come back raw, (R, B, C); the fold sums their slots and
+            # takes |.| for Taylor in its one launch (|.| of the already-final slabs is a no-op)
+            take_abs = stats and mode == "taylor"
             for i, x, y, lb in self._coalesced_batches(False, big):
                 def fold(res, dev=x.device):
                     slabs = [res[m] for m in uniq]
-                    sums = [accs[first[m]].ensure_sum(res[m].shape[1], dev, m.num_features) for m in uniq]
+                    sums = [accs[first[m]].ensure_sum(res[m].shape[-1], dev, m.num_features) for m in uniq]
                     for j in range(0, len(slabs), 16):
-                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], False, 0)
+                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], take_abs, 0)
 
                 if pipe is not None and pipe.take(x, y, lambda slot, x=x, y=y, lb=lb: eng.grad_scores(
-                        x, y, set(uniq), mode, loss_batch=lb), fold):
+                        x, y, set(uniq), mode, loss_batch=lb, raw_slabs=True), fold):
                     for m in uniq:
                         accs[first[m]].count += x.shape[0]
                     continue
                 with trace_range("tp.forward_backward"):
-                    res = eng.grad_scores(x, y, set(uniq), mode, crit, loss_batch=lb)
+                    res = eng.grad_scores(x, y, set(uniq), mode, crit, loss_batch=lb, raw_slabs=stats)
                 if stats:
                     slabs = [res[m] for m in uniq]
-                    sums = [accs[first[m]].ensure_sum(res[m].shape[1], x.device, m.num_features) for m in uniq]
+                    sums = [accs[first[m]].ensure_sum(res[m].shape[-1], x.device, m.num_features) for m in uniq]
                     for j in range(0, len(slabs), 16):
-                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], False, 0)
+                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], take_abs, 0)
                     for m in uniq:
                         accs[first[m]].count += x.shape[0]
                 else:

@@ -448,12 +448,15 @@ class ResNetEngine:
         return run(cfg, sp), None
 
     def grad_scores(self, x: torch.Tensor, y: torch.Tensor, want, mode: str, criterion=None,
-                    loss_batch: Optional[int] = None):
+                    loss_batch: Optional[int] = None, raw_slabs: bool = False):
         """One engine forward + input-gradient-only backward of the loss (mean cross-entropy on
         the fused kernel, or ``criterion`` through autograd on the logits); returns
         {BN module: (B, C_padded) per-sample ``ops.channel_reduce`` score} for the block BNs in
         ``want`` (evaluation modules of conv1/conv2 of each block). No weight gradients, no
-        autograd graph; the backward stops at the earliest block holding a wanted BN."""
+        autograd graph; the backward stops at the earliest block holding a wanted BN.
+        ``raw_slabs``: a score that came from a data-gradient epilogue stays its raw (R, B, C_padded)
+        partial-slot slab (no slot sum, no |.|) for ``ops.score_fold_`` to finish in its single
+        launch (take_abs for "taylor"; |.| of the other, already final slabs changes nothing)."""
         T = ops.require()
         P = self._pack()
         logits, saved = self.forward(x, save=True)
@@ -480,8 +483,11 @@ class ResNetEngine:
                 tm = ({"taylor": 0, "taylor_signed": 0, "sensitivity": 1}.get(mode) if bn in want else None)
                 g, tay = self._dgrad(T, e["convs"][ci], g, a_prev, tay_mode=tm)  # dL/d(bn_{ci} output), masked
                 if tay is not None:  # partials from the data-gradient epilogue
-                    sums = tay.sum(0)
-                    out[bn] = sums.abs_() if mode == "taylor" else sums
+                    if raw_slabs:
+                        out[bn] = tay
+                    else:
+                        sums = tay.sum(0)
+                        out[bn] = sums.abs_() if mode == "taylor" else sums
                 elif bn in want:
                     out[bn] = ops.channel_reduce(a_prev.permute(0, 3, 1, 2), g.permute(0, 3, 1, 2), mode)
             if bi == first:
