@@ -92,6 +92,20 @@ def _wgrad_splits(P, tiles):
     return sp
 
 
+def _wgrad_wave_splits(P, tiles):
+    """Split counts that fill whole waves of one or two co-resident blocks per CU: a power-of-two
+    split can leave a mostly empty last wave (ResNet-50's 7-px 3x3 wgrad: 144 tiles x 4 splits =
+    2.25 waves of its one-block-per-CU 128x128 kernel)."""
+    slices = math.ceil(P / 32)
+    out = set()
+    for per_cu in (1, 2):
+        for waves in (1, 2, 3, 4):
+            sp = waves * per_cu * _CU // max(1, tiles)
+            if 1 <= sp <= max(1, slices // 8):
+                out.add(sp)
+    return sorted(out)
+
+
 # TORCHPRUNER_BN_EPI_STATS=0: training BN always runs its own statistics pass (A/B switch)
 _EPI_STATS = os.environ.get("TORCHPRUNER_BN_EPI_STATS", "1") != "0"
 
@@ -227,8 +241,10 @@ def _conv_wgrad(g, xh, meta):
 
     cands = []
     for cfg, (bm, bn) in ((0, (128, 128)), (2, (128, 64)), (1, (64, 64))):
-        sp = _wgrad_splits(P, math.ceil(cout_p / bm) * math.ceil(kk / bn))
+        tiles = math.ceil(cout_p / bm) * math.ceil(kk / bn)
+        sp = _wgrad_splits(P, tiles)
         cands += [(cfg, sp)] + ([(cfg, sp // 2)] if sp > 1 else [])
+        cands += [(cfg, s_) for s_ in _wgrad_wave_splits(P, tiles) if s_ not in (sp, sp // 2)]
     H, W = meta[5], meta[6]
     if ks == 3 and stride == 1 and pad == 1 and H % 2 == 0 and W % 2 == 0 and cin_p % 32 == 0:
         tiles = g.shape[0] * (H // 2) * (W // 2)
