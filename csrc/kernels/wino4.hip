@@ -1435,33 +1435,39 @@ __global__ __launch_bounds__(256, 1) void wino4_wide(Args p) {
 // data-gradient operand (w'[k][c] = w[c][k], taps rotated 180 degrees).
 __global__ __launch_bounds__(256) void weight_transform(const float* __restrict__ w, float* __restrict__ u, int K, int C,
                                                         int flip_t, int S0, int S1, int lay) {
-  const double Gm[6][3] = {{0.25, 0.0, 0.0},
-                           {-1.0 / 6, -1.0 / 6, -1.0 / 6},
-                           {-1.0 / 6, 1.0 / 6, -1.0 / 6},
-                           {1.0 / 24, 1.0 / 12, 1.0 / 6},
-                           {1.0 / 24, -1.0 / 12, 1.0 / 6},
-                           {0.0, 0.0, 1.0}};
-  const long long total = (long long)(C / 8) * (K / TK) * U_IMG;
+  // one thread per (c, k): its 9 taps are read once and all 36 points formed with compile-time G
+  // indices (the per-point version re-read the taps 36x and indexed G at run time); same fp64
+  // products and summation order per point as before, so the same rounded U
+  constexpr double Gm[6][3] = {{0.25, 0.0, 0.0},
+                               {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                               {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                               {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                               {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                               {0.0, 0.0, 1.0}};
+  const long long total = (long long)C * K;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int word = (int)(t % U_IMG);
-    const long long img = t / U_IMG;
-    const int kb = (int)(img % (K / TK)), cb = (int)(img / (K / TK));
-    const int lo = word & 1, gs = (word >> 1) & 3, j = (word >> 3) & 15, nh = (word >> 7) & 1, hi = word >> 8;
-    const int e = lay ? hi / 18 : lo, x = lay ? 2 * (hi % 18) + lo : hi;
-    const int g = gs ^ ((j >> 3) << 1);
-    const int c = 8 * cb + 2 * g + e, k = TK * kb + 16 * nh + j;
-    const int i = x / 6, jj = x % 6;
+    const int c = (int)(t / K), k = (int)(t - (long long)c * K);
     const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
-    double acc = 0.0;
-    if (r0 < S0 && r1 < S1) {
-      const float* src = w + ((long long)r0 * S1 + r1) * 9;
+    const bool ok = r0 < S0 && r1 < S1;
+    double wv[9];
+    const float* src = w + ((long long)(ok ? r0 : 0) * S1 + (ok ? r1 : 0)) * 9;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) wv[tap] = ok ? (double)src[flip_t ? 8 - tap : tap] : 0.0;
+    const int cb = c >> 3, cc = c & 7, g = cc >> 1, e = cc & 1;
+    const int kb = k / TK, kk = k - kb * TK, nh = kk >> 4, j = kk & 15;
+    const int gs = g ^ ((j >> 3) << 1);
+    float* dst = u + ((long long)cb * (K / TK) + kb) * U_IMG + (nh << 7) + (j << 3) + (gs << 1);
+#pragma unroll
+    for (int x = 0; x < NPT; ++x) {
+      const int i = x / 6, jj = x % 6;
+      double acc = 0.0;
+#pragma unroll
       for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) {
-          const int tap = flip_t ? (2 - a) * 3 + (2 - b) : a * 3 + b;
-          acc += Gm[i][a] * (double)src[tap] * Gm[jj][b];
-        }
+#pragma unroll
+        for (int b = 0; b < 3; ++b) acc += Gm[i][a] * wv[a * 3 + b] * Gm[jj][b];
+      const int hi = lay ? e * 18 + x / 2 : x, lo = lay ? (x & 1) : e;
+      dst[(hi << 8) + lo] = (float)acc;
     }
-    u[t] = (float)acc;
   }
 }
 
@@ -1485,7 +1491,7 @@ extern "C" hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, i
                                        hipStream_t st) {
   if (K % 32 || C % 8 || K <= 0 || C <= 0 || S0 <= 0 || S1 <= 0) return hipErrorInvalidValue;
   if (flip_t ? (S0 > C || S1 > K) : (S0 > K || S1 > C)) return hipErrorInvalidValue;
-  const long long total = (long long)(C / 8) * (K / 32) * tp::w4::U_IMG;
+  const long long total = (long long)C * K;  // one thread per (input, output channel) pair
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
   tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1, tp::w4::kernel_mode() >= 2);
   return hipGetLastError();
