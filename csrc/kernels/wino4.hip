@@ -1444,9 +1444,14 @@ __global__ __launch_bounds__(256) void weight_transform(const float* __restrict_
                                {1.0 / 24, 1.0 / 12, 1.0 / 6},
                                {1.0 / 24, -1.0 / 12, 1.0 / 6},
                                {0.0, 0.0, 1.0}};
+  // lanes enumerate (g slot, j) of one (e, nh) so that for each point a wave's 64 stores land in
+  // one 128-word span of the image (stride 2) instead of 8 words apart
   const long long total = (long long)C * K;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(t / K), k = (int)(t - (long long)c * K);
+    const int gs_ = (int)(t & 3), j_ = (int)((t >> 2) & 15), e_ = (int)((t >> 6) & 1), nh_ = (int)((t >> 7) & 1);
+    const long long rest = t >> 8;
+    const int kb_ = (int)(rest % (K / TK)), cb_ = (int)(rest / (K / TK));
+    const int c = 8 * cb_ + 2 * (gs_ ^ ((j_ >> 3) << 1)) + e_, k = TK * kb_ + 16 * nh_ + j_;
     const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
     const bool ok = r0 < S0 && r1 < S1;
     double wv[9];
