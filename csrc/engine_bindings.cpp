@@ -82,7 +82,11 @@ int tp_conv_gen_tay_slots(int cfg, int HWo);
 hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
                                float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
                                float* b, double* ws, const double* pre, int G, const float* res, int relu, uint8_t* mko,
-                               hipStream_t st);
+                               long long* nbt, hipStream_t st);
+hipError_t tp_bn_fwd_train4(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
+                            float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
+                            float* b, double* ws, const float* res, int relu, uint8_t* mko, long long* nbt,
+                            hipStream_t st);
 hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                           int ks, int stride, int pad, int Kpad, int cfg, int splits, float* fin, int fin_co,
                           int fin_ci, const long long* fs, hipStream_t st);
@@ -867,7 +871,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
                                                              const c10::optional<at::Tensor>& running_mean,
                                                              const c10::optional<at::Tensor>& running_var, double eps,
                                                              double momentum, const c10::optional<at::Tensor>& res,
-                                                             bool relu, const c10::optional<at::Tensor>& pre) {
+                                                             bool relu, const c10::optional<at::Tensor>& pre,
+                                                             const c10::optional<at::Tensor>& num_batches) {
   need(x, "x", -1);
   const int64_t C = x.size(-1), P = x.numel() / std::max<int64_t>(C, 1);
   TORCH_CHECK(C % 4 == 0 && P > 0, "bn_train_fwd needs C % 4 == 0 and a non-empty batch");
@@ -889,6 +894,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
     TORCH_CHECK(res->sizes() == x.sizes(), "res must have x's shape");
     rp = res->data_ptr<float>();
   }
+  long long* nbt = nullptr;  // the module's num_batches_tracked, incremented by the finalize kernel
+  if (num_batches.has_value() && num_batches->defined()) {
+    TORCH_CHECK(num_batches->is_cuda() && num_batches->scalar_type() == at::kLong && num_batches->numel() == 1 &&
+                    num_batches->device() == x.device(), "num_batches must be a one-element int64 GPU tensor");
+    nbt = reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>());
+  }
   auto y = at::empty_like(x);
   auto mk = at::empty({relu ? P * C / 4 : 0}, x.options().dtype(at::kByte));
   auto stats = at::empty({4, C}, x.options());  // mean, invstd, a, b
@@ -902,13 +913,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
     TP_CHECK_HIP(tp_bn_fwd_train_pre(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
                                      (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(),
                                      pre->data_ptr<double>(), (int)G, rp, relu ? 1 : 0,
-                                     relu ? mk.data_ptr<uint8_t>() : nullptr, cur_stream()));
+                                     relu ? mk.data_ptr<uint8_t>() : nullptr, nbt, cur_stream()));
     return {y, stats[0], stats[1], mk};
   }
   auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
-  TP_CHECK_HIP(tp_bn_fwd_train3(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
+  TP_CHECK_HIP(tp_bn_fwd_train4(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
                                 (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(), rp,
-                                relu ? 1 : 0, relu ? mk.data_ptr<uint8_t>() : nullptr, cur_stream()));
+                                relu ? 1 : 0, relu ? mk.data_ptr<uint8_t>() : nullptr, nbt, cur_stream()));
   return {y, stats[0], stats[1], mk};
 }
 
@@ -970,8 +981,8 @@ void register_engine_ops_def(torch::Library& m) {
         "int ks, int stride, int pad, int cfg, int splits) -> Tensor");
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
   m.def("bn_train_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float eps, float momentum, Tensor? res=None, bool relu=False, Tensor? pre=None) -> (Tensor, Tensor, Tensor, "
-        "Tensor)");
+        "float eps, float momentum, Tensor? res=None, bool relu=False, Tensor? pre=None, "
+        "Tensor(c!)? num_batches=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx, Tensor? ym=None, "
         "bool want_dres=False, Tensor? mask=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "

@@ -159,8 +159,10 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize(const double* __restrict_
                                                        float eps, float momentum, float* __restrict__ run_mean,
                                                        float* __restrict__ run_var, float* __restrict__ mean,
                                                        float* __restrict__ invstd, float* __restrict__ a,
-                                                       float* __restrict__ b) {
+                                                       float* __restrict__ b, long long* __restrict__ nbt) {
   const int cl = threadIdx.x % 16, gl = threadIdx.x / 16, c = blockIdx.x * 16 + cl;
+  // the module's num_batches_tracked += 1 (one lane, plain vector store): no separate add launch
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
   double s, q;
   fold_groups(part, groups, C, c, cl, gl, s, q);
   if (gl != 0 || c >= C) return;
@@ -286,10 +288,10 @@ extern "C" int tp_bn_groups(int P, int C) { return tp::bn_groups(P, C); }
 
 // Fused block tail: y = relu?(BN(x) + res?) (res: the residual branch, same shape as x).
 // mko (nullable, relu only): the ReLU bit mask, P*C/4 bytes (bit q of byte p*C/4 + c/4 = y[p][c+q] > 0)
-extern "C" hipError_t tp_bn_fwd_train3(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
+extern "C" hipError_t tp_bn_fwd_train4(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
                                        float eps, float momentum, float* run_mean, float* run_var, float* mean,
                                        float* invstd, float* a, float* b, double* ws, const float* res, int relu,
-                                       uint8_t* mko, hipStream_t st) {
+                                       uint8_t* mko, long long* nbt, hipStream_t st) {
   using namespace tp;
   if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
   const int groups = bn_groups(P, C);
@@ -297,7 +299,7 @@ extern "C" hipError_t tp_bn_fwd_train3(const float* x, float* y, int P, int C, c
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<0><<<grid, BN_T, 0, st>>>(x, nullptr, nullptr, nullptr, ws, P, C, rpg);
   bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
-                                                    mean, invstd, a, b);
+                                                    mean, invstd, a, b, nbt);
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
       x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
@@ -311,18 +313,27 @@ extern "C" hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C
                                           const float* beta, float eps, float momentum, float* run_mean,
                                           float* run_var, float* mean, float* invstd, float* a, float* b,
                                           double* ws, const double* pre, int G, const float* res, int relu,
-                                          uint8_t* mko, hipStream_t st) {
+                                          uint8_t* mko, long long* nbt, hipStream_t st) {
   using namespace tp;
   if (C % 4 || G <= 0 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
   const int G2 = std::min(G, 256), per = (G + G2 - 1) / G2;
   const int groups = (G + per - 1) / per;
   bn_fold_tiles<<<dim3((C + 63) / 64, groups), 256, 0, st>>>(pre, G, C, ws, per);
   bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
-                                                    mean, invstd, a, b);
+                                                    mean, invstd, a, b, nbt);
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
       x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
   return hipGetLastError();
+}
+
+// num_batches_tracked-free entry (``nbt`` = null)
+extern "C" hipError_t tp_bn_fwd_train3(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
+                                       float eps, float momentum, float* run_mean, float* run_var, float* mean,
+                                       float* invstd, float* a, float* b, double* ws, const float* res, int relu,
+                                       uint8_t* mko, hipStream_t st) {
+  return tp_bn_fwd_train4(x, y, P, C, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, a, b, ws, res, relu,
+                          mko, nullptr, st);
 }
 
 extern "C" hipError_t tp_bn_fwd_train2(const float* x, float* y, int P, int C, const float* gamma, const float* beta,

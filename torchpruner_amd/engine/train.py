@@ -295,10 +295,14 @@ class _NativeConv2dStats(torch.autograd.Function):
         ctx.save_for_backward(*saved)
         if part is not None:
             ctx.mark_non_differentiable(part)
+        # no zero-filled fp64 gradient for the statistics output (one fill launch per conv otherwise)
+        ctx.set_materialize_grads(False)
         return _as_nchw(y), part
 
     @staticmethod
     def backward(ctx, gy, _gpart):
+        if gy is None:
+            return (None,) * 6
         return _NativeConv2d.backward(ctx, gy)
 
 
@@ -337,6 +341,7 @@ class _NativeBlockEntry(torch.autograd.Function):
         for t in (p1, pd):
             if t is not None:
                 ctx.mark_non_differentiable(t)
+        ctx.set_materialize_grads(False)  # backward takes None gradients (no fp64 zero fills)
         return out + (p1, pd)
 
     @staticmethod
@@ -388,14 +393,15 @@ class _NativeBN2d(torch.autograd.Function):
     running-stat update, the normalisation, and the backward, on ``tpamd.bn_train_*``."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, nbt=None):
         T = ops.require()
         xh = x.permute(0, 2, 3, 1)
         if not xh.is_contiguous():
             xh = xh.contiguous()
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
-        y, mean, invstd, _ = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum))
+        y, mean, invstd, _ = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum),
+                                            num_batches=nbt)
         ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd)
         ctx.has_w, ctx.has_b = weight is not None, bias is not None
         return _as_nchw(y)
@@ -408,7 +414,7 @@ class _NativeBN2d(torch.autograd.Function):
         dx, dgamma, dbeta, _ = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
                                               ctx.needs_input_grad[0])
         return (dx.permute(0, 3, 1, 2) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
-                dbeta if ctx.has_b else None, None, None, None, None)
+                dbeta if ctx.has_b else None, None, None, None, None, None)
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -424,14 +430,14 @@ class _NativeBNAct(torch.autograd.Function):
     ATen ReLU / add / threshold-backward passes of the unfused block disappear."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu, pre=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu, pre=None, nbt=None):
         T = ops.require()
         xh = _nhwc(x)
         rh = _nhwc(res) if res is not None else None
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         y, mean, invstd, mk = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
-                                             bool(relu), pre)
+                                             bool(relu), pre, nbt)
         # the backward masks by the ReLU bit mask (1 byte per 4 channels) instead of re-reading y
         ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd, mk)
         ctx.has_w, ctx.has_b, ctx.relu, ctx.has_res = weight is not None, bias is not None, relu, res is not None
@@ -447,7 +453,17 @@ class _NativeBNAct(torch.autograd.Function):
                                                  ctx.needs_input_grad[0], None, want_res, mk if ctx.relu else None)
         return (_as_nchw(dx) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
                 dbeta if ctx.has_b else None, None, None, None, None, _as_nchw(dres) if want_res else None, None,
-                None)
+                None, None)
+
+
+def _bn_counter(bn):
+    """The module's ``num_batches_tracked`` when the BN finalize kernel can increment it in place
+    (fixed momentum, an int64 GPU scalar): one launch fewer per BN than ``add_(1)``. ``None`` when
+    the counter must be bumped on the host side first (cumulative average, momentum=None)."""
+    t = bn.num_batches_tracked if bn.track_running_stats else None
+    if t is None or bn.momentum is None or not t.is_cuda or t.dtype != torch.int64 or t.numel() != 1:
+        return None
+    return t
 
 
 def _bn_fusable(bn, x, res=None) -> bool:
@@ -468,8 +484,8 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: 
         if res is not None:
             y = y + res
         return F.relu(y) if relu else y
-    momentum = bn.momentum
-    if bn.track_running_stats and bn.num_batches_tracked is not None:
+    momentum, nbt = bn.momentum, _bn_counter(bn)
+    if nbt is None and bn.track_running_stats and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
         if momentum is None:
             momentum = 1.0 / float(bn.num_batches_tracked)
@@ -478,7 +494,7 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: 
     if pre is not None and (pre.dim() != 3 or pre.shape[2] != x.shape[1]):
         pre = None
     return _NativeBNAct.apply(x, bn.weight, bn.bias, rm, rv, bn.eps, momentum if momentum is not None else 0.0, res,
-                              relu, pre)
+                              relu, pre, nbt)
 
 
 def _block_kind(m) -> str | None:
@@ -565,14 +581,15 @@ def _native_bn_forward(self, x):
           and (self.weight is None or self.weight.dtype == torch.float32))
     if not ok:
         return type(self).forward(self, x)
-    momentum = self.momentum
-    if self.track_running_stats and self.num_batches_tracked is not None:
+    momentum, nbt = self.momentum, _bn_counter(self)
+    if nbt is None and self.track_running_stats and self.num_batches_tracked is not None:
         self.num_batches_tracked.add_(1)
         if momentum is None:  # cumulative moving average
             momentum = 1.0 / float(self.num_batches_tracked)
     rm = self.running_mean if self.track_running_stats else None
     rv = self.running_var if self.track_running_stats else None
-    return _NativeBN2d.apply(x, self.weight, self.bias, rm, rv, self.eps, momentum if momentum is not None else 0.0)
+    return _NativeBN2d.apply(x, self.weight, self.bias, rm, rv, self.eps, momentum if momentum is not None else 0.0,
+                             nbt)
 
 
 class _NativeMaxPool(torch.autograd.Function):
