@@ -128,25 +128,28 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
   }
 }
 
-// Sum of the row-group partials of 16 channels per block: 16 group lanes stride over the
-// groups (coalesced 16-channel rows), then a fixed-order LDS fold (deterministic).
+// Sum of the row-group partials of 16 channels per block (1024 threads): 64 group lanes stride
+// over the groups (coalesced 16-channel rows), then lane 0 folds the 64 lane sums in order
+// (deterministic). 64 lanes, not 16: the 64-channel BNs of the 56-px stage have 1024 groups and
+// only 4 blocks, and the finalize ran ~22 us there as a chain of 64 dependent load pairs.
+constexpr int BN_FIN_T = 1024, BN_FIN_GL = BN_FIN_T / 16;
 __device__ __forceinline__ void fold_groups(const double* __restrict__ part, int groups, int C, int c, int cl, int gl,
                                             double& s, double& q) {
-  __shared__ double red[2][16][16];
+  __shared__ double red[2][BN_FIN_GL][16];
   s = 0.0;
   q = 0.0;
   if (c < C)
-    for (int i = gl; i < groups; i += 16) {
+    for (int i = gl; i < groups; i += BN_FIN_GL) {
       s += part[(size_t)(2 * i) * C + c];
       q += part[(size_t)(2 * i + 1) * C + c];
     }
   red[0][gl][cl] = s;
   red[1][gl][cl] = q;
   __syncthreads();
+  if (gl != 0) return;
   s = 0.0;
   q = 0.0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < BN_FIN_GL; ++i) {
     s += red[0][i][cl];
     q += red[1][i][cl];
   }
@@ -154,7 +157,7 @@ __device__ __forceinline__ void fold_groups(const double* __restrict__ part, int
 
 // Forward finalize: mean / invstd for the apply pass, running statistics (PyTorch semantics:
 // running_var takes the unbiased variance), and the affine folded into (a, b).
-__global__ __launch_bounds__(256) void bn_fwd_finalize(const double* __restrict__ part, int groups, int P, int C,
+__global__ __launch_bounds__(BN_FIN_T) void bn_fwd_finalize(const double* __restrict__ part, int groups, int P, int C,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, float momentum, float* __restrict__ run_mean,
                                                        float* __restrict__ run_var, float* __restrict__ mean,
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize(const double* __restrict_
 
 // Backward finalize: dgamma = sum(g * xhat), dbeta = sum(g), and the coefficients of
 // dx = a * g + k1 + k2 * x  (k1, k2 fold the mean-subtraction terms).
-__global__ __launch_bounds__(256) void bn_bwd_finalize(const double* __restrict__ part, int groups, int P, int C,
+__global__ __launch_bounds__(BN_FIN_T) void bn_bwd_finalize(const double* __restrict__ part, int groups, int P, int C,
                                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                        float* __restrict__ dbeta, float* __restrict__ a,
@@ -298,7 +301,7 @@ extern "C" hipError_t tp_bn_fwd_train4(const float* x, float* y, int P, int C, c
   const int rpg = (P + groups - 1) / groups;
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<0><<<grid, BN_T, 0, st>>>(x, nullptr, nullptr, nullptr, ws, P, C, rpg);
-  bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
+  bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
                                                     mean, invstd, a, b, nbt);
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
@@ -319,7 +322,7 @@ extern "C" hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C
   const int G2 = std::min(G, 256), per = (G + G2 - 1) / G2;
   const int groups = (G + per - 1) / per;
   bn_fold_tiles<<<dim3((C + 63) / 64, groups), 256, 0, st>>>(pre, G, C, ws, per);
-  bn_fwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
+  bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
                                                     mean, invstd, a, b, nbt);
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
@@ -364,7 +367,7 @@ extern "C" hipError_t tp_bn_bwd_train3(const float* g, const float* x, float* dx
   const int rpg = (P + groups - 1) / groups;
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym, mk);
-  bn_bwd_finalize<<<(C + 15) / 16, 256, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
+  bn_bwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
   if (dx || dres) {
     const unsigned n4 = (unsigned)((long long)P * C / 4);
     bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(

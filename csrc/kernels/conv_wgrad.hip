@@ -12,7 +12,7 @@
 // = 32 (mod 64) words so the two lane halves hit disjoint banks.
 //
 // The pixel range is split over grid.y (split-K): partial slabs [split][Cout][Kpad] are summed
-// in split order by wgrad_combine (deterministic, no atomics).
+// in a fixed order by wgrad_combine_par (deterministic, no atomics).
 #include "tp_common.h"
 
 namespace tp {
@@ -183,32 +183,45 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void conv_wgrad(WgradAr
     }
 }
 
-// split combine straight into the final layout (one thread per GEMM element, split order)
-__global__ __launch_bounds__(256) void wgrad_combine_fin(const float* __restrict__ slabs, WgradArgs p, int splits) {
-  const long long n = (long long)p.Cout * p.Kpad;
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
-    const int co = (int)(t / p.Kpad), k = (int)(t - (long long)co * p.Kpad);
-    const long long o = wgrad_fin_off(p, co, k);
-    if (o < 0) continue;
-    float s = slabs[t];
-    for (int q = 1; q < splits; ++q) s += slabs[q * n + t];
-    p.fin[o] = s;
-  }
-}
-
-// dW = sum of the split slabs in split order (float4 per thread); columns >= Kc are zero.
-__global__ __launch_bounds__(256) void wgrad_combine(const float* __restrict__ slabs, float* __restrict__ dw,
-                                                     int splits, long long n4) {
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += (long long)gridDim.x * blockDim.x) {
-    float4 s = reinterpret_cast<const float4*>(slabs)[t];
-    for (int q = 1; q < splits; ++q) {
-      const float4 v = reinterpret_cast<const float4*>(slabs)[q * n4 + t];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
+// Split combine, deterministic: a block owns 64 consecutive GEMM elements; its SL waves
+// (SL = min(8, splits), blockDim = 64 * SL) each sum the splits q = wave, wave + SL, ... in
+// increasing order (4 loads in flight), then wave 0 adds the SL lane sums in wave order. The
+// old one-thread-per-element walk over the 64-256 split slabs of the big-map wgrads left ~2
+// waves per CU with one dependent load at a time (~200 GB/s). FIN: write straight into the
+// final weight layout (wgrad_fin_off); otherwise dw[t].
+template <bool FIN>
+__global__ __launch_bounds__(512) void wgrad_combine_par(const float* __restrict__ slabs, WgradArgs p,
+                                                         float* __restrict__ dw, int splits, long long n) {
+  __shared__ float red[8][64];
+  const int tl = threadIdx.x & 63, sl = threadIdx.x >> 6, SL = blockDim.x >> 6;
+  for (long long base = (long long)blockIdx.x * 64; base < n; base += (long long)gridDim.x * 64) {
+    const long long t = base + tl;
+    float s = 0.f;
+    if (t < n) {
+      int q = sl;
+      for (; q + 3 * SL < splits; q += 4 * SL) {
+        const float v0 = slabs[(long long)q * n + t], v1 = slabs[(long long)(q + SL) * n + t];
+        const float v2 = slabs[(long long)(q + 2 * SL) * n + t], v3 = slabs[(long long)(q + 3 * SL) * n + t];
+        s += v0;
+        s += v1;
+        s += v2;
+        s += v3;
+      }
+      for (; q < splits; q += SL) s += slabs[(long long)q * n + t];
     }
-    reinterpret_cast<float4*>(dw)[t] = s;
+    red[sl][tl] = s;
+    __syncthreads();
+    if (sl == 0 && t < n) {
+      for (int i = 1; i < SL; ++i) s += red[i][tl];
+      if constexpr (FIN) {
+        const int co = (int)(t / p.Kpad), k = (int)(t - (long long)co * p.Kpad);
+        const long long o = wgrad_fin_off(p, co, k);
+        if (o >= 0) p.fin[o] = s;
+      } else {
+        dw[t] = s;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -287,14 +300,13 @@ extern "C" hipError_t tp_conv_wgrad3(const float* g, const float* x, float* dw, 
     default: return hipErrorInvalidValue;
   }
   if (e != hipSuccess || splits == 1) return e;
-  if (fin) {
-    const unsigned grid = (unsigned)std::min<long long>(ceil_div((long long)Cout * Kpad, 256), 4096);
-    wgrad_combine_fin<<<grid, 256, 0, st>>>(ws, a, splits);
-    return hipGetLastError();
-  }
-  const long long n4 = (long long)batch * Cout * Kpad / 4;
-  const unsigned grid = (unsigned)std::min<long long>(ceil_div(n4, 256), 4096);
-  wgrad_combine<<<grid, 256, 0, st>>>(ws, dw, splits, n4);
+  const long long n = fin ? (long long)Cout * Kpad : (long long)batch * Cout * Kpad;
+  const int sl = std::min(8, splits);
+  const unsigned grid = (unsigned)std::min<long long>(ceil_div(n, 64), 16384);
+  if (fin)
+    wgrad_combine_par<true><<<grid, 64 * sl, 0, st>>>(ws, a, nullptr, splits, n);
+  else
+    wgrad_combine_par<false><<<grid, 64 * sl, 0, st>>>(ws, a, dw, splits, n);
   return hipGetLastError();
 }
 

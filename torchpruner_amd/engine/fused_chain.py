@@ -113,6 +113,7 @@ def _wino4_ok(H, W, C, K):
 
 _W4_SPLITS = os.environ.get("TORCHPRUNER_W4_SPLITS", "1") != "0"
 _TUNER_LOG = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") != "0"  # print every timed kernel choice
+_TUNER_LOG_ALL = os.environ.get("TORCHPRUNER_TUNER_LOG", "0") == "2"  # ... and every candidate's time
 _TUNE_ROUNDS = int(os.environ.get("TORCHPRUNER_TUNE_ROUNDS", "3"))
 _TUNE_MARGIN = float(os.environ.get("TORCHPRUNER_TUNE_MARGIN", "0.02"))
 
@@ -317,6 +318,9 @@ class Autotuner:
         if _TUNER_LOG:
             print(f"[tuner] {key} -> {best[1]} ({best[0] / 2 * 1e3:.1f} us{f', {conc} in flight' if conc > 1 else ''})",
                   file=sys.stderr, flush=True)
+            if _TUNER_LOG_ALL:
+                print("[tuner]     " + ", ".join(f"{c}: {times[c] / 2 * 1e3:.1f}" for c in sorted(times, key=times.get)),
+                      file=sys.stderr, flush=True)
         return best[1]
 
 
