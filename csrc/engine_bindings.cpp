@@ -62,6 +62,7 @@ hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u,
 hipError_t tp_wino_weights(const float* w, float* u, int K, int C, int flip_t, hipStream_t st);
 hipError_t tp_wino_weights2(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
 hipError_t tp_wino_weights_bf16(const float* w, void* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
+hipError_t tp_pack_conv_weights_multi(const long long* desc, int n, long long total, hipStream_t st);
 hipError_t tp_pack_conv_weight(const float* w, float* out, int O, int I, int KS, int rows, int cols, int cpad, int mode,
                                hipStream_t st);
 long long tp_wino_wgrad_ws_elems(int B, int H, int W, int Cin, int Cout, int splits);
@@ -95,6 +96,8 @@ hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, const float* 
 hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* perm, int B, int C, int N, int p0,
                                   int cnt, int Kc, float* T, float* Wsub, hipStream_t st);
 hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
+hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, long long st0,
+                                    long long st1, int st2, int st3, hipStream_t st);
 int tp_wino4_u_img();
 int tp_wino4_ok(int H, int W, int C, int K);
 int tp_wino4_taylor_slots(int S);
@@ -304,6 +307,53 @@ at::Tensor pack_conv_weight(const at::Tensor& w, int64_t rows, int64_t cols, int
   return out;
 }
 
+// Every operand of ``pack_conv_weight`` for a list of weights in one launch: outs[i] (rows, cols)
+// <- ws[i] per cfg[4i:4i+4] = (rows, cols, cpad, mode). ws may be strided (channels_last
+// parameters are read in place). The descriptors travel through pinned memory (async copy).
+void pack_conv_weights_multi(const std::vector<at::Tensor>& ws, const std::vector<at::Tensor>& outs,
+                             const std::vector<int64_t>& cfg) {
+  constexpr int D = 14;
+  const int64_t n = (int64_t)ws.size();
+  TORCH_CHECK(n > 0 && (int64_t)outs.size() == n && (int64_t)cfg.size() == 4 * n,
+              "pack_conv_weights_multi: ws, outs and 4 ints per operand");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ws[0].device());
+  auto hd = at::empty({n * D}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+  int64_t* h = hd.data_ptr<int64_t>();
+  int64_t total = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const at::Tensor& w = ws[i];
+    const at::Tensor& o = outs[i];
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(2) == w.size(3) &&
+                    w.device() == ws[0].device(), "pack_conv_weights_multi: fp32 (O, I, KS, KS) GPU weights");
+    const int64_t rows = cfg[4 * i], cols = cfg[4 * i + 1], cpad = cfg[4 * i + 2], mode = cfg[4 * i + 3];
+    const int64_t O = w.size(0), I = w.size(1);
+    TORCH_CHECK(mode >= 0 && mode <= 2 && rows > 0 && cols > 0 && cpad > 0 &&
+                    (mode == 0 ? (rows >= O && cpad >= I) : (rows >= I && cpad >= O)),
+                "pack_conv_weights_multi: bad operand shape");
+    TORCH_CHECK(o.is_cuda() && o.scalar_type() == at::kFloat && o.is_contiguous() && o.numel() == rows * cols &&
+                    o.device() == w.device(), "pack_conv_weights_multi: out must be a contiguous fp32 (rows, cols)");
+    int64_t* d = h + i * D;
+    d[0] = reinterpret_cast<int64_t>(w.data_ptr<float>());
+    d[1] = reinterpret_cast<int64_t>(o.data_ptr<float>());
+    d[2] = total;
+    d[3] = O;
+    d[4] = I;
+    d[5] = w.size(2);
+    d[6] = rows;
+    d[7] = cols;
+    d[8] = cpad;
+    d[9] = mode;
+    d[10] = w.stride(0);
+    d[11] = w.stride(1);
+    d[12] = w.stride(2);
+    d[13] = w.stride(3);
+    total += (rows * cols + 4095) / 4096 * 4096;  // next operand on a chunk boundary (PACK_CHUNK)
+  }
+  auto dd = hd.to(ws[0].device(), /*non_blocking=*/true);
+  TP_CHECK_HIP(tp_pack_conv_weights_multi(reinterpret_cast<const long long*>(dd.data_ptr<int64_t>()), (int)n,
+                                          (long long)total, cur_stream()));
+}
+
 // Shapley prefix-delta operands: z (B, C) block output, W (N, C) next Linear, perm (n) int32
 // permutation; returns T (cnt*B, Kc) lower-triangular gathered activations and Wsub (N, Kc).
 std::tuple<at::Tensor, at::Tensor> prefix_tri_operands(const at::Tensor& z, const at::Tensor& w, const at::Tensor& perm,
@@ -450,7 +500,9 @@ at::Tensor conv_wino_dgrad(const at::Tensor& g, const c10::optional<at::Tensor>&
 
 // ---- Winograd F(4x4,3x3) (wino4.hip): square 4/8/16/32-pixel maps --------------------------------
 at::Tensor wino4_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C) {
-  need(w, "w", 4);
+  // strided weights welcome (channels_last parameters are read in place)
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4, "w must be a 4-d float32 GPU tensor");
+  TORCH_CHECK(w.stride(0) > 0 && w.stride(1) > 0 && w.stride(2) > 0 && w.stride(3) > 0, "w: positive strides only");
   TORCH_CHECK(w.size(2) == 3 && w.size(3) == 3, "w must be (.., .., 3, 3)");
   if (K <= 0) K = flip_t ? w.size(1) : w.size(0);
   if (C <= 0) C = flip_t ? w.size(0) : w.size(1);
@@ -459,8 +511,9 @@ at::Tensor wino4_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C)
               "weight wider than the padded GEMM");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(w.device());
   auto u = at::empty({C / 8, K / 32, (int64_t)tp_wino4_u_img()}, w.options());
-  TP_CHECK_HIP(tp_wino4_weights(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
-                                (int)w.size(0), (int)w.size(1), cur_stream()));
+  TP_CHECK_HIP(tp_wino4_weights_strided(w.data_ptr<float>(), u.data_ptr<float>(), (int)K, (int)C, flip_t ? 1 : 0,
+                                        (int)w.size(0), (int)w.size(1), w.stride(0), w.stride(1), (int)w.stride(2),
+                                        (int)w.stride(3), cur_stream()));
   return u;
 }
 
@@ -988,6 +1041,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "
         "-> Tensor");
   m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");
+  m.def("pack_conv_weights_multi(Tensor[] ws, Tensor(a!)[] outs, int[] cfg) -> ()");
   m.def("conv_gen_stats(Tensor x, Tensor w, Tensor? shift, int ks, int stride, int pad, int cfg) -> (Tensor, Tensor)");
   m.def("wino_wgrad(Tensor g, Tensor x, int cfg, int splits, Tensor(a!) out) -> ()");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
@@ -1030,6 +1084,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_gen_bwd", &conv_gen_bwd);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("pack_conv_weight", &pack_conv_weight);
+  m.impl("pack_conv_weights_multi", &pack_conv_weights_multi);
   m.impl("conv_gen_stats", &conv_gen_stats);
   m.impl("wino_wgrad", &wino_wgrad);
   m.impl("bn_train_fwd", &bn_train_fwd);

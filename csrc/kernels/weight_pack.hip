@@ -10,6 +10,12 @@
 //   mode 2  strided (transposed-gather) data-gradient operand, natural taps:
 //           out[ci][k], k = (kh*KS + kw)*cpad + co -> w[co][ci][kh][kw]
 // Every slot outside the real weight (padded channels, columns past KS*KS*cpad) is zero.
+//
+// pack_conv_weights_multi: every operand of a training step in ONE launch (engine/train.py
+// _PackSet: all packs go stale together at the optimizer step). A descriptor per operand (int64
+// x PACK_DESC: w, out, start, O, I, KS, rows, cols, cpad, mode, strides of w in elements — a
+// channels_last parameter is read in place, no contiguous copy); a flat element space over the
+// operands (start = chunk-aligned prefix offset), one descriptor search per 4096-element chunk.
 #include "tp_common.h"
 
 namespace tp {
@@ -36,7 +42,59 @@ __global__ __launch_bounds__(256) void pack_conv_weight(const float* __restrict_
   }
 }
 
+constexpr int PACK_DESC = 14, PACK_CHUNK = 4096;  // operands start on PACK_CHUNK-element boundaries
+
+// A block walks whole chunks; every element of a chunk belongs to one operand (aligned starts),
+// so the descriptor search runs once per chunk (block-uniform) instead of once per element.
+__global__ __launch_bounds__(256) void pack_conv_weights_multi(const long long* __restrict__ desc, int n,
+                                                               long long total) {
+  const long long chunks = (total + PACK_CHUNK - 1) / PACK_CHUNK;
+  for (long long ch = blockIdx.x; ch < chunks; ch += gridDim.x) {
+    const long long base = ch * PACK_CHUNK;
+    int lo = 0, hi = n - 1;  // last descriptor with start <= base
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (desc[mid * PACK_DESC + 2] <= base) lo = mid;
+      else hi = mid - 1;
+    }
+    const long long* d = desc + lo * PACK_DESC;
+    const float* w = reinterpret_cast<const float*>(d[0]);
+    float* out = reinterpret_cast<float*>(d[1]);
+    const int O = (int)d[3], I = (int)d[4], KS = (int)d[5], rows = (int)d[6], cols = (int)d[7], cpad = (int)d[8];
+    const int mode = (int)d[9];
+    const long long s0 = d[10], s1 = d[11], s2 = d[12], s3 = d[13];
+    const long long size = (long long)rows * cols, off = base - d[2];
+    for (int e = threadIdx.x; e < PACK_CHUNK; e += blockDim.x) {
+      const long long i = off + e;
+      if (i >= size) break;
+      const int r = (int)(i / cols), k = (int)(i - (long long)r * cols);
+      const int tap = k / cpad, c = k - tap * cpad;
+      float v = 0.f;
+      if (tap < KS * KS) {
+        int kh = tap / KS, kw = tap - kh * KS;
+        const int co = mode == 0 ? r : c, ci = mode == 0 ? c : r;
+        if (mode == 1) {
+          kh = KS - 1 - kh;
+          kw = KS - 1 - kw;
+        }
+        if (co < O && ci < I) v = w[co * s0 + ci * s1 + kh * s2 + kw * s3];
+      }
+      out[i] = v;
+    }
+  }
+}
+
 }  // namespace tp
+
+// desc: n descriptors of PACK_DESC int64 on the device (pointers already validated by the
+// caller: the binding checks every one against live tensors), starts ascending and multiples of
+// PACK_CHUNK; total = the last start + its rows * cols
+extern "C" hipError_t tp_pack_conv_weights_multi(const long long* desc, int n, long long total, hipStream_t st) {
+  if (n <= 0 || total <= 0) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, (long long)tp::PACK_CHUNK), 8192);
+  tp::pack_conv_weights_multi<<<grid, 256, 0, st>>>(desc, n, total);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t tp_pack_conv_weight(const float* w, float* out, int O, int I, int KS, int rows, int cols,
                                           int cpad, int mode, hipStream_t st) {

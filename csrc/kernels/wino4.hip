@@ -1434,7 +1434,8 @@ __global__ __launch_bounds__(256, 1) void wino4_wide(Args p) {
 // (((e*18 + x/2)*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + (x & 1) holds U[x][c = 8cb + 2g + e][k]. fp64, rounded once. flip_t: the
 // data-gradient operand (w'[k][c] = w[c][k], taps rotated 180 degrees).
 __global__ __launch_bounds__(256) void weight_transform(const float* __restrict__ w, float* __restrict__ u, int K, int C,
-                                                        int flip_t, int S0, int S1, int lay) {
+                                                        int flip_t, int S0, int S1, int lay, long long st0,
+                                                        long long st1, int st2, int st3) {
   // one thread per (c, k): its 9 taps are read once and all 36 points formed with compile-time G
   // indices (the per-point version re-read the taps 36x and indexed G at run time); same fp64
   // products and summation order per point as before, so the same rounded U
@@ -1455,9 +1456,13 @@ __global__ __launch_bounds__(256) void weight_transform(const float* __restrict_
     const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
     const bool ok = r0 < S0 && r1 < S1;
     double wv[9];
-    const float* src = w + ((long long)(ok ? r0 : 0) * S1 + (ok ? r1 : 0)) * 9;
+    // w's element strides st0..st3 (a channels_last parameter is read in place)
+    const float* src = w + (ok ? r0 : 0) * st0 + (ok ? r1 : 0) * st1;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) wv[tap] = ok ? (double)src[flip_t ? 8 - tap : tap] : 0.0;
+    for (int tap = 0; tap < 9; ++tap) {
+      const int tt = flip_t ? 8 - tap : tap;
+      wv[tap] = ok ? (double)src[(tt / 3) * st2 + (tt % 3) * st3] : 0.0;
+    }
     const int cb = c >> 3, cc = c & 7, g = cc >> 1, e = cc & 1;
     const int kb = k / TK, kk = k - kb * TK, nh = kk >> 4, j = kk & 15;
     const int gs = g ^ ((j >> 3) << 1);
@@ -1492,14 +1497,22 @@ static int kernel_mode() {
 
 // U images of a 3x3 weight for wino4: (C/8, K/32, 9216) floats. w: (S0, S1, 3, 3) = the forward
 // weight (Cout, Cin, 3, 3), possibly narrower than the padded GEMM; flip_t as tp_wino_weights2.
-extern "C" hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1,
-                                       hipStream_t st) {
+// strides: w's element strides (st0, st1, st2, st3) — (S1*9, 9, 3, 1) when contiguous
+extern "C" hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, int C, int flip_t, int S0, int S1,
+                                               long long st0, long long st1, int st2, int st3, hipStream_t st) {
   if (K % 32 || C % 8 || K <= 0 || C <= 0 || S0 <= 0 || S1 <= 0) return hipErrorInvalidValue;
   if (flip_t ? (S0 > C || S1 > K) : (S0 > K || S1 > C)) return hipErrorInvalidValue;
+  if (st0 <= 0 || st1 <= 0 || st2 <= 0 || st3 <= 0) return hipErrorInvalidValue;
   const long long total = (long long)C * K;  // one thread per (input, output channel) pair
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
-  tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1, tp::w4::kernel_mode() >= 2);
+  tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1, tp::w4::kernel_mode() >= 2, st0, st1,
+                                                 st2, st3);
   return hipGetLastError();
+}
+
+extern "C" hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1,
+                                       hipStream_t st) {
+  return tp_wino4_weights_strided(w, u, K, C, flip_t, S0, S1, (long long)S1 * 9, 9, 3, 1, st);
 }
 
 extern "C" int tp_wino4_u_img() { return tp::w4::U_IMG; }

@@ -18,7 +18,8 @@ for fmt in fmts:
     if fmt == "native":
         from torchpruner_amd.engine.train import enable_native_convs
         print(f"native convs: {len(enable_native_convs(m))}", flush=True)
-    opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    fused = os.environ.get("OPT_FUSED", "0") != "0"  # torch's fused SGD (one kernel) vs foreach
+    opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4, **({"fused": True} if fused else {}))
     x = torch.randn(B, 3, 224, 224, device="cuda").contiguous(memory_format=mf)
     y = torch.randint(0, 1000, (B,), device="cuda")
 

@@ -297,6 +297,52 @@ def test_pack_conv_weight(cuda, O, I, KS, cpad_i, cpad_o):
     assert torch.equal(T.pack_conv_weight(w, cpad_i, KS * KS * cpad_o, cpad_o, 2), ref2)
 
 
+def test_pack_conv_weights_multi_and_pack_set(cuda):
+    """One multi-operand launch == the per-operand pack for contiguous and channels_last weights;
+    the training pack cache repacks after an in-place update (version counter) and serves hits
+    between updates without a launch."""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.train import _PackSet
+    T = ops.require()
+    shapes = [(64, 32, 3, 32, 64, 0), (40, 36, 3, 64, 64, 1), (64, 3, 7, 4, 64, 0), (52, 20, 1, 32, 64, 2),
+              (30, 17, 5, 32, 32, 1)]
+    ws, outs, cfg, refs = [], [], [], []
+    for i, (O, I, KS, ci, co, mode) in enumerate(shapes):
+        w = torch.randn(O, I, KS, KS, device=cuda)
+        if i % 2:
+            w = w.contiguous(memory_format=torch.channels_last)
+        rows, cp = (co, ci) if mode == 0 else (ci, co)
+        cols = -(-KS * KS * cp // 32) * 32
+        ws.append(w)
+        outs.append(torch.full((rows, cols), float("nan"), device=cuda))
+        cfg += [rows, cols, cp, mode]
+        refs.append(T.pack_conv_weight(w.contiguous(), rows, cols, cp, mode))
+    T.pack_conv_weights_multi(ws, outs, cfg)
+    for o, r in zip(outs, refs):
+        assert torch.equal(o, r)
+    ps = _PackSet()
+    w = ws[1]
+    a = ps.get(T, w, *cfg[4:8])
+    assert torch.equal(a, refs[1])
+    assert ps.get(T, w, *cfg[4:8]) is a  # hit: same buffer, no repack
+    with torch.no_grad():
+        w.mul_(2.0)  # in-place: version bump -> the next request repacks
+    b = ps.get(T, w, *cfg[4:8])
+    assert b is a and torch.equal(b, 2.0 * refs[1])
+
+
+def test_wino4_weights_channels_last(cuda):
+    """The F(4x4) weight transform reads a channels_last parameter in place: same U images."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    w = torch.randn(64, 40, 3, 3, device=cuda)
+    wl = w.contiguous(memory_format=torch.channels_last)
+    assert not wl.is_contiguous()
+    for flip in (False, True):
+        K, C = (64, 64) if not flip else (64, 64)
+        assert torch.equal(T.wino4_weights(wl, flip, K, C), T.wino4_weights(w, flip, K, C))
+
+
 @pytest.mark.parametrize("O,I", [(40, 36), (64, 32)])
 def test_wino_weights_padded_source(cuda, O, I):
     """Winograd images from an UNPADDED weight == images of the zero-padded weight."""
@@ -417,3 +463,38 @@ def test_conv_gen_stats(cuda, cfg, B, H, W, Cin, Cout):
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["foreach", "fused"])
+def test_pack_cache_follows_optimizer_steps(cuda, kind):
+    """The batched weight-pack cache must see every optimizer step: torch's fused SGD updates the
+    parameters without bumping their version counters (the post-step hook and the forward epoch
+    catch it). Losses with the cache == losses with one pack per call, step by step."""
+    from torchpruner_amd.engine import train as tr
+    from torchpruner_amd.models import resnet18
+    runs = []
+    saved = tr._BATCH_PACK
+    try:
+        for batch_pack in (False, True):
+            tr._BATCH_PACK = batch_pack
+            torch.manual_seed(0)
+            m = resnet18(num_classes=10).to(cuda).to(memory_format=torch.channels_last).train()
+            sw = tr.enable_native_convs(m)
+            opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9, **{kind: True})
+            x = torch.randn(8, 3, 32, 32, device=cuda).contiguous(memory_format=torch.channels_last)
+            y = torch.randint(0, 10, (8,), device=cuda)
+            losses = []
+            with tr.TUNER.fixed():
+                for _ in range(4):
+                    opt.zero_grad(set_to_none=True)
+                    loss = F.cross_entropy(m(x), y)
+                    loss.backward()
+                    opt.step()
+                    losses.append(loss.item())
+            tr.disable_native_convs(sw)
+            runs.append(losses)
+    finally:
+        tr._BATCH_PACK = saved
+    assert runs[0][-1] < runs[0][0]
+    for a, b in zip(*runs):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), runs

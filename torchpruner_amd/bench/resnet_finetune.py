@@ -57,6 +57,14 @@ def _timed(fn, world):
     return out, (pdist.all_max_float(dt) if world > 1 else dt)
 
 
+def _sgd(params, lr, dev):
+    """SGD momentum 0.9, wd 1e-4 (the finetune recipe); torch's fused kernel on the GPU (one
+    launch per step instead of ~13 multi-tensor foreach launches, +1.5% on the ResNet-50 step)."""
+    params = list(params)
+    kw = {"fused": True} if torch.device(dev).type == "cuda" else {}
+    return torch.optim.SGD(params, lr=lr, momentum=0.9, weight_decay=1e-4, **kw)
+
+
 def finetune_throughput(dev, world, rank, steps=10, warmup=3, batch=128, res=224, frac=0.2, seed=0,
                         score_batch=64, rounds=2):
     torch.manual_seed(seed)
@@ -64,7 +72,7 @@ def finetune_throughput(dev, world, rank, steps=10, warmup=3, batch=128, res=224
     sync = pdist.sync_module(model)
     enable_native_convs(model)
     wrapper = PrunableDDP(model, device=dev)
-    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt = _sgd(model.parameters(), 0.01, dev)
     pruner = Pruner(model, (3, res, res), dev, optimizer=opt)
     shape = (3, res, res)
 
@@ -107,7 +115,7 @@ def finetune_throughput(dev, world, rank, steps=10, warmup=3, batch=128, res=224
             "prune": f"{rounds} rounds, each {frac:.0%} of every prunable bottleneck conv (conv1/conv2) by Taylor "
                      "scores, then DDP rewrap and a timed finetune segment; the value is over all rounds",
             "rounds": per_round,
-            "params_before_after": [params0, count_parameters(model)], "optimizer": "SGD momentum 0.9, wd 1e-4",
+            "params_before_after": [params0, count_parameters(model)], "optimizer": "SGD momentum 0.9, wd 1e-4 (torch fused kernel on GPU)",
             "ddp": f"PrunableDDP (bucket_cap_mb={wrapper.bucket_cap_mb}), rewrapped after every prune",
             "kernels": "native training convs / BN (engine/train.py)", "prune_rewrap_s": t_prune,
             "new_shape_warmup_s": t_warm, "in_sync": params_in_sync(model),
@@ -135,7 +143,7 @@ def prune_finetune_quality(dev, world, rank, seed=0, cfg=None):
         torch.manual_seed(seed)
         teacher = resnet50(num_classes=cfg["classes"]).to(dev).to(memory_format=torch.channels_last)
         enable_native_convs(teacher)
-        opt = torch.optim.SGD(teacher.parameters(), lr=cfg["lr"], momentum=0.9, weight_decay=1e-4)
+        opt = _sgd(teacher.parameters(), cfg["lr"], dev)
         done, part, top1 = 0, 0, 0.0
         while done < cfg["teacher_max_steps"] and top1 < cfg["teacher_target"]:
             n = min(cfg["check_every"], cfg["teacher_max_steps"] - done)
@@ -159,7 +167,7 @@ def prune_finetune_quality(dev, world, rank, seed=0, cfg=None):
         model.load_state_dict(state)
         enable_native_convs(model)
         wrapper = PrunableDDP(model, device=dev)
-        opt = torch.optim.SGD(model.parameters(), lr=cfg["ft_lr"], momentum=0.9, weight_decay=1e-4)
+        opt = _sgd(model.parameters(), cfg["ft_lr"], dev)
         pruner = Pruner(model, shape, dev, optimizer=opt)
         model.eval()
         graph = get_resnet_pruning_graph(model)

@@ -39,6 +39,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from . import epochs
 
 # tile configs of conv_mfma.hip: 0=128x128, 1=256x64, 2=64x64, 3=128x64 (4 waves);
 # 4=128x128, 5=256x64, 6=128x64 (8 waves)
@@ -533,6 +534,7 @@ class FusedChainEngine:
             for t in (b.linear.weight, b.linear.bias):
                 if t is not None:
                     key.append((t.data_ptr(), t._version, tuple(t.shape)))
+        key.append(epochs.engine_key())  # fused optimizers / native BN stats leave versions alone
         return tuple(key)
 
     @torch.no_grad()

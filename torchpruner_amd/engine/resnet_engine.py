@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from . import epochs
 from .fused_chain import (_CU, _W4_SPLITS, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, logits_grad,
                           sk_candidates, taylor_slots, winograd_weights)
 
@@ -170,6 +171,7 @@ class ResNetEngine:
         for t in (self.plan.fc.weight, self.plan.fc.bias):
             if t is not None:
                 key.append((t.data_ptr(), t._version, tuple(t.shape)))
+        key.append(epochs.engine_key())  # fused optimizers / native BN stats leave versions alone
         return tuple(key)
 
     @torch.no_grad()

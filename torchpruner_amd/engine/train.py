@@ -37,6 +37,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from . import epochs
 from .fused_chain import _CU, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, sk_candidates
 from .resnet_engine import wino4_cands
 
@@ -110,6 +111,60 @@ def _wgrad_wave_splits(P, tiles):
 _EPI_STATS = os.environ.get("TORCHPRUNER_BN_EPI_STATS", "1") != "0"
 
 
+# TORCHPRUNER_BATCH_WEIGHT_PACK=0: one pack launch per operand and use (A/B switch)
+_BATCH_PACK = os.environ.get("TORCHPRUNER_BATCH_WEIGHT_PACK", "1") != "0"
+
+
+class _PackSet:
+    """The zero-padded GEMM operands of the fp32 conv weights (``pack_conv_weight`` modes 0-2),
+    cached across uses and repacked TOGETHER by one ``pack_conv_weights_multi`` launch: the
+    optimizer step updates every weight at once, so the first request after it finds all packs
+    stale and one launch refreshes them all (ResNet-50: 81 pack launches per training step -> 2,
+    the descriptor copy and the kernel). An entry is stale when its weight's autograd version
+    counter moved (in-place ops on the parameter) or an epoch moved (:mod:`.epochs`: any
+    torch.optim step — fused kernels do not bump versions —, any forward of a native-conv model). Not seen: writes
+    through ``param.data`` by hand between two forwards of a submodule called directly; use
+    ``TORCHPRUNER_BATCH_WEIGHT_PACK=0`` for such loops. Entries hold a reference to their weight
+    (no dangling pointer) and are dropped after a whole step without a request (pruned layers)."""
+
+    def __init__(self):
+        self.entries = {}  # key -> [weight view, out, cfg, (version, OPT, FWD) packed at, last generation used]
+        self.gen = 0
+
+    def get(self, T, w, rows, cols, cpad_, mode):
+        key = (w.data_ptr(), tuple(w.shape), tuple(w.stride()), str(w.device), rows, cols, cpad_, mode)
+        e = self.entries.get(key)
+        now = (w._version, epochs.OPT[0], epochs.FWD[0])
+        if e is not None and e[3] == now:
+            e[4] = self.gen
+            return e[1]
+        if e is None:
+            e = [w, torch.empty((rows, cols), dtype=torch.float32, device=w.device), (rows, cols, cpad_, mode), None,
+                 self.gen]
+            self.entries[key] = e
+        else:  # the weights moved on (optimizer step / new forward): a new generation, unused entries go
+            self.gen += 1
+            self.entries = {k: v for k, v in self.entries.items() if v[4] >= self.gen - 2}
+            e[4] = self.gen
+        ep = (epochs.OPT[0], epochs.FWD[0])
+        stale = [v for v in self.entries.values() if v[3] != (v[0]._version, *ep) and v[0].device == w.device]
+        T.pack_conv_weights_multi([v[0] for v in stale], [v[1] for v in stale], [c for v in stale for c in v[2]])
+        for v in stale:
+            v[3] = (v[0]._version, *ep)
+        return e[1]
+
+
+_PACKS = _PackSet()
+
+
+def _pack(T, w, rows, cols, cpad_, mode, shared):
+    """Packed GEMM operand of weight ``w``; ``shared``: w is the parameter's own storage (its
+    version counter tracks the optimizer) -> the batched cache, else one launch now."""
+    if shared and _BATCH_PACK:
+        return _PACKS.get(T, w, rows, cols, cpad_, mode)
+    return T.pack_conv_weight(w.contiguous(), rows, cols, cpad_, mode)
+
+
 def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
     """Forward of one native conv: returns (y NHWC (B, Ho, Wo, Cout), saved (xh, w32), meta,
     part). With ``stats``, ``part`` is the per-tile BatchNorm statistics of y from the GEMM
@@ -124,7 +179,9 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
     if cin_p != Cin:
         xh = F.pad(xh, (0, cin_p - Cin))
     xh = xh.float().contiguous()
-    w32 = weight.detach().float().contiguous()  # the parameter itself for fp32 weights: no copy
+    wd = weight.detach()
+    w32 = wd if wd.dtype == torch.float32 else wd.float()  # the parameter itself for fp32 weights: no copy
+    shared = w32 is wd  # (may be channels_last: the pack / transform kernels read it in place)
     kk = T.conv_gen_k(ks, cin_p)
     shift = F.pad(bias.detach().float(), (0, cout_p - Cout)).contiguous() if bias is not None else None
     Ho, Wo = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
@@ -136,14 +193,14 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
     def run(cfg, sp):
         if cfg in (WINO, WINO_LDS):  # Winograd F(2x2,3x3): 2.25x fewer multiplies
             if "u" not in cache:
-                cache["u"] = T.wino_weights(w32, False, cout_p, cin_p)
+                cache["u"] = T.wino_weights(w32.contiguous(), False, cout_p, cin_p)
             return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
         if cfg == WINO4S:  # Winograd F(4x4,3x3): 4x fewer multiplies (band geometry on ResNet's maps)
             if "u4" not in cache:
                 cache["u4"] = T.wino4_weights(w32, False, cout_p, cin_p)
             return T.conv_wino4_fwd(xh, cache["u4"], None, shift, False, False, None, sp, 3)[0]
         if "wk" not in cache:  # [cout_p][(kh, kw, ci)] zero-padded GEMM operand
-            cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
+            cache["wk"] = _pack(T, w32, cout_p, kk, cin_p, 0, shared)
         return T.conv_gen(xh, cache["wk"], None, shift, False, None, None, ks, stride, pad, cfg, sp)
 
     cands = TUNER.candidates(M, cout_p, kk)
@@ -158,7 +215,7 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
     part = None
     if stats and _EPI_STATS and cfg not in (WINO, WINO_LDS, WINO4S) and sp == 1:
         if "wk" not in cache:
-            cache["wk"] = T.pack_conv_weight(w32, cout_p, kk, cin_p, 0)
+            cache["wk"] = _pack(T, w32, cout_p, kk, cin_p, 0, shared)
         y, part = T.conv_gen_stats(xh, cache["wk"], shift, ks, stride, pad, cfg)
         if cout_p != Cout:
             part = part[..., :Cout].contiguous()
@@ -190,6 +247,7 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
     # stride 1: dgrad = stride-1 conv of g with flipped taps, padding ks-1-pad;
     # strided 1x1 / 3x3: transposed gather kernel, natural tap order
     transposed = stride != 1
+    shared = meta[8] == torch.float32  # w32 is the parameter's own storage (see _conv_fwd)
     assert res is None or not transposed
     pad_b = pad if transposed else ks - 1 - pad
     M, K = B * H * W, ks * ks * cout_p
@@ -199,14 +257,14 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
     def run(cfg, sp):
         if cfg in (WINO, WINO_LDS):  # stride-1 3x3 dgrad = Winograd conv of g, flipped taps
             if "ut" not in cache:
-                cache["ut"] = T.wino_weights(w32, True, cin_p, cout_p)
+                cache["ut"] = T.wino_weights(w32.contiguous(), True, cin_p, cout_p)
             return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
         if cfg == WINO4S:
             if "ut4" not in cache:
                 cache["ut4"] = T.wino4_weights(w32, True, cin_p, cout_p)
             return T.conv_wino4_fwd(g, cache["ut4"], None, None, False, False, None, sp, 3)[0]
         if "wt" not in cache:  # [ci][(kh, kw, co)], flipped for stride 1
-            cache["wt"] = T.pack_conv_weight(w32, cin_p, K, cout_p, 2 if transposed else 1)
+            cache["wt"] = _pack(T, w32, cin_p, K, cout_p, 2 if transposed else 1, shared)
         return T.conv_gen_bwd(g, cache["wt"], res, res_stride, None, ks, stride if transposed else 1, pad_b, H, W,
                               transposed, cfg, sp)
 
@@ -402,6 +460,8 @@ class _NativeBN2d(torch.autograd.Function):
         b = bias.detach() if bias is not None else None
         y, mean, invstd, _ = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum),
                                             num_batches=nbt)
+        if running_mean is not None:
+            epochs.bump_stats()  # running stats written by the kernel: no version bump
         ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd)
         ctx.has_w, ctx.has_b = weight is not None, bias is not None
         return _as_nchw(y)
@@ -438,6 +498,8 @@ class _NativeBNAct(torch.autograd.Function):
         b = bias.detach() if bias is not None else None
         y, mean, invstd, mk = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
                                              bool(relu), pre, nbt)
+        if running_mean is not None:
+            epochs.bump_stats()
         # the backward masks by the ReLU bit mask (1 byte per 4 channels) instead of re-reading y
         ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd, mk)
         ctx.has_w, ctx.has_b, ctx.relu, ctx.has_res = weight is not None, bias is not None, relu, res is not None
@@ -727,6 +789,9 @@ def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True, dr
     if not ops.available() or ops.backend() == "torch":
         return []
     from .resnet_engine import _is_resnet
+    if not getattr(model, "_tp_pack_epoch_hook", False):  # every forward starts a pack epoch (_PackSet)
+        model.register_forward_pre_hook(epochs.bump_fwd)
+        model._tp_pack_epoch_hook = True
     switched = []
     for m in model.modules():
         if "forward" in m.__dict__:
