@@ -96,6 +96,7 @@ hipError_t tp_prefix_delta_gemm(const float* T, const float* Wsub, const float* 
 hipError_t tp_prefix_tri_operands(const float* z, const float* W, const int* perm, int B, int C, int N, int p0,
                                   int cnt, int Kc, float* T, float* Wsub, hipStream_t st);
 hipError_t tp_wino4_weights(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, hipStream_t st);
+hipError_t tp_wino4_weights_multi(const long long* desc, int n, long long total, hipStream_t st);
 hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, long long st0,
                                     long long st1, int st2, int st3, hipStream_t st);
 int tp_wino4_u_img();
@@ -347,7 +348,12 @@ void pack_conv_weights_multi(const std::vector<at::Tensor>& ws, const std::vecto
     d[11] = w.stride(1);
     d[12] = w.stride(2);
     d[13] = w.stride(3);
-    total += (rows * cols + 4095) / 4096 * 4096;  // next operand on a chunk boundary (PACK_CHUNK)
+    if (mode == 0) {
+      total += (rows * cols + 4095) / 4096 * 4096;  // next operand on a chunk boundary (PACK_CHUNK)
+    } else {  // one 4096-element chunk per 64 x 64 (ci, co) tile of a tap
+      TORCH_CHECK(cols == w.size(2) * w.size(2) * cpad, "pack_conv_weights_multi: dgrad operands need cols = KS*KS*cpad");
+      total += ((rows + 63) / 64) * w.size(2) * w.size(2) * ((cpad + 63) / 64) * 4096;
+    }
   }
   auto dd = hd.to(ws[0].device(), /*non_blocking=*/true);
   TP_CHECK_HIP(tp_pack_conv_weights_multi(reinterpret_cast<const long long*>(dd.data_ptr<int64_t>()), (int)n,
@@ -515,6 +521,51 @@ at::Tensor wino4_weights(const at::Tensor& w, bool flip_t, int64_t K, int64_t C)
                                         (int)w.size(0), (int)w.size(1), w.stride(0), w.stride(1), (int)w.stride(2),
                                         (int)w.stride(3), cur_stream()));
   return u;
+}
+
+void need_u4(const at::Tensor& u, int64_t C, int64_t K);
+
+// F(4x4) U images of many 3x3 weights in one launch: us[i] <- ws[i] per cfg[3i:3i+3] = (K, C,
+// flip_t) (the padded GEMM widths, as wino4_weights). ws may be strided (channels_last).
+void wino4_weights_multi(const std::vector<at::Tensor>& ws, const std::vector<at::Tensor>& us,
+                         const std::vector<int64_t>& cfg) {
+  constexpr int D = 12;
+  const int64_t n = (int64_t)ws.size();
+  TORCH_CHECK(n > 0 && (int64_t)us.size() == n && (int64_t)cfg.size() == 3 * n,
+              "wino4_weights_multi: ws, us and 3 ints per operand");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ws[0].device());
+  auto hd = at::empty({n * D}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+  int64_t* h = hd.data_ptr<int64_t>();
+  int64_t total = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const at::Tensor& w = ws[i];
+    const int64_t K = cfg[3 * i], C = cfg[3 * i + 1], flip = cfg[3 * i + 2];
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
+                    w.device() == ws[0].device() && w.stride(0) > 0 && w.stride(1) > 0 && w.stride(2) > 0 &&
+                    w.stride(3) > 0, "wino4_weights_multi: fp32 (O, I, 3, 3) GPU weights");
+    TORCH_CHECK(K > 0 && C > 0 && K % 32 == 0 && C % 8 == 0 &&
+                    (flip ? (w.size(0) <= C && w.size(1) <= K) : (w.size(0) <= K && w.size(1) <= C)),
+                "wino4_weights_multi: bad padded widths");
+    need_u4(us[i], C, K);
+    TORCH_CHECK(us[i].device() == w.device(), "wino4_weights_multi: u on w's device");
+    int64_t* d = h + i * D;
+    d[0] = reinterpret_cast<int64_t>(w.data_ptr<float>());
+    d[1] = reinterpret_cast<int64_t>(us[i].data_ptr<float>());
+    d[2] = total;
+    d[3] = K;
+    d[4] = C;
+    d[5] = flip ? 1 : 0;
+    d[6] = w.size(0);
+    d[7] = w.size(1);
+    d[8] = w.stride(0);
+    d[9] = w.stride(1);
+    d[10] = w.stride(2);
+    d[11] = w.stride(3);
+    total += C * K;  // a multiple of 256: every block stays inside one operand
+  }
+  auto dd = hd.to(ws[0].device(), /*non_blocking=*/true);
+  TP_CHECK_HIP(tp_wino4_weights_multi(reinterpret_cast<const long long*>(dd.data_ptr<int64_t>()), (int)n,
+                                      (long long)total, cur_stream()));
 }
 
 void need_u4(const at::Tensor& u, int64_t C, int64_t K) {
@@ -1024,6 +1075,7 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("wino_staged_ok(int H, int W, bool unpool) -> bool",
         [](int64_t H, int64_t W, bool unpool) -> bool { return tp_wino_staged_ok((int)H, (int)W, unpool ? 1 : 0) != 0; });
   m.def("wino4_taylor_slots(int S) -> int", [](int64_t S) -> int64_t { return tp_wino4_taylor_slots((int)S); });
+  m.def("wino4_u_img() -> int", []() -> int64_t { return tp_wino4_u_img(); });
   m.def("wino4_lds_bytes(int S, int variant=0) -> int",
         [](int64_t S, int64_t variant) -> int64_t { return tp_wino4_lds_bytes((int)S, (int)variant); });
   m.def("nchw_to_nhwc_pad(Tensor x, int Cp) -> Tensor");
@@ -1042,6 +1094,7 @@ void register_engine_ops_def(torch::Library& m) {
         "-> Tensor");
   m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");
   m.def("pack_conv_weights_multi(Tensor[] ws, Tensor(a!)[] outs, int[] cfg) -> ()");
+  m.def("wino4_weights_multi(Tensor[] ws, Tensor(a!)[] us, int[] cfg) -> ()");
   m.def("conv_gen_stats(Tensor x, Tensor w, Tensor? shift, int ks, int stride, int pad, int cfg) -> (Tensor, Tensor)");
   m.def("wino_wgrad(Tensor g, Tensor x, int cfg, int splits, Tensor(a!) out) -> ()");
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
@@ -1085,6 +1138,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("pack_conv_weight", &pack_conv_weight);
   m.impl("pack_conv_weights_multi", &pack_conv_weights_multi);
+  m.impl("wino4_weights_multi", &wino4_weights_multi);
   m.impl("conv_gen_stats", &conv_gen_stats);
   m.impl("wino_wgrad", &wino_wgrad);
   m.impl("bn_train_fwd", &bn_train_fwd);

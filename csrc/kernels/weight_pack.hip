@@ -46,6 +46,8 @@ constexpr int PACK_DESC = 14, PACK_CHUNK = 4096;  // operands start on PACK_CHUN
 
 // A block walks whole chunks; every element of a chunk belongs to one operand (aligned starts),
 // so the descriptor search runs once per chunk (block-uniform) instead of once per element.
+// Mode 0 operands: ceil(rows * cols / PACK_CHUNK) element chunks; modes 1 / 2: one chunk per
+// (64-row ci tile, tap, 64-column co tile) — requires cols == KS * KS * cpad (the dgrad operands).
 __global__ __launch_bounds__(256) void pack_conv_weights_multi(const long long* __restrict__ desc, int n,
                                                                long long total) {
   const long long chunks = (total + PACK_CHUNK - 1) / PACK_CHUNK;
@@ -63,7 +65,31 @@ __global__ __launch_bounds__(256) void pack_conv_weights_multi(const long long* 
     const int O = (int)d[3], I = (int)d[4], KS = (int)d[5], rows = (int)d[6], cols = (int)d[7], cpad = (int)d[8];
     const int mode = (int)d[9];
     const long long s0 = d[10], s1 = d[11], s2 = d[12], s3 = d[13];
-    const long long size = (long long)rows * cols, off = base - d[2];
+    const long long off = base - d[2];
+    if (mode != 0) {  // data-gradient operands: one 64 (ci) x 64 (co) tile of one tap per chunk, through LDS
+      // (out rows are ci, the weight's contiguous dim is co's neighbour ci: a direct per-element
+      // copy read one 4-byte word per 64-byte line; the transpose makes both sides coalesced)
+      __shared__ float tile[64][65];
+      const int q = (int)(off / PACK_CHUNK), ct = (cpad + 63) / 64, taps = KS * KS;
+      const int co_t = q % ct, tap = (q / ct) % taps, ci_t = q / (ct * taps);
+      int kh = tap / KS, kw = tap - kh * KS;
+      if (mode == 1) {
+        kh = KS - 1 - kh;
+        kw = KS - 1 - kw;
+      }
+      for (int e = threadIdx.x; e < PACK_CHUNK; e += blockDim.x) {
+        const int lco = e >> 6, lci = e & 63, co = co_t * 64 + lco, ci = ci_t * 64 + lci;
+        tile[lco][lci] = co < O && ci < I ? w[co * s0 + ci * s1 + kh * s2 + kw * s3] : 0.f;
+      }
+      __syncthreads();
+      for (int e = threadIdx.x; e < PACK_CHUNK; e += blockDim.x) {
+        const int lci = e >> 6, lco = e & 63, co = co_t * 64 + lco, ci = ci_t * 64 + lci;
+        if (ci < rows && co < cpad) out[(long long)ci * cols + tap * cpad + co] = tile[lco][lci];
+      }
+      __syncthreads();
+      continue;
+    }
+    const long long size = (long long)rows * cols;
     for (int e = threadIdx.x; e < PACK_CHUNK; e += blockDim.x) {
       const long long i = off + e;
       if (i >= size) break;

@@ -1433,9 +1433,9 @@ __global__ __launch_bounds__(256, 1) void wino4_wide(Args p) {
 // of image (cb, kb) holds U[x][c = 8cb + 2g + e][k = 32kb + 16nh + j]; layout 1 (MODE 2): word
 // (((e*18 + x/2)*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + (x & 1) holds U[x][c = 8cb + 2g + e][k]. fp64, rounded once. flip_t: the
 // data-gradient operand (w'[k][c] = w[c][k], taps rotated 180 degrees).
-__global__ __launch_bounds__(256) void weight_transform(const float* __restrict__ w, float* __restrict__ u, int K, int C,
-                                                        int flip_t, int S0, int S1, int lay, long long st0,
-                                                        long long st1, int st2, int st3) {
+__device__ __forceinline__ void weight_transform_one(long long t, const float* __restrict__ w, float* __restrict__ u,
+                                                     int K, int C, int flip_t, int S0, int S1, int lay, long long st0,
+                                                     long long st1, int st2, int st3) {
   // one thread per (c, k): its 9 taps are read once and all 36 points formed with compile-time G
   // indices (the per-point version re-read the taps 36x and indexed G at run time); same fp64
   // products and summation order per point as before, so the same rounded U
@@ -1447,37 +1447,63 @@ __global__ __launch_bounds__(256) void weight_transform(const float* __restrict_
                                {0.0, 0.0, 1.0}};
   // lanes enumerate (g slot, j) of one (e, nh) so that for each point a wave's 64 stores land in
   // one 128-word span of the image (stride 2) instead of 8 words apart
+  const int gs_ = (int)(t & 3), j_ = (int)((t >> 2) & 15), e_ = (int)((t >> 6) & 1), nh_ = (int)((t >> 7) & 1);
+  const long long rest = t >> 8;
+  const int kb_ = (int)(rest % (K / TK)), cb_ = (int)(rest / (K / TK));
+  const int c = 8 * cb_ + 2 * (gs_ ^ ((j_ >> 3) << 1)) + e_, k = TK * kb_ + 16 * nh_ + j_;
+  const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
+  const bool ok = r0 < S0 && r1 < S1;
+  double wv[9];
+  // w's element strides st0..st3 (a channels_last parameter is read in place)
+  const float* src = w + (ok ? r0 : 0) * st0 + (ok ? r1 : 0) * st1;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int tt = flip_t ? 8 - tap : tap;
+    wv[tap] = ok ? (double)src[(tt / 3) * st2 + (tt % 3) * st3] : 0.0;
+  }
+  const int cb = c >> 3, cc = c & 7, g = cc >> 1, e = cc & 1;
+  const int kb = k / TK, kk = k - kb * TK, nh = kk >> 4, j = kk & 15;
+  const int gs = g ^ ((j >> 3) << 1);
+  float* dst = u + ((long long)cb * (K / TK) + kb) * U_IMG + (nh << 7) + (j << 3) + (gs << 1);
+#pragma unroll
+  for (int x = 0; x < NPT; ++x) {
+    const int i = x / 6, jj = x % 6;
+    double acc = 0.0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) acc += Gm[i][a] * wv[a * 3 + b] * Gm[jj][b];
+    const int hi = lay ? e * 18 + x / 2 : x, lo = lay ? (x & 1) : e;
+    dst[(hi << 8) + lo] = (float)acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void weight_transform(const float* __restrict__ w, float* __restrict__ u, int K, int C,
+                                                        int flip_t, int S0, int S1, int lay, long long st0,
+                                                        long long st1, int st2, int st3) {
   const long long total = (long long)C * K;
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int gs_ = (int)(t & 3), j_ = (int)((t >> 2) & 15), e_ = (int)((t >> 6) & 1), nh_ = (int)((t >> 7) & 1);
-    const long long rest = t >> 8;
-    const int kb_ = (int)(rest % (K / TK)), cb_ = (int)(rest / (K / TK));
-    const int c = 8 * cb_ + 2 * (gs_ ^ ((j_ >> 3) << 1)) + e_, k = TK * kb_ + 16 * nh_ + j_;
-    const int r0 = flip_t ? c : k, r1 = flip_t ? k : c;
-    const bool ok = r0 < S0 && r1 < S1;
-    double wv[9];
-    // w's element strides st0..st3 (a channels_last parameter is read in place)
-    const float* src = w + (ok ? r0 : 0) * st0 + (ok ? r1 : 0) * st1;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int tt = flip_t ? 8 - tap : tap;
-      wv[tap] = ok ? (double)src[(tt / 3) * st2 + (tt % 3) * st3] : 0.0;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x)
+    weight_transform_one(t, w, u, K, C, flip_t, S0, S1, lay, st0, st1, st2, st3);
+}
+
+// Every U image set of a training step in one launch: descriptor d (W4_DESC int64: w, u, start,
+// K, C, flip_t, S0, S1, st0, st1, st2, st3), starts multiples of 256 (C*K is: C % 8, K % 32), so
+// a block's 256 (c, k) threads all belong to one operand (block-uniform descriptor search).
+constexpr int W4_DESC = 12;
+__global__ __launch_bounds__(256) void weight_transform_multi(const long long* __restrict__ desc, int n,
+                                                              long long total, int lay) {
+  for (long long blk = blockIdx.x; blk * 256 < total; blk += gridDim.x) {
+    const long long base = blk * 256;
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (desc[mid * W4_DESC + 2] <= base) lo = mid;
+      else hi = mid - 1;
     }
-    const int cb = c >> 3, cc = c & 7, g = cc >> 1, e = cc & 1;
-    const int kb = k / TK, kk = k - kb * TK, nh = kk >> 4, j = kk & 15;
-    const int gs = g ^ ((j >> 3) << 1);
-    float* dst = u + ((long long)cb * (K / TK) + kb) * U_IMG + (nh << 7) + (j << 3) + (gs << 1);
-#pragma unroll
-    for (int x = 0; x < NPT; ++x) {
-      const int i = x / 6, jj = x % 6;
-      double acc = 0.0;
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) acc += Gm[i][a] * wv[a * 3 + b] * Gm[jj][b];
-      const int hi = lay ? e * 18 + x / 2 : x, lo = lay ? (x & 1) : e;
-      dst[(hi << 8) + lo] = (float)acc;
-    }
+    const long long* d = desc + lo * W4_DESC;
+    weight_transform_one(base - d[2] + threadIdx.x, reinterpret_cast<const float*>(d[0]), reinterpret_cast<float*>(d[1]),
+                         (int)d[3], (int)d[4], (int)d[5], (int)d[6], (int)d[7], lay, d[8], d[9], (int)d[10],
+                         (int)d[11]);
   }
 }
 
@@ -1507,6 +1533,15 @@ extern "C" hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, 
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
   tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1, tp::w4::kernel_mode() >= 2, st0, st1,
                                                  st2, st3);
+  return hipGetLastError();
+}
+
+// desc: n descriptors of W4_DESC int64 on the device (validated by the binding against live
+// tensors), starts ascending in (c, k) threads: start[i+1] = start[i] + C_i * K_i
+extern "C" hipError_t tp_wino4_weights_multi(const long long* desc, int n, long long total, hipStream_t st) {
+  if (n <= 0 || total <= 0 || total % 256) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)std::min<long long>(total / 256, 16384);
+  tp::w4::weight_transform_multi<<<grid, 256, 0, st>>>(desc, n, total, tp::w4::kernel_mode() >= 2);
   return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ hipError_t tp_gemm1x1_ws(const float* x, const float* w, int B, int H, int W, in
                          const float* scale, const float* shift, int relu, float slope, const float* res,
                          const float* mask, float* apoz, float* out, int variant, hipStream_t st);
 hipError_t tp_pack_conv_weights_multi(const long long* desc, int n, long long total, hipStream_t st);
+hipError_t tp_wino4_weights_multi(const long long* desc, int n, long long total, hipStream_t st);
 hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, long long st0,
                                     long long st1, int st2, int st3, hipStream_t st);
 hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
@@ -136,6 +137,7 @@ int main() {
                        reinterpret_cast<const uint8_t*>(n)) == hipErrorInvalidValue);  // dgrad without act
   EXPECT(tp_pack_conv_weights_multi(nullptr, 0, 16, nullptr) == hipErrorInvalidValue);  // no operands
   EXPECT(tp_pack_conv_weights_multi(nullptr, 2, 0, nullptr) == hipErrorInvalidValue);   // nothing to write
+  EXPECT(tp_wino4_weights_multi(nullptr, 1, 100, nullptr) == hipErrorInvalidValue);     // not whole blocks
   EXPECT(tp_wino4_weights_strided(n, n, 64, 64, 0, 64, 64, 0, 9, 3, 1, nullptr) == hipErrorInvalidValue);  // stride 0
   EXPECT(tp_wino4_weights_strided(n, n, 64, 64, 0, 96, 64, 576, 9, 3, 1, nullptr) == hipErrorInvalidValue);  // S0 > K
 

@@ -322,12 +322,12 @@ def test_pack_conv_weights_multi_and_pack_set(cuda):
         assert torch.equal(o, r)
     ps = _PackSet()
     w = ws[1]
-    a = ps.get(T, w, *cfg[4:8])
+    a = ps.get(T, w, "pack", tuple(cfg[4:8]), tuple(cfg[4:6]))
     assert torch.equal(a, refs[1])
-    assert ps.get(T, w, *cfg[4:8]) is a  # hit: same buffer, no repack
+    assert ps.get(T, w, "pack", tuple(cfg[4:8]), tuple(cfg[4:6])) is a  # hit: same buffer, no repack
     with torch.no_grad():
         w.mul_(2.0)  # in-place: version bump -> the next request repacks
-    b = ps.get(T, w, *cfg[4:8])
+    b = ps.get(T, w, "pack", tuple(cfg[4:8]), tuple(cfg[4:6]))
     assert b is a and torch.equal(b, 2.0 * refs[1])
 
 
@@ -339,8 +339,16 @@ def test_wino4_weights_channels_last(cuda):
     wl = w.contiguous(memory_format=torch.channels_last)
     assert not wl.is_contiguous()
     for flip in (False, True):
-        K, C = (64, 64) if not flip else (64, 64)
-        assert torch.equal(T.wino4_weights(wl, flip, K, C), T.wino4_weights(w, flip, K, C))
+        assert torch.equal(T.wino4_weights(wl, flip, 64, 64), T.wino4_weights(w, flip, 64, 64))
+    # the multi-operand launch (training caches): one launch for several weights, both layouts
+    w2 = torch.randn(32, 64, 3, 3, device=cuda)
+    us = [torch.full((8, 2, T.wino4_u_img()), float("nan"), device=cuda),
+          torch.full((8, 2, T.wino4_u_img()), float("nan"), device=cuda),
+          torch.full((4, 2, T.wino4_u_img()), float("nan"), device=cuda)]
+    T.wino4_weights_multi([wl, w, w2], us, [64, 64, 0, 64, 64, 1, 64, 32, 1])
+    assert torch.equal(us[0], T.wino4_weights(w, False, 64, 64))
+    assert torch.equal(us[1], T.wino4_weights(w, True, 64, 64))
+    assert torch.equal(us[2], T.wino4_weights(w2, True, 64, 32))
 
 
 @pytest.mark.parametrize("O,I", [(40, 36), (64, 32)])

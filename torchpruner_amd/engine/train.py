@@ -128,29 +128,34 @@ class _PackSet:
     (no dangling pointer) and are dropped after a whole step without a request (pruned layers)."""
 
     def __init__(self):
-        self.entries = {}  # key -> [weight view, out, cfg, (version, OPT, FWD) packed at, last generation used]
+        # key -> [weight view, out, kind, cfg, (version, OPT, FWD) packed at, last generation used]
+        self.entries = {}
         self.gen = 0
 
-    def get(self, T, w, rows, cols, cpad_, mode):
-        key = (w.data_ptr(), tuple(w.shape), tuple(w.stride()), str(w.device), rows, cols, cpad_, mode)
+    def get(self, T, w, kind, cfg, out_shape):
+        """kind "pack": cfg = (rows, cols, cpad, mode) of pack_conv_weight; "w4": cfg = (K, C,
+        flip_t) of wino4_weights."""
+        key = (kind, w.data_ptr(), tuple(w.shape), tuple(w.stride()), str(w.device), cfg)
         e = self.entries.get(key)
         now = (w._version, epochs.OPT[0], epochs.FWD[0])
-        if e is not None and e[3] == now:
-            e[4] = self.gen
+        if e is not None and e[4] == now:
+            e[5] = self.gen
             return e[1]
         if e is None:
-            e = [w, torch.empty((rows, cols), dtype=torch.float32, device=w.device), (rows, cols, cpad_, mode), None,
-                 self.gen]
+            e = [w, torch.empty(out_shape, dtype=torch.float32, device=w.device), kind, cfg, None, self.gen]
             self.entries[key] = e
         else:  # the weights moved on (optimizer step / new forward): a new generation, unused entries go
             self.gen += 1
-            self.entries = {k: v for k, v in self.entries.items() if v[4] >= self.gen - 2}
-            e[4] = self.gen
+            self.entries = {k: v for k, v in self.entries.items() if v[5] >= self.gen - 2}
+            e[5] = self.gen
         ep = (epochs.OPT[0], epochs.FWD[0])
-        stale = [v for v in self.entries.values() if v[3] != (v[0]._version, *ep) and v[0].device == w.device]
-        T.pack_conv_weights_multi([v[0] for v in stale], [v[1] for v in stale], [c for v in stale for c in v[2]])
+        stale = [v for v in self.entries.values() if v[4] != (v[0]._version, *ep) and v[0].device == w.device]
+        for kd, fn in (("pack", T.pack_conv_weights_multi), ("w4", T.wino4_weights_multi)):
+            lst = [v for v in stale if v[2] == kd]
+            if lst:
+                fn([v[0] for v in lst], [v[1] for v in lst], [c for v in lst for c in v[3]])
         for v in stale:
-            v[3] = (v[0]._version, *ep)
+            v[4] = (v[0]._version, *ep)
         return e[1]
 
 
@@ -159,10 +164,17 @@ _PACKS = _PackSet()
 
 def _pack(T, w, rows, cols, cpad_, mode, shared):
     """Packed GEMM operand of weight ``w``; ``shared``: w is the parameter's own storage (its
-    version counter tracks the optimizer) -> the batched cache, else one launch now."""
+    version counter tracks in-place updates) -> the batched cache, else one launch now."""
     if shared and _BATCH_PACK:
-        return _PACKS.get(T, w, rows, cols, cpad_, mode)
+        return _PACKS.get(T, w, "pack", (rows, cols, cpad_, mode), (rows, cols))
     return T.pack_conv_weight(w.contiguous(), rows, cols, cpad_, mode)
+
+
+def _u4(T, w, K, C, flip, shared):
+    """F(4x4) U images of a 3x3 weight (``wino4_weights(w, flip, K, C)``), batched like _pack."""
+    if shared and _BATCH_PACK:
+        return _PACKS.get(T, w, "w4", (K, C, int(flip)), (C // 8, K // 32, T.wino4_u_img()))
+    return T.wino4_weights(w, flip, K, C)
 
 
 def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
@@ -197,7 +209,7 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
             return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
         if cfg == WINO4S:  # Winograd F(4x4,3x3): 4x fewer multiplies (band geometry on ResNet's maps)
             if "u4" not in cache:
-                cache["u4"] = T.wino4_weights(w32, False, cout_p, cin_p)
+                cache["u4"] = _u4(T, w32, cout_p, cin_p, False, shared)
             return T.conv_wino4_fwd(xh, cache["u4"], None, shift, False, False, None, sp, 3)[0]
         if "wk" not in cache:  # [cout_p][(kh, kw, ci)] zero-padded GEMM operand
             cache["wk"] = _pack(T, w32, cout_p, kk, cin_p, 0, shared)
@@ -261,7 +273,7 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
             return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
         if cfg == WINO4S:
             if "ut4" not in cache:
-                cache["ut4"] = T.wino4_weights(w32, True, cin_p, cout_p)
+                cache["ut4"] = _u4(T, w32, cin_p, cout_p, True, shared)
             return T.conv_wino4_fwd(g, cache["ut4"], None, None, False, False, None, sp, 3)[0]
         if "wt" not in cache:  # [ci][(kh, kw, co)], flipped for stride 1
             cache["wt"] = _pack(T, w32, cin_p, K, cout_p, 2 if transposed else 1, shared)
