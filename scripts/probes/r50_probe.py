@@ -1,3 +1,5 @@
+"""ResNet-50 B=64 eval forward on MIOpen (default vs deterministic) and the APoZ channel reduction
+on a 64x64x112x112 NHWC activation: early-round timing references."""
 import sys, os; sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import time, torch
 import torch.nn.functional as F
