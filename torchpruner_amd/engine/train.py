@@ -225,7 +225,8 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
             cands = cands + wino4_cands(B, H, cout_p, cin_p)
     cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
     part = None
-    if stats and _EPI_STATS and cfg not in (WINO, WINO_LDS, WINO4S) and sp == 1:
+    stats_ok = (ks in (1, 3, 5) and cin_p % 32 == 0) or (ks in (3, 5, 7) and cin_p == 4)  # conv_gen_stats' shapes
+    if stats and stats_ok and _EPI_STATS and cfg not in (WINO, WINO_LDS, WINO4S) and sp == 1:
         if "wk" not in cache:
             cache["wk"] = _pack(T, w32, cout_p, kk, cin_p, 0, shared)
         y, part = T.conv_gen_stats(xh, cache["wk"], shift, ks, stride, pad, cfg)
@@ -377,9 +378,10 @@ class _NativeConv2dStats(torch.autograd.Function):
 
 
 def conv_stats(conv: nn.Conv2d, x: torch.Tensor):
-    """``(conv(x), tile statistics or None)`` — a native 1x1 conv computes its output's BN
-    statistics in the GEMM epilogue; anything else runs the module (statistics None)."""
-    if "forward" in conv.__dict__ and conv.forward.__func__ is _native_forward and _geom(conv)[0] == 1 \
+    """``(conv(x), tile statistics or None)`` — a native conv whose tuned kernel is a one-pass
+    implicit GEMM computes its output's BN statistics in the epilogue (1x1, strided 3x3, the
+    packed-tap stem; Winograd picks return None); anything else runs the module (None)."""
+    if "forward" in conv.__dict__ and conv.forward.__func__ is _native_forward \
             and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.weight.dtype == torch.float32 \
             and _fits(conv, x):
         ks, s, p = _geom(conv)
@@ -614,12 +616,14 @@ def _native_block_forward(self, x):
         out = bn_act(self.bn1, y1, relu=True, pre=p1)
     else:
         identity = self.downsample(x) if self.downsample is not None else x
-        out = bn_act(self.bn1, self.conv1(x), relu=True)
+        y1, p1 = conv_stats(self.conv1, x)
+        out = bn_act(self.bn1, y1, relu=True, pre=p1)
+    y2, p2 = conv_stats(self.conv2, out)
     if _block_kind(self) == "bottleneck":
-        out = bn_act(self.bn2, self.conv2(out), relu=True)
+        out = bn_act(self.bn2, y2, relu=True, pre=p2)
         y3, p3 = conv_stats(self.conv3, out)
         return bn_act(self.bn3, y3, res=identity, relu=True, pre=p3)
-    return bn_act(self.bn2, self.conv2(out), res=identity, relu=True)
+    return bn_act(self.bn2, y2, res=identity, relu=True, pre=p2)
 
 
 def _native_sequential_forward(self, x):
@@ -642,7 +646,8 @@ def _native_resnet_forward(self, x):
     """ResNet training forward with the stem's BN+ReLU fused (the blocks patch themselves)."""
     if not (self.training and x.is_cuda):
         return type(self).forward(self, x)
-    x = self.maxpool(bn_act(self.bn1, self.conv1(x), relu=True))
+    y, p = conv_stats(self.conv1, x)
+    x = self.maxpool(bn_act(self.bn1, y, relu=True, pre=p))
     x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
     return self.fc(torch.flatten(self.avgpool(x), 1))
 
@@ -792,9 +797,10 @@ def enable_native_convs(model: nn.Module, bn: bool = True, fuse: bool = True, dr
     training mode) through the native kernels (instance-level ``forward`` override; pruning keeps
     working because weights are re-packed per call). With ``bn`` and ``fuse``, residual blocks,
     ResNet stems and ``nn.Sequential`` containers also fuse their BN(+residual)+ReLU tails in
-    training mode — the fused BN / ReLU modules (and a bottleneck's conv1 / downsample conv, run by
-    the block's entry node) are then not called, so forward hooks on them do not fire (attribution
-    passes use ``fuse=False``). Also switched: ``nn.Linear`` (MFMA GEMM), ``nn.MaxPool2d``,
+    training mode — the fused BN / ReLU modules (and the convs run by a block's entry node or with
+    epilogue BN statistics: a bottleneck's conv1 / downsample, every block's conv2 / conv3, the
+    stem conv) are then not called, so forward hooks on them do not fire (attribution passes use
+    ``fuse=False``, eval-mode forwards are unchanged). Also switched: ``nn.Linear`` (MFMA GEMM), ``nn.MaxPool2d``,
     ``nn.AdaptiveAvgPool2d`` and, with ``dropout``, training-mode ``nn.Dropout`` (Philox masks
     seeded from torch's CPU RNG: a different random stream than PyTorch's dropout). Returns the
     switched modules; undo with :func:`disable_native_convs`."""
