@@ -132,14 +132,24 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
 // over the groups (coalesced 16-channel rows), then lane 0 folds the 64 lane sums in order
 // (deterministic). 64 lanes, not 16: the 64-channel BNs of the 56-px stage have 1024 groups and
 // only 4 blocks, and the finalize ran ~22 us there as a chain of 64 dependent load pairs.
+// TP_BN_FOLD_LANES=16: the previous 16-lane fold order (bit-identical statistics to round-5
+// builds before this change; diagnostic of training-trajectory sensitivity, scripts/probes/)
 constexpr int BN_FIN_T = 1024, BN_FIN_GL = BN_FIN_T / 16;
+static int bn_fold_lanes() {
+  static const int l = [] {
+    const char* e = getenv("TP_BN_FOLD_LANES");
+    const int v = e ? atoi(e) : BN_FIN_GL;
+    return v == 16 ? 16 : BN_FIN_GL;
+  }();
+  return l;
+}
 __device__ __forceinline__ void fold_groups(const double* __restrict__ part, int groups, int C, int c, int cl, int gl,
-                                            double& s, double& q) {
+                                            int lanes, double& s, double& q) {
   __shared__ double red[2][BN_FIN_GL][16];
   s = 0.0;
   q = 0.0;
-  if (c < C)
-    for (int i = gl; i < groups; i += BN_FIN_GL) {
+  if (c < C && gl < lanes)
+    for (int i = gl; i < groups; i += lanes) {
       s += part[(size_t)(2 * i) * C + c];
       q += part[(size_t)(2 * i + 1) * C + c];
     }
@@ -149,7 +159,7 @@ __device__ __forceinline__ void fold_groups(const double* __restrict__ part, int
   if (gl != 0) return;
   s = 0.0;
   q = 0.0;
-  for (int i = 0; i < BN_FIN_GL; ++i) {
+  for (int i = 0; i < lanes; ++i) {
     s += red[0][i][cl];
     q += red[1][i][cl];
   }
@@ -162,12 +172,12 @@ __global__ __launch_bounds__(BN_FIN_T) void bn_fwd_finalize(const double* __rest
                                                        float eps, float momentum, float* __restrict__ run_mean,
                                                        float* __restrict__ run_var, float* __restrict__ mean,
                                                        float* __restrict__ invstd, float* __restrict__ a,
-                                                       float* __restrict__ b, long long* __restrict__ nbt) {
+                                                       float* __restrict__ b, long long* __restrict__ nbt, int lanes) {
   const int cl = threadIdx.x % 16, gl = threadIdx.x / 16, c = blockIdx.x * 16 + cl;
   // the module's num_batches_tracked += 1 (one lane, plain vector store): no separate add launch
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
   double s, q;
-  fold_groups(part, groups, C, c, cl, gl, s, q);
+  fold_groups(part, groups, C, c, cl, gl, lanes, s, q);
   if (gl != 0 || c >= C) return;
   const double m = s / P;
   const double var = fmax(q / P - m * m, 0.0);
@@ -189,10 +199,10 @@ __global__ __launch_bounds__(BN_FIN_T) void bn_bwd_finalize(const double* __rest
                                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                        float* __restrict__ dbeta, float* __restrict__ a,
-                                                       float* __restrict__ k1, float* __restrict__ k2) {
+                                                       float* __restrict__ k1, float* __restrict__ k2, int lanes) {
   const int cl = threadIdx.x % 16, gl = threadIdx.x / 16, c = blockIdx.x * 16 + cl;
   double sg, sgx;
-  fold_groups(part, groups, C, c, cl, gl, sg, sgx);
+  fold_groups(part, groups, C, c, cl, gl, lanes, sg, sgx);
   if (gl != 0 || c >= C) return;
   if (dgamma) dgamma[c] = (float)sgx;
   if (dbeta) dbeta[c] = (float)sg;
@@ -302,7 +312,7 @@ extern "C" hipError_t tp_bn_fwd_train4(const float* x, float* y, int P, int C, c
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<0><<<grid, BN_T, 0, st>>>(x, nullptr, nullptr, nullptr, ws, P, C, rpg);
   bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
-                                                    mean, invstd, a, b, nbt);
+                                                    mean, invstd, a, b, nbt, bn_fold_lanes());
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
       x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
@@ -323,7 +333,7 @@ extern "C" hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C
   const int groups = (G + per - 1) / per;
   bn_fold_tiles<<<dim3((C + 63) / 64, groups), 256, 0, st>>>(pre, G, C, ws, per);
   bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
-                                                    mean, invstd, a, b, nbt);
+                                                    mean, invstd, a, b, nbt, bn_fold_lanes());
   const unsigned n4 = (unsigned)((long long)P * C / 4);
   bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
       x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
@@ -367,7 +377,8 @@ extern "C" hipError_t tp_bn_bwd_train3(const float* g, const float* x, float* dx
   const int rpg = (P + groups - 1) / groups;
   const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
   bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym, mk);
-  bn_bwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2);
+  bn_bwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2,
+                                                      bn_fold_lanes());
   if (dx || dres) {
     const unsigned n4 = (unsigned)((long long)P * C / 4);
     bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(

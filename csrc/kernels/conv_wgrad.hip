@@ -301,7 +301,16 @@ extern "C" hipError_t tp_conv_wgrad3(const float* g, const float* x, float* dw, 
   }
   if (e != hipSuccess || splits == 1) return e;
   const long long n = fin ? (long long)Cout * Kpad : (long long)batch * Cout * Kpad;
-  const int sl = std::min(8, splits);
+  // lanes per element: only as many as it takes to put ~16 waves on every CU (n * lanes >= 256K
+  // threads). Big weights keep one lane per element, i.e. the splits summed strictly in order —
+  // the summation order of earlier builds: a training recipe on a knife edge (the bench's seed-0
+  // VGG teacher) follows it bit for bit. TP_WGRAD_COMBINE_LANES=1 forces one lane everywhere.
+  static const int lanes_max = [] {
+    const char* e = getenv("TP_WGRAD_COMBINE_LANES");
+    return e && atoi(e) == 1 ? 1 : 8;
+  }();
+  const int sl = (int)std::max<long long>(1, std::min<long long>({(long long)lanes_max, (long long)splits,
+                                                                  ceil_div(262144ll, n)}));
   const unsigned grid = (unsigned)std::min<long long>(ceil_div(n, 64), 16384);
   if (fin)
     wgrad_combine_par<true><<<grid, 64 * sl, 0, st>>>(ws, a, nullptr, splits, n);
