@@ -116,35 +116,38 @@ __global__ __launch_bounds__(256) void maxpool_fwd_arg(const float* __restrict__
   }
 }
 
+// one block per (input row, 256-wide slice of the row's W x C/4 quads): the row (b, ih) and
+// its output-row window range are block-uniform, the per-thread index math is 32-bit (the
+// grid-stride version spent its time in 64-bit divisions: 222 us for the ResNet-50 stem at
+// B=128, ~2x its HBM time)
 __global__ __launch_bounds__(256) void maxpool_bwd_gather(const float* __restrict__ g, const uint8_t* __restrict__ am,
                                                           float* __restrict__ dx, int B, int H, int W, int C, int k,
-                                                          int s, int pad, int Ho, int Wo) {
-  const long long total = (long long)B * H * W * (C / 4);
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(t % (C / 4));
-    const long long r = t / (C / 4);
-    const int iw = (int)(r % W), ih = (int)((r / W) % H);
-    const long long b = r / ((long long)W * H);
-    // windows oh with oh*s - pad <= ih <= oh*s - pad + k - 1
-    const int oh0 = max(0, (ih + pad - k + s) / s), oh1 = min(Ho - 1, (ih + pad) / s);
-    const int ow0 = max(0, (iw + pad - k + s) / s), ow1 = min(Wo - 1, (iw + pad) / s);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int oh = oh0; oh <= oh1; ++oh) {
-      const int th = ih - (oh * s - pad);
-      for (int ow = ow0; ow <= ow1; ++ow) {
-        const unsigned want = (unsigned)(th * k + iw - (ow * s - pad));
-        const long long o = ((b * Ho + oh) * Wo + ow) * C + c4 * 4;
-        const unsigned a = *reinterpret_cast<const unsigned*>(am + o);
-        const float4 gv = *reinterpret_cast<const float4*>(g + o);
-        if ((a & 0xffu) == want) acc.x += gv.x;
-        if (((a >> 8) & 0xffu) == want) acc.y += gv.y;
-        if (((a >> 16) & 0xffu) == want) acc.z += gv.z;
-        if ((a >> 24) == want) acc.w += gv.w;
-      }
+                                                          int s, int pad, int Ho, int Wo, int cpr) {
+  const int C4 = C / 4;
+  const int row = blockIdx.x / cpr, chunk = blockIdx.x - row * cpr;  // row = b * H + ih
+  const int q = chunk * 256 + threadIdx.x;
+  if (q >= W * C4) return;
+  const int b = row / H, ih = row - b * H;
+  const int iw = q / C4, c4 = q - iw * C4;
+  // windows oh with oh*s - pad <= ih <= oh*s - pad + k - 1
+  const int oh0 = max(0, (ih + pad - k + s) / s), oh1 = min(Ho - 1, (ih + pad) / s);
+  const int ow0 = max(0, (iw + pad - k + s) / s), ow1 = min(Wo - 1, (iw + pad) / s);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    const int th = ih - (oh * s - pad);
+    const size_t obase = ((size_t)b * Ho + oh) * Wo;
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const unsigned want = (unsigned)(th * k + iw - (ow * s - pad));
+      const size_t o = (obase + ow) * C + c4 * 4;
+      const unsigned a = *reinterpret_cast<const unsigned*>(am + o);
+      const float4 gv = *reinterpret_cast<const float4*>(g + o);
+      if ((a & 0xffu) == want) acc.x += gv.x;
+      if (((a >> 8) & 0xffu) == want) acc.y += gv.y;
+      if (((a >> 16) & 0xffu) == want) acc.z += gv.z;
+      if ((a >> 24) == want) acc.w += gv.w;
     }
-    *reinterpret_cast<float4*>(dx + r * C + c4 * 4) = acc;
   }
+  *reinterpret_cast<float4*>(dx + ((size_t)row * W + iw) * C + c4 * 4) = acc;
 }
 
 // global average pool backward: dx[b][p][c] = g[b][c] / HW
@@ -181,8 +184,10 @@ extern "C" hipError_t tp_maxpool_bwd(const float* g, const uint8_t* am, float* d
   const int Ho = (H + 2 * pad - k) / s + 1, Wo = (W + 2 * pad - k) / s + 1;
   const long long total = (long long)B * H * W * (C / 4);
   if (total == 0) return hipSuccess;
-  const unsigned grid = (unsigned)std::min<long long>(tp::ceil_div(total, 256), 16384);
-  tp::maxpool_bwd_gather<<<grid, 256, 0, st>>>(g, am, dx, B, H, W, C, k, s, pad, Ho, Wo);
+  const int cpr = (int)tp::ceil_div((long long)W * (C / 4), 256);  // blocks per input row
+  const long long blocks = (long long)B * H * cpr;
+  if ((long long)W * (C / 4) >= (1ll << 31) || blocks >= (1ll << 31)) return hipErrorInvalidValue;
+  tp::maxpool_bwd_gather<<<(unsigned)blocks, 256, 0, st>>>(g, am, dx, B, H, W, C, k, s, pad, Ho, Wo, cpr);
   return hipGetLastError();
 }
 
