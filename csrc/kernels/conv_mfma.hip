@@ -34,6 +34,8 @@ __device__ __forceinline__ uint2 bf16x4_of(const f32x4 v) {
 
 constexpr int CFG_BF16 = 256;  // tile-config flag: bf16 operands (conv_igemm BF), fp32 accumulation
 constexpr int CFG_SK = 32;     // tile-config flag: stream-K split of the tiles x k-slices space (GEN 1, one K pass)
+constexpr int CFG_SB = 64;     // tile-config flag: single-buffered LDS stage (GEN 1 1x1 forward, one K pass): half the
+                               // LDS, twice the co-resident blocks for the short-K convs (profiles/train/lowk_*)
 constexpr int CFG_WS = 16;     // cfgs 16..18: persistent warp-specialised 1x1 GEMM (gemm_ws.hip), 1x1 stride-s
                                // GEN 1 convs and their dgrads (no split-K, no bnpart, dense residual)
 
@@ -70,6 +72,7 @@ struct ConvArgs {
   const float* res;         // EPI_FWD: residual [M][N] added before the ReLU (nullable)
   float* apoz;              // EPI_FWD: [B][N] counts of positive outputs (exact integers), nullable
   int epi_lds;              // GEN: 1 -> two-phase LDS-transposed forward epilogue (TP_GEN_EPI=0 disables)
+  int sb;                   // GEN 1 1x1 EPI_FWD: 1 -> the single-buffered (SB) instantiation (CFG_SB)
   int tay_group;            // EPI_BWD: >0 -> N = P pixel groups x tay_group channels (a dense-GEMM conv);
                             // Taylor of column n goes to slot n / tay_group of a (P, B, tay_group) slab
   // GEN dgrad epilogue (ResNet backward engine)
@@ -196,12 +199,19 @@ __device__ __forceinline__ float4 res_quad(const ConvArgs& p, long long pix, int
 // staged into LDS (rows of 32 bf16 = 16 dwords, padded to 20: 80-B rows keep the 16-B fragment
 // reads conflict-free), products on v_mfma_f32_32x32x16_bf16 with fp32 accumulation; loads,
 // epilogues and every output stay fp32. 16x the fp32 MFMA rate: the K slice is 2 MFMAs, not 16.
+// SB: one LDS stage instead of two (the next K slice still loads into registers under the
+// MFMAs; an extra barrier per slice before it is stored): for short-K GEMMs (K = 64-128, two to
+// four slices) whose blocks are load -> MFMA -> epilogue back to back, twice the co-resident
+// blocks overlap one block's epilogue / loads with another's MFMAs.
 template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, int EPI, int GEN = 0, bool BF = false,
-          bool SK = false>
+          bool SK = false, bool SB = false>
 __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, WM, WN) / 128) void conv_igemm(ConvArgs p) {
   using T = Tile<BM, BN, WM, WN>;
   constexpr int BK = T::BK, LDK = T::LDK;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
+  static_assert(!SB || (GEN == 1 && !BF && !SK && EPI == EPI_FWD), "single-buffered LDS: GEN 1 forward only");
+  constexpr int SMEM_SB = (BM + BN) * LDK > BM * (BN + 4) + 8 * BN ? (BM + BN) * LDK : BM * (BN + 4) + 8 * BN;
+  constexpr int SMEM = SB ? SMEM_SB : 2 * (BM + BN) * LDK;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
   constexpr int STAGE = (BM + BN) * LDK;  // floats per pipeline stage: A rows then B rows
   constexpr int LDKB = 20;                // BF: dwords per LDS row (32 bf16 + pad)
   constexpr int STAGEB = (BM + BN) * LDKB;
@@ -516,9 +526,17 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         }
         __builtin_amdgcn_s_setprio(0);
       }
-      if (more) store_tile(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
+      if constexpr (SB) {  // one stage: every wave is done reading it before the next slice lands
+        if (more) {
+          __syncthreads();
+          store_tile(0);
+        }
+        __syncthreads();
+      } else {
+        if (more) store_tile(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      }
     }
   }
   if (sk_mode == SK_PART) {  // stream-K: this block's K range of the tile, raw, one 256-B row per store
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
    if (p.epi_lds) {
     constexpr int LDT = BN + 4;
     constexpr int CB_IMG = 8;  // images per block whose counts are reduced in LDS
-    static_assert(BM * LDT + CB_IMG * BN <= 2 * (BM + BN) * LDK, "output tile must fit in the staging LDS");
+    static_assert(BM * LDT + CB_IMG * BN <= SMEM, "output tile must fit in the staging LDS");
     float* ts = smem;  // the main loop ended with a barrier
     float* cb = smem + BM * LDT;  // APoZ counts [image in block][column]
     const int b_first = m0 / p.HWo;
@@ -1475,6 +1493,13 @@ hipError_t launch_gen(const tp::ConvArgs& a, int splits, hipStream_t st) {
   }
   }
   dim3 grid(m_tiles * n_tiles, splits);
+  if constexpr (GEN == 1 && EPI == tp::EPI_FWD && KS == 1) {
+    if (a.sb) {
+      if (splits != 1) return hipErrorInvalidValue;
+      tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN, false, false, true><<<grid, NT, 0, st>>>(a);
+      return hipGetLastError();
+    }
+  }
   tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN><<<grid, NT, 0, st>>>(a);
   return hipGetLastError();
 }
@@ -1610,7 +1635,7 @@ extern "C" hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H,
 
 // M tile height of an implicit-GEMM tile config (the row count of a bnpart slab is ceil(M / it))
 extern "C" int tp_conv_tile_m(int cfg) {
-  switch (cfg & ~tp::CFG_SK) {
+  switch (cfg & ~(tp::CFG_SK | tp::CFG_SB)) {
     case 1: case 5: return 256;
     case 2: return 64;
     default: return 128;
@@ -1626,7 +1651,7 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
 // Taylor partial slots of tp_conv_gen4's ``tay_part`` for tile config cfg at Ho*Wo output pixels
 // per image; 0 = the config cannot produce them (a tile would span more than GEN_TAY_IMG images).
 extern "C" int tp_conv_gen_tay_slots(int cfg, int HWo) {
-  cfg &= ~tp::CFG_SK;
+  cfg &= ~(tp::CFG_SK | tp::CFG_SB);
   if (cfg == 4) return 0;  // its 8-wave 128x128 EPI_FWD_TAY build spills 29 VGPRs (the others do not)
   const int bm = tp_conv_tile_m(cfg);
   if (HWo <= 0 || (bm - 1) / HWo + 1 > tp::GEN_TAY_IMG) return 0;
@@ -1654,6 +1679,12 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
   using namespace tp;
   const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
   if ((gen != 2 && Cin % 32 != 0) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
+  const bool sb = cfg >= 0 && (cfg & CFG_SB);
+  if (sb) {  // single-buffered LDS stage: GEN 1 1x1 forward, one K pass, not with stream-K
+    cfg &= ~CFG_SB;
+    if (gen != 1 || ks != 1 || splits > 1 || (cfg & CFG_SK) || cfg >= CFG_WS || mask || tay_part)
+      return hipErrorInvalidValue;
+  }
   const bool sk = cfg >= 0 && (cfg & CFG_SK) && (cfg & ~CFG_SK) < CFG_WS;
   if (sk) {  // stream-K: GEN 1, one K pass, ``ws`` = the fixup slots (tp_conv_sk_ws_floats)
     cfg &= ~CFG_SK;
@@ -1719,6 +1750,7 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
     a.sk_blocks = -1;
     a.sk_ws = ws;
   }
+  a.sb = sb ? 1 : 0;
   if (a.tay_part) return gen_cfg<1, 1, EPI_FWD_TAY>(cfg, a, 1, st);
   if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);
   if (!ws) return hipErrorInvalidValue;

@@ -77,6 +77,12 @@ int main() {
          hipErrorInvalidValue);  // Cout % 4
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 5, 2, 2, 1, 16, 16, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
          hipErrorInvalidValue);  // transposed 5x5
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 3, 1, 1, 0, 0, 0, 64 | 2, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // single-buffered LDS stage: 1x1 only
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 64 | 2, 2, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // single-buffered LDS stage: one K pass
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 64 | 32 | 2, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // single-buffered LDS stage: not with stream-K
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 0, n, n, n, n, 0) ==
          hipErrorInvalidValue);  // res_stride 0
   EXPECT(tp_conv_gen2(n, n, 4096, 256, 256, 64, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==

@@ -46,7 +46,7 @@ for (B, S, C, N) in [(128, 56, 64, 256), (128, 56, 256, 64), (128, 56, 64, 64), 
     cp = timeit(lambda: y2.copy_(y))
     rd = timeit(lambda: x.sum())
     print(f"B={B} S={S} {C}->{N}: in+out {mb:.0f} MB; copy(out) {cp:.1f} us, sum(in) {rd:.1f} us", flush=True)
-    for cfg in range(7):
+    for cfg in list(range(7)) + [64 + 2, 64 + 3, 64 + 6]:  # 64 + c: single-buffered LDS stage (CFG_SB)
         try:
             t0 = timeit(lambda: T.conv_gen(x, w, None, None, False, None, None, 1, 1, 0, cfg, 1))
             t1 = timeit(lambda: T.conv_gen_stats(x, w, None, 1, 1, 0, cfg))

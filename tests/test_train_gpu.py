@@ -506,3 +506,25 @@ def test_pack_cache_follows_optimizer_steps(cuda, kind):
     assert runs[0][-1] < runs[0][0]
     for a, b in zip(*runs):
         assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), runs
+
+
+@pytest.mark.parametrize("B,S,C,N,stride", [(4, 14, 64, 256, 1), (3, 28, 128, 64, 2), (2, 7, 256, 96, 1)])
+def test_single_stage_lds_gemm_matches(cuda, B, S, C, N, stride):
+    """cfg | CFG_SB (one LDS stage, short-K 1x1 forward) == the double-buffered kernel bit for bit
+    (same MFMA order), with and without the BN-statistics epilogue; vs fp64 as well."""
+    from torchpruner_amd import ops
+    from torchpruner_amd.engine.fused_chain import CFG_SB
+    T = ops.require()
+    torch.manual_seed(0)
+    x = torch.randn(B, S, S, C, device=cuda)
+    w = torch.randn(N, T.conv_gen_k(1, C), device=cuda) * 0.1
+    shift = torch.randn(N, device=cuda)
+    ref = torch.einsum("bhwc,nc->bhwn", x[:, ::stride, ::stride].double(), w[:, :C].double()) + shift.double()
+    for c in (2, 3, 4, 6):
+        y0 = T.conv_gen(x, w, None, shift, False, None, None, 1, stride, 0, c, 1)
+        y1 = T.conv_gen(x, w, None, shift, False, None, None, 1, stride, 0, CFG_SB | c, 1)
+        assert torch.equal(y0, y1), c
+        torch.testing.assert_close(y1.double(), ref, rtol=1e-4, atol=1e-4)
+        s0, p0 = T.conv_gen_stats(x, w, shift, 1, stride, 0, c)
+        s1, p1 = T.conv_gen_stats(x, w, shift, 1, stride, 0, CFG_SB | c)
+        assert torch.equal(s0, s1) and torch.equal(p0, p1), c

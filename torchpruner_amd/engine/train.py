@@ -38,7 +38,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from . import epochs
-from .fused_chain import _CU, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, sk_candidates
+from .fused_chain import _CU, CFG_SB, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, sk_candidates
 from .resnet_engine import wino4_cands
 
 
@@ -218,6 +218,8 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
     cands = TUNER.candidates(M, cout_p, kk)
     if cin_p != 4:
         cands = cands + sk_candidates(T, cands, ks, M, cout_p)
+    if ks == 1 and cin_p % 32 == 0 and kk <= 256:  # short K: the single-buffered LDS stage (2x blocks per CU)
+        cands = cands + [(CFG_SB | c, 1) for c in (2, 3, 6)]
     if wino:
         sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cout_p, cin_p)
         cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
