@@ -1682,7 +1682,7 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
   const bool sb = cfg >= 0 && (cfg & CFG_SB);
   if (sb) {  // single-buffered LDS stage: GEN 1 1x1 forward, one K pass, not with stream-K
     cfg &= ~CFG_SB;
-    if (gen != 1 || ks != 1 || splits > 1 || (cfg & CFG_SK) || cfg >= CFG_WS || mask || tay_part)
+    if (gen != 1 || ks != 1 || splits > 1 || (cfg & CFG_SK) || cfg >= CFG_WS || tay_part)
       return hipErrorInvalidValue;
   }
   const bool sk = cfg >= 0 && (cfg & CFG_SK) && (cfg & ~CFG_SK) < CFG_WS;

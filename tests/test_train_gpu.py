@@ -528,3 +528,14 @@ def test_single_stage_lds_gemm_matches(cuda, B, S, C, N, stride):
         s0, p0 = T.conv_gen_stats(x, w, shift, 1, stride, 0, c)
         s1, p1 = T.conv_gen_stats(x, w, shift, 1, stride, 0, CFG_SB | c)
         assert torch.equal(s0, s1) and torch.equal(p0, p1), c
+        if stride == 1:  # the data gradient with the ReLU mask of the input activation
+            g = torch.randn(B, S, S, N, device=cuda)
+            wt = w[:, :C].t().contiguous()
+            if wt.shape[1] % 32:
+                wt = F.pad(wt, (0, 32 - wt.shape[1] % 32))
+            gp = F.pad(g, (0, wt.shape[1] - N))
+            d0 = T.conv_gen_bwd(gp, wt, None, 1, x, 1, 1, 0, S, S, False, c, 1, None, 0)
+            d1 = T.conv_gen_bwd(gp, wt, None, 1, x, 1, 1, 0, S, S, False, CFG_SB | c, 1, None, 0)
+            assert torch.equal(d0, d1), c
+            dref = torch.einsum("bhwn,nc->bhwc", g.double(), w[:, :C].double()) * (x > 0)
+            torch.testing.assert_close(d1.double(), dref, rtol=1e-4, atol=1e-4)

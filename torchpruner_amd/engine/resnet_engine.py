@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from . import epochs
-from .fused_chain import (_CU, _W4_SPLITS, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, logits_grad,
+from .fused_chain import (_CU, _W4_SPLITS, CFG_SB, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, logits_grad,
                           sk_candidates, taylor_slots, winograd_weights)
 
 _W4_SIZES = (56, 28, 14, 7, 32, 16, 8, 4)  # square maps of the F(4x4) kernel (band geometry for the first four)
@@ -234,6 +234,8 @@ class ResNetEngine:
         cands = TUNER.candidates(M, N, K)
         if C != 4:
             cands = cands + sk_candidates(T, cands, ks, M, N)
+            if ks == 1 and K <= 256:  # short K: the single-buffered LDS stage (twice the blocks per CU)
+                cands = cands + [(CFG_SB | c, 1) for c in (2, 3, 6)]
         if "u" in e and res is None:  # odd H / W: partial last tile row / column (direct loads)
             sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)
             cands = [(WINO_LDS, sp0), (WINO, sp0)] + ([(WINO_LDS, 1)] if sp0 > 1 else []) + cands
@@ -412,6 +414,8 @@ class ResNetEngine:
         else:
             cands = TUNER.candidates(M, N, K)
             cands = cands + sk_candidates(T, cands, ks, M, N, tay=False)
+            if ks == 1 and K <= 256:
+                cands = cands + [(CFG_SB | c, 1) for c in (2, 3, 6)]
         wino_ok = "ut" in e and res is None and mask is not None
         if wino_ok:
             sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), N, C)
@@ -423,7 +427,8 @@ class ResNetEngine:
         # 1x1 dgrads with fused Taylor partials: one K pass, tiles spanning <= 4 images
         gen_tay = tay_mode is not None and ks == 1 and not transposed and mask is not None and res is None
         if gen_tay:
-            cands = list(dict.fromkeys((c, 1) for c, _ in cands if c >= 0 and T.conv_gen_tay_slots(c, Ho * Wo) > 0))
+            cands = list(dict.fromkeys((c, 1) for c, _ in cands
+                                       if c >= 0 and not c & CFG_SB and T.conv_gen_tay_slots(c, Ho * Wo) > 0))
             key = key + ("tay",)
             gen_tay = bool(cands)
 

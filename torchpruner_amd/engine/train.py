@@ -286,6 +286,8 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
     cands = TUNER.candidates(M, cin_p, K) if not transposed else [(c, 1) for c in (0, 3, 4, 1, 5, 6, 2)]
     if not transposed:
         cands = cands + sk_candidates(T, cands, ks, M, cin_p)
+        if ks == 1 and K <= 256:  # short K: the single-buffered LDS stage
+            cands = cands + [(CFG_SB | c, 1) for c in (2, 3, 6)]
     if wino:
         cands = [(WINO_LDS, _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cin_p, cout_p)), (WINO, 1)] + cands
         if H == W:
