@@ -208,7 +208,8 @@ template <int BM, int BN, int WM, int WN, int KS, bool POOLED_M, bool UNPOOL, in
 __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, WM, WN) / 128) void conv_igemm(ConvArgs p) {
   using T = Tile<BM, BN, WM, WN>;
   constexpr int BK = T::BK, LDK = T::LDK;
-  static_assert(!SB || (GEN == 1 && !BF && !SK && EPI == EPI_FWD), "single-buffered LDS: GEN 1 forward only");
+  static_assert(!SB || (GEN == 1 && !BF && !SK && (EPI == EPI_FWD || EPI == EPI_FWD_TAY)),
+                "single-buffered LDS: GEN 1 forward / Taylor-partial data gradient only");
   constexpr int SMEM_SB = (BM + BN) * LDK > BM * (BN + 4) + 8 * BN ? (BM + BN) * LDK : BM * (BN + 4) + 8 * BN;
   constexpr int SMEM = SB ? SMEM_SB : 2 * (BM + BN) * LDK;
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
@@ -1493,7 +1494,7 @@ hipError_t launch_gen(const tp::ConvArgs& a, int splits, hipStream_t st) {
   }
   }
   dim3 grid(m_tiles * n_tiles, splits);
-  if constexpr (GEN == 1 && EPI == tp::EPI_FWD && KS == 1) {
+  if constexpr (GEN == 1 && (EPI == tp::EPI_FWD || EPI == tp::EPI_FWD_TAY) && KS == 1) {
     if (a.sb) {
       if (splits != 1) return hipErrorInvalidValue;
       tp::conv_igemm<BM, BN, WM, WN, KS, false, false, EPI, GEN, false, false, true><<<grid, NT, 0, st>>>(a);
@@ -1682,7 +1683,7 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
   const bool sb = cfg >= 0 && (cfg & CFG_SB);
   if (sb) {  // single-buffered LDS stage: GEN 1 1x1 forward, one K pass, not with stream-K
     cfg &= ~CFG_SB;
-    if (gen != 1 || ks != 1 || splits > 1 || (cfg & CFG_SK) || cfg >= CFG_WS || tay_part)
+    if (gen != 1 || ks != 1 || splits > 1 || (cfg & CFG_SK) || cfg >= CFG_WS)
       return hipErrorInvalidValue;
   }
   const bool sk = cfg >= 0 && (cfg & CFG_SK) && (cfg & ~CFG_SK) < CFG_WS;

@@ -539,3 +539,12 @@ def test_single_stage_lds_gemm_matches(cuda, B, S, C, N, stride):
             assert torch.equal(d0, d1), c
             dref = torch.einsum("bhwn,nc->bhwc", g.double(), w[:, :C].double()) * (x > 0)
             torch.testing.assert_close(d1.double(), dref, rtol=1e-4, atol=1e-4)
+            R = T.conv_gen_tay_slots(c, S * S)
+            if R > 0:  # Taylor partials of the activation (the ResNet engine's 1x1 data gradients)
+                t0 = torch.zeros(R, B, C, device=cuda)
+                t1 = torch.zeros(R, B, C, device=cuda)
+                e0 = T.conv_gen_bwd(gp, wt, None, 1, x, 1, 1, 0, S, S, False, c, 1, t0, 0)
+                e1 = T.conv_gen_bwd(gp, wt, None, 1, x, 1, 1, 0, S, S, False, CFG_SB | c, 1, t1, 0)
+                assert torch.equal(e0, e1) and torch.equal(t0, t1), c
+                tref = (-(dref * x.double())).sum((1, 2))
+                torch.testing.assert_close(t1.double().sum(0), tref, rtol=1e-3, atol=1e-3)

@@ -427,8 +427,7 @@ class ResNetEngine:
         # 1x1 dgrads with fused Taylor partials: one K pass, tiles spanning <= 4 images
         gen_tay = tay_mode is not None and ks == 1 and not transposed and mask is not None and res is None
         if gen_tay:
-            cands = list(dict.fromkeys((c, 1) for c, _ in cands
-                                       if c >= 0 and not c & CFG_SB and T.conv_gen_tay_slots(c, Ho * Wo) > 0))
+            cands = list(dict.fromkeys((c, 1) for c, _ in cands if c >= 0 and T.conv_gen_tay_slots(c, Ho * Wo) > 0))
             key = key + ("tay",)
             gen_tay = bool(cands)
 
