@@ -466,9 +466,12 @@ def _b100(args, model, task, convs, dev, world, rank, timed_run, log, loader):
             bs = torch.utils.data.BatchSampler(torch.utils.data.SequentialSampler(ds), sb, drop_last=False)
             dl = torch.utils.data.DataLoader(ds, sampler=bs, batch_size=None, num_workers=1, pin_memory=True,
                                              persistent_workers=True)
-        TaylorAttributionMetric(model, dl, F.cross_entropy, dev).run_many(
+        # the DataLoader already holds only this rank's batches (i = rank, rank + world, ...): no
+        # second sharding inside run_many (shard_data=False: each rank scores its own loader, no
+        # collective; with the default sharding each rank would process only 1/world of its loader)
+        TaylorAttributionMetric(model, dl, F.cross_entropy, dev, shard_data=False).run_many(
             convs, find_best_evaluation_module=True)  # warm (and, persistent, the worker's fork)
-        hm = TaylorAttributionMetric(model, dl, F.cross_entropy, dev)
+        hm = TaylorAttributionMetric(model, dl, F.cross_entropy, dev, shard_data=False)
         _, hdt = timed_run(hm, convs)
         assert hm.last_path["path"] == "fused", hm.last_path
         host[kind] = (round(s_steps * sb * world / hdt, 1), hm.last_coalesce)

@@ -80,14 +80,17 @@ hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int
                         float* apoz, float* out, float* ws, double* bnpart, float* tay_part, int tay_mode,
                         hipStream_t st);
 int tp_conv_gen_tay_slots(int cfg, int HWo);
-hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
-                               float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
-                               float* b, double* ws, const double* pre, int G, const float* res, int relu, uint8_t* mko,
-                               long long* nbt, hipStream_t st);
-hipError_t tp_bn_fwd_train4(const float* x, float* y, int P, int C, const float* gamma, const float* beta, float eps,
-                            float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* a,
-                            float* b, double* ws, const float* res, int relu, uint8_t* mko, long long* nbt,
+hipError_t tp_bn_fwd_train_pre2(const float* x, float* y, int P, int C, int Cr, const float* gamma,
+                                const float* beta, float eps, float momentum, float* run_mean, float* run_var,
+                                float* mean, float* invstd, float* a, float* b, double* ws, const double* pre, int G,
+                                const float* res, int relu, uint8_t* mko, long long* nbt, hipStream_t st);
+hipError_t tp_bn_fwd_train5(const float* x, float* y, int P, int C, int Cr, const float* gamma, const float* beta,
+                            float eps, float momentum, float* run_mean, float* run_var, float* mean, float* invstd,
+                            float* a, float* b, double* ws, const float* res, int relu, uint8_t* mko, long long* nbt,
                             hipStream_t st);
+hipError_t tp_bn_bwd_train4(const float* g, const float* x, float* dx, int P, int C, int Cr, const float* gamma,
+                            const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a, float* k1,
+                            float* k2, double* ws, const float* ym, float* dres, const uint8_t* mk, hipStream_t st);
 hipError_t tp_conv_wgrad2(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                           int ks, int stride, int pad, int Kpad, int cfg, int splits, float* fin, int fin_co,
                           int fin_ci, const long long* fs, hipStream_t st);
@@ -103,6 +106,10 @@ int tp_wino4_u_img();
 int tp_wino4_ok(int H, int W, int C, int K);
 int tp_wino4_taylor_slots(int S);
 int tp_wino4_lds_bytes(int S, int variant);
+hipError_t tp_conv_wino4_ko(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
+                           const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
+                           float* taylor, float* apoz, int tay_mode, int splits, float* ws, int variant,
+                           hipStream_t st, const uint8_t* unpool_am, int ko);
 hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
                          const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act, float* taylor,
                          float* apoz, int tay_mode, int splits, float* ws, int variant, hipStream_t st,
@@ -578,13 +585,17 @@ std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at:
                                                   const c10::optional<at::Tensor>& scale,
                                                   const c10::optional<at::Tensor>& shift, bool relu, bool pool,
                                                   const c10::optional<at::Tensor>& apoz, int64_t splits,
-                                                  int64_t variant) {
+                                                  int64_t variant, int64_t ko) {
   need(x, "x", 4);
-  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = u.size(1) * 32;
-  need_u4(u, C, K);
-  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)C, (int)K), "F(4x4) Winograd needs square 4/8/16/32 (or, split-points "
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), Kc = u.size(1) * 32;
+  need_u4(u, C, Kc);
+  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)C, (int)Kc), "F(4x4) Winograd needs square 4/8/16/32 (or, split-points "
               "variant 3 without pooling, 56/28/14/7) maps, C % 8 == 0, "
-              "K % 32 == 0; got ", x.sizes(), " K=", K);
+              "K % 32 == 0; got ", x.sizes(), " K=", Kc);
+  // ko: stored output channels (pruned widths: the U images / MFMAs are 32-padded, HBM rows are not)
+  const int64_t K = ko > 0 ? ko : Kc;
+  TORCH_CHECK(K % 4 == 0 && K <= Kc && K > Kc - 32, "ko must be a multiple of 4 in (K - 32, K]; got ko=", ko, " K=", Kc);
+  TORCH_CHECK(K == Kc || splits <= 1, "ko < K needs one K pass (splits=1)");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
   const float* sc = opt_ptr(scale, K, "scale");
   const float* sh = opt_ptr(shift, K, "shift");
@@ -604,10 +615,10 @@ std::tuple<at::Tensor, at::Tensor> conv_wino4_fwd(const at::Tensor& x, const at:
   const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, C / 8));
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * H * W * K}, x.options());
-  TP_CHECK_HIP(tp_conv_wino4(x.data_ptr<float>(), u.data_ptr<float>(), (int)B, (int)H, (int)C, (int)K,
-                             pool ? EPI_FWD_POOL : EPI_FWD, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
-                             pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap, 0, (int)sp,
-                             sp > 1 ? ws.data_ptr<float>() : nullptr, (int)variant, cur_stream(), nullptr));
+  TP_CHECK_HIP(tp_conv_wino4_ko(x.data_ptr<float>(), u.data_ptr<float>(), (int)B, (int)H, (int)C, (int)Kc,
+                                pool ? EPI_FWD_POOL : EPI_FWD, sc, sh, relu ? 1 : 0, out.data_ptr<float>(),
+                                pool ? am.data_ptr<uint8_t>() : nullptr, nullptr, nullptr, ap, 0, (int)sp,
+                                sp > 1 ? ws.data_ptr<float>() : nullptr, (int)variant, cur_stream(), nullptr, (int)K));
   return {out, am};
 }
 
@@ -620,10 +631,14 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
                             const c10::optional<at::Tensor>& unpool_am) {
   need(g, "g", 4);
   need(act, "act", 4);
+  // Cin: the stored input-gradient channels (act's width); the U images cover Cin rounded up to 32
   const int64_t B = act.size(0), H = act.size(1), W = act.size(2), Cin = act.size(3), Cout = g.size(3);
-  need_u4(ut, Cout, Cin);
+  const int64_t Kc = ut.dim() == 3 ? ut.size(1) * 32 : 0;
+  need_u4(ut, Cout, Kc);
+  TORCH_CHECK(Cin % 4 == 0 && Cin <= Kc && Cin > Kc - 32, "act width must be the U images' output width up to its "
+              "32-granule; got ", Cin, " vs ", Kc);
   TORCH_CHECK(g.size(0) == B && g.size(1) == H && g.size(2) == W, "grad shape mismatch");
-  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)Cout, (int)Cin), "F(4x4) dgrad needs square 4/8/16/32/56/28/14/7 maps, "
+  TORCH_CHECK(tp_wino4_ok((int)H, (int)W, (int)Cout, (int)Kc), "F(4x4) dgrad needs square 4/8/16/32/56/28/14/7 maps, "
               "Cout % 8 == 0, Cin % 32 == 0");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
   const float* sc = opt_ptr(bn_scale, Cin, "bn_scale");
@@ -636,6 +651,7 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
     tay = taylor->data_ptr<float>();
   }
   const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(splits, Cout / 8));
+  TORCH_CHECK(Cin == Kc || sp == 1, "an unpadded output width needs one K pass (splits=1)");
   const uint8_t* unp = nullptr;
   if (unpool_am.has_value() && unpool_am->defined()) {
     const auto& m = *unpool_am;
@@ -649,10 +665,10 @@ at::Tensor conv_wino4_dgrad(const at::Tensor& g, const at::Tensor& ut, const at:
   if (want_out) out = unp ? at::empty({B, 2 * H, 2 * W, Cin}, g.options()) : at::empty({B, H, W, Cin}, g.options());
   at::Tensor ws;
   if (sp > 1) ws = at::empty({sp * B * H * W * Cin}, g.options());
-  TP_CHECK_HIP(tp_conv_wino4(g.data_ptr<float>(), ut.data_ptr<float>(), (int)B, (int)H, (int)Cout, (int)Cin, EPI_BWD,
-                             sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr, act.data_ptr<float>(),
-                             tay, nullptr, (int)tay_mode, (int)sp, sp > 1 ? ws.data_ptr<float>() : nullptr,
-                             (int)variant, cur_stream(), unp));
+  TP_CHECK_HIP(tp_conv_wino4_ko(g.data_ptr<float>(), ut.data_ptr<float>(), (int)B, (int)H, (int)Cout, (int)Kc,
+                                EPI_BWD, sc, nullptr, 0, want_out ? out.data_ptr<float>() : nullptr, nullptr,
+                                act.data_ptr<float>(), tay, nullptr, (int)tay_mode, (int)sp,
+                                sp > 1 ? ws.data_ptr<float>() : nullptr, (int)variant, cur_stream(), unp, (int)Cin));
   return out;
 }
 
@@ -682,8 +698,9 @@ at::Tensor conv_gen(const at::Tensor& x, const at::Tensor& w, const c10::optiona
   need(x, "x", 4);
   need(w, "w", 2);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
-  TORCH_CHECK((Cin % 32 == 0 && (ks == 1 || ks == 3 || ks == 5)) || (Cin == 4 && (ks == 3 || ks == 5 || ks == 7)),
-              "conv_gen supports ks 1/3/5 with Cin % 32 == 0, or ks 3/5/7 with a 4-channel input");
+  TORCH_CHECK((Cin % 4 == 0 && Cin >= 8 && (ks == 1 || ks == 3 || ks == 5)) ||
+                  (Cin == 4 && (ks == 3 || ks == 5 || ks == 7)),
+              "conv_gen supports ks 1/3/5 with Cin % 4 == 0 (>= 8), or ks 3/5/7 with a 4-channel input");
   TORCH_CHECK(w.size(1) == tp_conv_gen_k((int)ks, (int)Cin), "weight K mismatch");
   TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
   TORCH_CHECK(Cout % 4 == 0, "conv_gen needs Cout % 4 == 0");
@@ -798,9 +815,9 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
   need(g, "g", 4);
   need(wt, "wt", 2);
   const int64_t B = g.size(0), H = g.size(1), W = g.size(2), C = g.size(3), N = wt.size(0);
-  TORCH_CHECK(C % 32 == 0 && (ks == 1 || ks == 3 || (ks == 5 && !transposed)),
-              "conv_gen_bwd needs C % 32 == 0 and ks 1/3 (5 for stride-1 convs)");
-  TORCH_CHECK(wt.size(1) == ks * ks * C, "wt must be (N, ks*ks*C)");
+  TORCH_CHECK(C % 4 == 0 && C >= 8 && (ks == 1 || ks == 3 || (ks == 5 && !transposed)),
+              "conv_gen_bwd needs C % 4 == 0 (>= 8) and ks 1/3 (5 for stride-1 convs)");
+  TORCH_CHECK(wt.size(1) == tp_conv_gen_k((int)ks, (int)C), "wt must be (N, ks*ks*ceil32(C))");
   TORCH_CHECK(N % 4 == 0 && res_stride >= 1 && stride >= 1 && pad >= 0, "bad N/stride/pad");
   if (!transposed) {
     TORCH_CHECK(stride == 1, "non-transposed conv_gen_bwd is stride 1");
@@ -921,8 +938,9 @@ std::tuple<at::Tensor, at::Tensor> conv_gen_stats(const at::Tensor& x, const at:
   need(x, "x", 4);
   need(w, "w", 2);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
-  TORCH_CHECK((Cin % 32 == 0 && (ks == 1 || ks == 3 || ks == 5)) || (Cin == 4 && (ks == 3 || ks == 5 || ks == 7)),
-              "conv_gen_stats supports ks 1/3/5 with Cin % 32 == 0, or ks 3/5/7 with a 4-channel input");
+  TORCH_CHECK((Cin % 4 == 0 && Cin >= 8 && (ks == 1 || ks == 3 || ks == 5)) ||
+                  (Cin == 4 && (ks == 3 || ks == 5 || ks == 7)),
+              "conv_gen_stats supports ks 1/3/5 with Cin % 4 == 0 (>= 8), or ks 3/5/7 with a 4-channel input");
   TORCH_CHECK(w.size(1) == tp_conv_gen_k((int)ks, (int)Cin), "weight K mismatch");
   TORCH_CHECK(stride >= 1 && pad >= 0 && Cout % 4 == 0, "bad geometry / Cout % 4");
   const int64_t Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
@@ -969,26 +987,31 @@ void wino_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t cfg, int64_t s
 // Updates running_mean / running_var in place (momentum, unbiased variance) when given.
 // Training BN on (.., C) channels-last data; optional fused residual add and ReLU:
 // y = relu?(BN(x) + res?). Returns (y, mean, invstd).
-// With ``relu`` also returns the ReLU bit mask (P*C/4 bytes; else an empty tensor) for bn_train_bwd.
+// With ``relu`` also returns the ReLU bit mask (ceil(P*C/4) bytes; else an empty tensor) for bn_train_bwd.
+// Any C (C % 4 == 0: float4 rows; else per-element). ``cr`` (0 = C): the channels with parameters /
+// running statistics; x's channels c >= cr are the zero padding of a pruned width (outputs 0).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                                              const c10::optional<at::Tensor>& beta,
                                                              const c10::optional<at::Tensor>& running_mean,
                                                              const c10::optional<at::Tensor>& running_var, double eps,
                                                              double momentum, const c10::optional<at::Tensor>& res,
                                                              bool relu, const c10::optional<at::Tensor>& pre,
-                                                             const c10::optional<at::Tensor>& num_batches) {
+                                                             const c10::optional<at::Tensor>& num_batches,
+                                                             int64_t cr) {
   need(x, "x", -1);
   const int64_t C = x.size(-1), P = x.numel() / std::max<int64_t>(C, 1);
-  TORCH_CHECK(C % 4 == 0 && P > 0, "bn_train_fwd needs C % 4 == 0 and a non-empty batch");
+  TORCH_CHECK(C > 0 && P > 0, "bn_train_fwd needs a non-empty batch");
+  const int64_t Cr = cr > 0 ? cr : C;
+  TORCH_CHECK(Cr <= C, "cr must be <= the channel count");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  const float* ga = opt_ptr(gamma, C, "gamma");
-  const float* be = opt_ptr(beta, C, "beta");
+  const float* ga = opt_ptr(gamma, Cr, "gamma");
+  const float* be = opt_ptr(beta, Cr, "beta");
   float* rm = nullptr;
   float* rv = nullptr;
   if (running_mean.has_value() && running_mean->defined()) {
     need(*running_mean, "running_mean", 1);
     need(*running_var, "running_var", 1);
-    TORCH_CHECK(running_mean->numel() == C && running_var->numel() == C, "running stats must have C elements");
+    TORCH_CHECK(running_mean->numel() == Cr && running_var->numel() == Cr, "running stats must have cr elements");
     rm = running_mean->data_ptr<float>();
     rv = running_var->data_ptr<float>();
   }
@@ -1005,8 +1028,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
     nbt = reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>());
   }
   auto y = at::empty_like(x);
-  auto mk = at::empty({relu ? P * C / 4 : 0}, x.options().dtype(at::kByte));
-  auto stats = at::empty({4, C}, x.options());  // mean, invstd, a, b
+  auto mk = at::empty({relu ? (P * C + 3) / 4 : 0}, x.options().dtype(at::kByte));
+  const int64_t Cs = (C + 3) / 4 * 4;  // row stride: every row 16-byte aligned (float4 reads) for any C
+  auto stats = at::empty({4, Cs}, x.options()).narrow(1, 0, C);  // mean, invstd, a, b
   float* sp = stats.data_ptr<float>();
   if (pre.has_value() && pre->defined()) {  // statistics reduced per tile by the producing conv
     TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kDouble && pre->is_contiguous() && pre->dim() == 3 &&
@@ -1014,15 +1038,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
                 "pre must be conv_gen_stats' (G, 2, C) fp64 tile statistics");
     const int64_t G = pre->size(0);
     auto ws = at::empty({2 * std::min<int64_t>(G, 256) * C}, x.options().dtype(at::kDouble));
-    TP_CHECK_HIP(tp_bn_fwd_train_pre(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
-                                     (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(),
+    TP_CHECK_HIP(tp_bn_fwd_train_pre2(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, (int)Cr, ga, be, (float)eps,
+                                     (float)momentum, rm, rv, sp, sp + Cs, sp + 2 * Cs, sp + 3 * Cs, ws.data_ptr<double>(),
                                      pre->data_ptr<double>(), (int)G, rp, relu ? 1 : 0,
                                      relu ? mk.data_ptr<uint8_t>() : nullptr, nbt, cur_stream()));
     return {y, stats[0], stats[1], mk};
   }
   auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
-  TP_CHECK_HIP(tp_bn_fwd_train4(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, ga, be, (float)eps,
-                                (float)momentum, rm, rv, sp, sp + C, sp + 2 * C, sp + 3 * C, ws.data_ptr<double>(), rp,
+  TP_CHECK_HIP(tp_bn_fwd_train5(x.data_ptr<float>(), y.data_ptr<float>(), (int)P, (int)C, (int)Cr, ga, be, (float)eps,
+                                (float)momentum, rm, rv, sp, sp + Cs, sp + 2 * Cs, sp + 3 * Cs, ws.data_ptr<double>(), rp,
                                 relu ? 1 : 0, relu ? mk.data_ptr<uint8_t>() : nullptr, nbt, cur_stream()));
   return {y, stats[0], stats[1], mk};
 }
@@ -1033,14 +1057,16 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
     const at::Tensor& g, const at::Tensor& x, const c10::optional<at::Tensor>& gamma, const at::Tensor& mean,
     const at::Tensor& invstd, bool want_dx, const c10::optional<at::Tensor>& ym, bool want_dres,
-    const c10::optional<at::Tensor>& mask) {
+    const c10::optional<at::Tensor>& mask, int64_t cr) {
   need(g, "g", -1);
   need(x, "x", -1);
   TORCH_CHECK(g.sizes() == x.sizes(), "g and x must have the same shape");
   const int64_t C = x.size(-1), P = x.numel() / std::max<int64_t>(C, 1);
-  TORCH_CHECK(C % 4 == 0 && P > 0, "bn_train_bwd needs C % 4 == 0");
+  TORCH_CHECK(C > 0 && P > 0, "bn_train_bwd needs a non-empty batch");
+  const int64_t Cr = cr > 0 ? cr : C;
+  TORCH_CHECK(Cr <= C, "cr must be <= the channel count");
   at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  const float* ga = opt_ptr(gamma, C, "gamma");
+  const float* ga = opt_ptr(gamma, Cr, "gamma");
   const float* mp = opt_ptr(mean, C, "mean");
   const float* ip = opt_ptr(invstd, C, "invstd");
   const float* yp = nullptr;
@@ -1052,21 +1078,22 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
   const uint8_t* mkp = nullptr;
   if (mask.has_value() && mask->defined() && mask->numel() > 0) {
     TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
-                    mask->numel() == P * C / 4 && mask->device() == x.device(),
-                "mask must be bn_train_fwd's ReLU bit mask (P*C/4 uint8)");
+                    mask->numel() == (P * C + 3) / 4 && mask->device() == x.device(),
+                "mask must be bn_train_fwd's ReLU bit mask (ceil(P*C/4) uint8)");
     mkp = mask->data_ptr<uint8_t>();
   }
-  auto coef = at::empty({5, C}, x.options());  // dgamma, dbeta, a, k1, k2
+  const int64_t Cs = (C + 3) / 4 * 4;
+  auto coef = at::empty({5, Cs}, x.options());  // dgamma, dbeta, a, k1, k2 (16-byte aligned rows)
   auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   at::Tensor dx, dres;
   if (want_dx) dx = at::empty_like(x);
   if (want_dres) dres = at::empty_like(x);
   float* cp = coef.data_ptr<float>();
-  TP_CHECK_HIP(tp_bn_bwd_train3(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
-                                (int)P, (int)C, ga, mp, ip, cp, cp + C, cp + 2 * C, cp + 3 * C, cp + 4 * C,
+  TP_CHECK_HIP(tp_bn_bwd_train4(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
+                                (int)P, (int)C, (int)Cr, ga, mp, ip, cp, cp + Cs, cp + 2 * Cs, cp + 3 * Cs, cp + 4 * Cs,
                                 ws.data_ptr<double>(), mkp ? nullptr : yp, want_dres ? dres.data_ptr<float>() : nullptr,
                                 mkp, cur_stream()));
-  return {dx, coef[0], coef[1], dres};
+  return {dx, coef[0].narrow(0, 0, Cr), coef[1].narrow(0, 0, Cr), dres};
 }
 
 void register_engine_ops_def(torch::Library& m) {
@@ -1087,9 +1114,9 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_gen_k(int ks, int Cin) -> int", &conv_gen_k);
   m.def("bn_train_fwd(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float eps, float momentum, Tensor? res=None, bool relu=False, Tensor? pre=None, "
-        "Tensor(c!)? num_batches=None) -> (Tensor, Tensor, Tensor, Tensor)");
+        "Tensor(c!)? num_batches=None, int cr=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx, Tensor? ym=None, "
-        "bool want_dres=False, Tensor? mask=None) -> (Tensor, Tensor, Tensor, Tensor)");
+        "bool want_dres=False, Tensor? mask=None, int cr=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "
         "-> Tensor");
   m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");
@@ -1116,7 +1143,7 @@ void register_engine_ops_def(torch::Library& m) {
         "Tensor(a!)? taylor, bool want_out, int splits, bool staged=True, int tay_mode=0) -> Tensor");
   m.def("wino4_weights(Tensor w, bool flip_t, int K=0, int C=0) -> Tensor");
   m.def("conv_wino4_fwd(Tensor x, Tensor u, Tensor? scale, Tensor? shift, bool relu, bool pool, "
-        "Tensor(a!)? apoz=None, int splits=1, int variant=0) -> (Tensor, Tensor)");
+        "Tensor(a!)? apoz=None, int splits=1, int variant=0, int ko=0) -> (Tensor, Tensor)");
   m.def("conv_wino4_dgrad(Tensor g, Tensor ut, Tensor act, Tensor? bn_scale, Tensor(a!)? taylor, bool want_out, "
         "int tay_mode=0, int splits=1, int variant=0, Tensor? unpool_am=None) -> Tensor");
 }

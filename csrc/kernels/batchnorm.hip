@@ -2,7 +2,11 @@
 // normalisation and the backward pass of the finetune loop, deterministic (fixed-order
 // two-level reductions, no atomics).
 //
-//   x: P rows (= B*H*W pixels) x C channels, C % 4 == 0
+//   x: P rows (= B*H*W pixels) x C channels. C % 4 == 0: float4 rows (V4); any other C (pruned
+//      widths left unpadded): the same kernels with per-element loads (scalar tail per row)
+//   Cr <= C: channels carrying parameters (gamma / beta / running statistics); channels c >= Cr
+//      are the zero padding of a pruned width carried at the kernels' granule: a = b = 0 there,
+//      so they stay exact zeros forward and backward, and no statistic is written for them
 //   stats   : partial[g][0|1][c] = sum / sum of squares over row group g  (pass 1)
 //             finalize: mean, biased var -> invstd, running-stat update  (pass 2, fp64)
 //   forward : y = x * a[c] + b[c],  a = gamma * invstd, b = beta - mean * a
@@ -22,6 +26,8 @@ constexpr int BN_T = 256, BN_CQ = 16, BN_RL = BN_T / BN_CQ;  // 16 column quads 
 // is g where y > 0 and 0 elsewhere (NaN y -> 0, as the ATen threshold backward)
 // or, cheaper, by the forward's ReLU bit mask mk (one byte per 4 channels, bit q = y[c+q] > 0:
 // 1/16 of the bytes of reading y back)
+// The ReLU bit mask: byte i holds flat elements 4i..4i+3 of the (P, C) activation (bit q = element
+// 4i + q > 0) — for C % 4 == 0 that is "byte p*C/4 + c/4, bit = c % 4".
 __device__ __forceinline__ float4 relu_mask4(float4 d, const float* ym, size_t off, const uint8_t* mk = nullptr) {
   if (mk) {
     const unsigned m = mk[off >> 2];
@@ -32,7 +38,31 @@ __device__ __forceinline__ float4 relu_mask4(float4 d, const float* ym, size_t o
   return make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f, m.w > 0.f ? d.w : 0.f);
 }
 
-template <int MODE>
+// 4 channels c..c+3 of row r: one float4 (V4) or per-element loads guarded by c + q < C
+template <bool V4>
+__device__ __forceinline__ float4 ld4(const float* __restrict__ t, size_t row_off, int c, int C) {
+  if (V4) return *reinterpret_cast<const float4*>(t + row_off + c);
+  const float* q = t + row_off + c;
+  return make_float4(q[0], c + 1 < C ? q[1] : 0.f, c + 2 < C ? q[2] : 0.f, c + 3 < C ? q[3] : 0.f);
+}
+// relu_mask4 for any C: element e = off + q reads bit (e & 3) of byte e >> 2
+template <bool V4>
+__device__ __forceinline__ float4 relu_mask4g(float4 d, const float* ym, size_t off, const uint8_t* mk, int c, int C) {
+  if (V4) return relu_mask4(d, ym, off, mk);
+  float v[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const size_t e = off + q;
+    bool keep = true;
+    if (c + q >= C) keep = false;
+    else if (mk) keep = (mk[e >> 2] >> (e & 3)) & 1u;
+    else if (ym) keep = ym[e] > 0.f;
+    v[q] = keep ? v[q] : 0.f;
+  }
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <int MODE, bool V4 = true>
 __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, const float* __restrict__ g,
                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
                                                    double* __restrict__ part, int P, int C, int rows_per_group,
@@ -46,8 +76,8 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
   if (c < C) {
     float4 mu = s0, is = s0;
     if (MODE == 1) {
-      mu = *reinterpret_cast<const float4*>(mean + c);
-      is = *reinterpret_cast<const float4*>(invstd + c);
+      mu = ld4<V4>(mean, 0, c, C);
+      is = ld4<V4>(invstd, 0, c, C);
     }
     // 4 independent rows per iteration: 4 (8 in backward) loads in flight per thread
     constexpr int U = 4;
@@ -56,10 +86,10 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
       float4 v[U], d[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        v[u] = *reinterpret_cast<const float4*>(x + (size_t)(r + u * BN_RL) * C + c);
+        v[u] = ld4<V4>(x, (size_t)(r + u * BN_RL) * C, c, C);
         if (MODE == 1)
-          d[u] = relu_mask4(*reinterpret_cast<const float4*>(g + (size_t)(r + u * BN_RL) * C + c), ym,
-                            (size_t)(r + u * BN_RL) * C + c, mk);
+          d[u] = relu_mask4g<V4>(ld4<V4>(g, (size_t)(r + u * BN_RL) * C, c, C), ym, (size_t)(r + u * BN_RL) * C + c,
+                                 mk, c, C);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -85,7 +115,7 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
       }
     }
     for (; r < r1; r += BN_RL) {
-      const float4 v = *reinterpret_cast<const float4*>(x + (size_t)r * C + c);
+      const float4 v = ld4<V4>(x, (size_t)r * C, c, C);
       if (MODE == 0) {
         s0.x += v.x;
         s0.y += v.y;
@@ -96,8 +126,7 @@ __global__ __launch_bounds__(BN_T) void bn_partial(const float* __restrict__ x, 
         s1.z += v.z * v.z;
         s1.w += v.w * v.w;
       } else {
-        const float4 d =
-            relu_mask4(*reinterpret_cast<const float4*>(g + (size_t)r * C + c), ym, (size_t)r * C + c, mk);
+        const float4 d = relu_mask4g<V4>(ld4<V4>(g, (size_t)r * C, c, C), ym, (size_t)r * C + c, mk, c, C);
         s0.x += d.x;
         s0.y += d.y;
         s0.z += d.z;
@@ -168,6 +197,7 @@ __device__ __forceinline__ void fold_groups(const double* __restrict__ part, int
 // Forward finalize: mean / invstd for the apply pass, running statistics (PyTorch semantics:
 // running_var takes the unbiased variance), and the affine folded into (a, b).
 __global__ __launch_bounds__(BN_FIN_T) void bn_fwd_finalize(const double* __restrict__ part, int groups, int P, int C,
+                                                       int Cr,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, float momentum, float* __restrict__ run_mean,
                                                        float* __restrict__ run_var, float* __restrict__ mean,
@@ -184,6 +214,11 @@ __global__ __launch_bounds__(BN_FIN_T) void bn_fwd_finalize(const double* __rest
   const float is = (float)(1.0 / sqrt(var + (double)eps));
   mean[c] = (float)m;
   invstd[c] = is;
+  if (c >= Cr) {  // zero padding of a pruned width: stays zero
+    a[c] = 0.f;
+    b[c] = 0.f;
+    return;
+  }
   if (run_mean) {
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)m;
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(P > 1 ? var * P / (P - 1) : var);
@@ -196,6 +231,7 @@ __global__ __launch_bounds__(BN_FIN_T) void bn_fwd_finalize(const double* __rest
 // Backward finalize: dgamma = sum(g * xhat), dbeta = sum(g), and the coefficients of
 // dx = a * g + k1 + k2 * x  (k1, k2 fold the mean-subtraction terms).
 __global__ __launch_bounds__(BN_FIN_T) void bn_bwd_finalize(const double* __restrict__ part, int groups, int P, int C,
+                                                       int Cr,
                                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                        float* __restrict__ dbeta, float* __restrict__ a,
@@ -204,6 +240,12 @@ __global__ __launch_bounds__(BN_FIN_T) void bn_bwd_finalize(const double* __rest
   double sg, sgx;
   fold_groups(part, groups, C, c, cl, gl, lanes, sg, sgx);
   if (gl != 0 || c >= C) return;
+  if (c >= Cr) {
+    a[c] = 0.f;
+    k1[c] = 0.f;
+    k2[c] = 0.f;
+    return;
+  }
   if (dgamma) dgamma[c] = (float)sgx;
   if (dbeta) dbeta[c] = (float)sg;
   const double is = invstd[c], ga = gamma ? gamma[c] : 1.0;
@@ -223,7 +265,55 @@ __global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, con
                                                 unsigned C4, const float* __restrict__ res = nullptr, int relu = 0,
                                                 const float* __restrict__ ym = nullptr,
                                                 float* __restrict__ dres = nullptr,
-                                                uint8_t* __restrict__ mk = nullptr) {
+                                                uint8_t* __restrict__ mk = nullptr);
+
+// bn_apply for C % 4 != 0: thread t owns flat elements 4t..4t+3 (< n) — the ReLU mask byte t —
+// each with its own channel (e % C), per-element loads and stores
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_apply_any(const float* __restrict__ x, const float* __restrict__ g,
+                                                    const float* __restrict__ a, const float* __restrict__ b,
+                                                    const float* __restrict__ k2, float* __restrict__ out,
+                                                    unsigned long long n, unsigned C,
+                                                    const float* __restrict__ res = nullptr, int relu = 0,
+                                                    const float* __restrict__ ym = nullptr,
+                                                    float* __restrict__ dres = nullptr,
+                                                    uint8_t* __restrict__ mk = nullptr) {
+  const unsigned long long n4 = (n + 3) / 4;
+  for (unsigned long long t = blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += (unsigned long long)gridDim.x * blockDim.x) {
+    unsigned bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned long long e = 4 * t + q;
+      if (e >= n) break;
+      const unsigned c = (unsigned)(e % C);
+      const float v = x[e];
+      if (BWD) {
+        float d = g[e];
+        if (mk) d = ((mk[t] >> q) & 1u) ? d : 0.f;
+        else if (ym) d = ym[e] > 0.f ? d : 0.f;
+        if (dres) dres[e] = d;
+        if (out) out[e] = d * a[c] + b[c] + k2[c] * v;
+      } else {
+        float o = v * a[c] + b[c];
+        if (res) o += res[e];
+        if (relu) {
+          o = nan_relu(o);
+          bits |= o > 0.f ? (1u << q) : 0u;
+        }
+        out[e] = o;
+      }
+    }
+    if (!BWD && relu && mk) mk[t] = (uint8_t)bits;
+  }
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ x, const float* __restrict__ g,
+                                                const float* __restrict__ a, const float* __restrict__ b,
+                                                const float* __restrict__ k2, float* __restrict__ out, unsigned n4,
+                                                unsigned C4, const float* __restrict__ res, int relu,
+                                                const float* __restrict__ ym, float* __restrict__ dres,
+                                                uint8_t* __restrict__ mk) {
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += gridDim.x * blockDim.x) {
     const unsigned c = (t % C4) * 4;
     const float4 v = reinterpret_cast<const float4*>(x)[t];
@@ -299,45 +389,85 @@ inline int bn_groups(int P, int C) {
 // Workspace: ws holds 2 * groups * C doubles (groups = tp_bn_groups(P, C)).
 extern "C" int tp_bn_groups(int P, int C) { return tp::bn_groups(P, C); }
 
-// Fused block tail: y = relu?(BN(x) + res?) (res: the residual branch, same shape as x).
-// mko (nullable, relu only): the ReLU bit mask, P*C/4 bytes (bit q of byte p*C/4 + c/4 = y[p][c+q] > 0)
+namespace tp {
+// launch bn_apply (float4 rows) or bn_apply_any (per-element) over the whole (P, C) activation
+template <bool BWD>
+static void apply_launch(const float* x, const float* g, const float* a, const float* b, const float* k2, float* out,
+                         long long P, int C, const float* res, int relu, const float* ym, float* dres, uint8_t* mk,
+                         hipStream_t st) {
+  const long long n = P * C;
+  if (C % 4 == 0) {
+    const unsigned n4 = (unsigned)(n / 4);
+    bn_apply<BWD><<<(unsigned)std::min<long long>(ceil_div((long long)n4, 256), 8192), 256, 0, st>>>(
+        x, g, a, b, k2, out, n4, (unsigned)(C / 4), res, relu, ym, dres, mk);
+  } else {
+    const long long n4 = (n + 3) / 4;
+    bn_apply_any<BWD><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
+        x, g, a, b, k2, out, (unsigned long long)n, (unsigned)C, res, relu, ym, dres, mk);
+  }
+}
+
+template <int MODE>
+static void partial_launch(dim3 grid, const float* x, const float* g, const float* mean, const float* invstd,
+                           double* ws, int P, int C, int rpg, const float* ym, const uint8_t* mk, hipStream_t st) {
+  if (C % 4 == 0) bn_partial<MODE, true><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym, mk);
+  else bn_partial<MODE, false><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym, mk);
+}
+}  // namespace tp
+
+// Fused block tail: y = relu?(BN(x) + res?) (res: the residual branch, same shape as x). Any C;
+// channels c >= Cr are zero padding (no parameters, outputs 0).
+// mko (nullable, relu only): the ReLU bit mask, ceil(P*C/4) bytes (byte i, bit q = flat element 4i+q > 0)
+extern "C" hipError_t tp_bn_fwd_train5(const float* x, float* y, int P, int C, int Cr, const float* gamma,
+                                       const float* beta, float eps, float momentum, float* run_mean, float* run_var,
+                                       float* mean, float* invstd, float* a, float* b, double* ws, const float* res,
+                                       int relu, uint8_t* mko, long long* nbt, hipStream_t st) {
+  using namespace tp;
+  if (C <= 0 || P <= 0 || Cr <= 0 || Cr > C || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int groups = bn_groups(P, C);
+  const int rpg = (P + groups - 1) / groups;
+  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
+  partial_launch<0>(grid, x, nullptr, nullptr, nullptr, ws, P, C, rpg, nullptr, nullptr, st);
+  bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, Cr, gamma, beta, eps, momentum, run_mean,
+                                                    run_var, mean, invstd, a, b, nbt, bn_fold_lanes());
+  apply_launch<false>(x, nullptr, a, b, nullptr, y, P, C, res, relu, nullptr, nullptr, relu ? mko : nullptr, st);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t tp_bn_fwd_train4(const float* x, float* y, int P, int C, const float* gamma, const float* beta,
                                        float eps, float momentum, float* run_mean, float* run_var, float* mean,
                                        float* invstd, float* a, float* b, double* ws, const float* res, int relu,
                                        uint8_t* mko, long long* nbt, hipStream_t st) {
-  using namespace tp;
-  if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
-  const int groups = bn_groups(P, C);
-  const int rpg = (P + groups - 1) / groups;
-  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
-  bn_partial<0><<<grid, BN_T, 0, st>>>(x, nullptr, nullptr, nullptr, ws, P, C, rpg);
-  bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
-                                                    mean, invstd, a, b, nbt, bn_fold_lanes());
-  const unsigned n4 = (unsigned)((long long)P * C / 4);
-  bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
-      x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
-  return hipGetLastError();
+  return tp_bn_fwd_train5(x, y, P, C, C, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, a, b, ws, res,
+                          relu, mko, nbt, st);
 }
 
 // Forward with the batch statistics already reduced per conv tile (``pre``: [G][2][C] sums and
 // sums of squares over the tiles' rows, from the producing conv's epilogue): no statistics pass
 // over x. ws holds 2 * min(G, 256) * C doubles.
+extern "C" hipError_t tp_bn_fwd_train_pre2(const float* x, float* y, int P, int C, int Cr, const float* gamma,
+                                           const float* beta, float eps, float momentum, float* run_mean,
+                                           float* run_var, float* mean, float* invstd, float* a, float* b,
+                                           double* ws, const double* pre, int G, const float* res, int relu,
+                                           uint8_t* mko, long long* nbt, hipStream_t st) {
+  using namespace tp;
+  if (C <= 0 || P <= 0 || Cr <= 0 || Cr > C || G <= 0 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int G2 = std::min(G, 256), per = (G + G2 - 1) / G2;
+  const int groups = (G + per - 1) / per;
+  bn_fold_tiles<<<dim3((C + 63) / 64, groups), 256, 0, st>>>(pre, G, C, ws, per);
+  bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, Cr, gamma, beta, eps, momentum, run_mean,
+                                                    run_var, mean, invstd, a, b, nbt, bn_fold_lanes());
+  apply_launch<false>(x, nullptr, a, b, nullptr, y, P, C, res, relu, nullptr, nullptr, relu ? mko : nullptr, st);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t tp_bn_fwd_train_pre(const float* x, float* y, int P, int C, const float* gamma,
                                           const float* beta, float eps, float momentum, float* run_mean,
                                           float* run_var, float* mean, float* invstd, float* a, float* b,
                                           double* ws, const double* pre, int G, const float* res, int relu,
                                           uint8_t* mko, long long* nbt, hipStream_t st) {
-  using namespace tp;
-  if (C % 4 || G <= 0 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
-  const int G2 = std::min(G, 256), per = (G + G2 - 1) / G2;
-  const int groups = (G + per - 1) / per;
-  bn_fold_tiles<<<dim3((C + 63) / 64, groups), 256, 0, st>>>(pre, G, C, ws, per);
-  bn_fwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, beta, eps, momentum, run_mean, run_var,
-                                                    mean, invstd, a, b, nbt, bn_fold_lanes());
-  const unsigned n4 = (unsigned)((long long)P * C / 4);
-  bn_apply<false><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
-      x, nullptr, a, b, nullptr, y, n4, (unsigned)(C / 4), res, relu, nullptr, nullptr, relu ? mko : nullptr);
-  return hipGetLastError();
+  return tp_bn_fwd_train_pre2(x, y, P, C, C, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, a, b, ws,
+                              pre, G, res, relu, mko, nbt, st);
 }
 
 // num_batches_tracked-free entry (``nbt`` = null)
@@ -365,26 +495,31 @@ extern "C" hipError_t tp_bn_fwd_train(const float* x, float* y, int P, int C, co
 }
 
 // Backward of the fused tail: ym = the block output y (ReLU mask; nullable), dres = gradient of
-// the residual input (nullable). dx nullable (dgamma / dbeta only).
+// the residual input (nullable). dx nullable (dgamma / dbeta only). Channels c >= Cr: padding
+// (dx = 0 there, no dgamma / dbeta written).
 // mk (nullable): the forward's ReLU bit mask, used instead of ym
+extern "C" hipError_t tp_bn_bwd_train4(const float* g, const float* x, float* dx, int P, int C, int Cr,
+                                       const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                       float* dbeta, float* a, float* k1, float* k2, double* ws, const float* ym,
+                                       float* dres, const uint8_t* mk, hipStream_t st) {
+  using namespace tp;
+  if (C <= 0 || P <= 0 || Cr <= 0 || Cr > C || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int groups = bn_groups(P, C);
+  const int rpg = (P + groups - 1) / groups;
+  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
+  partial_launch<1>(grid, x, g, mean, invstd, ws, P, C, rpg, ym, mk, st);
+  bn_bwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, Cr, gamma, mean, invstd, dgamma, dbeta, a, k1,
+                                                      k2, bn_fold_lanes());
+  if (dx || dres)
+    apply_launch<true>(x, g, a, k1, k2, dx, P, C, nullptr, 0, ym, dres, const_cast<uint8_t*>(mk), st);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t tp_bn_bwd_train3(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
                                        const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
                                        float* k1, float* k2, double* ws, const float* ym, float* dres,
                                        const uint8_t* mk, hipStream_t st) {
-  using namespace tp;
-  if (C % 4 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
-  const int groups = bn_groups(P, C);
-  const int rpg = (P + groups - 1) / groups;
-  const dim3 grid((C + BN_CQ * 4 - 1) / (BN_CQ * 4), groups);
-  bn_partial<1><<<grid, BN_T, 0, st>>>(x, g, mean, invstd, ws, P, C, rpg, ym, mk);
-  bn_bwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2,
-                                                      bn_fold_lanes());
-  if (dx || dres) {
-    const unsigned n4 = (unsigned)((long long)P * C / 4);
-    bn_apply<true><<<(unsigned)std::min<long long>(ceil_div(n4, 256), 8192), 256, 0, st>>>(
-        x, g, a, k1, k2, dx, n4, (unsigned)(C / 4), nullptr, 0, ym, dres, const_cast<uint8_t*>(mk));
-  }
-  return hipGetLastError();
+  return tp_bn_bwd_train4(g, x, dx, P, C, C, gamma, mean, invstd, dgamma, dbeta, a, k1, k2, ws, ym, dres, mk, st);
 }
 
 extern "C" hipError_t tp_bn_bwd_train2(const float* g, const float* x, float* dx, int P, int C, const float* gamma,

@@ -36,8 +36,6 @@ constexpr int CFG_BF16 = 256;  // tile-config flag: bf16 operands (conv_igemm BF
 constexpr int CFG_SK = 32;     // tile-config flag: stream-K split of the tiles x k-slices space (GEN 1, one K pass)
 constexpr int CFG_SB = 64;     // tile-config flag: single-buffered LDS stage (GEN 1 1x1 forward, one K pass): half the
                                // LDS, twice the co-resident blocks for the short-K convs (profiles/train/lowk_*)
-constexpr int CFG_WS = 16;     // cfgs 16..18: persistent warp-specialised 1x1 GEMM (gemm_ws.hip), 1x1 stride-s
-                               // GEN 1 convs and their dgrads (no split-K, no bnpart, dense residual)
 
 enum Epi : int {
   EPI_FWD = 0,       // y = relu?(acc*scale[n] + shift[n]) stored NHWC
@@ -233,7 +231,10 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
   const int m0 = (tile / n_tiles) * BM;
   const int n0 = (tile % n_tiles) * BN;
   if (m0 >= m_tiles * BM) return;
-  const int cin_tiles = p.Cin / BK;
+  // K slices per tap: GEN 1 / 3 take any Cin % 4 == 0 (pruned widths); the last slice of a tap is
+  // zero-filled past Cin in the loads (the weight operand is 32-padded per tap), so activations
+  // keep their real width in HBM
+  const int cin_tiles = (p.Cin + BK - 1) / BK;
   unsigned tmask = (1u << (KS * KS)) - 1u;  // GEN 3: taps any row of this tile can use
   if constexpr (GEN == 3) {
     if (p.parity) {
@@ -348,7 +349,8 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
       for (int i = 0; i < T::A_CHUNKS; ++i) {
         const int th = a_oh[i] - kh, tw = a_ow[i] - kw;
         const int yh = s2 ? th >> 1 : th / s, yw = s2 ? tw >> 1 : tw / s;
-        const bool ok = a_mask[i] && th >= 0 && tw >= 0 && yh * s == th && yw * s == tw && yh < p.H && yw < p.W;
+        const bool ok = a_mask[i] && th >= 0 && tw >= 0 && yh * s == th && yw * s == tw && yh < p.H && yw < p.W &&
+                        cs * BK + a_c4[i] * 4 < p.Cin;
         const unsigned vo = ok ? (unsigned)(a_off[i] + (yh * p.W + yw) * p.Cin + cs * BK + a_c4[i] * 4) * 4u : OOB;
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
         ra[i] = g;
@@ -362,7 +364,8 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
       const unsigned coff = (unsigned)(ld_cs * BK) * 4u;
 #pragma unroll
       for (int i = 0; i < T::A_CHUNKS; ++i) {
-        const f32x4 g = buf_load_f32x4(xr, (int)(a_k1[i] != OOB ? a_k1[i] + coff : OOB), 0, 0);
+        const bool cok = ld_cs * BK + a_c4[i] * 4 < p.Cin;  // past a pruned width: zeros
+        const f32x4 g = buf_load_f32x4(xr, (int)(a_k1[i] != OOB && cok ? a_k1[i] + coff : OOB), 0, 0);
         ra[i] = g;
       }
       ++ld_cs;
@@ -378,7 +381,8 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           c = ld_cs * BK + a_c4[i] * 4;
         }
         const int ih = a_oh[i] + tap / KS, iw = a_ow[i] + tap % KS;
-        const bool ok = a_mask[i] && tap < KS * KS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const bool ok = a_mask[i] && tap < KS * KS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W &&
+                        (GEN == 2 || c < p.Cin);
         const unsigned vo = ok ? (unsigned)(a_off[i] + (ih * p.W + iw) * p.Cin + c) * 4u : OOB;
         const f32x4 g = buf_load_f32x4(xr, (int)vo, 0, 0);
         ra[i] = g;
@@ -1549,10 +1553,6 @@ hipError_t gen_dispatch(int ks, int gen, int cfg, const tp::ConvArgs& a, int spl
 }
 }  // namespace
 
-extern "C" hipError_t tp_gemm1x1_ws(const float* x, const float* w, int B, int H, int W, int Cin, int N, int stride,
-                                    const float* scale, const float* shift, int relu, float slope, const float* res,
-                                    const float* mask, float* apoz, float* out, int variant, hipStream_t st);
-
 // Workspace floats a stream-K GEN 1 launch of tile config ``cfg`` (without the CFG_SK flag) needs at
 // this GEMM shape (0: stream-K does not apply: transposed / strided-gather, 5x5, or the tiles are
 // fewer than the co-resident blocks or already a multiple of them). ``tay``: the data-gradient
@@ -1564,8 +1564,10 @@ extern "C" long long tp_conv_sk_ws_floats(int cfg, int ks, int transposed, int t
   return 0;
 }
 
+// GEMM K of a GEN conv's weight operand: 4-channel packed taps, else every tap's channels padded
+// to the 32-wide K slice (Cin % 4 == 0: pruned widths read zeros past Cin)
 extern "C" int tp_conv_gen_k(int ks, int Cin) {
-  return Cin == 4 ? (ks * ks * 4 + 31) / 32 * 32 : ks * ks * Cin;
+  return Cin == 4 ? (ks * ks * 4 + 31) / 32 * 32 : ks * ks * ((Cin + 31) / 32 * 32);
 }
 
 extern "C" hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
@@ -1679,22 +1681,17 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
                                    double* bnpart, float* tay_part, int tay_mode, hipStream_t st) {
   using namespace tp;
   const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
-  if ((gen != 2 && Cin % 32 != 0) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
+  if ((gen != 2 && (Cin % 4 != 0 || Cin < 8)) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
   const bool sb = cfg >= 0 && (cfg & CFG_SB);
   if (sb) {  // single-buffered LDS stage: GEN 1 1x1 forward, one K pass, not with stream-K
     cfg &= ~CFG_SB;
-    if (gen != 1 || ks != 1 || splits > 1 || (cfg & CFG_SK) || cfg >= CFG_WS)
+    if (gen != 1 || ks != 1 || splits > 1 || (cfg & CFG_SK) || cfg >= 16)
       return hipErrorInvalidValue;
   }
-  const bool sk = cfg >= 0 && (cfg & CFG_SK) && (cfg & ~CFG_SK) < CFG_WS;
+  const bool sk = cfg >= 0 && (cfg & CFG_SK) && (cfg & ~CFG_SK) < 16;
   if (sk) {  // stream-K: GEN 1, one K pass, ``ws`` = the fixup slots (tp_conv_sk_ws_floats)
     cfg &= ~CFG_SK;
     if (gen != 1 || splits > 1 || !ws || (ks != 1 && ks != 3)) return hipErrorInvalidValue;
-  }
-  if (cfg >= CFG_WS && cfg < CFG_WS + 3) {  // persistent warp-specialised 1x1 kernel (gemm_ws.hip)
-    if (gen != 1 || ks != 1 || pad != 0 || res_stride != 1 || bnpart) return hipErrorInvalidValue;
-    return tp_gemm1x1_ws(x, w, B, H, W, Cin, Cout, stride, scale, shift, relu, 0.f, res, mask, apoz, out,
-                         cfg - CFG_WS, st);
   }
   if (gen == 3 && (ks != 1 && ks != 3)) return hipErrorInvalidValue;
   ConvArgs a{};
@@ -1741,7 +1738,7 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
     a.bnpart = bnpart;
   }
   if (tay_part) {
-    if (splits > 1 || !mask || gen != 1 || cfg >= CFG_WS || tp_conv_gen_tay_slots(cfg, a.HWo) == 0)
+    if (splits > 1 || !mask || gen != 1 || cfg >= 16 || tp_conv_gen_tay_slots(cfg, a.HWo) == 0)
       return hipErrorInvalidValue;
     a.tay_part = tay_part;
     a.tay_mode = tay_mode;

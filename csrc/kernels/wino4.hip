@@ -90,6 +90,7 @@ struct Args {
   const float* x;     // NHWC (B, S, S, C): the input (forward) or the output gradient (dgrad)
   const float* u;     // U images [C/8][K/32][U_IMG]
   int B, C, K, P;     // P = output tiles = B * (S/4)^2
+  int ko;             // output channels per pixel (<= K): channels k >= ko are neither read nor stored
   long long x_elems;
   const float* scale; // FWD: BN scale (K); BWD: previous layer's BN scale (K), nullable
   const float* shift; // FWD: BN shift (K), nullable
@@ -310,10 +311,12 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
   const bool want_part = EPI == BWD ? p.taylor != nullptr : p.apoz != nullptr;
   const int c4 = lane & 7;
   const int k = k0 + 4 * c4;
+  const int KO = p.ko;          // output row width (pruned widths: K rounded up to 32 in the MFMAs only)
+  const bool kok = k < KO;      // this lane's 4 channels are stored (KO % 4 == 0)
   const float* ysrc = (c4 < 4 ? ya : yb) + (c4 & 3) * 4;
   f32x4 sc4 = {1.f, 1.f, 1.f, 1.f}, sh4 = {0.f, 0.f, 0.f, 0.f};
-  if (p.scale) sc4 = *reinterpret_cast<const f32x4*>(p.scale + k);
-  if (EPI != BWD && p.shift) sh4 = *reinterpret_cast<const f32x4*>(p.shift + k);
+  if (p.scale && kok) sc4 = *reinterpret_cast<const f32x4*>(p.scale + k);
+  if (EPI != BWD && p.shift && kok) sh4 = *reinterpret_cast<const f32x4*>(p.shift + k);
 
 #pragma unroll
   for (int hf = 0; hf < HALVES; ++hf) {
@@ -356,8 +359,8 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
           const int q = qq + 8 * h2;
           const int yy = 4 * tr + (q >> 2), xx = 4 * tc + (q & 3);
           const long long pix = ((long long)b * S + yy) * S + xx;
-          const bool ok = pt < p.P && tbv < TBR && (!PART_TILE || (yy < S && xx < S));
-          apre[tt][h2] = ok ? *reinterpret_cast<const f32x4*>(p.act + pix * p.K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const bool ok = kok && pt < p.P && tbv < TBR && (!PART_TILE || (yy < S && xx < S));
+          apre[tt][h2] = ok ? *reinterpret_cast<const f32x4*>(p.act + pix * KO + k) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
@@ -391,9 +394,11 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
             }
           }
           const int b = pt / TI, ti = pt - b * TI, tr = ti / TPR, tc = ti - tr * TPR;
-          const long long o = (((long long)b * (S / 2) + 2 * tr + py) * (S / 2) + 2 * tc + px) * p.K + k;
-          *reinterpret_cast<f32x4*>(p.out + o) = best;
-          *reinterpret_cast<unsigned*>(p.out_argmax + o) = arg;
+          const long long o = (((long long)b * (S / 2) + 2 * tr + py) * (S / 2) + 2 * tc + px) * KO + k;
+          if (kok) {
+            *reinterpret_cast<f32x4*>(p.out + o) = best;
+            *reinterpret_cast<unsigned*>(p.out_argmax + o) = arg;
+          }
         }
         if (want_part) {  // per-(tile, channel) count over the 4 pooled pixels (lanes ^8, ^16)
 #pragma unroll
@@ -434,28 +439,28 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
                 if (p.relu) v[e] = nan_relu(v[e]);
                 sum[e] += v[e] > 0.f ? 1.f : 0.f;
               }
-              *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+              if (kok) *reinterpret_cast<f32x4*>(p.out + pix * KO + k) = v;
             } else {  // BWD
               const f32x4 a = apre[EPI == BWD ? tt : 0][h2];
 #pragma unroll
               for (int e = 0; e < 4; ++e) sum[e] += tay_term(p.tay_mode, yv[e], a[e]);
-              if (p.out) {
+              if (p.out && kok) {
                 f32x4 v;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = a[e] > 0.f ? yv[e] * sc4[e] : 0.f;
                 if (p.unp) {  // the 2x2 window of this pooled pixel: v at its argmax, 0 elsewhere
-                  const unsigned am4 = *reinterpret_cast<const unsigned*>(p.unp + pix * p.K + k);
+                  const unsigned am4 = *reinterpret_cast<const unsigned*>(p.unp + pix * KO + k);
                   const int yy = 4 * tr + (q >> 2), xx = 4 * tc + (q & 3);
-                  const long long o00 = (((long long)b * 2 * S + 2 * yy) * 2 * S + 2 * xx) * p.K + k;
+                  const long long o00 = (((long long)b * 2 * S + 2 * yy) * 2 * S + 2 * xx) * KO + k;
 #pragma unroll
                   for (int w = 0; w < 4; ++w) {
                     f32x4 o;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) o[e] = ((am4 >> (8 * e)) & 0xffu) == (unsigned)w ? v[e] : 0.f;
-                    *reinterpret_cast<f32x4*>(p.out + o00 + ((long long)(w >> 1) * 2 * S + (w & 1)) * p.K) = o;
+                    *reinterpret_cast<f32x4*>(p.out + o00 + ((long long)(w >> 1) * 2 * S + (w & 1)) * KO) = o;
                   }
                 } else {
-                  *reinterpret_cast<f32x4*>(p.out + pix * p.K + k) = v;
+                  *reinterpret_cast<f32x4*>(p.out + pix * KO + k) = v;
                 }
               }
             }
@@ -481,15 +486,15 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
     for (int t = tid; t < nimg * TK; t += 64 * NW) {
       const int il = t / TK, kk = t - il * TK;
       const int b = b0 + il;
-      if (b >= p.B) continue;
+      if (b >= p.B || k0 + kk >= KO) continue;
       const int s0 = max(0, b * TI - t0), s1 = min(TBR, (b + 1) * TI - t0);
       float s = 0.f;
       for (int ti = s0; ti < s1; ++ti) s += part[ti * TK + kk];
       if constexpr (EPI == BWD) {
         const int slot = blk - (b * TPR) / Band<S>::BR;
-        p.taylor[((long long)slot * p.B + b) * p.K + k0 + kk] += s;
+        p.taylor[((long long)slot * p.B + b) * KO + k0 + kk] += s;
       } else {
-        if (s > 0.f) atomicAdd(p.apoz + (long long)b * p.K + k0 + kk, s);
+        if (s > 0.f) atomicAdd(p.apoz + (long long)b * KO + k0 + kk, s);
       }
     }
     return;
@@ -504,253 +509,19 @@ __device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[PPW][NPT], 
   for (int t = tid; t < NIB * TK; t += 64 * NW) {
     const int il = t / TK, kk = t - il * TK;
     const int b = b0 + il;
-    if (b >= p.B) continue;
+    if (b >= p.B || k0 + kk >= KO) continue;
     float s = 0.f;
     for (int ti = 0; ti < TIB; ++ti) s += part[(il * TIB + ti) * TK + kk];
     constexpr bool split_img = TI > TB;
     if constexpr (EPI == BWD) {
       const int slot = split_img ? (t0 / TB) % (TI / TB) : 0;
-      p.taylor[((long long)slot * p.B + b) * p.K + k0 + kk] += s;
+      p.taylor[((long long)slot * p.B + b) * KO + k0 + kk] += s;
     } else if constexpr (split_img) {
-      if (s > 0.f) atomicAdd(p.apoz + (long long)b * p.K + k0 + kk, s);
+      if (s > 0.f) atomicAdd(p.apoz + (long long)b * KO + k0 + kk, s);
     } else {
-      p.apoz[(long long)b * p.K + k0 + kk] += s;
+      p.apoz[(long long)b * KO + k0 + kk] += s;
     }
   }
-}
-
-// MODE 0: one block per CU, U and X double-buffered, the next chunk's DMA and transform
-// software-pipelined under the current chunk's MFMAs (one wave per SIMD).
-// MODE 1: two blocks per CU (<= 80 KB of LDS each), single-buffered: each block stages, waits,
-// transforms and multiplies in turn, and the other block's waves fill the SIMDs meanwhile.
-template <int EPI, int S, int MODE>
-__global__ __launch_bounds__(256, MODE ? 2 : 1) void wino4_f4x3(Args p) {
-  using G = Geo<S>;
-  constexpr int TPR = S / 4, TI = TPR * TPR;
-  constexpr int PL = plane_slots<S>();
-  constexpr int XR = x_rounds<S>();
-  constexpr int XB = MODE ? (XR > 9 ? XR : 9) * 1024 : XR * 1024;
-  // separate objects per buffer: the compiler's LDS-DMA alias tracking tells them apart
-  __shared__ __attribute__((aligned(16))) float us0[U_IMG];
-  __shared__ __attribute__((aligned(16))) float us1[MODE ? 4 : U_IMG];
-  __shared__ __attribute__((aligned(16))) float xs0[XB];
-  __shared__ __attribute__((aligned(16))) float xs1[MODE ? 4 : XB];
-  __shared__ __attribute__((aligned(16))) float pts[MODE ? TILES * TK : 4];
-  static_assert(TILES * TPL <= U_IMG && TILES * TPL <= (MODE ? XB : U_IMG), "epilogue tile buffers");
-  static_assert(TILES * TK <= XR * 1024, "partial-sum buffer must fit an X buffer");
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j = lane & 15, g = lane >> 4;
-  const int n_k = p.K / TK;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int kb = tile % n_k, k0 = kb * TK;
-  const int blk_p = tile / n_k;
-  const int t0 = blk_p * TILES;
-  const int b0 = t0 / TI;
-  const int nh = wave >> 1;  // output-channel half of this wave
-
-  const __amdgpu_buffer_rsrc_t urs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, (int)((long long)(p.C / 8) * n_k * U_IMG * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t xrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)(p.x_elems * 4), 0x00020000);
-
-  // this lane's tile (MFMA row j) and its patch's first slot in a plane of the staged region
-  const int tib = (wave & 1) * 16 + j;
-  const int il = tib / TI, ti = tib - il * TI, tr = ti / TPR, tc = ti - tr * TPR;
-  const int sbase = S == 4 ? il * G::IP : il * G::IP + 4 * tr * G::RWP + 5 * tc;
-  const int poff = ((g >> 1) * PL + sbase) * 4 + (g & 1) * 2;  // float offset: plane g/2, channels 2g, 2g+1
-
-  // DMA source byte offsets (channel 0 of a chunk) of this thread's slot in each round
-  unsigned xsrc[XR];
-#pragma unroll
-  for (int i = 0; i < XR; ++i) {
-    const int slot = i * 256 + tid;
-    const int h = slot / PL, s = slot - h * PL;
-    const int im = s / G::IP, rem = s - im * G::IP;
-    int xx, yy;
-    bool ok;
-    if constexpr (S == 4) {
-      yy = rem / 4;
-      xx = rem - yy * 4;
-      ok = rem < 16;
-    } else {
-      const int row = rem / G::RWP, colp = rem - row * G::RWP;
-      const int blk5 = colp / 5, w5 = colp - blk5 * 5;
-      xx = 4 * blk5 + w5 - 1;
-      yy = row - 1 + (S == 32 ? 16 * (blk_p & 1) : 0);  // S = 32: the block is one image half
-      ok = w5 != 4 && row < G::RH && xx >= 0 && xx < S && yy >= 0 && yy < S;
-    }
-    const int b = b0 + im;
-    ok = ok && h < 2 && im < G::NI && b < p.B;
-    xsrc[i] = ok ? (unsigned)(((((long long)b * S + yy) * S + xx) * p.C + 4 * h) * 4) : OOB;
-  }
-
-  auto stage_u = [&](int c0, float* ud) {
-    if (p.dbg & 1) return;
-    const unsigned ub = (unsigned)(((c0 >> 3) * n_k + kb) * U_IMG) * 4u;
-#pragma unroll
-    for (int i = 0; i < U_ROUNDS; ++i) dma16(urs, ud + (i * 256 + wave * 64) * 4, (unsigned)(i * 256 + tid) * 16u, ub);
-  };
-  auto stage_x = [&](int c0, float* xd) {
-    if (p.dbg & 2) return;
-#pragma unroll
-    for (int i = 0; i < XR; ++i) dma16(xrs, xd + (i * 256 + wave * 64) * 4, xsrc[i], (unsigned)c0 * 4u);
-  };
-
-  // the lane's 6x6 patch of channels (2g, 2g+1) (raw; transformed in place by transform())
-  auto load_patch = [&](const float* xb, float (&v0)[36], float (&v1)[36]) {
-    const float* p0 = xb + poff;
-    // column-major issue order: the first column transform can start after 6 reads (lgkmcnt
-    // retires in order)
-#pragma unroll
-    for (int q = 0; q < 6; ++q)
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        float2 d = {0.f, 0.f};
-        if constexpr (S == 4) {
-          if (r >= 1 && r <= 4 && q >= 1 && q <= 4) d = *reinterpret_cast<const float2*>(p0 + ((r - 1) * 4 + (q - 1)) * 4);
-        } else {
-          d = *reinterpret_cast<const float2*>(p0 + (r * G::RWP + q + (q >= 4 ? 1 : 0)) * 4);
-        }
-        v0[r * 6 + q] = d.x;
-        v1[r * 6 + q] = d.y;
-        // keep every read a single ds_read_b64: a merged ds_read2_b64 is banked in 16-lane groups
-        // mod 32 banks, where the 16 tiles of a wave can only cover 8 bank quads (2-way conflicts);
-        // the layout is conflict-free for ds_read_b64's 32-lane groups mod 64 banks
-        __builtin_amdgcn_sched_barrier(0);
-      }
-  };
-
-  const int nc = p.C / 8;
-  f32x4 acc[NPT];
-#pragma unroll
-  for (int x = 0; x < NPT; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // B operands of lane (j, g): U[x][c = 2g + e][k = 16 nh + j], e = 0, 1 as one float2 (g slot
-  // XOR-swizzled by j >> 3: conflict-free ds_read_b64)
-  const int uoff = nh * 128 + j * 8 + 2 * (g ^ ((j >> 3) << 1));
-
-  // One chunk c, ONE barrier: on entry U(c) and X(c+1) (both issued at the top of chunk c-1) must
-  // have landed; after the barrier U(c+1) (into the buffer of U(c-1)) and X(c+2) (into the buffer
-  // of X(c), whose patches every wave read at the top of chunk c-1) are issued — a full chunk of
-  // lead each — and the next patch is read. The 72 MFMAs of chunk c are then interleaved with
-  // the transform of chunk c+1 (in-order issue: one wave per SIMD hides the VALU work only if
-  // it sits between the MFMAs, so the schedule is pinned with sched_group_barrier).
-  auto chunk = [&](int c, const float* ub, float* un, const float* xn, float* xf, const float (&va0)[36],
-                   const float (&va1)[36], float (&vn0)[36], float (&vn1)[36]) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (c + 1 < nc) stage_u(8 * (c + 1), un);
-    if (c + 2 < nc) stage_x(8 * (c + 2), xf);
-    // 18 steps of 4 MFMAs (points 2i, 2i+1 x both channel halves). Steps 0-8 only run MFMAs (the
-    // current V dies as they go); step 8 issues the next patch's 36 reads (column-major), steps
-    // 10-17 run its 24 length-6 transforms (12 column passes, then 12 row passes), 3 per step.
-    // This keeps the live set at ~36 current + 72 next V registers (accumulators in AGPRs), and
-    // one sched_barrier per step pins the interleave: the wave is alone on its SIMD, so VALU work
-    // only hides between its own MFMAs. (The last chunk reads and transforms a stale patch:
-    // harmless, keeps the schedule uniform.)
-    const float* ul = ub + uoff;
-    float2 wq[2][2];  // B operands of two point pairs ahead
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      wq[s2][0] = *reinterpret_cast<const float2*>(ul + (2 * s2) * 256);
-      __builtin_amdgcn_sched_barrier(0);
-      wq[s2][1] = *reinterpret_cast<const float2*>(ul + (2 * s2 + 1) * 256);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int i = 0; i < NPT / 2; ++i) {
-      const int x = 2 * i;
-      const float2 wa = wq[i & 1][0], wb = wq[i & 1][1];
-      if (i + 2 < NPT / 2) {
-        wq[i & 1][0] = *reinterpret_cast<const float2*>(ul + (x + 4) * 256);
-        __builtin_amdgcn_sched_barrier(0);  // two ds_read_b64, not one ds_read2st64_b64
-        wq[i & 1][1] = *reinterpret_cast<const float2*>(ul + (x + 5) * 256);
-      }
-      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(va0[x], wa.x, acc[x], 0, 0, 0);
-      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(va0[x + 1], wb.x, acc[x + 1], 0, 0, 0);
-      acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(va1[x], wa.y, acc[x], 0, 0, 0);
-      acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(va1[x + 1], wb.y, acc[x + 1], 0, 0, 0);
-      if (i == 8) load_patch(xn, vn0, vn1);
-      constexpr int T0 = 10;  // first transform step
-      const int k_lo = i < T0 ? 0 : (i - T0) * 3, k_hi = i < T0 ? 0 : (i - T0 + 1) * 3;
-#pragma unroll
-      for (int k = k_lo; k < k_hi; ++k) transform_step(vn0, vn1, k);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  if constexpr (MODE == 1) {
-    float v0[36], v1[36];
-    for (int c = 0; c < nc; ++c) {
-      __syncthreads();  // the previous chunk's patch and U reads are done: the buffers are free
-      stage_u(8 * c, us0);
-      stage_x(8 * c, xs0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      load_patch(xs0, v0, v1);
-      input_transform(v0);
-      input_transform(v1);
-      const float* ul = us0 + uoff;
-      // B operands one point pair ahead, each read its own ds_read_b64 (see load_patch)
-      float2 qa = *reinterpret_cast<const float2*>(ul);
-      __builtin_amdgcn_sched_barrier(0);
-      float2 qb = *reinterpret_cast<const float2*>(ul + 256);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int x = 0; x < NPT; x += 2) {
-        const float2 wa = qa, wb = qb;
-        if (x + 2 < NPT) {
-          qa = *reinterpret_cast<const float2*>(ul + (x + 2) * 256);
-          __builtin_amdgcn_sched_barrier(0);
-          qb = *reinterpret_cast<const float2*>(ul + (x + 3) * 256);
-        }
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x], wa.x, acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[x + 1], wb.x, acc[x + 1], 0, 0, 0);
-        acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x], wa.y, acc[x], 0, 0, 0);
-        acc[x + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[x + 1], wb.y, acc[x + 1], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __syncthreads();
-    if (p.dbg & 16) {
-      float t = 0.f;
-#pragma unroll
-      for (int x = 0; x < NPT; ++x) t += acc[x][0];
-      if (t == 1234.5f) p.out[0] = t;
-      return;
-    }
-    epilogue<EPI, S, 4>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us0, xs0, pts);
-    return;
-  }
-  float a0[36], a1[36], b0v[36], b1v[36];
-  // prologue: U(0), X(0), X(1) in flight; V(0) formed before the loop
-  stage_u(0, us0);
-  stage_x(0, xs0);
-  if (nc > 1) stage_x(8, xs1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  load_patch(xs0, a0, a1);
-  input_transform(a0);
-  input_transform(a1);
-  for (int c = 0; c < nc; ++c) {
-    const bool odd = c & 1;
-    chunk(c, odd ? us1 : us0, odd ? us0 : us1, odd ? xs0 : xs1, odd ? xs1 : xs0, a0, a1, b0v, b1v);
-#pragma unroll
-    for (int t = 0; t < 36; ++t) {
-      a0[t] = b0v[t];
-      a1[t] = b1v[t];
-    }
-  }
-  __syncthreads();  // the main loop's LDS reads are done: reuse us0/us1 (outputs), xs0 (partials)
-  if (p.dbg & 16) {
-    float t = 0.f;
-#pragma unroll
-    for (int x = 0; x < NPT; ++x) t += acc[x][0] + a0[x] + a1[x];
-    if (t == 1234.5f) p.out[0] = t;  // keeps the main loop alive
-    return;
-  }
-  epilogue<EPI, S, 4>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us0, us1, xs0);
 }
 
 
@@ -1182,253 +953,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void wino4_m2(Args p) {
   else epilogue<EPI, S, 4, 1, SPLITP>(p, *reinterpret_cast<f32x4(*)[1][NPT]>(&acc), t0, k0, us, xs0, xs1);
 }
 
-// WIDE: one block of 4 waves per CU (one wave per SIMD) = 64 tiles x 32 output channels; wave w
-// owns the 16 tiles of group w x BOTH 16-channel halves (72 accumulator tiles, 288 registers).
-//
-// Why: fp32 VALU work does not hide under fp32 MFMAs on gfx950 (profiles/wino4/
-// microbench_mfma_valu_lds.txt), so the input transform's cost per MFMA is what bounds the MODE 2/3
-// kernels (MFMA util 0.37-0.6). There, a wave multiplies each transformed patch by 16 output
-// channels and the two waves of a 16-tile group transform the same patches. Here each patch is
-// transformed once per block and feeds 32 channels: half the transform VALU and half the LDS-DMA
-// bytes per MFMA (the 36-KB U image of a chunk serves 64 tiles instead of 32). The price is one
-// wave per SIMD (no second block to run during a barrier), so the DMA runs well ahead: X is
-// double-buffered (1.5 chunks of lead), U in parity halves (each issued half a chunk ahead).
-// Same U images (layout 1), same staged X geometry (GeoT<S, 64>) and epilogues as MODE 2.
-// 288 accumulator registers do not fit the 256 AGPRs: with builtins the compiler shuffles them
-// between AGPRs, VGPRs and scratch inside the MFMA loop (261 v_accvgpr moves + scratch per chunk,
-// measured in the .s). So the MFMAs are inline asm with the accumulators pinned by constraint:
-// points 0-31 ("a": 256 AGPRs) and points 32-35 ("v": 32 VGPRs). hipcc pads no hazard inside an
-// asm string (cdna_hip_programming.md §5.7): the first group of each parity opens with s_nop 1 (a
-// VALU-written A operand, or the zeroed accumulators, -> MFMA), consecutive MFMAs on one
-// accumulator take it whole as C (no wait states), and the loop ends with s_nop 15 before the
-// epilogue reads them.
-#define W4W_AGPR_POINTS 32
-#define W4W_MFMA4(C, NOP, c0, c1, c2, c3, a0, a1, w0, w1)                                             \
-  asm volatile(NOP                                                                                    \
-               "v_mfma_f32_16x16x4_f32 %0, %4, %6, %0\n\t"                                           \
-               "v_mfma_f32_16x16x4_f32 %1, %4, %8, %1\n\t"                                           \
-               "v_mfma_f32_16x16x4_f32 %2, %5, %7, %2\n\t"                                           \
-               "v_mfma_f32_16x16x4_f32 %3, %5, %9, %3"                                               \
-               : "+" C(c0), "+" C(c1), "+" C(c2), "+" C(c3)                                           \
-               : "v"(a0), "v"(a1), "v"(w0.x), "v"(w0.y), "v"(w1.x), "v"(w1.y))
-
-template <int EPI, int S>
-__global__ __launch_bounds__(256, 1) void wino4_wide(Args p) {
-  constexpr int NW = 4, TB = 64;
-  using G = GeoT<S, TB>;
-  constexpr int TPR = S / 4, TI = TPR * TPR;
-  constexpr int PL = G::NI * G::IP;
-  constexpr int NXI = (2 * PL + 63) / 64;  // X DMA wave-instructions (64 16-B slots each)
-  constexpr int KX = (NXI + NW - 1) / NW;
-  constexpr int XN = (NXI > 34 ? NXI : 34) * 256;  // >= 32 * TPL floats (an epilogue half)
-  __shared__ __attribute__((aligned(16))) float us[U_IMG];
-  __shared__ __attribute__((aligned(16))) float xs0[XN];
-  __shared__ __attribute__((aligned(16))) float xs1[XN];
-  static_assert(32 * TPL <= XN && TB * TK <= U_IMG, "epilogue buffers");
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = lane & 15, g = lane >> 4;
-  const int n_k = p.K / TK;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int kb = tile % n_k, k0 = kb * TK;
-  const int blk_p = tile / n_k;
-  const int t0 = blk_p * TB;
-  const int b0 = t0 / TI;
-
-  const i32x4v urs = raw_rsrc(p.u, (unsigned)((long long)(p.C / 8) * n_k * U_IMG * 4));
-  const i32x4v xrs = raw_rsrc(p.x, (unsigned)(p.x_elems * 4));
-
-  const int tib = wave * 16 + j;
-  const int il = tib / TI, ti = tib - il * TI, tr = ti / TPR, tc = ti - tr * TPR;
-  const int sbase = S == 4 ? il * G::IP : il * G::IP + 4 * tr * G::RWP + (G::PAD ? 5 : 4) * tc;
-  const int poff = ((g >> 1) * PL + sbase) * 4 + (g & 1) * 2;  // plane g/2, channels 2g, 2g+1
-
-  // X DMA sources, 16 bits per instruction (pixel index in the block's images, plane, valid)
-  unsigned xcode[(KX + 1) / 2];
-#pragma unroll
-  for (int i = 0; i < (KX + 1) / 2; ++i) xcode[i] = 0u;
-#pragma unroll
-  for (int i = 0; i < KX; ++i) {
-    const int slot = (wave + NW * i) * 64 + lane;
-    const int h = slot / PL, s = slot - h * PL;
-    const int im = s / G::IP, rem = s - im * G::IP;
-    int xx, yy;
-    bool ok;
-    if constexpr (S == 4) {
-      yy = rem / 4;
-      xx = rem - yy * 4;
-      ok = rem < 16;
-    } else {
-      const int row = rem / G::RWP, colp = rem - row * G::RWP;
-      int w5 = 0;
-      if constexpr (G::PAD) {
-        const int blk5 = colp / 5;
-        w5 = colp - blk5 * 5;
-        xx = 4 * blk5 + w5 - 1;
-      } else {
-        xx = colp - 1;
-      }
-      yy = row - 1;
-      ok = w5 != 4 && row < G::RH && xx >= 0 && xx < S && yy >= 0 && yy < S;
-    }
-    ok = ok && h < 2 && im < G::NI && b0 + im < p.B;
-    const unsigned code = ok ? (unsigned)((im * S + yy) * S + xx) | ((unsigned)h << 11) | 0x1000u : 0u;
-    xcode[i >> 1] |= code << (16 * (i & 1));
-  }
-  static_assert(G::NI * S * S <= 2048, "X pixel code");
-  const unsigned xbase = (unsigned)b0 * S * S * (unsigned)p.C * 4u;
-  const unsigned lane16 = (unsigned)lane * 16u;
-  const unsigned c4 = (unsigned)p.C * 4u;
-
-  auto stage_u = [&](int c0, int hf) {  // U half hf (18 point pairs) of chunk c0/8
-    if (p.dbg & 1) return;
-    const unsigned ub = (unsigned)(((c0 >> 3) * n_k + kb) * U_IMG) * 4u;
-#pragma unroll
-    for (int i = 0; i < (18 + NW - 1) / NW; ++i) {
-      const int pt = wave + NW * i;
-      if (pt < 18) {
-        const int q = hf * 18 + pt;
-        dma16_asm(urs, lds_addr(us + q * 256), lane16, ub + (unsigned)q * 1024u);
-      }
-    }
-  };
-  auto stage_x = [&](int c0, float* xd) {
-    if (p.dbg & 2) return;
-#pragma unroll
-    for (int i = 0; i < KX; ++i)
-      if (wave + NW * i < NXI) {
-        const unsigned code = xcode[i >> 1] >> (16 * (i & 1));
-        const unsigned off = (code & 0x1000u) ? xbase + (code & 0x7ffu) * c4 + ((code >> 7) & 16u) : OOB;
-        dma16_asm(xrs, lds_addr(xd + (wave + NW * i) * 256), off, (unsigned)c0 * 4u);
-      }
-  };
-
-  const int nc_all = p.C / 8, cps = (nc_all + (int)gridDim.y - 1) / (int)gridDim.y;
-  const int c_lo = (int)blockIdx.y * cps, nc = min(nc_all, c_lo + cps);
-  f32x4 acc[2][NPT];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int x = 0; x < NPT; ++x) acc[h][x] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* ul = us + j * 8 + 2 * (g ^ ((j >> 3) << 1));  // + nh * 128 + (e * 18 + pair) * 256
-  // U DMAs per wave per half: waves 0, 1 issue 5, waves 2, 3 issue 4 (18 point pairs over 4 waves)
-  const int nu = (18 - wave + NW - 1) / NW;
-  const int nx = (NXI - wave + NW - 1) / NW;  // this wave's X DMAs per chunk
-  // wait until at most the ``keep`` youngest of this wave's DMAs are in flight (vmcnt is in-order)
-  auto wait_keep = [&](int keep) {
-    switch (keep) {
-      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-      case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-      case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-      case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-      case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-      case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-      case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-      case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-      case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-      case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-      case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
-      case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-      case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
-      case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-  };
-
-  // DMA order per wave: [X(c_lo)] [X(c_lo+1)] U0(c_lo) | per chunk c: U1(c) ... U0(c+1) X(c+2)
-  // Top of chunk c (in flight, youngest last): U0(c) is followed by nothing at c = c_lo except
-  // itself; later X(c+1) was issued after U0(c) (same mid-chunk batch: U0(c) then X(c+1)), so
-  // U0(c) + X(c) landed <=> at most this wave's X(c+1) DMAs are still in flight.
-  stage_x(8 * c_lo, xs0);
-  stage_u(8 * c_lo, 0);
-  if (c_lo + 1 < nc) stage_x(8 * (c_lo + 1), xs1);
-  for (int c = c_lo; c < nc; ++c) {
-    float* xb = ((c - c_lo) & 1) ? xs1 : xs0;  // X(c)
-    // c_lo: issued X(c), U0(c), X(c+1): keep X(c+1). c > c_lo: ... U0(c), X(c+1): keep X(c+1).
-    wait_keep(c + 1 < nc ? nx : 0);
-    lds_barrier();  // U0(c), X(c) visible; every wave is done with U1(c-1)
-    stage_u(8 * c, 1);
-    f2v v[36];
-    {
-      const float* p0 = xb + poff;
-#pragma unroll
-      for (int q = 0; q < 6; ++q)
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          f2v d = {0.f, 0.f};
-          if constexpr (S == 4) {
-            if (r >= 1 && r <= 4 && q >= 1 && q <= 4) d = *reinterpret_cast<const f2v*>(p0 + ((r - 1) * 4 + (q - 1)) * 4);
-          } else {
-            d = *reinterpret_cast<const f2v*>(p0 + (r * G::RWP + q + (G::PAD && q >= 4 ? 1 : 0)) * 4);
-          }
-          v[r * 6 + q] = d;
-          __builtin_amdgcn_sched_barrier(0);  // one ds_read_b64 each (no ds_read2 merging)
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 6; ++q) bt6p(v[q], v[6 + q], v[12 + q], v[18 + q], v[24 + q], v[30 + q]);
-#pragma unroll
-    for (int r = 0; r < 6; ++r) bt6p(v[6 * r], v[6 * r + 1], v[6 * r + 2], v[6 * r + 3], v[6 * r + 4], v[6 * r + 5]);
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      if (e == 1) {
-        // U1(c) landed: in flight after it is nothing this chunk (X(c+1) was issued before it)
-        wait_keep(0);
-        lds_barrier();  // U1(c) visible; every wave is done with U0(c) and with its X(c) patch
-        if (c + 1 < nc) stage_u(8 * (c + 1), 0);
-        if (c + 2 < nc) stage_x(8 * (c + 2), xb);
-      }
-      const float* ue = ul + e * 18 * 256;
-      float2 wq[2][2];  // [pair parity][channel half]
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          wq[s2][h] = *reinterpret_cast<const float2*>(ue + s2 * 256 + h * 128);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-      for (int i = 0; i < 18; ++i) {
-        const float2 w0 = wq[i & 1][0], w1 = wq[i & 1][1];
-        if (i + 2 < 18) {
-          wq[i & 1][0] = *reinterpret_cast<const float2*>(ue + (i + 2) * 256);
-          __builtin_amdgcn_sched_barrier(0);
-          wq[i & 1][1] = *reinterpret_cast<const float2*>(ue + (i + 2) * 256 + 128);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        const int x = 2 * i;
-        const float a0 = e ? v[x].y : v[x].x, a1 = e ? v[x + 1].y : v[x + 1].x;
-        // the first group of a parity follows the transform / DMA-issue VALU code: 2 wait states;
-        // later groups follow only the B-operand ds_reads and their s_waitcnt (checked in the .s)
-        if (i == 0) W4W_MFMA4("a", "s_nop 1\n\t", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
-        else if (x < W4W_AGPR_POINTS) W4W_MFMA4("a", "", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
-        else W4W_MFMA4("v", "", acc[0][x], acc[1][x], acc[0][x + 1], acc[1][x + 1], a0, a1, w0, w1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-  (void)nu;
-  // the last MFMA's results -> the epilogue's reads: 12 wait states for an 8-pass XDL op
-  asm volatile("s_nop 15\n\ts_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (p.dbg & 16) {
-    float t = 0.f;
-#pragma unroll
-    for (int x = 0; x < NPT; ++x) t += acc[0][x][0] + acc[1][x][0];
-    if (t == 1234.5f) p.out[0] = t;
-    return;
-  }
-  epilogue<EPI, S, 4, 2>(p, acc, t0, k0, xs0, xs1, us);
-}
-
 // U = G g G^T into the LDS images: layout 0 (MODE 0/1): word ((x*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + e
 // of image (cb, kb) holds U[x][c = 8cb + 2g + e][k = 32kb + 16nh + j]; layout 1 (MODE 2): word
 // (((e*18 + x/2)*2 + nh)*16 + j)*8 + 2*(g ^ 2*(j >> 3)) + (x & 1) holds U[x][c = 8cb + 2g + e][k]. fp64, rounded once. flip_t: the
@@ -1507,13 +1031,14 @@ __global__ __launch_bounds__(256) void weight_transform_multi(const long long* _
   }
 }
 
-// TP_W4_MODE (read once): 0 pipelined 1 block/CU, 1 two blocks/CU, 2 packed transforms, 8 waves per
-// block, 3 (default) packed transforms, two 4-wave blocks per CU (the blocks' barriers are
-// independent, so one block's patch reads / transform run under the other's MFMAs: 1.3x MODE 2)
+// TP_W4_MODE (read once): 2 packed transforms, one 8-wave block per CU; 3 (default) packed
+// transforms, two 4-wave blocks per CU (the blocks' barriers are independent, so one block's patch
+// reads / transform run under the other's MFMAs: 1.3x MODE 2). The round-3 MODE 0/1 prototypes and
+// the WIDE kernel were measured slower and removed (profiles/wino4/).
 static int kernel_mode() {
   static const int mode = [] {
     const char* m = getenv("TP_W4_MODE");
-    return m ? atoi(m) : 3;
+    return m && atoi(m) == 2 ? 2 : 3;
   }();
   return mode;
 }
@@ -1531,7 +1056,7 @@ extern "C" hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, 
   if (st0 <= 0 || st1 <= 0 || st2 <= 0 || st3 <= 0) return hipErrorInvalidValue;
   const long long total = (long long)C * K;  // one thread per (input, output channel) pair
   const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
-  tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1, tp::w4::kernel_mode() >= 2, st0, st1,
+  tp::w4::weight_transform<<<grid, 256, 0, st>>>(w, u, K, C, flip_t, S0, S1, 1, st0, st1,
                                                  st2, st3);
   return hipGetLastError();
 }
@@ -1541,7 +1066,7 @@ extern "C" hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, 
 extern "C" hipError_t tp_wino4_weights_multi(const long long* desc, int n, long long total, hipStream_t st) {
   if (n <= 0 || total <= 0 || total % 256) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)std::min<long long>(total / 256, 16384);
-  tp::w4::weight_transform_multi<<<grid, 256, 0, st>>>(desc, n, total, tp::w4::kernel_mode() >= 2);
+  tp::w4::weight_transform_multi<<<grid, 256, 0, st>>>(desc, n, total, 1);
   return hipGetLastError();
 }
 
@@ -1584,24 +1109,28 @@ extern "C" hipError_t tp_conv_epilogue_slabs(const float* ws, int splits, int B,
                                               uint8_t* out_argmax, const float* act, float* taylor,
                                               float* apoz, int tay_mode, hipStream_t st);
 
-// variant 0: the TP_W4_MODE kernel (default MODE 3); variant 1: the WIDE kernel (64-tile blocks,
-// one wave per SIMD, each wave 16 tiles x 32 outputs); variant 2: MODE 3 with spread U DMA;
+// variant 0: the TP_W4_MODE kernel (default MODE 3); variant 2: MODE 3 with spread U DMA;
 // variant 3: MODE 3 with split points (each wave 18 points x 32 outputs, half the transform).
-extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi,
-                                    const float* scale, const float* shift, int relu, float* out, uint8_t* out_argmax,
-                                    const float* act, float* taylor, float* apoz, int tay_mode, int splits,
-                                    float* ws, int variant, hipStream_t st, const uint8_t* unpool_am) {
+// ko (0 = K): output channels stored per pixel (K rounded down to them: ko % 4 == 0, K - 32 < ko <=
+// K): the U images and the MFMAs cover K = ko rounded up to 32, the outputs, activations, BN
+// scale / shift, Taylor / APoZ slabs have ko channels — pruned widths stay unpadded in HBM.
+extern "C" hipError_t tp_conv_wino4_ko(const float* x, const float* u, int B, int S, int C, int K, int epi,
+                                       const float* scale, const float* shift, int relu, float* out,
+                                       uint8_t* out_argmax, const float* act, float* taylor, float* apoz, int tay_mode,
+                                       int splits, float* ws, int variant, hipStream_t st, const uint8_t* unpool_am,
+                                       int ko) {
   using namespace tp::w4;
   if (!tp_wino4_ok(S, S, C, K) || B <= 0) return hipErrorInvalidValue;
+  if (ko == 0) ko = K;
+  if (ko % 4 || ko > K || ko <= K - TK) return hipErrorInvalidValue;
   // band geometry (56 / 28 / 14 / 7-pixel maps): the split-points kernel, no pooling / unpooling
   const bool band = wino4_band_size(S);
   if (band && (variant != 3 || epi == FWD_POOL || unpool_am)) return hipErrorInvalidValue;
   const int nc = C / 8;
   splits = std::max(1, std::min(splits, nc));
   splits = (nc + (nc + splits - 1) / splits - 1) / ((nc + splits - 1) / splits);  // no empty split
-  if (variant < 0 || variant > 3) return hipErrorInvalidValue;
-  const bool wide = variant == 1;
-  if (splits > 1 && ((variant == 0 && kernel_mode() < 2) || !ws)) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 3 || variant == 1) return hipErrorInvalidValue;
+  if (splits > 1 && (!ws || ko != K)) return hipErrorInvalidValue;  // the slab combine writes K-wide rows
   if (epi < 0 || epi > 2 || (epi == BWD && !act) || (epi != BWD && !out) || (epi == FWD_POOL && !out_argmax))
     return hipErrorInvalidValue;
   // fused unpooling: the data gradient's full-resolution output, one K pass (the split-K combine
@@ -1614,6 +1143,7 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   a.B = B;
   a.C = C;
   a.K = K;
+  a.ko = ko;
   const int tpr = (S + 3) / 4;
   a.P = B * tpr * tpr;
   a.x_elems = (long long)B * S * S * C;
@@ -1638,9 +1168,9 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   }();
   a.dbg = dbg;
   // 5: MODE 3 with SPREAD DMA; 6: MODE 3 with split points
-  const int mode = wide ? 4 : variant == 2 ? 5 : variant == 3 ? 6 : kernel_mode();
-  const int tb = mode == 2 || mode == 4 ? 64 : TILES;  // MODE 3: 32-tile blocks
-  const int br = band ? 32 / tpr : 0;                  // band: whole tile rows per block
+  const int mode = variant == 2 ? 5 : variant == 3 ? 6 : kernel_mode();
+  const int tb = mode == 2 ? 64 : TILES;  // MODE 3: 32-tile blocks
+  const int br = band ? 32 / tpr : 0;     // band: whole tile rows per block
   const int n_p = band ? (B * tpr + br - 1) / br : (a.P + tb - 1) / tb, n_k = K / TK;
   const dim3 grid(n_p * n_k, splits);
   if (splits > 1) {
@@ -1660,40 +1190,32 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
       else if (S == 28) wino4_m2<PARTIAL, 28, 4, false, true><<<grid, 256, 0, st>>>(b);
       else if (S == 14) wino4_m2<PARTIAL, 14, 4, false, true><<<grid, 256, 0, st>>>(b);
       else wino4_m2<PARTIAL, 7, 4, false, true><<<grid, 256, 0, st>>>(b);
-      const hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-      return tp_conv_epilogue_slabs(ws, splits, B, S, S, K, epi, scale, epi == BWD ? nullptr : shift, relu, out,
-                                    out_argmax, act, epi == BWD ? taylor : nullptr, epi == BWD ? nullptr : apoz,
-                                    tay_mode, st);
-    }
+    } else {
 #define TP_W4P(SS)                                                                      \
   do {                                                                                  \
-    if (mode == 4) wino4_wide<PARTIAL, SS><<<grid, 256, 0, st>>>(b);                    \
-    else if (mode == 6) wino4_m2<PARTIAL, SS, 4, false, true><<<grid, 256, 0, st>>>(b); \
+    if (mode == 6) wino4_m2<PARTIAL, SS, 4, false, true><<<grid, 256, 0, st>>>(b);      \
     else if (mode == 5) wino4_m2<PARTIAL, SS, 4, true><<<grid, 256, 0, st>>>(b);        \
     else if (mode == 2) wino4_m2<PARTIAL, SS, 8><<<grid, 512, 0, st>>>(b);              \
     else wino4_m2<PARTIAL, SS, 4><<<grid, 256, 0, st>>>(b);                             \
   } while (0)
-    if (S == 32) TP_W4P(32);
-    else if (S == 16) TP_W4P(16);
-    else if (S == 8) TP_W4P(8);
-    else TP_W4P(4);
+      if (S == 32) TP_W4P(32);
+      else if (S == 16) TP_W4P(16);
+      else if (S == 8) TP_W4P(8);
+      else TP_W4P(4);
 #undef TP_W4P
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return tp_conv_epilogue_slabs(ws, splits, B, S, S, K, epi, scale, epi == BWD ? nullptr : shift, relu, out,
                                   out_argmax, act, epi == BWD ? taylor : nullptr, epi == BWD ? nullptr : apoz,
                                   tay_mode, st);
   }
-#define TP_W4(E, SS)                                              \
-  do {                                                            \
-    if (mode == 4) wino4_wide<E, SS><<<grid, 256, 0, st>>>(a);    \
-    else if (mode == 6) wino4_m2<E, SS, 4, false, true><<<grid, 256, 0, st>>>(a); \
-    else if (mode == 5) wino4_m2<E, SS, 4, true><<<grid, 256, 0, st>>>(a); \
-    else if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a); \
-    else if (mode == 3) wino4_m2<E, SS, 4><<<grid, 256, 0, st>>>(a); \
-    else if (mode == 1) wino4_f4x3<E, SS, 1><<<grid, 256, 0, st>>>(a); \
-    else wino4_f4x3<E, SS, 0><<<grid, 256, 0, st>>>(a);          \
+#define TP_W4(E, SS)                                                             \
+  do {                                                                           \
+    if (mode == 6) wino4_m2<E, SS, 4, false, true><<<grid, 256, 0, st>>>(a);     \
+    else if (mode == 5) wino4_m2<E, SS, 4, true><<<grid, 256, 0, st>>>(a);       \
+    else if (mode == 2) wino4_m2<E, SS, 8><<<grid, 512, 0, st>>>(a);             \
+    else wino4_m2<E, SS, 4><<<grid, 256, 0, st>>>(a);                            \
   } while (0)
 #define TP_W4S(E)                   \
   do {                              \
@@ -1723,29 +1245,32 @@ extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S
   return hipGetLastError();
 }
 
+extern "C" hipError_t tp_conv_wino4(const float* x, const float* u, int B, int S, int C, int K, int epi,
+                                    const float* scale, const float* shift, int relu, float* out, uint8_t* out_argmax,
+                                    const float* act, float* taylor, float* apoz, int tay_mode, int splits,
+                                    float* ws, int variant, hipStream_t st, const uint8_t* unpool_am) {
+  return tp_conv_wino4_ko(x, u, B, S, C, K, epi, scale, shift, relu, out, out_argmax, act, taylor, apoz, tay_mode,
+                          splits, ws, variant, st, unpool_am, K);
+}
+
 // static LDS bytes of a wino4 instantiation (occupancy / budget guard)
 extern "C" int tp_wino4_lds_bytes(int S, int variant) {
   using namespace tp::w4;
-  const int m = variant == 1 ? 4 : variant >= 2 ? 3 : kernel_mode();
+  const int m = variant >= 2 ? 3 : kernel_mode();
   const void* f = nullptr;
   if (wino4_band_size(S)) {
     f = S == 56 ? (const void*)wino4_m2<BWD, 56, 4, false, true>
         : S == 28 ? (const void*)wino4_m2<BWD, 28, 4, false, true>
         : S == 14 ? (const void*)wino4_m2<BWD, 14, 4, false, true>
                   : (const void*)wino4_m2<BWD, 7, 4, false, true>;
-    hipFuncAttributes at{};
-    if (hipFuncGetAttributes(&at, f) != hipSuccess) return -1;
-    return (int)at.sharedSizeBytes;
-  }
-#define TP_W4F(SS)                                                                            \
-  f = m == 4 ? (const void*)wino4_wide<BWD, SS>                                               \
-             : m == 2 ? (const void*)wino4_m2<BWD, SS, 8>                                     \
-             : m == 3 ? (const void*)wino4_m2<BWD, SS, 4> : (const void*)wino4_f4x3<BWD, SS, 0>
-  if (S == 32) TP_W4F(32);
-  else if (S == 16) TP_W4F(16);
-  else if (S == 8) TP_W4F(8);
-  else TP_W4F(4);
+  } else {
+#define TP_W4F(SS) f = m == 2 ? (const void*)wino4_m2<BWD, SS, 8> : (const void*)wino4_m2<BWD, SS, 4>
+    if (S == 32) TP_W4F(32);
+    else if (S == 16) TP_W4F(16);
+    else if (S == 8) TP_W4F(8);
+    else TP_W4F(4);
 #undef TP_W4F
+  }
   hipFuncAttributes at{};
   if (hipFuncGetAttributes(&at, f) != hipSuccess) return -1;
   return (int)at.sharedSizeBytes;

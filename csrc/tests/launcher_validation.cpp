@@ -31,9 +31,10 @@ hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u,
                         int unpool, int epi, int splits, int staged, const float* scale, const float* shift, int relu,
                         float* out, uint8_t* out_argmax, const float* act, float* taylor, float* apoz, float* ws,
                         int tay_mode, hipStream_t st);
-hipError_t tp_gemm1x1_ws(const float* x, const float* w, int B, int H, int W, int Cin, int N, int stride,
-                         const float* scale, const float* shift, int relu, float slope, const float* res,
-                         const float* mask, float* apoz, float* out, int variant, hipStream_t st);
+hipError_t tp_conv_wino4_ko(const float* x, const float* u, int B, int S, int C, int K, int epi, const float* scale,
+                            const float* shift, int relu, float* out, uint8_t* out_argmax, const float* act,
+                            float* taylor, float* apoz, int tay_mode, int splits, float* ws, int variant,
+                            hipStream_t st, const uint8_t* unpool_am, int ko);
 hipError_t tp_pack_conv_weights_multi(const long long* desc, int n, long long total, hipStream_t st);
 hipError_t tp_wino4_weights_multi(const long long* desc, int n, long long total, hipStream_t st);
 hipError_t tp_wino4_weights_strided(const float* w, float* u, int K, int C, int flip_t, int S0, int S1, long long st0,
@@ -55,6 +56,7 @@ static int failures = 0;
 int main() {
   // geometry helpers
   EXPECT(tp_conv_gen_k(3, 64) == 576);
+  EXPECT(tp_conv_gen_k(3, 104) == 9 * 128 && tp_conv_gen_k(1, 52) == 64);  // pruned widths: 32-padded taps
   EXPECT(tp_conv_gen_k(7, 4) == 224);
   EXPECT(tp_wino_taylor_slots(2, 2) == 1);
   EXPECT(tp_wino_taylor_slots(32, 32) == 4);
@@ -71,8 +73,8 @@ int main() {
 
   // launchers reject unsupported shapes before any GPU work (null pointers are never touched)
   float* n = nullptr;
-  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 48, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
-         hipErrorInvalidValue);  // Cin % 32
+  EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 50, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
+         hipErrorInvalidValue);  // Cin % 4 (pruned widths: any multiple of 4 from 8 up)
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 62, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
          hipErrorInvalidValue);  // Cout % 4
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 5, 2, 2, 1, 16, 16, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
@@ -100,19 +102,13 @@ int main() {
          hipErrorInvalidValue);  // bf16 U images (staged bit 1) without a staged input mode
   EXPECT(tp_conv_wino(n, nullptr, n, 2, 7, 7, 64, 64, 0, 0, 1, 3, n, n, 0, n, nullptr, n, n, n, n, 0, 0) ==
          hipErrorInvalidValue);  // bf16 on an odd map (direct loads only)
-  EXPECT(tp_bn_fwd_train(n, n, 16, 6, n, n, 1e-5f, 0.1f, n, n, n, n, n, n, nullptr, 0) == hipErrorInvalidValue);
-  // warp-specialised 1x1 GEMM (conv_gen cfgs 16-18): Cin % 32, N % 4, stride, slope, variant, 2^31-byte bounds,
-  // and the conv_gen entry's 1x1 / no-pad / dense-residual / no-bnpart gate
-  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 48, 64, 1, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
-  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 62, 1, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
-  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 64, 0, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
-  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 64, 1, n, n, 1, -0.5f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
-  EXPECT(tp_gemm1x1_ws(n, n, 2, 8, 8, 64, 64, 1, n, n, 0, 0.f, n, n, n, n, 3, 0) == hipErrorInvalidValue);
-  EXPECT(tp_gemm1x1_ws(n, n, 4096, 128, 128, 64, 64, 1, n, n, 0, 0.f, n, n, n, n, 0, 0) == hipErrorInvalidValue);
+  EXPECT(tp_bn_fwd_train(n, n, 0, 6, n, n, 1e-5f, 0.1f, n, n, n, n, n, n, nullptr, 0) == hipErrorInvalidValue);  // P = 0
+  EXPECT(tp_bn_fwd_train(n, n, 1 << 20, 1 << 12, n, n, 1e-5f, 0.1f, n, n, n, n, n, n, nullptr, 0) ==
+         hipErrorInvalidValue);  // P * C >= 2^32 elements
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 3, 1, 1, 0, 0, 0, 16, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
-         hipErrorInvalidValue);  // cfg 16 is 1x1 only
+         hipErrorInvalidValue);  // unknown tile config
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 17, 1, n, n, 0, n, 2, n, n, n, n, 0) ==
-         hipErrorInvalidValue);  // strided residual
+         hipErrorInvalidValue);  // unknown tile config
   // stream-K (cfg | 32): GEN 1 only, one K pass, a fixup workspace, ks 1 / 3; no workspace is
   // asked for where it cannot apply (transposed, 5x5, warp-specialised cfgs)
   EXPECT(tp_conv_gen2(n, n, 2, 8, 8, 64, 64, 3, 2, 1, 1, 16, 16, 32, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
@@ -127,7 +123,7 @@ int main() {
          hipErrorInvalidValue);  // 4-channel stem (GEN 2)
   EXPECT(tp_conv_sk_ws_floats(0, 1, 1, 0, 1 << 20, 512) == 0);  // transposed
   EXPECT(tp_conv_sk_ws_floats(0, 5, 0, 0, 1 << 20, 512) == 0);  // 5x5
-  EXPECT(tp_conv_sk_ws_floats(16, 1, 0, 0, 1 << 20, 512) == 0); // warp-specialised cfg
+  EXPECT(tp_conv_sk_ws_floats(16, 1, 0, 0, 1 << 20, 512) == 0); // unknown cfg
   EXPECT(tp_conv_sk_ws_floats(0, 3, 0, 1, 1 << 20, 512) == 0);  // Taylor partials are 1x1 only
   // F(4x4): VGG sizes and the band geometry's ResNet sizes; bands never pool / unpool and only the
   // split-points kernel (variant 3) has them; Taylor slots per image = the most bands overlapping it
@@ -141,6 +137,17 @@ int main() {
          hipErrorInvalidValue);  // band on the MODE 3 kernel
   EXPECT(tp_conv_wino4(n, n, 2, 14, 64, 64, 2, n, n, 0, n, nullptr, n, n, n, 0, 1, n, 3, 0,
                        reinterpret_cast<const uint8_t*>(n)) == hipErrorInvalidValue);  // dgrad without act
+  // unpadded output widths (ko): a multiple of 4 inside the last 32-channel block, one K pass
+  EXPECT(tp_conv_wino4_ko(n, n, 2, 56, 64, 64, 0, n, n, 1, n, nullptr, n, n, n, 0, 1, n, 3, 0, nullptr, 30) ==
+         hipErrorInvalidValue);  // ko % 4
+  EXPECT(tp_conv_wino4_ko(n, n, 2, 56, 64, 64, 0, n, n, 1, n, nullptr, n, n, n, 0, 1, n, 3, 0, nullptr, 28) ==
+         hipErrorInvalidValue);  // ko <= K - 32: a whole empty channel block
+  EXPECT(tp_conv_wino4_ko(n, n, 2, 56, 64, 64, 0, n, n, 1, n, nullptr, n, n, n, 0, 1, n, 3, 0, nullptr, 68) ==
+         hipErrorInvalidValue);  // ko > K
+  EXPECT(tp_conv_wino4_ko(n, n, 2, 56, 64, 64, 0, n, n, 1, n, nullptr, n, n, n, 0, 2, n, 3, 0, nullptr, 60) ==
+         hipErrorInvalidValue);  // split-K slabs are K wide
+  EXPECT(tp_conv_wino4_ko(n, n, 2, 32, 64, 64, 0, n, n, 1, n, nullptr, n, n, n, 0, 1, n, 1, 0, nullptr, 0) ==
+         hipErrorInvalidValue);  // the removed WIDE variant
   EXPECT(tp_pack_conv_weights_multi(nullptr, 0, 16, nullptr) == hipErrorInvalidValue);  // no operands
   EXPECT(tp_pack_conv_weights_multi(nullptr, 2, 0, nullptr) == hipErrorInvalidValue);   // nothing to write
   EXPECT(tp_wino4_weights_multi(nullptr, 1, 100, nullptr) == hipErrorInvalidValue);     // not whole blocks

@@ -1,0 +1,182 @@
+"""Pruned (odd) channel widths on the native training kernels (VERDICT r5 "next round" #1): the
+training BatchNorm at any width (per-element path when C % 4 != 0) and on padded activations
+(``cr`` < carried width), the implicit GEMMs' K tail (Cin % 32 != 0: the last 32-wide K slice of a
+tap is zero-filled past the real width in the loads), the F(4x4) kernels' unpadded output width
+(``ko``), and whole pruned residual blocks at ResNet-50's 56/28/14/7-pixel maps — each against an
+fp64 PyTorch reference. Widths: ResNet-50 after one / two 20 % prunes (52 / 103 / 205 / 410 and
+42 / 83), the reference's arbitrary index sets (pruner.py:94-115)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+WIDTHS = [42, 52, 83, 103, 205, 410]
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("C", WIDTHS)
+@pytest.mark.parametrize("affine", [True, False])
+def test_bn_any_width_matches_fp64(cuda, C, affine):
+    """Standalone native training BN at the module's own (unpadded) width: statistics, running
+    statistics, normalisation and backward vs fp64 F.batch_norm (C % 4 != 0: per-element path)."""
+    from torchpruner_amd.engine.train import native_convs
+    torch.manual_seed(C)
+    bn = torch.nn.BatchNorm2d(C, affine=affine).to(cuda).train()
+    if affine:
+        bn.weight.data.uniform_(0.5, 1.5)
+        bn.bias.data.uniform_(-0.5, 0.5)
+    ref = copy.deepcopy(bn).double()
+    x = _cl(torch.randn(3, C, 7, 9, device=cuda) * 3 + 1).requires_grad_(True)
+    gy = _cl(torch.randn(3, C, 7, 9, device=cuda))
+    xr = x.detach().double().requires_grad_(True)
+    with native_convs(bn) as sw:
+        assert sw == [bn]
+        y = bn(x)
+    y.backward(gy)
+    yr = ref(xr)
+    yr.backward(gy.double())
+    torch.testing.assert_close(y.double(), yr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x.grad.double(), xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_mean.double(), ref.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.running_var.double(), ref.running_var, rtol=1e-5, atol=1e-5)
+    if affine:
+        torch.testing.assert_close(bn.weight.grad.double(), ref.weight.grad, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(bn.bias.grad.double(), ref.bias.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("C", WIDTHS)
+@pytest.mark.parametrize("relu,with_res", [(True, False), (False, False), (True, True)])
+def test_bn_on_padded_activation(cuda, C, relu, with_res):
+    """bn_act on an activation carried at _act_w(C) channels (zeros past C): the real channels
+    match fp64 relu?(BN(x) + res?), the padding stays exactly zero forward and backward, and the
+    parameter / running-stat shapes stay the module's."""
+    from torchpruner_amd.engine.train import _act_w, bn_act
+    torch.manual_seed(C + 7)
+    Cp = _act_w(C)
+    bn = torch.nn.BatchNorm2d(C).to(cuda).train()
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-0.3, 0.3)
+    bn64 = copy.deepcopy(bn).double()
+    x = torch.randn(2, C, 14, 14, device=cuda) * 2 + 0.5
+    r = torch.randn(2, C, 14, 14, device=cuda) if with_res else None
+    xp = _cl(F.pad(x, (0, 0, 0, 0, 0, Cp - C))).requires_grad_(True)
+    rp = _cl(F.pad(r, (0, 0, 0, 0, 0, Cp - C))).requires_grad_(True) if with_res else None
+    y = bn_act(bn, xp, res=rp, relu=relu)
+    assert y.shape[1] == Cp
+    assert (y[:, C:] == 0).all()
+    gy = torch.randn_like(y)
+    gy[:, C:] = 0  # a consumer conv's data gradient is zero on the padding (zero weights there)
+    y.backward(gy)
+    x64 = x.double().requires_grad_(True)
+    r64 = r.double().requires_grad_(True) if with_res else None
+    y64 = bn64(x64) + (r64 if with_res else 0)
+    y64 = F.relu(y64) if relu else y64
+    y64.backward(gy[:, :C].double())
+    torch.testing.assert_close(y[:, :C].double(), y64, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(xp.grad[:, :C].double(), x64.grad, rtol=1e-4, atol=1e-4)
+    assert (xp.grad[:, C:] == 0).all()
+    if with_res:
+        torch.testing.assert_close(rp.grad[:, :C].double(), r64.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.weight.grad.double(), bn64.weight.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bn.bias.grad.double(), bn64.bias.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(bn.running_mean.double(), bn64.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.running_var.double(), bn64.running_var, rtol=1e-5, atol=1e-5)
+
+
+def _policy(pred):
+    """Autotuner.pinned policy: the first candidate ``pred`` accepts (else the untuned pick)."""
+    return lambda key, lst, M, N, K: next((c for c in lst if pred(c)), None)
+
+
+_FAMILIES = {
+    "igemm": lambda c: 0 <= c[0] <= 6,
+    "streamk": lambda c: c[0] >= 0 and c[0] & 32 and not c[0] & 64,
+    "sb": lambda c: c[0] >= 0 and c[0] & 64 > 0,
+    "wino4": lambda c: c[0] == -8,
+}
+
+
+@pytest.mark.parametrize("cin,cout", [(42, 83), (103, 52), (205, 410), (52, 205), (83, 103)])
+@pytest.mark.parametrize("ks,stride", [(1, 1), (1, 2), (3, 1), (3, 2)])
+@pytest.mark.parametrize("family", list(_FAMILIES))
+def test_conv_odd_widths_match_fp64(cuda, cin, cout, ks, stride, family):
+    """A native conv at pruned widths, with one kernel family pinned (implicit GEMM, stream-K,
+    single-buffered 1x1, F(4x4) band kernels): forward / input / weight gradients vs fp64, at the
+    module's width and from a padded (carried-width) input with a carried-width output."""
+    from torchpruner_amd.engine.fused_chain import TUNER
+    from torchpruner_amd.engine.train import _act_w, _NativeConv2d, native_convs
+    torch.manual_seed(cin * 3 + cout + ks + stride)
+    pad = ks // 2
+    conv = torch.nn.Conv2d(cin, cout, ks, stride=stride, padding=pad, bias=False).to(cuda)
+    x = _cl(torch.randn(2, cin, 14, 14, device=cuda))
+    c64 = copy.deepcopy(conv).double()
+    x64 = x.double().requires_grad_(True)
+    y64 = c64(x64)
+    g = torch.randn(y64.shape, device=cuda, dtype=torch.float64)
+    (y64 * g).sum().backward()
+    with TUNER.pinned(_policy(_FAMILIES[family])):
+        xa = x.clone().requires_grad_(True)
+        with native_convs(conv):
+            y = conv(xa)
+        (y * g.float()).sum().backward()
+        torch.testing.assert_close(y.double(), y64, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(xa.grad.double(), x64.grad, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(conv.weight.grad.double(), c64.weight.grad, rtol=1e-4, atol=2e-3)
+        # carried widths: padded input in, padded output out (the residual-block flow)
+        conv.weight.grad = None
+        cin_p, cout_p = _act_w(cin), _act_w(cout)
+        xp = _cl(F.pad(x, (0, 0, 0, 0, 0, cin_p - cin))).requires_grad_(True)
+        yp = _NativeConv2d.apply(xp, conv.weight, None, ks, stride, pad, True)
+        assert yp.shape[1] == cout_p and (yp[:, cout:] == 0).all()
+        gp = F.pad(g.float(), (0, 0, 0, 0, 0, cout_p - cout))
+        (yp * gp).sum().backward()
+        torch.testing.assert_close(yp[:, :cout].double(), y64, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(xp.grad[:, :cin].double(), x64.grad, rtol=1e-4, atol=1e-4)
+        assert (xp.grad[:, cin:] == 0).all()
+        torch.testing.assert_close(conv.weight.grad.double(), c64.weight.grad, rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("frac", [0.2, 0.36])
+def test_pruned_bottlenecks_resnet50_maps(cuda, frac):
+    """A ResNet-50-shaped net (one bottleneck per stage, 224 px: 56/28/14/7-pixel maps) pruned like
+    config #5 (``frac`` of every prunable bottleneck conv: 20 % = one round, 36 % ~ two), one
+    training step on the native kernels (carried widths through every block) vs fp32 autograd:
+    loss, every parameter gradient and the BN running statistics."""
+    import numpy as np
+    from torchpruner_amd import Pruner, get_resnet_pruning_graph
+    from torchpruner_amd.engine.train import native_convs
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    torch.manual_seed(1)
+    model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=10).to(cuda)
+    rng = np.random.RandomState(0)
+    pruner = Pruner(model, (3, 224, 224), cuda)
+    for module, cascade in get_resnet_pruning_graph(model):
+        n = module.weight.shape[0]
+        pruner.prune_model(module, rng.choice(n, int(n * frac), replace=False), cascade)
+    widths = sorted({m.out_channels for m in model.modules() if isinstance(m, torch.nn.Conv2d)})
+    assert any(w % 8 for w in widths), widths  # really odd widths
+    model = model.to(memory_format=torch.channels_last).train()
+    ref = copy.deepcopy(model)
+    x = _cl(torch.randn(2, 3, 224, 224, device=cuda))
+    y = torch.randint(0, 10, (2,), device=cuda)
+
+    def step(m, native):
+        m.zero_grad(set_to_none=True)
+        with native_convs(m, enable=native):
+            loss = F.cross_entropy(m(x), y)
+            loss.backward()
+        return float(loss), [p.grad.double() for p in m.parameters()]
+
+    l_n, g_n = step(model, True)
+    l_r, g_r = step(ref, False)
+    assert abs(l_n - l_r) < 1e-4 * max(1.0, abs(l_r))
+    for (name, _), a, b in zip(model.named_parameters(), g_n, g_r):
+        assert (a - b).abs().max().item() <= 2e-3 * b.abs().max().item() + 1e-6, name
+    for (n1, b1), (_, b2) in zip(model.named_buffers(), ref.named_buffers()):
+        torch.testing.assert_close(b1.float(), b2.float(), rtol=1e-4, atol=1e-5, msg=n1)

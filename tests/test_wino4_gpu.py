@@ -25,7 +25,7 @@ def _fwd_ref(x, w, sc, sh):
 
 
 @pytest.mark.parametrize("S,C,K,B", SHAPES)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])  # 1: wide, 2: MODE 3 + spread DMA, 3: split points
+@pytest.mark.parametrize("variant", [0, 2, 3])  # 2: MODE 3 + spread DMA, 3: split points
 def test_wino4_forward(cuda, S, C, K, B, variant):
     T = _ops()
     g = torch.Generator(device=cuda).manual_seed(S * 1000 + C + K)
@@ -62,7 +62,7 @@ def test_wino4_forward(cuda, S, C, K, B, variant):
 
 @pytest.mark.parametrize("S,C,K,B", SHAPES)
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 2, 3])
 def test_wino4_dgrad(cuda, S, C, K, B, mode, variant):
     """dgrad of conv(Cin=K -> Cout=C): g (B,S,S,C) -> dL/dact (B,S,S,K) with the W_BWD epilogue."""
     T = _ops()
@@ -86,7 +86,7 @@ def test_wino4_dgrad(cuda, S, C, K, B, mode, variant):
     got_t = tay.double().sum(0)
     errt = ((got_t - ref_t).abs().max() / ref_t.abs().max()).item()
     assert errt < 2e-5, errt
-    if S != 32 or variant == 1:
+    if S != 32:
         assert tay[1].abs().max().item() == 0.0  # whole images per block: slot 0 only
 
 
@@ -95,7 +95,7 @@ def test_wino4_deterministic_and_lds_budget(cuda):
     x = torch.randn(7, 16, 16, 64, device=cuda)
     w = torch.randn(128, 64, 3, 3, device=cuda) * 0.05
     u = T.wino4_weights(w, False, 0, 0)
-    for variant in (0, 1, 2, 3):
+    for variant in (0, 2, 3):
         a1, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None, 1, variant)
         a2, _ = T.conv_wino4_fwd(x, u, None, None, False, False, None, 1, variant)
         assert torch.equal(a1, a2)
@@ -116,7 +116,7 @@ def test_wino4_rejects_bad_shapes(cuda):
 
 @pytest.mark.parametrize("S,C,K,B", [(32, 64, 64, 3), (16, 128, 96, 2), (8, 256, 64, 5), (4, 512, 64, 7)])
 @pytest.mark.parametrize("splits", [2, 4])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 2, 3])
 def test_wino4_split_k(cuda, S, C, K, B, splits, variant):
     """Channel split-K (raw slabs + the deterministic combine) == one K pass, all epilogues."""
     T = _ops()

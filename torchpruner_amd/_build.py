@@ -197,7 +197,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
     return OUT
 
 
-SANITIZE_SOURCES = ("wino4", "conv_mfma", "conv_wgrad", "winograd", "batchnorm", "gemm_ws", "weight_pack")  # longest compile first
+SANITIZE_SOURCES = ("wino4", "conv_mfma", "conv_wgrad", "winograd", "batchnorm", "weight_pack")  # longest compile first
 
 
 def build_host_sanitizer(verbose: bool = False) -> Path:

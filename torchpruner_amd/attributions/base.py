@@ -542,10 +542,12 @@ class _AttributionMetric(ABC):
                     accs[owner[b]].add(engine.per_sample(res[b])[:, :engine.real_width(b)], i)
 
         big = (lambda x: engine.max_batch(tuple(x.shape[1:]))) if crit is None else None
-        for i, x, y, lb in self._coalesced_batches(pipe is not None, big):
-            run_batch(i, x, y, lb)
-        if pipe is not None:
-            pipe.join()
+        try:
+            for i, x, y, lb in self._coalesced_batches(pipe is not None, big):
+                run_batch(i, x, y, lb)
+        finally:  # the tuner's in-flight concurrency is reset even if a batch raises
+            if pipe is not None:
+                pipe.join()
         return [accs[owner[b]] for b in blocks]
 
     def _resnet_grad_engine(self, eval_modules, why=None):
@@ -623,36 +625,38 @@ class _AttributionMetric(ABC):
         pipe = _BatchPipeline(eng) if stats and self._ckpt is None and crit is None else None
         # batches past the kernels' descriptor range run in slices (whole-batch loss scaling)
         big = (lambda x: eng.max_batch(tuple(x.shape[1:]))) if crit is None else None
-        with torch.no_grad():
-            # stats: epilogue partial slabs come back raw, (R, B, C); the fold sums their slots and
-            # takes |.| for Taylor in its one launch (|.| of the already-final slabs is a no-op)
-            take_abs = stats and mode == "taylor"
-            for i, x, y, lb in self._coalesced_batches(False, big):
-                def fold(res, dev=x.device):
-                    slabs = [res[m] for m in uniq]
-                    sums = [accs[first[m]].ensure_sum(res[m].shape[-1], dev, m.num_features) for m in uniq]
-                    for j in range(0, len(slabs), 16):
-                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], take_abs, 0)
+        try:
+            with torch.no_grad():
+                # stats: epilogue partial slabs come back raw, (R, B, C); the fold sums their slots and
+                # takes |.| for Taylor in its one launch (|.| of the already-final slabs is a no-op)
+                take_abs = stats and mode == "taylor"
+                for i, x, y, lb in self._coalesced_batches(False, big):
+                    def fold(res, dev=x.device):
+                        slabs = [res[m] for m in uniq]
+                        sums = [accs[first[m]].ensure_sum(res[m].shape[-1], dev, m.num_features) for m in uniq]
+                        for j in range(0, len(slabs), 16):
+                            ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], take_abs, 0)
 
-                if pipe is not None and pipe.take(x, y, lambda slot, x=x, y=y, lb=lb: eng.grad_scores(
-                        x, y, set(uniq), mode, loss_batch=lb, raw_slabs=True), fold):
-                    for m in uniq:
-                        accs[first[m]].count += x.shape[0]
-                    continue
-                with trace_range("tp.forward_backward"):
-                    res = eng.grad_scores(x, y, set(uniq), mode, crit, loss_batch=lb, raw_slabs=stats)
-                if stats:
-                    slabs = [res[m] for m in uniq]
-                    sums = [accs[first[m]].ensure_sum(res[m].shape[-1], x.device, m.num_features) for m in uniq]
-                    for j in range(0, len(slabs), 16):
-                        ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], take_abs, 0)
-                    for m in uniq:
-                        accs[first[m]].count += x.shape[0]
-                else:
-                    for m in uniq:
-                        accs[first[m]].add(res[m][:, :m.num_features].contiguous(), i)
-        if pipe is not None:
-            pipe.join()
+                    if pipe is not None and pipe.take(x, y, lambda slot, x=x, y=y, lb=lb: eng.grad_scores(
+                            x, y, set(uniq), mode, loss_batch=lb, raw_slabs=True), fold):
+                        for m in uniq:
+                            accs[first[m]].count += x.shape[0]
+                        continue
+                    with trace_range("tp.forward_backward"):
+                        res = eng.grad_scores(x, y, set(uniq), mode, crit, loss_batch=lb, raw_slabs=stats)
+                    if stats:
+                        slabs = [res[m] for m in uniq]
+                        sums = [accs[first[m]].ensure_sum(res[m].shape[-1], x.device, m.num_features) for m in uniq]
+                        for j in range(0, len(slabs), 16):
+                            ops.score_fold_(slabs[j:j + 16], sums[j:j + 16], take_abs, 0)
+                        for m in uniq:
+                            accs[first[m]].count += x.shape[0]
+                    else:
+                        for m in uniq:
+                            accs[first[m]].add(res[m][:, :m.num_features].contiguous(), i)
+        finally:  # the tuner's in-flight concurrency is reset even if a batch raises
+            if pipe is not None:
+                pipe.join()
         return [accs[first[m]] for m in eval_modules]
 
     def _forward_capture_pass(self, eval_modules, on_out):

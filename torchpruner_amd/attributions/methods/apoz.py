@@ -51,39 +51,41 @@ class APoZAttributionMetric(_AttributionMetric):
         uniq = sorted(owner)
         stats = accs[0].mode == "stats"
         pipe = _BatchPipeline(engine, graph_replay=True) if stats and self._ckpt is None else None
-        with torch.no_grad():
-            # small batches coalesced into one launch (per-sample counts: no loss involved)
-            for i, x, _y, _lb in self._coalesced_batches(pipe is not None,
-                                                         lambda x: engine.max_batch(tuple(x.shape[1:]))):
-                B = x.shape[0]
+        try:
+            with torch.no_grad():
+                # small batches coalesced into one launch (per-sample counts: no loss involved)
+                for i, x, _y, _lb in self._coalesced_batches(pipe is not None,
+                                                             lambda x: engine.max_batch(tuple(x.shape[1:]))):
+                    B = x.shape[0]
 
-                def launch(slot, x=x):
-                    if engine.graphs_enabled(x.shape[0], pipelined=True):  # host-bound otherwise
-                        return engine.apoz_graphed(x, uniq, slot, warm=True)
-                    bufs = {b: torch.zeros(x.shape[0], engine._block_width(b), device=x.device) for b in uniq}
+                    def launch(slot, x=x):
+                        if engine.graphs_enabled(x.shape[0], pipelined=True):  # host-bound otherwise
+                            return engine.apoz_graphed(x, uniq, slot, warm=True)
+                        bufs = {b: torch.zeros(x.shape[0], engine._block_width(b), device=x.device) for b in uniq}
+                        engine.forward(x, stop_after=uniq[-1], apoz=bufs)
+                        return bufs
+
+                    def fold(bufs, dev=x.device):
+                        sums = [accs[owner[b]].ensure_sum(bufs[b].shape[1], dev, engine.real_width(b)) for b in uniq]
+                        ops.score_fold_([bufs[b] for b in uniq], sums, False, 0)
+
+                    if pipe is not None and pipe.take(x, None, launch, fold):  # two batches in flight (small B)
+                        for b in uniq:
+                            accs[owner[b]].count += B
+                        continue
+                    bufs = {b: torch.zeros(B, engine._block_width(b), device=x.device) for b in uniq}
                     engine.forward(x, stop_after=uniq[-1], apoz=bufs)
-                    return bufs
-
-                def fold(bufs, dev=x.device):
-                    sums = [accs[owner[b]].ensure_sum(bufs[b].shape[1], dev, engine.real_width(b)) for b in uniq]
-                    ops.score_fold_([bufs[b] for b in uniq], sums, False, 0)
-
-                if pipe is not None and pipe.take(x, None, launch, fold):  # two batches in flight (small B)
-                    for b in uniq:
-                        accs[owner[b]].count += B
-                    continue
-                bufs = {b: torch.zeros(B, engine._block_width(b), device=x.device) for b in uniq}
-                engine.forward(x, stop_after=uniq[-1], apoz=bufs)
-                if stats:
-                    sums = [accs[owner[b]].ensure_sum(bufs[b].shape[1], x.device, engine.real_width(b)) for b in uniq]
-                    ops.score_fold_([bufs[b] for b in uniq], sums, False, 0)
-                    for b in uniq:
-                        accs[owner[b]].count += B
-                else:
-                    for b in uniq:
-                        accs[owner[b]].add(bufs[b][:, :engine.real_width(b)], i)
-        if pipe is not None:
-            pipe.join()
+                    if stats:
+                        sums = [accs[owner[b]].ensure_sum(bufs[b].shape[1], x.device, engine.real_width(b)) for b in uniq]
+                        ops.score_fold_([bufs[b] for b in uniq], sums, False, 0)
+                        for b in uniq:
+                            accs[owner[b]].count += B
+                    else:
+                        for b in uniq:
+                            accs[owner[b]].add(bufs[b][:, :engine.real_width(b)], i)
+        finally:  # the tuner's in-flight concurrency is reset even if a batch raises
+            if pipe is not None:
+                pipe.join()
         return [accs[owner[b]] for b in blocks]
 
     def _engine_pass(self, eng, eval_modules, accs):
@@ -100,40 +102,42 @@ class APoZAttributionMetric(_AttributionMetric):
                 off += B * m.num_features
             return bufs
 
-        with torch.no_grad():
-            # batches past the kernels' descriptor range run in slices
-            for i, x, _y, _lb in self._coalesced_batches(False, lambda x: eng.max_batch(tuple(x.shape[1:]))):
-                B = x.shape[0]
+        try:
+            with torch.no_grad():
+                # batches past the kernels' descriptor range run in slices
+                for i, x, _y, _lb in self._coalesced_batches(False, lambda x: eng.max_batch(tuple(x.shape[1:]))):
+                    B = x.shape[0]
 
-                def launch(slot, x=x):
-                    bufs = views(torch.zeros(x.shape[0] * nf, device=x.device), x.shape[0])
+                    def launch(slot, x=x):
+                        bufs = views(torch.zeros(x.shape[0] * nf, device=x.device), x.shape[0])
+                        eng.forward(x, bufs)
+                        return bufs
+
+                    def fold(bufs, dev=x.device):
+                        sums = [accs[k].ensure_sum(m.num_features, dev) for k, m in enumerate(eval_modules)]
+                        ops.score_fold_([bufs[m] for m in eval_modules], sums, False, 0)
+
+                    if pipe is not None and pipe.take(x, None, launch, fold):  # two batches in flight
+                        for a in accs:
+                            a.count += B
+                        continue
+                    if arena is None or arena.shape[0] != B * sum(m.num_features for m in uniq) or not stats:
+                        arena = torch.zeros(B * sum(m.num_features for m in uniq), device=x.device)
+                    else:
+                        arena.zero_()
+                    bufs, off = {}, 0
+                    for m in uniq:
+                        bufs[m] = arena[off:off + B * m.num_features].view(B, m.num_features)
+                        off += B * m.num_features
                     eng.forward(x, bufs)
-                    return bufs
-
-                def fold(bufs, dev=x.device):
-                    sums = [accs[k].ensure_sum(m.num_features, dev) for k, m in enumerate(eval_modules)]
-                    ops.score_fold_([bufs[m] for m in eval_modules], sums, False, 0)
-
-                if pipe is not None and pipe.take(x, None, launch, fold):  # two batches in flight
-                    for a in accs:
-                        a.count += B
-                    continue
-                if arena is None or arena.shape[0] != B * sum(m.num_features for m in uniq) or not stats:
-                    arena = torch.zeros(B * sum(m.num_features for m in uniq), device=x.device)
-                else:
-                    arena.zero_()
-                bufs, off = {}, 0
-                for m in uniq:
-                    bufs[m] = arena[off:off + B * m.num_features].view(B, m.num_features)
-                    off += B * m.num_features
-                eng.forward(x, bufs)
-                if stats:  # one fold launch for every module's counts (fp64 column sums)
-                    sums = [accs[k].ensure_sum(m.num_features, x.device) for k, m in enumerate(eval_modules)]
-                    ops.score_fold_([bufs[m] for m in eval_modules], sums, False, 0)
-                    for a in accs:
-                        a.count += B
-                else:
-                    for k, m in enumerate(eval_modules):
-                        accs[k].add(bufs[m], i)
-        if pipe is not None:
-            pipe.join()
+                    if stats:  # one fold launch for every module's counts (fp64 column sums)
+                        sums = [accs[k].ensure_sum(m.num_features, x.device) for k, m in enumerate(eval_modules)]
+                        ops.score_fold_([bufs[m] for m in eval_modules], sums, False, 0)
+                        for a in accs:
+                            a.count += B
+                    else:
+                        for k, m in enumerate(eval_modules):
+                            accs[k].add(bufs[m], i)
+        finally:  # the tuner's in-flight concurrency is reset even if a batch raises
+            if pipe is not None:
+                pipe.join()

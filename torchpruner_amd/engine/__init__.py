@@ -16,9 +16,10 @@ def invalidate(model) -> bool:
     graphs). The engines re-pack when a parameter's storage or version counter changes, which
     covers optimizer steps, ``load_state_dict``, pruning and in-place edits under ``no_grad``;
     in-place edits through ``param.data`` bypass the version counter, so call this after them.
+    Also marks every cached training-conv weight pack stale (:func:`.train.invalidate_packs`).
     Returns True when something was cached."""
-    from . import fused_chain, resnet_engine
-    hit = False
+    from . import fused_chain, resnet_engine, train
+    hit = train.invalidate_packs() > 0
     for cache in (fused_chain._ENGINES, resnet_engine._ENGINES):
         if model in cache:
             if torch.cuda.is_available() and torch.cuda.is_initialized():

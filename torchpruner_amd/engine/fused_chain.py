@@ -50,7 +50,7 @@ WINO_LDS = -2  # the same with the block input region staged through LDS
 WINO_UNP = -3  # dgrad of a pooled layer: explicit vectorised unpool, then the staged kernel on the
                # dense full-resolution gradient (vs rebuilding it from pooled cells per chunk)
 WINO4 = -4  # Winograd F(4x4,3x3) kernel (wino4.hip): square 4/8/16/32-pixel maps, 1.78x fewer MFMAs
-WINO4W = -5  # the same transform, WIDE kernel: 64-tile blocks, one wave per SIMD, 32 outputs per wave
+# (-5 was the WIDE F(4x4) kernel: measured 0.8x MODE 3 on every VGG layer, removed in round 6)
 WINO_BF = -6  # bf16 operands (compute_dtype=bfloat16): the staged F(2x2) kernel with bf16 U images and
               # v_mfma_f32_16x16x16_bf16 (winograd.hip BF); fp32 transforms, accumulation and epilogues
 WINO_BF_UNP = -7  # its dgrad of a pooled layer after an explicit unpool (as WINO_UNP)
@@ -120,24 +120,16 @@ _TUNE_ROUNDS = int(os.environ.get("TORCHPRUNER_TUNE_ROUNDS", "3"))
 _TUNE_MARGIN = float(os.environ.get("TORCHPRUNER_TUNE_MARGIN", "0.02"))
 
 
-# the WIDE F(4x4) kernel (variant 1) is correct but measured 0.8x the MODE 3 kernel on every VGG
-# layer (profiles/wino4/round4_wide_vs_mode3.txt): opt-in candidate only
-_W4_WIDE = os.environ.get("TORCHPRUNER_W4_WIDE", "0") != "0"
-
-
-_W4_VARIANT = {WINO4: 0, WINO4W: 1, WINO4S: 3, WINO4S_FU: 3, WINO4_FU: 0}
+_W4_VARIANT = {WINO4: 0, WINO4S: 3, WINO4S_FU: 3, WINO4_FU: 0}
 _W4_FUSED = (WINO4S_FU, WINO4_FU)
 
 
 def _wino4_cands(B, H, W, K, C):
     """F(4x4) candidates: one K pass, plus channel-chunk split-K (raw slabs + the shared
     deterministic combine) when the tile grid alone cannot fill the chip (small batches); for
-    the split-points kernel (the untuned pick), MODE 3 (32-tile blocks, two per CU) and, opt-in,
-    WIDE (64-tile blocks, one per CU)."""
+    the split-points kernel (the untuned pick) and MODE 3 (32-tile blocks, two per CU)."""
     out = []
-    for kind, tb, per_cu in ((WINO4S, 32, 2), (WINO4, 32, 2), (WINO4W, 64, 1)):
-        if kind == WINO4W and not _W4_WIDE:
-            continue
+    for kind, tb, per_cu in ((WINO4S, 32, 2), (WINO4, 32, 2)):
         blocks = math.ceil(B * (H // 4) * (W // 4) / tb) * (K // 32)
         sp, chunks = 1, C // 8
         while _W4_SPLITS and blocks * sp < per_cu * _CU and sp * 2 <= chunks // 4 and sp < 16:
@@ -328,7 +320,7 @@ class Autotuner:
 
 TUNER = Autotuner()
 
-_KIND_NAMES = {WINO: "wino2_direct", WINO_LDS: "wino2", WINO_UNP: "wino2_unpool", WINO4: "wino4_m3", WINO4W: "wino4w",
+_KIND_NAMES = {WINO: "wino2_direct", WINO_LDS: "wino2", WINO_UNP: "wino2_unpool", WINO4: "wino4_m3",
                WINO_BF: "wino2_bf16", WINO_BF_UNP: "wino2_bf16_unpool", WINO4S: "wino4", -10: "first_direct",
                WINO4S_FU: "wino4_fused_unpool", WINO4_FU: "wino4_m3_fused_unpool"}
 
@@ -1231,13 +1223,13 @@ class FusedChainEngine:
         return res
 
 
-KERNEL_FAMILIES = ("wino4", "wino4_fused", "wino4_m3", "wino4w", "wino2", "wino2_direct", "igemm", "wino2_bf16")
+KERNEL_FAMILIES = ("wino4", "wino4_fused", "wino4_m3", "wino2", "wino2_direct", "igemm", "wino2_bf16")
 
 
 def family_policy(family: str, split: str = "min"):
     """A :meth:`Autotuner.pinned` policy that runs every layer it can on one kernel family:
     ``wino4`` F(4x4,3x3) (split-points kernel), ``wino4_fused`` the same with the data gradients of
-    pooled blocks unpooling in their epilogue, ``wino4_m3`` its MODE 3 kernel, ``wino4w`` its wide kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
+    pooled blocks unpooling in their epilogue, ``wino4_m3`` its MODE 3 kernel, ``wino2`` F(2x2,3x3) LDS-staged (+ explicit unpool), ``wino2_direct``
     F(2x2) with direct patch loads, ``igemm`` the implicit GEMM (dense 2x2 GEMM, VALU first
     layer; with bf16 operands the bf16 implicit GEMM), ``wino2_bf16`` the bf16 F(2x2) kernels
     (compute_dtype=bfloat16 only). ``split``: the fewest ("min") or most ("max") channel splits of
@@ -1252,8 +1244,6 @@ def family_policy(family: str, split: str = "min"):
             return k in (WINO4S_FU, WINO4S)
         if family == "wino4_m3":
             return k == WINO4
-        if family == "wino4w":
-            return k == WINO4W
         if family == "wino2":
             return k in (WINO_LDS, WINO_UNP)
         if family == "wino2_direct":

@@ -19,9 +19,13 @@ backward kernels (K5, ``tpamd.bn_train_*``), training-mode ``nn.Dropout`` on a c
 Philox kernel (K7b, mask regenerated in the backward), max-pool (argmax byte + gather backward)
 and global average pool on NHWC kernels, ``nn.Linear`` on the MFMA GEMM; the loss and the optimizer
 stay PyTorch ops (autograd composes everything), so any model works; only modules the kernels
-support are switched. Pruned (odd)
-channel counts are zero-padded to the kernels' granule inside the op and sliced off again:
-the parameters, their gradients and the optimizer state keep the module's real shapes.
+support are switched. Pruned (odd) channel counts run unpadded in the GEMMs' K loops (a tap's last
+32-wide K slice is zero-filled past the real width in the loads) and are carried between the
+kernels at a granule of 8 channels (:func:`_act_w`: the F(4x4) input granule; the zero channels are
+exact zeros through BN / ReLU / max-pool): inside a residual block or an ``nn.Sequential`` the
+padded activation flows conv -> BN -> conv without slice / pad copies, and the training BN takes
+the real width as its parameter count (``cr``). The parameters, their gradients and the
+optimizer state keep the module's real shapes.
 Every kernel choice is timed once per shape (``TUNER``, like ``cudnn.benchmark``) — a few
 milliseconds instead of a JIT compile.
 """
@@ -80,9 +84,25 @@ def eligible(conv: nn.Module) -> bool:
     return k[0] in (1, 3)
 
 
+def _act_w(c: int) -> int:
+    """Channel width a native activation carries: the next multiple of 8 (the F(4x4) kernel's input
+    granule; the implicit GEMMs take any multiple of 4, BN any width). A 20 %-pruned ResNet-50
+    layer of 103 channels carries 104 (the round-5 32-granule carried 128, VERDICT r5 #1)."""
+    return -(-max(c, 8) // 8) * 8
+
+
+def _r32(c: int) -> int:
+    return -(-c // 32) * 32
+
+
 def _cin_pad(ks: int, cin: int) -> int:
-    """Channel width the kernels see: 4 (packed taps) for tiny-Cin 3x3/5x5/7x7, else 32-granule."""
-    return 4 if (ks in (3, 5, 7) and cin <= 4) else cpad(cin)
+    """Input width the kernels see: 4 (packed taps) for tiny-Cin 3x3/5x5/7x7, else :func:`_act_w`."""
+    return 4 if (ks in (3, 5, 7) and cin <= 4) else _act_w(cin)
+
+
+def _kslice(cin_p: int) -> int:
+    """Channels per tap in a GEMM weight operand: 4 (packed taps) or the 32-wide K slices."""
+    return 4 if cin_p == 4 else _r32(cin_p)
 
 
 def _wgrad_splits(P, tiles):
@@ -146,8 +166,8 @@ class _PackSet:
             self.entries[key] = e
         else:  # the weights moved on (optimizer step / new forward): a new generation, unused entries go
             self.gen += 1
+            e[5] = self.gen  # before the sweep: the requested entry is never dropped (and is repacked below)
             self.entries = {k: v for k, v in self.entries.items() if v[5] >= self.gen - 2}
-            e[5] = self.gen
         ep = (epochs.OPT[0], epochs.FWD[0])
         stale = [v for v in self.entries.values() if v[4] != (v[0]._version, *ep) and v[0].device == w.device]
         for kd, fn in (("pack", T.pack_conv_weights_multi), ("w4", T.wino4_weights_multi)):
@@ -160,6 +180,16 @@ class _PackSet:
 
 
 _PACKS = _PackSet()
+
+
+def invalidate_packs() -> int:
+    """Mark every cached training-conv weight pack stale (repacked at its next use): the explicit
+    hook for weight writes the staleness check cannot see (``param.data`` edits between two
+    forwards of a submodule called directly). :func:`torchpruner_amd.engine.invalidate` calls it.
+    Returns the number of entries marked."""
+    for v in _PACKS.entries.values():
+        v[4] = None
+    return len(_PACKS.entries)
 
 
 def _pack(T, w, rows, cols, cpad_, mode, shared):
@@ -177,19 +207,22 @@ def _u4(T, w, K, C, flip, shared):
     return T.wino4_weights(w, flip, K, C)
 
 
-def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
-    """Forward of one native conv: returns (y NHWC (B, Ho, Wo, Cout), saved (xh, w32), meta,
-    part). With ``stats``, ``part`` is the per-tile BatchNorm statistics of y from the GEMM
-    epilogue ((G, 2, Cout) fp64, for ``bn_act(..., pre=part)``) when the tuned kernel is a
-    single-pass implicit GEMM, else None."""
+def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False, keep=False):
+    """Forward of one native conv: returns (y NHWC (B, Ho, Wo, C'), saved (xh, w32), meta, part).
+    ``x`` may carry more channels than the weight (a padded activation: zeros past the real width).
+    ``keep``: y keeps its carried width C' = _act_w(Cout) (zeros past Cout) for a consumer that
+    takes padded activations; else C' = Cout. With ``stats``, ``part`` is the per-tile BatchNorm
+    statistics of y from the GEMM epilogue ((G, 2, C') fp64, for ``bn_act(..., pre=part)``) when
+    the tuned kernel is a single-pass implicit GEMM, else None."""
     T = ops.require()
-    B, Cin, H, W = x.shape
-    Cout = weight.shape[0]
-    cin_p = _cin_pad(ks, Cin)
-    cout_p = cpad(Cout)
+    B, Cx, H, W = x.shape
+    Cout, Cin = weight.shape[0], weight.shape[1]
+    cin_p = _cin_pad(ks, Cx)
+    cout_p = _act_w(Cout)
+    k32 = _r32(cout_p)  # the Winograd kernels' output blocks (MFMA N); stores stop at cout_p
     xh = x.permute(0, 2, 3, 1)
-    if cin_p != Cin:
-        xh = F.pad(xh, (0, cin_p - Cin))
+    if cin_p != Cx:
+        xh = F.pad(xh, (0, cin_p - Cx))
     xh = xh.float().contiguous()
     wd = weight.detach()
     w32 = wd if wd.dtype == torch.float32 else wd.float()  # the parameter itself for fp32 weights: no copy
@@ -209,45 +242,47 @@ def _conv_fwd(x, weight, bias, ks, stride, pad, stats=False):
             return T.conv_wino_fwd(xh, cache["u"], None, shift, False, False, sp, cfg == WINO_LDS)[0]
         if cfg == WINO4S:  # Winograd F(4x4,3x3): 4x fewer multiplies (band geometry on ResNet's maps)
             if "u4" not in cache:
-                cache["u4"] = _u4(T, w32, cout_p, cin_p, False, shared)
-            return T.conv_wino4_fwd(xh, cache["u4"], None, shift, False, False, None, sp, 3)[0]
+                cache["u4"] = _u4(T, w32, k32, cin_p, False, shared)
+            return T.conv_wino4_fwd(xh, cache["u4"], None, shift, False, False, None, sp, 3, cout_p)[0]
         if "wk" not in cache:  # [cout_p][(kh, kw, ci)] zero-padded GEMM operand
-            cache["wk"] = _pack(T, w32, cout_p, kk, cin_p, 0, shared)
+            cache["wk"] = _pack(T, w32, cout_p, kk, _kslice(cin_p), 0, shared)
         return T.conv_gen(xh, cache["wk"], None, shift, False, None, None, ks, stride, pad, cfg, sp)
 
     cands = TUNER.candidates(M, cout_p, kk)
     if cin_p != 4:
         cands = cands + sk_candidates(T, cands, ks, M, cout_p)
-    if ks == 1 and cin_p % 32 == 0 and kk <= 256:  # short K: the single-buffered LDS stage (2x blocks per CU)
+    if ks == 1 and cin_p != 4 and kk <= 256:  # short K: the single-buffered LDS stage (2x blocks per CU)
         cands = cands + [(CFG_SB | c, 1) for c in (2, 3, 6)]
     if wino:
         sp0 = _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cout_p, cin_p)
         cands = [(WINO_LDS, sp0), (WINO, sp0)] + cands
-        if H == W:
-            cands = cands + wino4_cands(B, H, cout_p, cin_p)
+    if ks == 3 and stride == 1 and pad == 1 and H == W and cin_p != 4:
+        # unpadded output widths (cout_p < k32) need one K pass: the split slabs are k32 wide
+        cands = cands + [c for c in wino4_cands(B, H, k32, cin_p) if k32 == cout_p or c[1] == 1]
     cfg, sp = TUNER.choose(("tfwd", tuple(xh.shape), cout_p, ks, stride, pad), M, cout_p, kk, run, cands=cands)
     part = None
-    stats_ok = (ks in (1, 3, 5) and cin_p % 32 == 0) or (ks in (3, 5, 7) and cin_p == 4)  # conv_gen_stats' shapes
+    stats_ok = (ks in (1, 3, 5) and cin_p != 4) or (ks in (3, 5, 7) and cin_p == 4)  # conv_gen_stats' shapes
     if stats and stats_ok and _EPI_STATS and cfg not in (WINO, WINO_LDS, WINO4S) and sp == 1:
         if "wk" not in cache:
-            cache["wk"] = _pack(T, w32, cout_p, kk, cin_p, 0, shared)
+            cache["wk"] = _pack(T, w32, cout_p, kk, _kslice(cin_p), 0, shared)
         y, part = T.conv_gen_stats(xh, cache["wk"], shift, ks, stride, pad, cfg)
-        if cout_p != Cout:
+        if cout_p != Cout and not keep:
             part = part[..., :Cout].contiguous()
     else:
         y = run(cfg, sp)
-    if cout_p != Cout:
+    if cout_p != Cout and not keep:
         y = y[..., :Cout].contiguous()
-    meta = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride(), cin_p, cout_p)
+    meta = (ks, stride, pad, Cin, Cout, H, W, bias is not None, weight.dtype, weight.stride(), cin_p, cout_p, Cx)
     return y, (xh, w32), meta, part
 
 
 def _grad_nhwc(gy, meta):
-    """dL/dy (NCHW view) -> contiguous NHWC, zero-padded to the kernels' output-channel granule."""
-    Cout, cout_p = meta[4], meta[11]
+    """dL/dy (NCHW view) -> contiguous NHWC at the carried output width (a padded output's
+    gradient already has it: zeros past Cout)."""
+    cout_p = meta[11]
     g = gy.permute(0, 2, 3, 1).float()
-    if cout_p != Cout:
-        g = F.pad(g, (0, cout_p - Cout))
+    if g.shape[-1] != cout_p:
+        g = F.pad(g, (0, cout_p - g.shape[-1]))
     return g.contiguous()
 
 
@@ -257,15 +292,16 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
     with h, w % res_stride == 0 — the other branch's gradient of a tensor read twice (residual
     blocks), without a separate add pass."""
     T = ops.require()
-    ks, stride, pad, Cin, Cout, H, W, _, _, _, cin_p, cout_p = meta
+    ks, stride, pad, Cin, Cout, H, W, _, _, _, cin_p, cout_p = meta[:12]
     B, Ho, Wo = g.shape[0], g.shape[1], g.shape[2]
+    kin, n32 = _kslice(cout_p), _r32(cin_p)  # per-tap K slice width; the F(4x4) output blocks
     # stride 1: dgrad = stride-1 conv of g with flipped taps, padding ks-1-pad;
     # strided 1x1 / 3x3: transposed gather kernel, natural tap order
     transposed = stride != 1
     shared = meta[8] == torch.float32  # w32 is the parameter's own storage (see _conv_fwd)
     assert res is None or not transposed
     pad_b = pad if transposed else ks - 1 - pad
-    M, K = B * H * W, ks * ks * cout_p
+    M, K = B * H * W, ks * ks * kin
     wino = res is None and not transposed and _wino_ok(ks, 1, pad_b, Ho, Wo, cout_p, cin_p)
     cache = {}
 
@@ -276,10 +312,10 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
             return T.conv_wino_fwd(g, cache["ut"], None, None, False, False, sp, cfg == WINO_LDS)[0]
         if cfg == WINO4S:
             if "ut4" not in cache:
-                cache["ut4"] = _u4(T, w32, cin_p, cout_p, True, shared)
-            return T.conv_wino4_fwd(g, cache["ut4"], None, None, False, False, None, sp, 3)[0]
+                cache["ut4"] = _u4(T, w32, n32, cout_p, True, shared)
+            return T.conv_wino4_fwd(g, cache["ut4"], None, None, False, False, None, sp, 3, cin_p)[0]
         if "wt" not in cache:  # [ci][(kh, kw, co)], flipped for stride 1
-            cache["wt"] = _pack(T, w32, cin_p, K, cout_p, 2 if transposed else 1, shared)
+            cache["wt"] = _pack(T, w32, cin_p, K, kin, 2 if transposed else 1, shared)
         return T.conv_gen_bwd(g, cache["wt"], res, res_stride, None, ks, stride if transposed else 1, pad_b, H, W,
                               transposed, cfg, sp)
 
@@ -290,8 +326,8 @@ def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
             cands = cands + [(CFG_SB | c, 1) for c in (2, 3, 6)]
     if wino:
         cands = [(WINO_LDS, _wino_splits(B * ((H + 1) // 2) * ((W + 1) // 2), cin_p, cout_p)), (WINO, 1)] + cands
-        if H == W:
-            cands = cands + wino4_cands(B, H, cin_p, cout_p)
+    if res is None and not transposed and ks == 3 and pad_b == 1 and H == W and cin_p != 4:
+        cands = cands + [c for c in wino4_cands(B, H, n32, cout_p) if n32 == cin_p or c[1] == 1]
     key = ("tdgrad", tuple(g.shape), cin_p, ks, stride, pad, res is not None and res_stride)
     cfg, sp = TUNER.choose(key, M, cin_p, K, run, cands=cands)
     return run(cfg, sp)
@@ -334,10 +370,19 @@ def _conv_wgrad(g, xh, meta):
     return torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=wdtype, device=g.device).copy_(dw32)
 
 
+def _dx_nchw(dxh, meta):
+    """Input gradient NHWC (B, H, W, cin_p) -> (B, Cx, H, W) for the forward's input of Cx channels
+    (a channels_last view when cin_p == Cx, the carried width of a padded input)."""
+    Cx = meta[12]
+    if dxh.shape[-1] != Cx:
+        dxh = dxh[..., :Cx]
+    return dxh.permute(0, 3, 1, 2)
+
+
 class _NativeConv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, ks, stride, pad):
-        y, saved, ctx.meta, _ = _conv_fwd(x, weight, bias, ks, stride, pad)
+    def forward(ctx, x, weight, bias, ks, stride, pad, keep=False):
+        y, saved, ctx.meta, _ = _conv_fwd(x, weight, bias, ks, stride, pad, keep=keep)
         ctx.save_for_backward(*saved)
         return _as_nchw(y)
 
@@ -345,19 +390,20 @@ class _NativeConv2d(torch.autograd.Function):
     def backward(ctx, gy):
         xh, w32 = ctx.saved_tensors
         meta = ctx.meta
-        ks, stride, pad, Cin, _, H, W, has_bias = meta[:8]
+        ks, stride, pad, Cin, Cout, H, W, has_bias = meta[:8]
         g = _grad_nhwc(gy, meta)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             if ks != 7:
-                dx = _conv_dgrad(g, w32, meta)[..., :Cin].permute(0, 3, 1, 2).to(gy.dtype)
+                dx = _dx_nchw(_conv_dgrad(g, w32, meta), meta).to(gy.dtype)
             else:  # 7x7 stem input gradient (rarely needed: the input is data)
-                dx = torch.nn.grad.conv2d_input((g.shape[0], Cin, H, W), w32.to(gy.dtype), gy, stride, pad)
+                dx = torch.nn.grad.conv2d_input((g.shape[0], meta[12], H, W), F.pad(w32, (0, 0, 0, 0, 0,
+                                                meta[12] - Cin)).to(gy.dtype), gy[:, :Cout], stride, pad)
         if ctx.needs_input_grad[1]:
             dw = _conv_wgrad(g, xh, meta)
         if has_bias and ctx.needs_input_grad[2]:
-            db = gy.sum((0, 2, 3))
-        return dx, dw, db, None, None, None
+            db = gy[:, :Cout].sum((0, 2, 3))
+        return dx, dw, db, None, None, None, None
 
 
 class _NativeConv2dStats(torch.autograd.Function):
@@ -365,8 +411,8 @@ class _NativeConv2dStats(torch.autograd.Function):
     None), computed in the GEMM epilogue: the following training BN skips its statistics pass."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, ks, stride, pad):
-        y, saved, ctx.meta, part = _conv_fwd(x, weight, bias, ks, stride, pad, stats=True)
+    def forward(ctx, x, weight, bias, ks, stride, pad, keep=False):
+        y, saved, ctx.meta, part = _conv_fwd(x, weight, bias, ks, stride, pad, stats=True, keep=keep)
         ctx.save_for_backward(*saved)
         if part is not None:
             ctx.mark_non_differentiable(part)
@@ -377,20 +423,26 @@ class _NativeConv2dStats(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, _gpart):
         if gy is None:
-            return (None,) * 6
+            return (None,) * 7
         return _NativeConv2d.backward(ctx, gy)
 
 
-def conv_stats(conv: nn.Conv2d, x: torch.Tensor):
+def _real(x: torch.Tensor, c: int) -> torch.Tensor:
+    """The first ``c`` channels of a (possibly padded) activation (the tensor itself if it has c)."""
+    return x if x.shape[1] == c else x[:, :c]
+
+
+def conv_stats(conv: nn.Conv2d, x: torch.Tensor, keep: bool = False):
     """``(conv(x), tile statistics or None)`` — a native conv whose tuned kernel is a one-pass
     implicit GEMM computes its output's BN statistics in the epilogue (1x1, strided 3x3, the
-    packed-tap stem; Winograd picks return None); anything else runs the module (None)."""
+    packed-tap stem; Winograd picks return None); anything else runs the module (None). ``x`` may
+    be a padded activation; ``keep``: the output keeps its carried width (zeros past Cout)."""
     if "forward" in conv.__dict__ and conv.forward.__func__ is _native_forward \
             and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.weight.dtype == torch.float32 \
             and _fits(conv, x):
         ks, s, p = _geom(conv)
-        return _NativeConv2dStats.apply(x, conv.weight, conv.bias, ks, s, p)
-    return conv(x), None
+        return _NativeConv2dStats.apply(x, conv.weight, conv.bias, ks, s, p, keep)
+    return conv(_real(x, conv.in_channels)), None
 
 
 class _NativeBlockEntry(torch.autograd.Function):
@@ -404,7 +456,7 @@ class _NativeBlockEntry(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, wd, bd, ds_stride):
         # (conv1 output, identity-branch pre-BN, and the two outputs' BN tile statistics or None)
-        y1, saved1, ctx.meta1, p1 = _conv_fwd(x, w1, b1, 1, 1, 0, stats=True)
+        y1, saved1, ctx.meta1, p1 = _conv_fwd(x, w1, b1, 1, 1, 0, stats=True, keep=True)  # carried width
         ctx.has_ds = wd is not None
         pd = None
         if ctx.has_ds:
@@ -427,7 +479,7 @@ class _NativeBlockEntry(torch.autograd.Function):
         else:
             xh, w1 = ctx.saved_tensors
         m1 = ctx.meta1
-        Cin = m1[3]
+        Cx = m1[12]
         dx = dw1 = db1 = dwd = dbd = None
         g1h = _grad_nhwc(g1, m1) if g1 is not None else None
         res, res_stride, gdh = None, 1, None
@@ -443,18 +495,18 @@ class _NativeBlockEntry(torch.autograd.Function):
                     res_stride = md[1]
             elif ctx.needs_input_grad[0]:
                 res = _nhwc(gid).float()
-                if m1[10] != Cin:
-                    res = F.pad(res, (0, m1[10] - Cin))
+                if m1[10] != res.shape[-1]:
+                    res = F.pad(res, (0, m1[10] - res.shape[-1]))
                 res = res.contiguous()
         if ctx.needs_input_grad[0]:
             if g1h is None:  # only the identity branch carries a gradient (rare): dgrad of zeros + res
                 B, H, W = xh.shape[0], xh.shape[1], xh.shape[2]
                 g1h = torch.zeros((B, H, W, m1[11]), dtype=torch.float32, device=xh.device)
-            dx = _conv_dgrad(g1h, w1, m1, res, res_stride)[..., :Cin].permute(0, 3, 1, 2)
+            dx = _dx_nchw(_conv_dgrad(g1h, w1, m1, res, res_stride), m1)
         if ctx.needs_input_grad[1] and g1 is not None:
             dw1 = _conv_wgrad(g1h, xh, m1)
         if m1[7] and ctx.needs_input_grad[2] and g1 is not None:
-            db1 = g1.sum((0, 2, 3))
+            db1 = g1[:, :m1[4]].sum((0, 2, 3))
         if ctx.has_ds and gdh is not None:
             md = ctx.meta_d
             if ctx.needs_input_grad[3]:
@@ -469,7 +521,7 @@ class _NativeBN2d(torch.autograd.Function):
     running-stat update, the normalisation, and the backward, on ``tpamd.bn_train_*``."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, nbt=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, nbt=None, cr=0):
         T = ops.require()
         xh = x.permute(0, 2, 3, 1)
         if not xh.is_contiguous():
@@ -477,7 +529,8 @@ class _NativeBN2d(torch.autograd.Function):
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         y, mean, invstd, _ = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum),
-                                            num_batches=nbt)
+                                            num_batches=nbt, cr=int(cr))
+        ctx.cr = int(cr)
         if running_mean is not None:
             epochs.bump_stats()  # running stats written by the kernel: no version bump
         ctx.save_for_backward(xh, w if w is not None else torch.empty(0, device=x.device), mean, invstd)
@@ -490,9 +543,9 @@ class _NativeBN2d(torch.autograd.Function):
         xh, w, mean, invstd = ctx.saved_tensors
         g = gy.permute(0, 2, 3, 1).contiguous()
         dx, dgamma, dbeta, _ = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
-                                              ctx.needs_input_grad[0])
+                                              ctx.needs_input_grad[0], cr=ctx.cr)
         return (dx.permute(0, 3, 1, 2) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
-                dbeta if ctx.has_b else None, None, None, None, None, None)
+                dbeta if ctx.has_b else None, None, None, None, None, None, None)
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -508,14 +561,16 @@ class _NativeBNAct(torch.autograd.Function):
     ATen ReLU / add / threshold-backward passes of the unfused block disappear."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu, pre=None, nbt=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu, pre=None, nbt=None, cr=0):
         T = ops.require()
         xh = _nhwc(x)
         rh = _nhwc(res) if res is not None else None
         w = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
+        # cr: the module's channels; x may carry more (a padded activation: zeros, kept zero)
         y, mean, invstd, mk = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
-                                             bool(relu), pre, nbt)
+                                             bool(relu), pre, nbt, int(cr))
+        ctx.cr = int(cr)
         if running_mean is not None:
             epochs.bump_stats()
         # the backward masks by the ReLU bit mask (1 byte per 4 channels) instead of re-reading y
@@ -530,10 +585,11 @@ class _NativeBNAct(torch.autograd.Function):
         g = _nhwc(gy)
         want_res = ctx.has_res and ctx.needs_input_grad[7]
         dx, dgamma, dbeta, dres = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
-                                                 ctx.needs_input_grad[0], None, want_res, mk if ctx.relu else None)
+                                                 ctx.needs_input_grad[0], None, want_res, mk if ctx.relu else None,
+                                                 ctx.cr)
         return (_as_nchw(dx) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
                 dbeta if ctx.has_b else None, None, None, None, None, _as_nchw(dres) if want_res else None, None,
-                None, None)
+                None, None, None)
 
 
 def _bn_counter(bn):
@@ -547,8 +603,10 @@ def _bn_counter(bn):
 
 
 def _bn_fusable(bn, x, res=None) -> bool:
+    """Training BN on the native kernels: any width (float4 rows when C % 4 == 0, per-element
+    otherwise), x at the module's width or a padded activation carrying more (zeros)."""
     return (isinstance(bn, nn.BatchNorm2d) and bn.training and x.is_cuda and x.dtype == torch.float32
-            and x.dim() == 4 and x.shape[1] % 4 == 0 and x.numel() > 0
+            and x.dim() == 4 and x.shape[1] >= bn.num_features and x.numel() > 0
             and (bn.weight is None or bn.weight.dtype == torch.float32)
             and (res is None or (res.shape == x.shape and res.dtype == x.dtype and res.is_cuda)))
 
@@ -560,9 +618,9 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: 
     per tile by the producing conv's epilogue (:func:`conv_stats`), which skips the statistics
     pass over x."""
     if not _bn_fusable(bn, x, res):
-        y = bn(x)
+        y = bn(_real(x, bn.num_features))
         if res is not None:
-            y = y + res
+            y = y + _real(res, bn.num_features)
         return F.relu(y) if relu else y
     momentum, nbt = bn.momentum, _bn_counter(bn)
     if nbt is None and bn.track_running_stats and bn.num_batches_tracked is not None:
@@ -574,7 +632,7 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: 
     if pre is not None and (pre.dim() != 3 or pre.shape[2] != x.shape[1]):
         pre = None
     return _NativeBNAct.apply(x, bn.weight, bn.bias, rm, rv, bn.eps, momentum if momentum is not None else 0.0, res,
-                              relu, pre, nbt)
+                              relu, pre, nbt, bn.num_features)
 
 
 def _block_kind(m) -> str | None:
@@ -611,6 +669,8 @@ def _native_block_forward(self, x):
     if not (self.training and x.is_cuda):
         return type(self).forward(self, x)
     entry = _entry_convs(self, x)
+    # block-internal activations (conv1 / conv2 outputs: the widths a structured prune cuts) flow at
+    # their carried width (_act_w) from conv to BN to conv; the block output has its real width
     if entry is not None:
         c1, dconv, dbn = entry
         y1, idp, p1, pd = _NativeBlockEntry.apply(x, c1.weight, c1.bias, dconv.weight if dconv is not None else None,
@@ -620,19 +680,27 @@ def _native_block_forward(self, x):
         out = bn_act(self.bn1, y1, relu=True, pre=p1)
     else:
         identity = self.downsample(x) if self.downsample is not None else x
-        y1, p1 = conv_stats(self.conv1, x)
+        y1, p1 = conv_stats(self.conv1, x, keep=True)
         out = bn_act(self.bn1, y1, relu=True, pre=p1)
-    y2, p2 = conv_stats(self.conv2, out)
     if _block_kind(self) == "bottleneck":
+        y2, p2 = conv_stats(self.conv2, out, keep=True)
         out = bn_act(self.bn2, y2, relu=True, pre=p2)
         y3, p3 = conv_stats(self.conv3, out)
         return bn_act(self.bn3, y3, res=identity, relu=True, pre=p3)
+    y2, p2 = conv_stats(self.conv2, out)
     return bn_act(self.bn2, y2, res=identity, relu=True, pre=p2)
 
 
+# modules a padded activation (zeros past the real width) may pass through unchanged in meaning
+_PAD_SAFE = (nn.ReLU, nn.MaxPool2d, nn.Dropout)
+
+
 def _native_sequential_forward(self, x):
-    """nn.Sequential training forward fusing every (BatchNorm2d, ReLU) pair (VGG features)."""
+    """nn.Sequential training forward fusing every (BatchNorm2d, ReLU) pair (VGG features). Native
+    convs keep their carried output width through BN / ReLU / max-pool / dropout into the next
+    conv (no slice / pad copies at pruned widths); any other module gets the real width."""
     mods = list(self.children())
+    real = None  # real channel count while x is a padded activation
     i = 0
     while i < len(mods):
         m = mods[i]
@@ -641,9 +709,20 @@ def _native_sequential_forward(self, x):
             x = bn_act(m, x, relu=True)
             i += 2
             continue
+        if "forward" in m.__dict__ and getattr(m.forward, "__func__", None) is _native_forward \
+                and self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 \
+                and m.weight.dtype == torch.float32 and _fits(m, x):
+            ks, s, p = _geom(m)
+            x = _NativeConv2d.apply(x, m.weight, m.bias, ks, s, p, True)
+            real = m.out_channels if x.shape[1] != m.out_channels else None
+            i += 1
+            continue
+        native_bn = "forward" in m.__dict__ and getattr(m.forward, "__func__", None) is _native_bn_forward
+        if real is not None and not (native_bn and _bn_fusable(m, x)) and type(m) not in _PAD_SAFE:
+            x, real = x[:, :real], None
         x = m(x)
         i += 1
-    return x
+    return x if real is None else x[:, :real]
 
 
 def _native_resnet_forward(self, x):
@@ -657,9 +736,11 @@ def _native_resnet_forward(self, x):
 
 
 def _native_bn_forward(self, x):
-    """BatchNorm2d.forward with the training branch on the native kernels (eval mode and any
-    input the kernels do not take — non-channels_last, C % 4 != 0 — use the module's own)."""
-    ok = (self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] % 4 == 0
+    """BatchNorm2d.forward with the training branch on the native kernels (any width; eval mode and
+    inputs the kernels do not take — non-channels_last — use the module's own). A padded activation
+    (more channels than the module: zeros) stays padded."""
+    ok = (self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+          and x.shape[1] >= self.num_features
           and x.is_contiguous(memory_format=torch.channels_last) and x.numel() > 0
           and (self.weight is None or self.weight.dtype == torch.float32))
     if not ok:
@@ -672,7 +753,7 @@ def _native_bn_forward(self, x):
     rm = self.running_mean if self.track_running_stats else None
     rv = self.running_var if self.track_running_stats else None
     return _NativeBN2d.apply(x, self.weight, self.bias, rm, rv, self.eps, momentum if momentum is not None else 0.0,
-                             nbt)
+                             nbt, self.num_features)
 
 
 class _NativeMaxPool(torch.autograd.Function):
@@ -741,7 +822,7 @@ def _fits(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     ks, s, p = _geom(conv)
     B, Cin, H, W = x.shape
     Ho, Wo = (H + 2 * p - ks) // s + 1, (W + 2 * p - ks) // s + 1
-    cin_p, cout_p = _cin_pad(ks, Cin), cpad(conv.out_channels)
+    cin_p, cout_p = _cin_pad(ks, Cin), _act_w(conv.out_channels)
     return B * H * W * cin_p * 4 <= _MAX_BYTES and B * Ho * Wo * cout_p * 4 <= _MAX_BYTES and Ho > 0 and Wo > 0
 
 
@@ -781,7 +862,7 @@ def _native_linear_forward(self, x):
     w = self.weight
     if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and w.dtype == torch.float32 and w.dim() == 2
             and x.shape[0] > 0 and x.shape[1] == w.shape[1] and (self.bias is None or self.bias.shape == w.shape[:1])
-            and x.shape[0] * max(cpad(w.shape[0]), cpad(w.shape[1])) * 4 <= _MAX_BYTES):
+            and x.shape[0] * max(_act_w(w.shape[0]), _act_w(w.shape[1])) * 4 <= _MAX_BYTES):
         return type(self).forward(self, x)
     B, (n_out, n_in) = x.shape[0], w.shape
     y = _NativeConv2d.apply(x.reshape(B, n_in, 1, 1), w.reshape(n_out, n_in, 1, 1), self.bias, 1, 1, 0)
