@@ -92,7 +92,7 @@ def parse():
                     help="accuracy protocol over seeds seed..seed+K-1 (each its own teacher); top-1 figures "
                          "are means over the seeds, per-seed values are listed")
     ap.add_argument("--teacher-steps", type=int, default=None)
-    ap.add_argument("--extras", default="generic,bf16,b100,resnet,shapley,finetune,quality5",
+    ap.add_argument("--extras", default="generic,bf16,b100,pruned,resnet,shapley,finetune,quality5",
                     help="comma-separated extras to run (with --no-extras: none)")
     ap.add_argument("--finetune-steps", type=int, default=10)
     ap.add_argument("--finetune-batch", type=int, default=128)
@@ -256,7 +256,7 @@ def run(args) -> int:
     }
 
     if not args.no_extras:
-        result.update(extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase))
+        result.update(extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase, scores))
         if "b100_tuner_choices" in result:
             result["tuner_choices"]["b100"] = result.pop("b100_tuner_choices")
 
@@ -302,7 +302,7 @@ def run(args) -> int:
     return 0
 
 
-def extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase):
+def extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase, scores):
     """Same-algorithm library baseline + BASELINE configs #3 / #4 / #5 (all ranks, sharded)."""
     from torchpruner_amd.data import ShardLoader
 
@@ -324,6 +324,8 @@ def extras(args, model, task, convs, dev, world, rank, timed_run, log, value, ph
         timed_phase("bf16", _bf16, args, model, convs, dev, world, timed_run, log, value, loader)
     if "b100" in want:
         timed_phase("b100", _b100, args, model, task, convs, dev, world, rank, timed_run, log, loader)
+    if "pruned" in want:
+        timed_phase("pruned", _pruned, args, model, task, convs, scores, dev, world, timed_run, log, value, loader)
     if "resnet" in want:
         timed_phase("resnet", _resnet, args, dev, world, timed_run, log)
     if "shapley" in want:
@@ -496,6 +498,67 @@ def _b100(args, model, task, convs, dev, world, rank, timed_run, log, loader):
         f"{out['vgg_taylor_b100_host_loader_img_s']:.0f} img/s from a host DataLoader (per-sample collate "
         f"{out['vgg_taylor_b100_host_loader_per_sample_img_s']:.0f}) "
         f"({time.perf_counter() - t0:.1f}s)")
+    return out
+
+
+def _pruned(args, model, task, convs, scores, dev, world, timed_run, log, value, loader):
+    """The headline workload on the network a 50 % prune produces: the teacher with the lowest
+    half of EVERY conv's filters (by the headline's all-reduced Taylor scores) really pruned
+    through ``Pruner.prune_model`` + ``get_vgg_pruning_graph`` (widths 32/64/128/256, ~1/4 of the
+    conv MACs), then the same fp32 ``run_many`` over its 13 convs at the same batch — whether the
+    engine turns the pruned FLOPs into speed on the attribution side (reference flow: the model
+    pruner.py:21-57 produces, scored by taylor.py:31-49)."""
+    import copy
+
+    import numpy as np
+    import torch
+    import torch.nn.functional as F
+
+    from torchpruner_amd import Pruner, TaylorAttributionMetric, get_vgg_pruning_graph
+    from torchpruner_amd.engine.fused_chain import TUNER, tuner_choices
+    out = {}
+
+    def conv_macs(net):  # conv multiply-adds of one image (forward hooks, one eval forward)
+        tot = []
+        hs = [m.register_forward_hook(lambda m, i, o: tot.append(o[0].numel() * m.in_channels * m.kernel_size[0]
+                                                                 * m.kernel_size[1]))
+              for m in net.modules() if isinstance(m, torch.nn.Conv2d)]
+        with torch.no_grad():
+            net.eval()(torch.zeros(1, 3, 32, 32, device=dev))
+        for h in hs:
+            h.remove()
+        return sum(tot)
+
+    t0 = time.perf_counter()
+    pm = copy.deepcopy(model)
+    graph = [(m, c) for m, c in get_vgg_pruning_graph(pm) if isinstance(m, torch.nn.Conv2d)]
+    by_conv = {id(c): s for c, s in zip([m for m in pm.features if isinstance(m, torch.nn.Conv2d)], scores)}
+    pruner = Pruner(pm, (3, 32, 32), dev, sync_indices=False)  # scores are identical on every rank
+    for module, cascade in graph:
+        s = by_conv[id(module)]
+        pruner.prune_model(module, np.argsort(s, kind="stable")[: len(s) // 2], cascading_modules=cascade)
+    pconvs = [m for m in pm.features if isinstance(m, torch.nn.Conv2d)]
+    macs = conv_macs(pm) / conv_macs(model)
+    B = args.batch
+    before = set(TUNER.cache)
+    TaylorAttributionMetric(pm, loader(1, args.seed + 31, B), F.cross_entropy, dev).run_many(
+        pconvs, find_best_evaluation_module=True)  # autotune the new shapes (untimed)
+    pmet = TaylorAttributionMetric(pm, loader(args.steps, args.seed + 32, B), F.cross_entropy, dev)
+    _, pdt = timed_run(pmet, pconvs)
+    assert pmet.last_path["path"] == "fused", pmet.last_path
+    v = args.steps * B * world / pdt
+    out["vgg_taylor_pruned50_img_s"] = round(v, 1)
+    out["pruned50_vs_dense"] = round(v / value, 2)
+    out["pruned50_config"] = {"widths": [c.out_channels for c in pconvs], "per_gpu_batch": B, "dtype": "fp32",
+                              "conv_mac_fraction": round(macs, 4),
+                              "params": sum(p.numel() for p in pm.parameters()),
+                              "prune": "lowest 50% of every conv's filters by the headline's Taylor scores, "
+                                       "Pruner.prune_model + get_vgg_pruning_graph cascade (one shot)",
+                              "tuner_choices": tuner_choices({k: v for k, v in TUNER.cache.items()
+                                                              if k not in before})}
+    log(f"[bench] 50%-pruned VGG16 (conv MACs x{macs:.3f}): {v:.0f} img/s = x{v / value:.2f} the dense headline "
+        f"({time.perf_counter() - t0:.1f}s)")
+    del pm, pmet
     return out
 
 

@@ -146,8 +146,11 @@ def test_conv_odd_widths_match_fp64(cuda, cin, cout, ks, stride, family):
 def test_pruned_bottlenecks_resnet50_maps(cuda, frac):
     """A ResNet-50-shaped net (one bottleneck per stage, 224 px: 56/28/14/7-pixel maps) pruned like
     config #5 (``frac`` of every prunable bottleneck conv: 20 % = one round, 36 % ~ two), one
-    training step on the native kernels (carried widths through every block) vs fp32 autograd:
-    loss, every parameter gradient and the BN running statistics."""
+    training step on the native kernels (carried widths through every block) vs an fp64 autograd
+    oracle: the loss, every parameter gradient and the BN running statistics are about as close to
+    fp64 as the fp32 library step (MIOpen / ATen) is — within 3x its error or 2e-3 relative
+    (batch-statistics BN on 4 images amplifies fp32 rounding: both fp32 paths deviate from fp64 by
+    up to ~1 % on some layers, so a fixed tolerance would only test the batch size)."""
     import numpy as np
     from torchpruner_amd import Pruner, get_resnet_pruning_graph
     from torchpruner_amd.engine.train import native_convs
@@ -162,21 +165,28 @@ def test_pruned_bottlenecks_resnet50_maps(cuda, frac):
     widths = sorted({m.out_channels for m in model.modules() if isinstance(m, torch.nn.Conv2d)})
     assert any(w % 8 for w in widths), widths  # really odd widths
     model = model.to(memory_format=torch.channels_last).train()
-    ref = copy.deepcopy(model)
-    x = _cl(torch.randn(2, 3, 224, 224, device=cuda))
-    y = torch.randint(0, 10, (2,), device=cuda)
+    lib = copy.deepcopy(model)
+    m64 = copy.deepcopy(model).double()
+    x = _cl(torch.randn(4, 3, 224, 224, device=cuda))
+    y = torch.randint(0, 10, (4,), device=cuda)
 
-    def step(m, native):
+    def step(m, native, xx):
         m.zero_grad(set_to_none=True)
         with native_convs(m, enable=native):
-            loss = F.cross_entropy(m(x), y)
+            loss = F.cross_entropy(m(xx), y)
             loss.backward()
         return float(loss), [p.grad.double() for p in m.parameters()]
 
-    l_n, g_n = step(model, True)
-    l_r, g_r = step(ref, False)
-    assert abs(l_n - l_r) < 1e-4 * max(1.0, abs(l_r))
-    for (name, _), a, b in zip(model.named_parameters(), g_n, g_r):
-        assert (a - b).abs().max().item() <= 2e-3 * b.abs().max().item() + 1e-6, name
-    for (n1, b1), (_, b2) in zip(model.named_buffers(), ref.named_buffers()):
-        torch.testing.assert_close(b1.float(), b2.float(), rtol=1e-4, atol=1e-5, msg=n1)
+    l_n, g_n = step(model, True, x)
+    l_l, g_l = step(lib, False, x)
+    l_r, g_r = step(m64, False, x.double())
+    assert abs(l_n - l_r) <= max(3 * abs(l_l - l_r), 1e-5 * max(1.0, abs(l_r)))
+    for (name, _), a, b, r in zip(model.named_parameters(), g_n, g_l, g_r):
+        scale = r.abs().max().item() + 1e-30
+        e_nat, e_lib = (a - r).abs().max().item() / scale, (b - r).abs().max().item() / scale
+        assert e_nat <= max(3 * e_lib, 2e-3), (name, e_nat, e_lib)
+    for (n1, b1), (_, b2), (_, b3) in zip(model.named_buffers(), lib.named_buffers(), m64.named_buffers()):
+        if b1.is_floating_point():
+            e_nat = (b1.double() - b3).abs().max().item()
+            e_lib = (b2.double() - b3).abs().max().item()
+            assert e_nat <= max(3 * e_lib, 1e-5 * (b3.abs().max().item() + 1)), (n1, e_nat, e_lib)

@@ -340,7 +340,7 @@ def _conv_wgrad(g, xh, meta):
     """Weight gradient in the parameter's exact shape / strides (DDP bucket views expect them),
     written by the wgrad kernel / its split combine straight from the GEMM (no re-layout copies)."""
     T = ops.require()
-    ks, stride, pad, Cin, Cout, _, _, _, wdtype, w_strides, cin_p, cout_p = meta
+    ks, stride, pad, Cin, Cout, _, _, _, wdtype, w_strides, cin_p, cout_p = meta[:12]
     kk = -(-ks * ks * cin_p // 32) * 32
     P = g.shape[0] * g.shape[1] * g.shape[2]
     dw32 = torch.empty_strided((Cout, Cin, ks, ks), w_strides, dtype=torch.float32, device=g.device)
