@@ -672,6 +672,7 @@ def accuracy(args, model, task, convs, scores, cfg, dev, log):
     lw_r = float(np.mean([layerwise_mask_top1([rng.random_sample(c.out_channels) for c in convs], xv, yv)
                           for _ in range(3)]))
     runs = [{"seed": args.seed, "top1_before": before}]
+    runs[0].update(pq.layerwise_auc(model, task, args.seed))
     runs[0].update(pq.oneshot_top1(model, task, args.seed, cfg, xv, yv))
     params = None
     for method in ("taylor", "random"):
@@ -723,6 +724,26 @@ def accuracy(args, model, task, convs, scores, cfg, dev, log):
             "per_seed": [round(float(d), 4) for d in d1], "mean": round(float(d1.mean()), 4),
             "std": round(float(d1.std(ddof=1)) if len(d1) > 1 else 0.0, 4), "taylor_wins": int((d1 > 0).sum()),
             "seeds": int(len(d1))}
+    # the reference's layerwise-robustness AUC (nbVGG:1233-1285, 1521-1527) per seed, paired
+    for mth in ("taylor", "random", "sv"):
+        out[f"layerwise_auc_{mth}"] = round(float(np.mean([r[f"layerwise_auc_{mth}"] for r in runs])), 4)
+    for mth in ("taylor", "sv"):
+        d2 = np.array([r[f"layerwise_auc_{mth}"] - r["layerwise_auc_random"] for r in runs])
+        out[f"layerwise_auc_{mth}_minus_random"] = {
+            "per_seed": [round(float(d), 4) for d in d2], "mean": round(float(d2.mean()), 4),
+            "std": round(float(d2.std(ddof=1)) if len(d2) > 1 else 0.0, 4),
+            f"{mth}_better": int((d2 < 0).sum()), "seeds": int(len(d2))}
+    out["layerwise_auc_per_seed"] = {mth: [round(r[f"layerwise_auc_{mth}"], 4) for r in runs]
+                                     for mth in ("taylor", "random", "sv")}
+    out["layerwise_auc_per_layer_seed0"] = {mth: runs[0][f"layerwise_auc_{mth}_per_layer"]
+                                            for mth in ("taylor", "random", "sv")}
+    out["layerwise_auc_protocol"] = dict(pq.LAYERWISE, layers=13, unit="mean loss increase per removed unit "
+                                         "(nbVGG:1521-1527), units removed in ascending-score order after BN+ReLU, "
+                                         "lower is better", kernel_choices="TUNER.fixed()")
+    log(f"[bench] layerwise AUC (nbVGG protocol, lower is better) over seeds {out['quality_seeds']}: Taylor "
+        f"{out['layerwise_auc_taylor']:.4f}, SV {out['layerwise_auc_sv']:.4f}, Random {out['layerwise_auc_random']:.4f}"
+        f"; Taylor better on {out['layerwise_auc_taylor_minus_random']['taylor_better']}/{len(runs)} seeds, SV on "
+        f"{out['layerwise_auc_sv_minus_random']['sv_better']}/{len(runs)}")
     out["oneshot_protocol"] = {"fracs": list(pq.ONESHOT_FRACS), "bn_recal_batches": pq.ONESHOT_RECAL,
                                "finetune_steps": 0, "taylor_score_imgs": cfg["score_imgs"],
                                "kernel_choices": "TUNER.fixed()"}

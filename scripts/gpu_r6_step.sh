@@ -1,8 +1,10 @@
-# round-6 GPU step: full GPU suite, then a kernel trace of the pruned (round-1) ResNet-50 training step
-mkdir -p gpurun_out/prof_pruned
-export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest -q -m gpu --timeout 300 --timeout-method thread tests > gpurun_out/gpu_suite.log 2>&1
-rc=$?; echo EXIT $rc >> gpurun_out/gpu_suite.log; tail -8 gpurun_out/gpu_suite.log
+# round-6 GPU step: pruned-width block test, then the teacher-robustness probe (wgrad combine order A/B)
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_pruned_widths_gpu.py -k bottlenecks > gpurun_out/t3.log 2>&1
+rc=$?; tail -3 gpurun_out/t3.log
 [ $rc -le 1 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pruned -o r1 -- python scripts/probes/pruned_train_probe.py --rounds 1 --steps 5 > gpurun_out/prof_pruned/probe.log 2>&1
-rc=$?; grep pruned_train gpurun_out/prof_pruned/probe.log; exit $rc
+R="lr=0.05 lr=0.02 lr=0.02,noise=3.0,modes=64"
+timeout -k 10 400 python -u scripts/probes/teacher_robustness.py --seeds 0 1 2 --recipes $R > gpurun_out/teach_default.log 2>&1
+rc=$?; grep recipe gpurun_out/teach_default.log; [ $rc -eq 0 ] || exit $rc
+TP_WGRAD_COMBINE_LANES=1 timeout -k 10 400 python -u scripts/probes/teacher_robustness.py --seeds 0 1 2 --recipes $R > gpurun_out/teach_lanes1.log 2>&1
+rc=$?; grep recipe gpurun_out/teach_lanes1.log; exit $rc

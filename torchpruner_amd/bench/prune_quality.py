@@ -31,11 +31,13 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from .. import Pruner, TaylorAttributionMetric, get_vgg_pruning_graph
+from .. import Pruner, ShapleyAttributionMetric, TaylorAttributionMetric, get_vgg_pruning_graph
 from ..data import DeviceLoader, PrototypeTask
 from ..engine.fused_chain import TUNER
 from ..engine.train import native_convs
 from ..models import prunable_vgg16
+from ..utils import find_best_module_for_attributions
+from ..utils.ablation import ablation_curve
 from ..utils.train import recalibrate_bn
 
 # Calibrated on MI355X. Round 3 (profiles/prune_quality_sweep.md, 27 configurations x 3-5 seeds): a
@@ -189,6 +191,56 @@ def oneshot_top1(teacher, task, seed, cfg, xv, yv):
     return out
 
 
+# The reference's own quality measure (nbVGG:1233-1285, AUC nbVGG:1521-1527): per conv, the units
+# are removed one at a time in ascending-score order (after BN + ReLU, simulated pruning) on held-out
+# ablation images; the AUC is the loss increase summed over every removal step and every layer,
+# divided by the total unit count (lower = the ranking removed the unimportant units first).
+# Scores on ``attr_imgs`` held-out attribution images at B=100 (nbVGG:193-196); SV with
+# sv_samples=5; Random averaged over ``random_draws`` permutations (the notebook runs it 3x).
+LAYERWISE = dict(attr_imgs=1000, ablation_imgs=1000, sv_samples=5, random_draws=3)
+
+
+def layerwise_auc(model, task, seed, methods=("taylor", "random", "sv"), lw=None):
+    """{"layerwise_auc_<method>": AUC, "layerwise_auc_<method>_per_layer": [...]} of one model."""
+    lw = dict(LAYERWISE, **(lw or {}))
+    dev = next(model.parameters()).device
+    model.eval()
+    convs = [m for m in model.features if isinstance(m, torch.nn.Conv2d)]
+    evs = [find_best_module_for_attributions(model, c) for c in convs]
+    xs, ys = task.sample(lw["attr_imgs"], seed * 7 + 101)
+    xt, yt = task.sample(lw["ablation_imgs"], seed * 7 + 102)
+    scores = {}
+    with TUNER.fixed():
+        if "taylor" in methods:
+            scores["taylor"] = [[s] for s in TaylorAttributionMetric(
+                model, DeviceLoader(xs, ys, 100), F.cross_entropy, dev, shard_data=False).run_many(
+                    convs, find_best_evaluation_module=True)]
+        if "sv" in methods:
+            np.random.seed(seed * 13 + 5)  # the metric's permutations (numpy global RNG, as the reference)
+            sv = ShapleyAttributionMetric(model, DeviceLoader(xs, ys, 100), F.cross_entropy, dev,
+                                          sv_samples=lw["sv_samples"], shard_data=False)
+            scores["sv"] = [[sv.run(c, find_best_evaluation_module=True)] for c in convs]
+        if "random" in methods:
+            rng = np.random.RandomState(seed * 17 + 3)
+            scores["random"] = [[rng.random_sample(c.out_channels) for _ in range(lw["random_draws"])]
+                                for c in convs]
+        out = {}
+        for mth, per_conv in scores.items():
+            tot, units, per_layer = 0.0, 0, []
+            for ev, runs in zip(evs, per_conv):
+                inc = []
+                for sc in runs:
+                    losses, _ = ablation_curve(model, ev, np.argsort(sc, kind="stable"), xt, yt, F.cross_entropy)
+                    inc.append(float(np.sum(losses[1:] - losses[0])))
+                n = len(runs[0])
+                tot += float(np.mean(inc))
+                units += n
+                per_layer.append(round(float(np.mean(inc)) / n, 4))
+            out[f"layerwise_auc_{mth}"] = tot / units
+            out[f"layerwise_auc_{mth}_per_layer"] = per_layer
+    return out
+
+
 def weights_digest(model) -> str:
     h = hashlib.sha256()
     for t in model.state_dict().values():
@@ -204,6 +256,7 @@ def run_protocol(seed=0, device="cuda", log=None, **overrides):
     xv, yv = task.sample(cfg["val_imgs"], seed * 7 + 3)
     before = top1(teacher, xv, yv)
     out = {"seed": seed, "top1_before": before, "teacher_digest": weights_digest(teacher)}
+    out.update(layerwise_auc(teacher, task, seed))
     out.update(oneshot_top1(teacher, task, seed, cfg, xv, yv))
     for method in ("taylor", "random"):
         m = iterative_prune(copy.deepcopy(teacher), task, method, seed, cfg, log=log)
