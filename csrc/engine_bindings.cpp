@@ -965,7 +965,8 @@ void wino_wgrad(const at::Tensor& g, const at::Tensor& x, int64_t cfg, int64_t s
   need(x, "x", 4);
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = g.size(3);
   TORCH_CHECK(g.size(0) == B && g.size(1) == H && g.size(2) == W, "g must be (B, H, W, Cout) of a same-size conv");
-  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && Cin % 32 == 0 && Cout % 4 == 0, "wino_wgrad needs even H/W, Cin % 32, Cout % 4");
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && Cin % 4 == 0 && Cin >= 8 && Cout % 4 == 0,
+              "wino_wgrad needs even H/W, Cin % 4 (>= 8), Cout % 4");
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 4 && out.size(2) == 3 &&
                   out.size(3) == 3 && out.size(0) <= Cout && out.size(1) <= Cin && out.device() == g.device(),
               "out must be a float32 (Cout_r, Cin_r, 3, 3) tensor on the device");

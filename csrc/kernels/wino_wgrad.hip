@@ -131,28 +131,33 @@ extern "C" hipError_t tp_conv_wgrad3(const float* g, const float* x, float* dw, 
                                      float* fin, int fin_co, int fin_ci, const long long* fs, int batch,
                                      long long g_bstride, long long x_bstride, hipStream_t st);
 
-// Workspace (floats) of tp_wino_wgrad: V (16*T*Cin) + dM (16*T*Cout) + dU (16*Cout*Cin) + the
-// split slabs of the batched GEMM (splits*16*Cout*Cin).
+// Workspace (floats) of tp_wino_wgrad: V (16*T*Cin) + dM (16*T*Cout) + dU (16*Cout*Kp) + the
+// split slabs of the batched GEMM (splits*16*Cout*Kp); Kp = Cin rounded up to the GEMM's 32-wide
+// K granule (pruned widths: the padded columns of dU are zeros nobody reads).
 extern "C" long long tp_wino_wgrad_ws_elems(int B, int H, int W, int Cin, int Cout, int splits) {
   const long long T = (long long)B * (H / 2) * (W / 2);
-  return 16 * T * Cin + 16 * T * Cout + 16ll * Cout * Cin * (1 + (splits > 1 ? splits : 0));
+  const long long Kp = (Cin + 31) / 32 * 32;
+  return 16 * T * Cin + 16 * T * Cout + 16ll * Cout * Kp * (1 + (splits > 1 ? splits : 0));
 }
 
-// g (B, H, W, Cout), x (B, H, W, Cin) NHWC; H, W even; Cin % 32 == 0, Cout % 4 == 0. Writes the
-// (fin_co, fin_ci, 3, 3) parameter-layout gradient with element strides fs.
+// g (B, H, W, Cout), x (B, H, W, Cin) NHWC; H, W even; Cin % 4 == 0 (any pruned width carried at
+// a multiple of 4), Cout % 4 == 0. Writes the (fin_co, fin_ci, 3, 3) parameter-layout gradient with
+// element strides fs.
 extern "C" hipError_t tp_wino_wgrad(const float* g, const float* x, float* ws, int B, int H, int W, int Cin, int Cout,
                                     int cfg, int splits, float* fin, int fin_co, int fin_ci, const long long* fs,
                                     hipStream_t st) {
   using namespace tp;
-  if ((H & 1) || (W & 1) || Cin % 32 || Cout % 4 || !fin || !fs || fin_co > Cout || fin_ci > Cin || splits < 1)
+  if ((H & 1) || (W & 1) || Cin % 4 || Cin < 8 || Cout % 4 || !fin || !fs || fin_co > Cout || fin_ci > Cin ||
+      splits < 1)
     return hipErrorInvalidValue;
+  const int Kp = (Cin + 31) / 32 * 32;
   const long long T = (long long)B * (H / 2) * (W / 2);
   if (T <= 0) return hipErrorInvalidValue;
   if (T * Cin * 4 >= (1ll << 31) || T * Cout * 4 >= (1ll << 31) || T >= (1ll << 31)) return hipErrorInvalidValue;
   float* v = ws;
   float* m = v + 16 * T * Cin;
   float* du = m + 16 * T * Cout;
-  float* slabs = du + 16ll * Cout * Cin;
+  float* slabs = du + 16ll * Cout * Kp;
   const FastDiv fd_timg((unsigned)((H / 2) * (W / 2))), fd_w2((unsigned)(W / 2));
   unsigned grid = (unsigned)std::min<long long>(ceil_div(T * (Cin / 4), 256), 16384);
   wgrad_x_transform<<<grid, 256, 0, st>>>(x, v, B, H, W, Cin, T, fd_timg, fd_w2);
@@ -161,10 +166,10 @@ extern "C" hipError_t tp_wino_wgrad(const float* g, const float* x, float* ws, i
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // 16 GEMMs dU[xi] = dM[xi]^T V[xi] over the T tiles: "1x1 conv" weight gradients of (1, T, 1, C)
-  e = tp_conv_wgrad3(m, v, du, splits > 1 ? slabs : nullptr, 1, (int)T, 1, Cin, Cout, 1, 1, 0, Cin, cfg, splits,
+  e = tp_conv_wgrad3(m, v, du, splits > 1 ? slabs : nullptr, 1, (int)T, 1, Cin, Cout, 1, 1, 0, Kp, cfg, splits,
                      nullptr, 0, 0, nullptr, 16, T * Cout, T * Cin, st);
   if (e != hipSuccess) return e;
   grid = (unsigned)std::min<long long>(ceil_div((long long)fin_co * fin_ci, 256), 16384);
-  wgrad_out_transform<<<grid, 256, 0, st>>>(du, fin, Cout, Cin, fin_co, fin_ci, fs[0], fs[1], fs[2], fs[3]);
+  wgrad_out_transform<<<grid, 256, 0, st>>>(du, fin, Cout, Kp, fin_co, fin_ci, fs[0], fs[1], fs[2], fs[3]);
   return hipGetLastError();
 }

@@ -357,7 +357,7 @@ def _conv_wgrad(g, xh, meta):
         cands += [(cfg, sp)] + ([(cfg, sp // 2)] if sp > 1 else [])
         cands += [(cfg, s_) for s_ in _wgrad_wave_splits(P, tiles) if s_ not in (sp, sp // 2)]
     H, W = meta[5], meta[6]
-    if ks == 3 and stride == 1 and pad == 1 and H % 2 == 0 and W % 2 == 0 and cin_p % 32 == 0:
+    if ks == 3 and stride == 1 and pad == 1 and H % 2 == 0 and W % 2 == 0 and cin_p != 4:
         tiles = g.shape[0] * (H // 2) * (W // 2)
         for cfg, (bm, bn) in ((0, (128, 128)), (2, (128, 64)), (1, (64, 64))):
             sp = _wgrad_splits(tiles, 16 * math.ceil(cout_p / bm) * math.ceil(cin_p / bn))
