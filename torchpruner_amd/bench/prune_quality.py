@@ -40,7 +40,7 @@ from ..utils import find_best_module_for_attributions
 from ..utils.ablation import ablation_curve
 from ..utils.train import recalibrate_bn
 
-# Calibrated on MI355X. Round 3 (profiles/prune_quality_sweep.md, 27 configurations x 3-5 seeds): a
+# Calibrated on MI355X. Round 3 (profiles/archive/prune_quality_sweep.md, 27 configurations x 3-5 seeds): a
 # 32-modes-per-class task the teacher fits, trained with weight decay 5e-3 — like a long CIFAR run,
 # this leaves channels of very unequal importance, which is the regime filter pruning targets
 # (with 5e-4 every channel still matters and any 50% subset retrains about equally well). But that

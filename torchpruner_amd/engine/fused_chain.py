@@ -953,7 +953,7 @@ class FusedChainEngine:
     # HIP-graph replay of the fused step (TORCHPRUNER_GRAPHS): "auto" (default) = for batches up to
     # GRAPH_MAX_B when two or more batches are in flight on the stream pipeline; "1" = also for
     # one batch at a time; "all" = any batch size; "0" = never. One batch at a time the step is
-    # GPU-bound down to B=8 (profiles/hip_graphs_taylor_step.txt), but with two batches in flight
+    # GPU-bound down to B=8 (profiles/archive/hip_graphs_taylor_step.txt), but with two batches in flight
     # the GPU finishes a B=100 step (~55 launches) faster than Python enqueues it: the host spent
     # 0.77-0.99 ms per batch in the pipeline against 0.85-1.04 ms of wall
     # (scripts/probes/b100_host_probe.py), so the pipelined launches replay one graph per slot. Large

@@ -4,7 +4,7 @@ and the convolutions of the generic attribution path (any model with standard co
 The reference finetunes with cuDNN convolutions (experiments/utils/train.py:11-48). On ROCm the
 library path is MIOpen, which JIT-compiles and benchmarks kernels for every new convolution
 shape: after each pruning round every pruned layer has a new shape, and the first steps of the
-round pay 20-40 s of compilation (profiles/resnet50_prune_finetune_1gpu.log). Here the
+round pay 20-40 s of compilation (profiles/archive/resnet50_prune_finetune_1gpu.log). Here the
 convolutions of a model run on the precompiled gfx950 kernels instead, through autograd:
 
   forward   implicit-GEMM fp32 MFMA conv (``tpamd.conv_gen``), bias in the epilogue
