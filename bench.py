@@ -672,15 +672,20 @@ def accuracy(args, model, task, convs, scores, cfg, dev, log):
     lw_r = float(np.mean([layerwise_mask_top1([rng.random_sample(c.out_channels) for c in convs], xv, yv)
                           for _ in range(3)]))
     runs = [{"seed": args.seed, "top1_before": before}]
+    t2 = time.perf_counter()
     runs[0].update(pq.layerwise_auc(model, task, args.seed))
+    log(f"[quality] seed {args.seed}: layerwise AUC Taylor {runs[0]['layerwise_auc_taylor']:.4f} / SV "
+        f"{runs[0]['layerwise_auc_sv']:.4f} / Random {runs[0]['layerwise_auc_random']:.4f} "
+        f"({time.perf_counter() - t2:.1f}s)")
     runs[0].update(pq.oneshot_top1(model, task, args.seed, cfg, xv, yv))
     params = None
     for method in ("taylor", "random"):
         m = pq.iterative_prune(copy.deepcopy(model), task, method, args.seed, cfg)
         runs[0][f"top1_pruned_{method}"] = pq.top1(m, xv, yv)
         params = sum(p.numel() for p in m.parameters())
+    log(f"[quality] seed {args.seed}: one-shot + iterative prunes done ({time.perf_counter() - t1:.1f}s)")
     for s in range(args.seed + 1, args.seed + max(1, args.quality_seeds)):
-        runs.append(pq.run_protocol(s, dev, **cfg))  # its own teacher, task and held-out set
+        runs.append(pq.run_protocol(s, dev, log=log, **cfg))  # its own teacher, task and held-out set
     mean = {k: float(np.mean([r[k] for r in runs])) for k in ("top1_before", "top1_pruned_taylor",
                                                              "top1_pruned_random")}
     std = {k: float(np.std([r[k] for r in runs])) for k in ("top1_before", "top1_pruned_taylor",
@@ -761,7 +766,7 @@ def accuracy(args, model, task, convs, scores, cfg, dev, log):
     # the same protocol with the reference's weight decay (cifar10.py:95-99), one seed: reported
     # alongside because the headline protocol's teacher_wd=5e-3 was chosen by a sweep
     t2 = time.perf_counter()
-    r = pq.run_protocol(args.seed, dev, **dict(cfg, teacher_wd=5e-4))
+    r = pq.run_protocol(args.seed, dev, layerwise=False, **dict(cfg, teacher_wd=5e-4))
     out["top1_pruned_50pct_wd5e-4"] = {"seed": args.seed, "before": round(r["top1_before"], 4),
                                        "taylor": round(r["top1_pruned_taylor"], 4),
                                        "random": round(r["top1_pruned_random"], 4)}

@@ -248,21 +248,33 @@ def weights_digest(model) -> str:
     return h.hexdigest()[:16]
 
 
-def run_protocol(seed=0, device="cuda", log=None, **overrides):
-    """Teacher + Taylor- and Random-pruned copies; returns a dict of top-1 figures."""
+def run_protocol(seed=0, device="cuda", log=None, layerwise=True, **overrides):
+    """Teacher + Taylor- and Random-pruned copies; returns a dict of top-1 figures (and, with
+    ``layerwise``, the teacher's layerwise ablation AUCs)."""
     cfg = dict(DEFAULTS, **overrides)
     t0 = time.perf_counter()
     teacher, task = make_teacher(seed, device, cfg)
     xv, yv = task.sample(cfg["val_imgs"], seed * 7 + 3)
     before = top1(teacher, xv, yv)
     out = {"seed": seed, "top1_before": before, "teacher_digest": weights_digest(teacher)}
-    out.update(layerwise_auc(teacher, task, seed))
+    t1 = time.perf_counter()
+    if layerwise:
+        out.update(layerwise_auc(teacher, task, seed))
+    t2 = time.perf_counter()
     out.update(oneshot_top1(teacher, task, seed, cfg, xv, yv))
+    t3 = time.perf_counter()
+    if log and layerwise:
+        log(f"[quality] seed {seed}: teacher {before:.4f} ({t1 - t0:.1f}s); layerwise AUC Taylor "
+            f"{out['layerwise_auc_taylor']:.4f} / SV {out['layerwise_auc_sv']:.4f} / Random "
+            f"{out['layerwise_auc_random']:.4f} ({t2 - t1:.1f}s); one-shot ({t3 - t2:.1f}s)")
     for method in ("taylor", "random"):
-        m = iterative_prune(copy.deepcopy(teacher), task, method, seed, cfg, log=log)
+        m = iterative_prune(copy.deepcopy(teacher), task, method, seed, cfg)
         out[f"top1_pruned_{method}"] = top1(m, xv, yv)
         out[f"digest_{method}"] = weights_digest(m)
         out["params_pruned"] = sum(p.numel() for p in m.parameters())
+        if log:
+            log(f"[quality] seed {seed}: iterative 50% prune, {method}: {out[f'top1_pruned_{method}']:.4f} "
+                f"({time.perf_counter() - t3:.1f}s)")
     out["params_before"] = sum(p.numel() for p in teacher.parameters())
     out["seconds"] = round(time.perf_counter() - t0, 1)
     out["config"] = cfg
