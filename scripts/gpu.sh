@@ -13,6 +13,7 @@
 #   pmc-lowk CFG            two PMC passes of the 64 -> 256 @ 56 px 1x1 training GEMM, tile config CFG
 #   dist N                  N ranks self-launched on this one GPU over gloo, every bench phase at reduced sizes
 #   teacher [recipes]       the accuracy protocol's teacher under both wgrad combine orders
+#   ddp-overlap [args]      DDP bucket ready times inside the native ResNet-50 backward (1 rank, RCCL)
 #   b100                    B=100 (the reference's attribution batch): bench extra + tuner log
 # Every GPU step runs under its own timeout; a failing step ends the script (no retries).
 set -o pipefail
@@ -117,6 +118,10 @@ case $task in
     step teach_default 600 python -u scripts/probes/teacher_robustness.py --seeds 0 1 2 --recipes $recipes
     TP_WGRAD_COMBINE_LANES=1 step teach_lanes1 600 python -u scripts/probes/teacher_robustness.py --seeds 0 1 2 --recipes $recipes
     grep -h recipe "$O/teach_default.log" "$O/teach_lanes1.log"
+    ;;
+  ddp-overlap)
+    step ddp_overlap 400 python -u scripts/probes/ddp_overlap_probe.py "$@"
+    grep ddp_overlap "$O/ddp_overlap.log"
     ;;
   b100)
     TORCHPRUNER_TUNER_LOG=1 step b100 400 python -u bench.py --steps 2 --warmup 1 --teacher-steps 0 --no-prune --no-baseline --extras b100

@@ -7,9 +7,14 @@ wrapper must be rebuilt after every prune: :class:`PrunableDDP` does that, re-br
 the (already identical, see Pruner's index broadcast R5) parameters from rank 0 (R7).
 
 Gradient all-reduce runs on RCCL over xGMI. xGMI is point-to-point (7 links x ~153 GB/s per
-MI355X); RCCL's ring/tree channels are per-link bound, so large buckets amortise the
-per-collective latency while the first bucket still overlaps the tail of backward. The
-default ``bucket_cap_mb=64`` puts a ResNet-50 (~102 MB of fp32 gradients) in 2 buckets.
+MI355X); RCCL's ring/tree channels are per-link bound, so buckets must be large enough to
+amortise the per-collective latency, but the LAST bucket is what stays exposed: it becomes
+ready only when the backward ends. Measured inside the native ResNet-50 backward (B=128,
+``scripts/probes/ddp_overlap_probe.py``, ``profiles/dist/ddp_bucket_overlap_r6.txt``): 91 of the
+97.5 MB of gradients (layers 2-4 + fc) are ready within the first 12 ms of a 25 ms backward, the
+stage-1 / stem tail produces the rest over the last 13 ms. With 64 MB buckets the last one holds
+32.6 MB (~0.34 ms of 8-rank ring at 200 GB/s bus bandwidth after the backward); with 16 MB it
+holds 8 MB (~0.11 ms) in 6 collectives, hence the default ``bucket_cap_mb=16``.
 """
 from __future__ import annotations
 
@@ -24,7 +29,7 @@ class PrunableDDP(nn.Module):
     """Wraps ``module`` in DDP when a multi-rank process group is live (identity otherwise)
     and rebuilds the wrapper on :meth:`rewrap` after pruning."""
 
-    def __init__(self, module: nn.Module, device=None, bucket_cap_mb: float = 64.0, **ddp_kwargs):
+    def __init__(self, module: nn.Module, device=None, bucket_cap_mb: float = 16.0, **ddp_kwargs):
         super().__init__()
         self.module = module
         self.device = device
