@@ -128,6 +128,7 @@ class ResNetEngine:
         self.plan = plan
         self._key = None
         self._packed = None
+        self._arena_sizes = {}  # grad_scores call shape -> floats of Taylor partial slabs it needs
 
     def max_batch(self, sample_shape) -> int:
         """Largest batch whose activations stay inside the kernels' 32-bit buffer descriptors
@@ -391,7 +392,23 @@ class ResNetEngine:
             e["wt"] = w4.permute(3, 1, 2, 0).reshape(ci, ks * ks * co).contiguous()
         return e
 
-    def _dgrad(self, T, e, g, mask, res=None, res_stride=1, low_res=False, tay_mode=None):
+    @staticmethod
+    def _slab(arena, R, B, N, dev):
+        """A zeroed (R, B, N) Taylor partial slab: a view into this call's arena (one zero-fill
+        for every layer instead of one per layer) when it fits, else its own allocation. The
+        arena records what the call asked for, so the next call of the same shape gets one that
+        fits (views start on 256-B boundaries)."""
+        n = R * B * N
+        if arena is None:
+            return torch.zeros(R, B, N, device=dev)
+        arena[2] += (n + 63) // 64 * 64
+        buf, off = arena[0], arena[1]
+        if buf is not None and off + n <= buf.numel():
+            arena[1] = off + (n + 63) // 64 * 64
+            return buf[off:off + n].view(R, B, N)
+        return torch.zeros(R, B, N, device=dev)
+
+    def _dgrad(self, T, e, g, mask, res=None, res_stride=1, low_res=False, tay_mode=None, arena=None):
         """dL/d(input) of conv ``e`` from g = dL/d(conv output) (BN scale folded in), plus
         ``res``, masked by ``mask`` (the input's post-ReLU activation). ``low_res``: a strided
         1x1 conv's gradient at the output resolution (scattered by the consumer's res_stride).
@@ -443,13 +460,13 @@ class ResNetEngine:
 
         cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands if cands else None)
         if tay_mode is not None and cfg in (WINO, WINO_LDS):
-            tay = torch.zeros(taylor_slots(Ho, Wo), B, N, device=g.device)
+            tay = self._slab(arena, taylor_slots(Ho, Wo), B, N, g.device)
             return run(cfg, sp, tay=tay), tay
         if tay_mode is not None and cfg == WINO4S:
-            tay = torch.zeros(T.wino4_taylor_slots(Ho), B, N, device=g.device)
+            tay = self._slab(arena, T.wino4_taylor_slots(Ho), B, N, g.device)
             return run(cfg, sp, tay=tay), tay
         if gen_tay:
-            tay = torch.zeros(T.conv_gen_tay_slots(cfg, Ho * Wo), B, N, device=g.device)
+            tay = self._slab(arena, T.conv_gen_tay_slots(cfg, Ho * Wo), B, N, g.device)
             return run(cfg, sp, tay=tay), tay
         return run(cfg, sp), None
 
@@ -479,6 +496,10 @@ class ResNetEngine:
         out = {}
         if first is None:
             return out
+        # one zero-filled arena for the call's Taylor partial slabs: [buffer, offset, floats asked]
+        akey = (tuple(x.shape), mode, tuple(sorted(i for i, m in enumerate(self.eval_modules()) if m in want)))
+        size = self._arena_sizes.get(akey)
+        arena = [torch.zeros(size, device=x.device) if size else None, 0, 0]
         for bi in range(len(blocks) - 1, first - 1, -1):
             blk, e = blocks[bi], P["blocks"][bi]
             x_in, inner, _ = saved[bi]
@@ -487,7 +508,8 @@ class ResNetEngine:
                 a_prev = inner[ci - 1]
                 bn = blk.convs[ci - 1].bn
                 tm = ({"taylor": 0, "taylor_signed": 0, "sensitivity": 1}.get(mode) if bn in want else None)
-                g, tay = self._dgrad(T, e["convs"][ci], g, a_prev, tay_mode=tm)  # dL/d(bn_{ci} output), masked
+                g, tay = self._dgrad(T, e["convs"][ci], g, a_prev, tay_mode=tm,
+                                     arena=arena)  # dL/d(bn_{ci} output), masked
                 if tay is not None:  # partials from the data-gradient epilogue
                     if raw_slabs:
                         out[bn] = tay
@@ -504,6 +526,8 @@ class ResNetEngine:
             else:
                 g_res, rs = g_s, 1
             g_s, _ = self._dgrad(T, e["convs"][0], g, x_in, res=g_res, res_stride=rs)
+        if arena[2] > (size or 0):
+            self._arena_sizes[akey] = arena[2]
         return out
 
     def eval_modules(self):
