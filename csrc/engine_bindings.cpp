@@ -850,11 +850,15 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
   sp = (kt + per - 1) / per;
   float* tp_ = nullptr;
   if (taylor.has_value() && taylor->defined()) {
-    // fused Taylor / Sensitivity partials (R, B, N) of the masked output (1x1, stride 1, one K pass)
-    const int R = tp_conv_gen_tay_slots((int)cfg, (int)(Ho * Wo));
-    TORCH_CHECK(!transposed && ks == 1 && mp != nullptr && sp == 1 && R > 0,
-                "conv_gen_bwd taylor partials need a 1x1 stride-1 dgrad with a mask, one K pass, and a tile "
-                "config spanning <= 4 images");
+    // fused Taylor / Sensitivity partials (R, B, N) of the masked output: a 1x1 stride-1 dgrad
+    // (one K pass), or a transposed 3x3 stride-2 one at even Ho / Wo (the parity row order: one
+    // slot range per stride phase, R = 4 x the slots of an Ho/2 x Wo/2 group)
+    const bool t3 = transposed && ks == 3 && stride == 2 && Ho % 2 == 0 && Wo % 2 == 0;
+    const int R = t3 ? 4 * tp_conv_gen_tay_slots((int)cfg, (int)(Ho * Wo / 4))
+                     : tp_conv_gen_tay_slots((int)cfg, (int)(Ho * Wo));
+    TORCH_CHECK(((!transposed && ks == 1) || t3) && mp != nullptr && sp == 1 && R > 0,
+                "conv_gen_bwd taylor partials need a mask and a 1x1 stride-1 dgrad (one K pass) or a transposed "
+                "3x3 stride-2 dgrad at even output size, and a tile config spanning <= 4 row groups");
     TORCH_CHECK(taylor->is_cuda() && taylor->scalar_type() == at::kFloat && taylor->is_contiguous() &&
                     taylor->numel() == (int64_t)R * B * N,
                 "taylor must be a contiguous float32 (R, B, N) GPU tensor with R = ", R);

@@ -42,7 +42,7 @@ enum Epi : int {
   EPI_FWD_POOL = 1,  // + 2x2 max-pool: pooled value + argmax byte
   EPI_BWD = 2,       // dgrad epilogue: Taylor partial of the consumer's activation, masked/scaled grad
   EPI_PARTIAL = 3,   // raw split-K partial slab (epilogue applied by conv_epilogue)
-  EPI_FWD_TAY = 4,   // GEN 1x1 data gradient: EPI_FWD's LDS epilogue + Taylor partials (tay_part); a
+  EPI_FWD_TAY = 4,   // GEN 1x1 / GEN 3 3x3 stride-2 data gradient: EPI_FWD's LDS epilogue + Taylor partials (tay_part); a
                      // separate instantiation so the partials' registers never burden EPI_FWD
 };
 
@@ -565,6 +565,10 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     float* ts = smem;  // the main loop ended with a barrier
     float* cb = smem + BM * LDT;  // APoZ counts [image in block][column]
     const int b_first = m0 / p.HWo;
+    // Taylor partial row groups: one image (GEN 1), or one (stride phase, image) of the parity
+    // row order (GEN 3: Ho / 2 x Wo / 2 contiguous rows each)
+    const int tgs = (GEN == 3 && p.parity) ? (p.Ho >> 1) * (p.Wo >> 1) : p.HWo;
+    const int g_first = m0 / tgs;
     const bool cb_lds = (EPI == EPI_FWD || EPI == EPI_FWD_TAY) && p.apoz && (min(m0 + BM, p.M) - 1) / p.HWo - b_first < CB_IMG;
     if (cb_lds)
       for (int t = tid; t < CB_IMG * BN; t += T::NT) cb[t] = 0.f;
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         *reinterpret_cast<float4*>(p.out + o) = v;
         if constexpr (EPI == EPI_FWD_TAY) {
           if (p.tay_part) {  // slot by image (static selects: no dynamic register indexing)
-            const int sl = m / p.HWo - b_first;
+            const int sl = m / tgs - g_first;
             float4 t;
             if (p.tay_mode) {
               t = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
@@ -739,16 +743,17 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
 #pragma unroll
         for (int i = 0; i < NTQ; ++i) *reinterpret_cast<float4*>(red + (i * RSTEP + row0) * BN + c4 * 4) = tq[i];
         __syncthreads();
-        const int n_img = min((min(m0 + BM, p.M) - 1) / p.HWo - b_first + 1, NTQ);
-        const int B = p.M / p.HWo, R = gen_tay_slots(BM, p.HWo);
-        for (int t = tid; t < n_img * BN; t += T::NT) {
+        const int n_grp = min((min(m0 + BM, p.M) - 1) / tgs - g_first + 1, NTQ);
+        const int B = p.M / p.HWo, R = gen_tay_slots(BM, tgs);
+        for (int t = tid; t < n_grp * BN; t += T::NT) {
           const int sl = t / BN, col = t - sl * BN;
           float acc = 0.f;
 #pragma unroll 4
           for (int r = 0; r < RSTEP; ++r) acc += red[(sl * RSTEP + r) * BN + col];
-          const int b = b_first + sl;
-          const int slot = m0 / BM - (b * p.HWo) / BM;
-          if (n0 + col < p.N && slot < R) p.tay_part[((long long)slot * B + b) * p.N + n0 + col] = acc;
+          const int grp = g_first + sl, cq = grp / B, b = grp - cq * B;  // cq: stride phase (GEN 3)
+          const int slot = m0 / BM - (grp * tgs) / BM;
+          if (n0 + col < p.N && slot < R)
+            p.tay_part[((long long)(cq * R + slot) * B + b) * p.N + n0 + col] = acc;
         }
       }
     }
@@ -1672,8 +1677,10 @@ extern "C" hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H,
 
 // ``bnpart`` (nullable): [ceil(M / tile_m(cfg))][2][Cout] doubles receiving the per-tile column
 // sums / sums of squares of the output (training BatchNorm statistics); no split-K then.
-// ``tay_part`` (nullable, needs ``mask``, no split-K, not transposed): [R][B][Cout] Taylor partials
-// (tp_conv_gen_tay_slots), every slot written or left as the caller zeroed it.
+// ``tay_part`` (nullable, needs ``mask``, no split-K; 1x1 stride 1, or transposed 3x3 stride 2 at
+// even Ho / Wo): [R][B][Cout] Taylor partials, R = tp_conv_gen_tay_slots(cfg, Ho * Wo) (transposed:
+// 4 x tp_conv_gen_tay_slots(cfg, Ho * Wo / 4), one slot range per stride phase), every slot
+// written or left as the caller zeroed it.
 extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
                                    int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
                                    const float* scale, const float* shift, int relu, const float* res,
@@ -1737,8 +1744,10 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
     if (splits > 1) return hipErrorInvalidValue;
     a.bnpart = bnpart;
   }
-  if (tay_part) {
-    if (splits > 1 || !mask || gen != 1 || cfg >= 16 || tp_conv_gen_tay_slots(cfg, a.HWo) == 0)
+  if (tay_part) {  // GEN 1: 1x1; GEN 3: the parity-ordered 3x3 stride-2 data gradient (4 phase groups)
+    const bool t3 = gen == 3 && a.parity && ks == 3;
+    if (splits > 1 || !mask || !((gen == 1 && ks == 1) || t3) || cfg >= 16 ||
+        tp_conv_gen_tay_slots(cfg, t3 ? a.HWo / 4 : a.HWo) == 0)
       return hipErrorInvalidValue;
     a.tay_part = tay_part;
     a.tay_mode = tay_mode;
@@ -1749,7 +1758,7 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
     a.sk_ws = ws;
   }
   a.sb = sb ? 1 : 0;
-  if (a.tay_part) return gen_cfg<1, 1, EPI_FWD_TAY>(cfg, a, 1, st);
+  if (a.tay_part) return gen == 3 ? gen_cfg<3, 3, EPI_FWD_TAY>(cfg, a, 1, st) : gen_cfg<1, 1, EPI_FWD_TAY>(cfg, a, 1, st);
   if (splits == 1) return gen_dispatch<EPI_FWD>(ks, gen, cfg, a, 1, st);
   if (!ws) return hipErrorInvalidValue;
   ConvArgs b = a;

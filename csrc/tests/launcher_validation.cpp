@@ -25,6 +25,12 @@ hipError_t tp_conv_gen2(const float* x, const float* w, int B, int H, int W, int
                         int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
                         const float* shift, int relu, const float* res, int res_stride, const float* mask,
                         float* apoz, float* out, float* ws, hipStream_t st);
+hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                        int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
+                        const float* shift, int relu, const float* res, int res_stride, const float* mask,
+                        float* apoz, float* out, float* ws, double* bnpart, float* tay_part, int tay_mode,
+                        hipStream_t st);
+int tp_conv_gen_tay_slots(int cfg, int HWo);
 hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                          int ks, int stride, int pad, int Kpad, int cfg, int splits, hipStream_t st);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
@@ -89,6 +95,21 @@ int main() {
          hipErrorInvalidValue);  // res_stride 0
   EXPECT(tp_conv_gen2(n, n, 4096, 256, 256, 64, 64, 3, 1, 1, 0, 0, 0, 0, 1, n, n, 0, n, 1, n, n, n, n, 0) ==
          hipErrorInvalidValue);  // exceeds the 32-bit buffer-descriptor range
+  // Taylor partials of the GEN data gradients: 1x1 stride 1, or transposed 3x3 stride 2 at even Ho / Wo
+  float* tp_ = reinterpret_cast<float*>(16);
+  const float* mk = reinterpret_cast<const float*>(16);
+  EXPECT(tp_conv_gen_tay_slots(2, 3136) == 50 && tp_conv_gen_tay_slots(0, 49) == 2);
+  EXPECT(tp_conv_gen_tay_slots(1, 49) == 0 && tp_conv_gen_tay_slots(4, 3136) == 0);  // > 4 images / spilling cfg
+  EXPECT(tp_conv_gen4(n, n, 2, 8, 8, 64, 64, 3, 1, 1, 0, 0, 0, 2, 1, n, n, 0, n, 1, mk, n, n, n, nullptr, tp_, 0, 0) ==
+         hipErrorInvalidValue);  // GEN 1 3x3: no partials
+  EXPECT(tp_conv_gen4(n, n, 2, 4, 4, 64, 64, 1, 2, 0, 1, 8, 8, 2, 1, n, n, 0, n, 1, mk, n, n, n, nullptr, tp_, 0, 0) ==
+         hipErrorInvalidValue);  // transposed 1x1: no partials
+  EXPECT(tp_conv_gen4(n, n, 2, 4, 4, 64, 64, 3, 2, 1, 1, 7, 7, 2, 1, n, n, 0, n, 1, mk, n, n, n, nullptr, tp_, 0, 0) ==
+         hipErrorInvalidValue);  // odd output: no parity row order
+  EXPECT(tp_conv_gen4(n, n, 2, 4, 4, 64, 64, 3, 2, 1, 1, 8, 8, 4, 1, n, n, 0, n, 1, mk, n, n, n, nullptr, tp_, 0, 0) ==
+         hipErrorInvalidValue);  // cfg 4: no partials
+  EXPECT(tp_conv_gen4(n, n, 2, 4, 4, 64, 64, 3, 2, 1, 1, 8, 8, 2, 1, n, n, 0, n, 1, nullptr, n, n, n, nullptr, tp_, 0,
+                      0) == hipErrorInvalidValue);  // no mask
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 6, 64, 3, 1, 1, 64, 0, 1, 0) == hipErrorInvalidValue);   // Cin % 4
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 96, 0, 1, 0) == hipErrorInvalidValue);  // Kpad small
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 576, 7, 1, 0) == hipErrorInvalidValue); // bad cfg

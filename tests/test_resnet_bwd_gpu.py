@@ -238,3 +238,50 @@ def test_conv_gen_bwd_taylor_partials(cuda, cfg, B, hw, C, N, tay_mode):
     tay2 = torch.zeros_like(tay)
     T.conv_gen_bwd(*args, tay2, tay_mode)
     assert torch.equal(tay, tay2)  # deterministic
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6])
+@pytest.mark.parametrize("B,in_hw,C,N", [(3, 14, 64, 32), (2, 28, 32, 64), (2, 56, 64, 32), (5, 8, 32, 32)])
+@pytest.mark.parametrize("tay_mode", [0, 1])
+def test_conv_gen_bwd_transposed_taylor_partials(cuda, cfg, B, in_hw, C, N, tay_mode):
+    """Strided 3x3 dgrad (transposed implicit GEMM, parity row order) with the Taylor / Sensitivity
+    partials in its LDS epilogue: one slot range per stride phase, the (4R, B, N) slots sum to the
+    fp64 reduction of the masked output, the output is bit-identical to the run without partials,
+    and the slots are deterministic."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    R = 4 * T.conv_gen_tay_slots(cfg, in_hw * in_hw // 4)
+    if R == 0:
+        pytest.skip("tile spans more than 4 (phase, image) row groups")
+    g = torch.Generator().manual_seed(cfg * 11 + in_hw + tay_mode)
+    wf = torch.randn(C, N, 3, 3, generator=g)  # forward conv N -> C, 3x3 stride 2 pad 1
+    H = (in_hw + 2 - 3) // 2 + 1
+    gy = torch.randn(B, H, H, C, generator=g)
+    mask = torch.randn(B, in_hw, in_hw, N, generator=g).clamp_min(0)
+    ref = _dgrad_ref(gy, wf, (in_hw, in_hw), 2, 1)
+    ref = torch.where(mask.double() > 0, ref, torch.zeros((), dtype=torch.float64))
+    tay_ref = ref.abs().sum((1, 2)) if tay_mode else (-(ref * mask.double())).sum((1, 2))
+    wt = wf.permute(1, 2, 3, 0).reshape(N, 9 * C).contiguous()
+    args = (gy.to(cuda), wt.to(cuda), None, 1, mask.to(cuda), 3, 2, 1, in_hw, in_hw, True, cfg, 1)
+    tay = torch.zeros(R, B, N, device=cuda)
+    out = T.conv_gen_bwd(*args, tay, tay_mode)
+    assert torch.equal(out, T.conv_gen_bwd(*args))
+    torch.testing.assert_close(out.cpu().double(), ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(tay.sum(0).cpu().double(), tay_ref, rtol=1e-4, atol=1e-3)
+    tay2 = torch.zeros_like(tay)
+    T.conv_gen_bwd(*args, tay2, tay_mode)
+    assert torch.equal(tay, tay2)
+
+
+def test_conv_gen_bwd_taylor_partials_rejects_unsupported(cuda):
+    """Odd output sizes (no parity row order) and transposed 1x1 dgrads take no partials."""
+    from torchpruner_amd import ops
+    T = ops.require()
+    gy = torch.randn(2, 4, 4, 32, device=cuda)
+    wt3 = torch.randn(32, 9 * 32, device=cuda)
+    wt1 = torch.randn(32, 32, device=cuda)
+    tay = torch.zeros(64, 2, 32, device=cuda)
+    with pytest.raises(RuntimeError):  # 7x7 from 4x4: odd
+        T.conv_gen_bwd(gy, wt3, None, 1, torch.ones(2, 7, 7, 32, device=cuda), 3, 2, 1, 7, 7, True, 2, 1, tay, 0)
+    with pytest.raises(RuntimeError):
+        T.conv_gen_bwd(gy, wt1, None, 1, torch.ones(2, 8, 8, 32, device=cuda), 1, 2, 0, 8, 8, True, 2, 1, tay, 0)

@@ -62,6 +62,7 @@ WINO4S_FU = -11  # its data gradient writing the output unpooled through the pre
 WINO4_FU = -12  # the same with the MODE 3 kernel
 CFG_SK = 32  # tile-config flag of the GEN implicit GEMM: stream-K (conv_mfma.hip launch_gen)
 CFG_SB = 64  # tile-config flag: single-buffered LDS stage (GEN 1 1x1 forward, one K pass; short-K convs)
+CFG_RED = 1 << 12  # tuner-only flag (never passed to a kernel): a plain dgrad + the separate channel reduction
 CFG_BF16 = 256  # tile-config flag of conv_igemm: bf16 operands / fp32 accumulation (opt-in, compute_dtype)
 _BF16_CFGS = (0, 2, 3)  # the implicit-GEMM tiles built with bf16 variants (conv_mfma.hip launch_any)
             # than F(2x2); dgrads of pooled layers take the explicit unpool first
@@ -330,6 +331,8 @@ def kernel_name(cfg: int) -> str:
     igemm (2x2 layers as one dense GEMM), ``bf16`` igemm variants, or a persistent 1x1 GEMM."""
     if cfg in _KIND_NAMES:
         return _KIND_NAMES[cfg]
+    if cfg >= CFG_RED:
+        return kernel_name(cfg - CFG_RED) + "+reduce"
     if CFG_SK <= cfg < CFG_SK + 7:
         return kernel_name(cfg - CFG_SK) + "_streamk"
     if CFG_SB <= cfg < CFG_SB + 7:

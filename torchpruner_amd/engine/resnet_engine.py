@@ -29,6 +29,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from . import epochs
+from .fused_chain import CFG_RED as _RED
 from .fused_chain import (_CU, _W4_SPLITS, CFG_SB, TUNER, WINO, WINO4S, WINO_LDS, _wino_splits, cpad, logits_grad,
                           sk_candidates, taylor_slots, winograd_weights)
 
@@ -412,8 +413,9 @@ class ResNetEngine:
         """dL/d(input) of conv ``e`` from g = dL/d(conv output) (BN scale folded in), plus
         ``res``, masked by ``mask`` (the input's post-ReLU activation). ``low_res``: a strided
         1x1 conv's gradient at the output resolution (scattered by the consumer's res_stride).
-        Returns (gradient, partial slab or None): with ``tay_mode`` 0, a Winograd 3x3 dgrad or a
-        1x1 dgrad (implicit GEMM, one K pass) also writes the per-(image, channel) partial sums of
+        Returns (gradient, partial slab or None): with ``tay_mode`` 0, a Winograd 3x3 dgrad, a
+        1x1 dgrad (implicit GEMM, one K pass) or a strided 3x3 one (transposed implicit GEMM,
+        even output size: one slot range per stride phase) also writes the per-(image, channel) partial sums of
         -(dL/da * a), a = ``mask``, into an (R, B, C) slab from its epilogue (one writer per
         element: deterministic), which saves the separate channel reduction's read of both
         tensors; ``tay_mode`` 1 (Sensitivity): sums of |dL/da| of the masked gradient (the
@@ -441,12 +443,23 @@ class ResNetEngine:
                 cands = cands + wino4_cands(B, H, N, C)
         key = ("rbwd", tuple(g.shape), N, ks, s, transposed, res is not None, res_stride, mask is not None)
 
-        # 1x1 dgrads with fused Taylor partials: one K pass, tiles spanning <= 4 images
-        gen_tay = tay_mode is not None and ks == 1 and not transposed and mask is not None and res is None
+        # implicit-GEMM dgrads with fused Taylor partials: 1x1 (one K pass, tiles spanning <= 4
+        # images), and the strided 3x3 ones (parity row order: <= 4 (phase, image) row groups)
+        gen_tay = tay_mode is not None and mask is not None and res is None and (
+            (ks == 1 and not transposed) or (transposed and ks == 3 and s == 2 and Ho % 2 == 0 and Wo % 2 == 0))
+
+        def tay_slots(c):
+            return 4 * T.conv_gen_tay_slots(c, Ho * Wo // 4) if transposed else T.conv_gen_tay_slots(c, Ho * Wo)
         if gen_tay:
-            cands = list(dict.fromkeys((c, 1) for c, _ in cands if c >= 0 and T.conv_gen_tay_slots(c, Ho * Wo) > 0))
-            key = key + ("tay",)
-            gen_tay = bool(cands)
+            # the tuner weighs each fused-partials config against every plain config followed by
+            # the separate channel reduction (tuner-only flag _RED): the configs that cannot carry
+            # the partials' registers are sometimes the fastest tiles
+            plain = list(dict.fromkeys((c, 1) for c, _ in cands if c >= 0))
+            tay_c = [(c, 1) for c, _ in plain if tay_slots(c) > 0]
+            gen_tay = bool(tay_c)
+            if gen_tay:
+                cands = tay_c + [(c | _RED, 1) for c, _ in plain]
+                key = key + ("tay",)
 
         def run(cfg, sp, gg=g, rr=res, mm=mask, tay=None):
             if cfg in (WINO, WINO_LDS):  # Sensitivity of the BN before the ReLU: |g| where a > 0 (mode 2)
@@ -458,7 +471,17 @@ class ResNetEngine:
             return T.conv_gen_bwd(gg, e["wt"], rr, res_stride, mm, ks, s if transposed else 1, pad, Ho, Wo,
                                   transposed, cfg, sp, tay, tay_mode or 0)
 
-        cfg, sp = TUNER.choose(key, M, N, K, run, cands=cands if cands else None)
+        def run_tay(cfg, sp):  # the tuner's view of a gen_tay candidate: kernel + partials or + reduction
+            if cfg & _RED:
+                o = run(cfg & ~_RED, sp)
+                ops.channel_reduce(mask.permute(0, 3, 1, 2), o.permute(0, 3, 1, 2),
+                                   "sensitivity" if tay_mode == 1 else "taylor")
+                return o
+            return run(cfg, sp, tay=torch.zeros(tay_slots(cfg), B, N, device=g.device))
+
+        cfg, sp = TUNER.choose(key, M, N, K, run_tay if gen_tay else run, cands=cands if cands else None)
+        if gen_tay and cfg & _RED:  # plain kernel: grad_scores runs the channel reduction
+            return run(cfg & ~_RED, sp), None
         if tay_mode is not None and cfg in (WINO, WINO_LDS):
             tay = self._slab(arena, taylor_slots(Ho, Wo), B, N, g.device)
             return run(cfg, sp, tay=tay), tay
@@ -466,7 +489,7 @@ class ResNetEngine:
             tay = self._slab(arena, T.wino4_taylor_slots(Ho), B, N, g.device)
             return run(cfg, sp, tay=tay), tay
         if gen_tay:
-            tay = self._slab(arena, T.conv_gen_tay_slots(cfg, Ho * Wo), B, N, g.device)
+            tay = self._slab(arena, tay_slots(cfg), B, N, g.device)
             return run(cfg, sp, tay=tay), tay
         return run(cfg, sp), None
 
