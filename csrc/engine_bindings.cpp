@@ -80,6 +80,16 @@ hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int
                         float* apoz, float* out, float* ws, double* bnpart, float* tay_part, int tay_mode,
                         hipStream_t st);
 int tp_conv_gen_tay_slots(int cfg, int HWo);
+hipError_t tp_conv_gen5(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                        int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
+                        const float* shift, int relu, const float* res, int res_stride, const float* mask,
+                        float* apoz, float* out, float* ws, double* bnpart, float* tay_part, int tay_mode,
+                        const uint8_t* res_bits, const float* bnb_y, const float* bnb_mean, const float* bnb_invstd,
+                        const uint8_t* bnb_bits, hipStream_t st);
+hipError_t tp_bn_bwd_train_pre(const float* g, const float* x, float* dx, int P, int C, int Cr, const float* gamma,
+                               const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
+                               float* k1, float* k2, double* ws, const double* pre, int G, const float* ym,
+                               float* dres, const uint8_t* mk, hipStream_t st);
 hipError_t tp_bn_fwd_train_pre2(const float* x, float* y, int P, int C, int Cr, const float* gamma,
                                 const float* beta, float eps, float momentum, float* run_mean, float* run_var,
                                 float* mean, float* invstd, float* a, float* b, double* ws, const double* pre, int G,
@@ -883,6 +893,69 @@ at::Tensor conv_gen_bwd(const at::Tensor& g, const at::Tensor& wt, const c10::op
 
 int64_t conv_gen_tay_slots(int64_t cfg, int64_t HWo) { return tp_conv_gen_tay_slots((int)cfg, (int)HWo); }
 
+static const uint8_t* bit_mask_ptr(const c10::optional<at::Tensor>& t, int64_t elems, const at::Tensor& like,
+                                   const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kByte && t->is_contiguous() && t->numel() == (elems + 3) / 4 &&
+                  t->device() == like.device(),
+              what, " must be a ReLU bit mask of ceil(elements / 4) uint8 on the device");
+  return t->data_ptr<uint8_t>();
+}
+
+// Data gradient of a 1x1 stride-1 conv (the training path's residual-block conv1) with the two
+// fusions of a bottleneck's backward (tp_conv_gen5):
+//   res_bits: ``res`` is the raw gradient of the block output's ReLU, masked here by its bit mask;
+//   bn_y / bn_mean / bn_invstd (/ bn_bits): the output gradient reaches a BatchNorm (+ ReLU) whose
+//     backward statistics (sum gm, sum gm * xhat) come back per M tile, [tiles][2][N] fp64.
+// Returns (dx (B, H, W, N), tile statistics or an empty tensor).
+std::tuple<at::Tensor, at::Tensor> conv_gen_bwd_bn(const at::Tensor& g, const at::Tensor& wt,
+                                                   const c10::optional<at::Tensor>& res, int64_t res_stride,
+                                                   const c10::optional<at::Tensor>& res_bits,
+                                                   const c10::optional<at::Tensor>& bn_y,
+                                                   const c10::optional<at::Tensor>& bn_mean,
+                                                   const c10::optional<at::Tensor>& bn_invstd,
+                                                   const c10::optional<at::Tensor>& bn_bits, int64_t cfg) {
+  need(g, "g", 4);
+  need(wt, "wt", 2);
+  const int64_t B = g.size(0), H = g.size(1), W = g.size(2), C = g.size(3), N = wt.size(0), M = B * H * W;
+  TORCH_CHECK(C % 4 == 0 && C >= 8 && N % 4 == 0, "conv_gen_bwd_bn needs C % 4 == 0 (>= 8) and N % 4 == 0");
+  TORCH_CHECK(wt.size(1) == tp_conv_gen_k(1, (int)C), "wt must be (N, ceil32(C))");
+  at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(g.device());
+  TORCH_CHECK(res_stride >= 1, "res_stride must be >= 1");
+  const float* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    need(*res, "res", 4);
+    const int64_t Hr = (H + res_stride - 1) / res_stride, Wr = (W + res_stride - 1) / res_stride;
+    TORCH_CHECK(res->size(0) == B && res->size(1) == Hr && res->size(2) == Wr && res->size(3) == N,
+                "res must be (B, ceil(H/s), ceil(W/s), N)");
+    rp = res->data_ptr<float>();
+  }
+  const uint8_t* rb = bit_mask_ptr(res_bits, M * N, g, "res_bits");
+  TORCH_CHECK(!rb || (rp && res_stride == 1), "res_bits needs a stride-1 res");
+  const float* yp = nullptr;
+  at::Tensor part;
+  if (bn_y.has_value() && bn_y->defined()) {
+    need(*bn_y, "bn_y", 4);
+    TORCH_CHECK(bn_y->size(0) == B && bn_y->size(1) == H && bn_y->size(2) == W && bn_y->size(3) == N,
+                "bn_y must be (B, H, W, N)");
+    yp = bn_y->data_ptr<float>();
+    part = at::empty({(M + tp_conv_tile_m((int)cfg) - 1) / tp_conv_tile_m((int)cfg), 2, N},
+                     g.options().dtype(at::kDouble));
+  }
+  const float* mp = yp ? opt_ptr(bn_mean, N, "bn_mean") : nullptr;
+  const float* ip = yp ? opt_ptr(bn_invstd, N, "bn_invstd") : nullptr;
+  TORCH_CHECK(!yp || (mp && ip), "bn_y needs bn_mean and bn_invstd");
+  const uint8_t* bb = yp ? bit_mask_ptr(bn_bits, M * N, g, "bn_bits") : nullptr;
+  auto out = at::empty({B, H, W, N}, g.options());
+  at::Tensor ws = sk_workspace(cfg, 1, false, false, M, N, g.options());
+  const int64_t cf = ws.defined() || cfg < 0 ? cfg : cfg & ~kCfgSK;
+  TP_CHECK_HIP(tp_conv_gen5(g.data_ptr<float>(), wt.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C, (int)N, 1, 1,
+                            0, 0, 0, 0, (int)cf, 1, nullptr, nullptr, 0, rp, (int)res_stride, nullptr, nullptr,
+                            out.data_ptr<float>(), ws.defined() ? ws.data_ptr<float>() : nullptr,
+                            yp ? part.data_ptr<double>() : nullptr, nullptr, 0, rb, yp, mp, ip, bb, cur_stream()));
+  return {out, part};
+}
+
 // Fixup-workspace floats of a stream-K GEN launch of tile config cfg at an M x N GEMM (0 = stream-K
 // does not apply; the launcher then runs the data-parallel grid).
 int64_t conv_sk_ws(int64_t cfg, int64_t ks, bool tay, int64_t M, int64_t N) {
@@ -1062,7 +1135,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_fwd(const at
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
     const at::Tensor& g, const at::Tensor& x, const c10::optional<at::Tensor>& gamma, const at::Tensor& mean,
     const at::Tensor& invstd, bool want_dx, const c10::optional<at::Tensor>& ym, bool want_dres,
-    const c10::optional<at::Tensor>& mask, int64_t cr) {
+    const c10::optional<at::Tensor>& mask, int64_t cr, const c10::optional<at::Tensor>& pre) {
   need(g, "g", -1);
   need(x, "x", -1);
   TORCH_CHECK(g.sizes() == x.sizes(), "g and x must have the same shape");
@@ -1089,11 +1162,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_train_bwd(
   }
   const int64_t Cs = (C + 3) / 4 * 4;
   auto coef = at::empty({5, Cs}, x.options());  // dgamma, dbeta, a, k1, k2 (16-byte aligned rows)
-  auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   at::Tensor dx, dres;
   if (want_dx) dx = at::empty_like(x);
   if (want_dres) dres = at::empty_like(x);
   float* cp = coef.data_ptr<float>();
+  if (pre.has_value() && pre->defined()) {  // statistics from the producing GEMM's epilogue (conv_gen_bwd_bn)
+    TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kDouble && pre->is_contiguous() && pre->dim() == 3 &&
+                    pre->size(1) == 2 && pre->size(2) == C && pre->size(0) > 0 && pre->device() == x.device(),
+                "pre must be (G, 2, C) float64 tile statistics");
+    const int64_t G = pre->size(0);
+    auto wsp = at::empty({2 * std::min<int64_t>(G, 256) * C}, x.options().dtype(at::kDouble));
+    TP_CHECK_HIP(tp_bn_bwd_train_pre(g.data_ptr<float>(), x.data_ptr<float>(),
+                                     want_dx ? dx.data_ptr<float>() : nullptr, (int)P, (int)C, (int)Cr, ga, mp, ip, cp,
+                                     cp + Cs, cp + 2 * Cs, cp + 3 * Cs, cp + 4 * Cs, wsp.data_ptr<double>(),
+                                     pre->data_ptr<double>(), (int)G, mkp ? nullptr : yp,
+                                     want_dres ? dres.data_ptr<float>() : nullptr, mkp, cur_stream()));
+    return {dx, coef[0].narrow(0, 0, Cr), coef[1].narrow(0, 0, Cr), dres};
+  }
+  auto ws = at::empty({2 * (int64_t)tp_bn_groups((int)P, (int)C) * C}, x.options().dtype(at::kDouble));
   TP_CHECK_HIP(tp_bn_bwd_train4(g.data_ptr<float>(), x.data_ptr<float>(), want_dx ? dx.data_ptr<float>() : nullptr,
                                 (int)P, (int)C, (int)Cr, ga, mp, ip, cp, cp + Cs, cp + 2 * Cs, cp + 3 * Cs, cp + 4 * Cs,
                                 ws.data_ptr<double>(), mkp ? nullptr : yp, want_dres ? dres.data_ptr<float>() : nullptr,
@@ -1121,7 +1207,7 @@ void register_engine_ops_def(torch::Library& m) {
         "float eps, float momentum, Tensor? res=None, bool relu=False, Tensor? pre=None, "
         "Tensor(c!)? num_batches=None, int cr=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_train_bwd(Tensor g, Tensor x, Tensor? gamma, Tensor mean, Tensor invstd, bool want_dx, Tensor? ym=None, "
-        "bool want_dres=False, Tensor? mask=None, int cr=0) -> (Tensor, Tensor, Tensor, Tensor)");
+        "bool want_dres=False, Tensor? mask=None, int cr=0, Tensor? pre=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv_wgrad(Tensor g, Tensor x, int ks, int stride, int pad, int cfg, int splits, Tensor(a!)? out=None) "
         "-> Tensor");
   m.def("pack_conv_weight(Tensor w, int rows, int cols, int cpad, int mode) -> Tensor");
@@ -1132,6 +1218,8 @@ void register_engine_ops_def(torch::Library& m) {
   m.def("conv_gen_bwd(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? mask, int ks, int stride, int pad, "
         "int Ho, int Wo, bool transposed, int cfg, int splits, Tensor(a!)? taylor=None, int tay_mode=0) -> Tensor");
   m.def("conv_gen_tay_slots(int cfg, int HWo) -> int", &conv_gen_tay_slots);
+  m.def("conv_gen_bwd_bn(Tensor g, Tensor wt, Tensor? res, int res_stride, Tensor? res_bits, Tensor? bn_y, Tensor? bn_mean, "
+        "Tensor? bn_invstd, Tensor? bn_bits, int cfg) -> (Tensor, Tensor)");
   m.def("conv_sk_ws(int cfg, int ks, bool tay, int M, int N) -> int", &conv_sk_ws);
   m.def("unpool2_nhwc(Tensor g, Tensor am) -> Tensor");
   m.def("conv_fwd(Tensor x, Tensor w, Tensor? scale, Tensor? shift, bool relu, bool pool, int ks, int cfg, "
@@ -1167,6 +1255,7 @@ void register_engine_ops_impl(torch::Library& m) {
   m.impl("avgpool_nhwc", &avgpool_nhwc);
   m.impl("conv_gen", &conv_gen);
   m.impl("conv_gen_bwd", &conv_gen_bwd);
+  m.impl("conv_gen_bwd_bn", &conv_gen_bwd_bn);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("pack_conv_weight", &pack_conv_weight);
   m.impl("pack_conv_weights_multi", &pack_conv_weights_multi);

@@ -515,6 +515,25 @@ extern "C" hipError_t tp_bn_bwd_train4(const float* g, const float* x, float* dx
   return hipGetLastError();
 }
 
+// Backward with the statistics (sum gm, sum gm * xhat) already reduced per conv tile by the GEMM
+// epilogue that produced g (``pre``: [G][2][C], tp_conv_gen5's bnb mode): no statistics pass over
+// g and x. ws holds 2 * min(G, 256) * C doubles.
+extern "C" hipError_t tp_bn_bwd_train_pre(const float* g, const float* x, float* dx, int P, int C, int Cr,
+                                          const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                          float* dbeta, float* a, float* k1, float* k2, double* ws, const double* pre,
+                                          int G, const float* ym, float* dres, const uint8_t* mk, hipStream_t st) {
+  using namespace tp;
+  if (C <= 0 || P <= 0 || Cr <= 0 || Cr > C || G <= 0 || (long long)P * C >= (1ll << 32)) return hipErrorInvalidValue;
+  const int G2 = std::min(G, 256), per = (G + G2 - 1) / G2;
+  const int groups = (G + per - 1) / per;
+  bn_fold_tiles<<<dim3((C + 63) / 64, groups), 256, 0, st>>>(pre, G, C, ws, per);
+  bn_bwd_finalize<<<(C + 15) / 16, BN_FIN_T, 0, st>>>(ws, groups, P, C, Cr, gamma, mean, invstd, dgamma, dbeta, a, k1,
+                                                      k2, bn_fold_lanes());
+  if (dx || dres)
+    apply_launch<true>(x, g, a, k1, k2, dx, P, C, nullptr, 0, ym, dres, const_cast<uint8_t*>(mk), st);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t tp_bn_bwd_train3(const float* g, const float* x, float* dx, int P, int C, const float* gamma,
                                        const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
                                        float* k1, float* k2, double* ws, const float* ym, float* dres,

@@ -96,7 +96,21 @@ struct ConvArgs {
   int sk_fixup;
   long long sk_iters;
   float* sk_ws;
+  // training data gradient of a residual block's conv1 (GEN 1, res_stride 1; see tp_conv_gen5):
+  const uint8_t* res_bits;  // the residual is the raw gradient of the block's ReLU output: masked here by
+                            // that ReLU's bit mask (byte (pix*N + n) / 4, bit n % 4), so the BN
+                            // backward never writes the masked copy
+  const float* bnb_y;       // with bnpart: the BatchNorm whose output this gradient reaches — its input
+  const float* bnb_mean;    // [M][N], batch mean / invstd [N] and its ReLU bit mask (nullable: no
+  const float* bnb_invstd;  // ReLU); the tile sums become (sum gm, sum gm * xhat), gm = the masked
+  const uint8_t* bnb_bits;  // gradient, xhat = (y - mean) * invstd: that BN's backward statistics
 };
+
+// one ReLU bit-mask nibble (channels n..n+3 of pixel pix, N % 4 == 0) applied to a quad
+__device__ __forceinline__ float4 bits_mask(const uint8_t* bits, long long pix, int N, int n, float4 v) {
+  const unsigned b = bits[(pix * N + n) >> 2];
+  return make_float4(b & 1u ? v.x : 0.f, b & 2u ? v.y : 0.f, b & 4u ? v.z : 0.f, b & 8u ? v.w : 0.f);
+}
 
 // Taylor slots R of the GEN epilogue partials for tile height bm: the M tiles an image can touch
 __host__ __device__ constexpr int gen_tay_slots(int bm, int HWo) { return (HWo + bm - 2) / bm + 1; }
@@ -586,9 +600,16 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     const int n = n0 + c4 * 4;
     const bool ncol_ok = n < p.N;
     float4 sc4 = make_float4(1.f, 1.f, 1.f, 1.f), sh4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 bm4 = make_float4(0.f, 0.f, 0.f, 0.f), bi4 = bm4;  // bnb: that BN's mean / invstd
     if constexpr (EPI == EPI_FWD || EPI == EPI_FWD_TAY) {
       if (ncol_ok && p.scale) sc4 = *reinterpret_cast<const float4*>(p.scale + n);
       if (ncol_ok && p.shift) sh4 = *reinterpret_cast<const float4*>(p.shift + n);
+    }
+    if constexpr (GEN == 1 && EPI == EPI_FWD) {
+      if (ncol_ok && p.bnb_y) {
+        bm4 = *reinterpret_cast<const float4*>(p.bnb_mean + n);
+        bi4 = *reinterpret_cast<const float4*>(p.bnb_invstd + n);
+      }
     }
     int cur_b = -1;
     float4 cnt = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -603,7 +624,7 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
     static_assert(BM % RSTEP == 0 && RPT % PF == 0, "epilogue row passes");
     const int row0 = tid / C4;
     for (int it0 = 0; it0 < RPT; it0 += PF) {
-      float4 rq[PF], mq[PF];
+      float4 rq[PF], mq[PF], yq[PF];
       long long pq[PF];
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
@@ -620,9 +641,14 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
         pq[u] = pix;
         rq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         mq[u] = make_float4(1.f, 1.f, 1.f, 1.f);
+        yq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (EPI != EPI_PARTIAL) {
           if (ok && p.res) rq[u] = res_quad(p, pix, n);
           if (ok && p.mask) mq[u] = *reinterpret_cast<const float4*>(p.mask + pix * p.N + n);
+        }
+        if constexpr (GEN == 1 && EPI == EPI_FWD) {
+          if (ok && p.res_bits) rq[u] = bits_mask(p.res_bits, pix, p.N, n, rq[u]);
+          if (ok && p.bnb_y) yq[u] = *reinterpret_cast<const float4*>(p.bnb_y + pix * p.N + n);
         }
       }
 #pragma unroll
@@ -676,14 +702,28 @@ __global__ __launch_bounds__(tile_threads(BM, BN, WM, WN), tile_threads(BM, BN, 
           }
         }
         if (p.bnpart) {
-          bs.x += v.x;
-          bs.y += v.y;
-          bs.z += v.z;
-          bs.w += v.w;
-          bq.x += v.x * v.x;
-          bq.y += v.y * v.y;
-          bq.z += v.z * v.z;
-          bq.w += v.w * v.w;
+          bool bwd_stats = false;
+          if constexpr (GEN == 1 && EPI == EPI_FWD) bwd_stats = p.bnb_y != nullptr;
+          if (bwd_stats) {  // that BN's backward statistics: (sum gm, sum gm * xhat)
+            const float4 gm = p.bnb_bits ? bits_mask(p.bnb_bits, pq[u], p.N, n, v) : v;
+            bs.x += gm.x;
+            bs.y += gm.y;
+            bs.z += gm.z;
+            bs.w += gm.w;
+            bq.x += gm.x * ((yq[u].x - bm4.x) * bi4.x);
+            bq.y += gm.y * ((yq[u].y - bm4.y) * bi4.y);
+            bq.z += gm.z * ((yq[u].z - bm4.z) * bi4.z);
+            bq.w += gm.w * ((yq[u].w - bm4.w) * bi4.w);
+          } else {
+            bs.x += v.x;
+            bs.y += v.y;
+            bs.z += v.z;
+            bs.w += v.w;
+            bq.x += v.x * v.x;
+            bq.y += v.y * v.y;
+            bq.z += v.z * v.z;
+            bq.w += v.w * v.w;
+          }
         }
         if (p.apoz) {  // exact integer counts: atomics are order-free
           const int b = m / p.HWo;
@@ -1681,11 +1721,36 @@ extern "C" hipError_t tp_conv_gen3(const float* x, const float* w, int B, int H,
 // even Ho / Wo): [R][B][Cout] Taylor partials, R = tp_conv_gen_tay_slots(cfg, Ho * Wo) (transposed:
 // 4 x tp_conv_gen_tay_slots(cfg, Ho * Wo / 4), one slot range per stride phase), every slot
 // written or left as the caller zeroed it.
+extern "C" hipError_t tp_conv_gen5(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   double* bnpart, float* tay_part, int tay_mode, const uint8_t* res_bits,
+                                   const float* bnb_y, const float* bnb_mean, const float* bnb_invstd,
+                                   const uint8_t* bnb_bits, hipStream_t st);
+
 extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
                                    int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
                                    const float* scale, const float* shift, int relu, const float* res,
                                    int res_stride, const float* mask, float* apoz, float* out, float* ws,
                                    double* bnpart, float* tay_part, int tay_mode, hipStream_t st) {
+  return tp_conv_gen5(x, w, B, H, W, Cin, Cout, ks, stride, pad, transposed, Ho_t, Wo_t, cfg, splits, scale, shift,
+                      relu, res, res_stride, mask, apoz, out, ws, bnpart, tay_part, tay_mode, nullptr, nullptr,
+                      nullptr, nullptr, nullptr, st);
+}
+
+// ``res_bits`` (nullable; GEN 1, res at stride 1, no mask, Cout % 4 == 0): res is masked element-wise
+// by a ReLU bit mask (byte (pix * Cout + n) / 4, bit n % 4) before the add. ``bnb_y`` (nullable; GEN 1,
+// one K pass, with ``bnpart``): ``bnpart`` receives per M tile (sum gm, sum gm * (bnb_y - bnb_mean) *
+// bnb_invstd) of the stored gradient gm (masked by ``bnb_bits`` when given) instead of the output's
+// (sum, sum of squares): the backward statistics of the BatchNorm that produced the conv's input.
+extern "C" hipError_t tp_conv_gen5(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks,
+                                   int stride, int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits,
+                                   const float* scale, const float* shift, int relu, const float* res,
+                                   int res_stride, const float* mask, float* apoz, float* out, float* ws,
+                                   double* bnpart, float* tay_part, int tay_mode, const uint8_t* res_bits,
+                                   const float* bnb_y, const float* bnb_mean, const float* bnb_invstd,
+                                   const uint8_t* bnb_bits, hipStream_t st) {
   using namespace tp;
   const int gen = transposed ? 3 : (Cin == 4 ? 2 : 1);
   if ((gen != 2 && (Cin % 4 != 0 || Cin < 8)) || Cout % 4 != 0 || res_stride < 1) return hipErrorInvalidValue;
@@ -1744,6 +1809,17 @@ extern "C" hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H,
     if (splits > 1) return hipErrorInvalidValue;
     a.bnpart = bnpart;
   }
+  if (res_bits && (gen != 1 || !res || res_stride != 1 || mask || splits > 1 || tay_part || Cout % 4 != 0))
+    return hipErrorInvalidValue;
+  if (bnb_y && (gen != 1 || !bnpart || !bnb_mean || !bnb_invstd || mask || relu || tay_part || Cout % 4 != 0))
+    return hipErrorInvalidValue;
+  if (bnb_bits && !bnb_y) return hipErrorInvalidValue;
+  a.res_bits = res_bits;
+  a.bnb_y = bnb_y;
+  a.bnb_mean = bnb_mean;
+  a.bnb_invstd = bnb_invstd;
+  a.bnb_bits = bnb_bits;
+  if (res_bits || bnb_y) a.epi_lds = 1;
   if (tay_part) {  // GEN 1: 1x1; GEN 3: the parity-ordered 3x3 stride-2 data gradient (4 phase groups)
     const bool t3 = gen == 3 && a.parity && ks == 3;
     if (splits > 1 || !mask || !((gen == 1 && ks == 1) || t3) || cfg >= 16 ||

@@ -548,3 +548,51 @@ def test_single_stage_lds_gemm_matches(cuda, B, S, C, N, stride):
                 assert torch.equal(e0, e1) and torch.equal(t0, t1), c
                 tref = (-(dref * x.double())).sum((1, 2))
                 torch.testing.assert_close(t1.double().sum(0), tref, rtol=1e-3, atol=1e-3)
+
+
+def test_bottleneck_backward_fusions(cuda):
+    """The bottleneck backward fusions (engine/train.py _BNLink): each block tail's BN statistics come
+    from the next block's conv1 dgrad epilogue and identity gradients reach conv1's epilogue unmasked
+    (masked there by the tail's ReLU bits). Gradients vs fp64 autograd on the same model, and both
+    fusions were taken; a second consumer of a block output (a tail hook adding to its gradient) makes
+    the tail fall back to its own statistics pass, still exact."""
+    from torchpruner_amd.engine import train as tr
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    if not tr._BWD_FUSE:
+        pytest.skip("TORCHPRUNER_BN_BWD_FUSE=0")
+    torch.manual_seed(3)
+    model = ResNet(Bottleneck, [2, 3, 1, 1], num_classes=10, width=16).to(cuda)
+    model = model.to(memory_format=torch.channels_last).train()
+    x = torch.randn(4, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=cuda)
+    m64 = copy.deepcopy(model).double()
+
+    def fp64_grads(extra):
+        m64.zero_grad(set_to_none=True)
+        feats = {}
+        h = m64.layer2[0].register_forward_hook(lambda m, i, o: feats.__setitem__("o", o))
+        loss = F.cross_entropy(m64(x.double()), y)
+        if extra:
+            loss = loss + (feats["o"] ** 2).mean() * 1e-2
+        loss.backward()
+        h.remove()
+        return [p.grad for p in m64.parameters()]
+
+    for extra in (False, True):
+        before = dict(tr.FUSE_COUNTS)
+        model.zero_grad(set_to_none=True)
+        feats = {}
+        h = model.layer2[0].register_forward_hook(lambda m, i, o: feats.__setitem__("o", o))
+        with tr.native_convs(model):
+            loss = F.cross_entropy(model(x), y)
+            if extra:  # a second consumer of a block output
+                loss = loss + (feats["o"] ** 2).mean() * 1e-2
+            loss.backward()
+        h.remove()
+        got = [p.grad.double() for p in model.parameters()]
+        ref = fp64_grads(extra)
+        for (name, _), a, b in zip(model.named_parameters(), got, ref):
+            assert (a - b).abs().max().item() <= 5e-3 * b.abs().max().item() + 1e-6, (extra, name)
+        taken = {k: tr.FUSE_COUNTS[k] - before[k] for k in before}
+        assert taken["raw_residual"] >= 3, taken  # identity blocks: 1 + 2 + 0 + 0 ... (+ later layers)
+        assert taken["bn_stats_from_dgrad"] >= 4, taken

@@ -135,6 +135,36 @@ _EPI_STATS = os.environ.get("TORCHPRUNER_BN_EPI_STATS", "1") != "0"
 _BATCH_PACK = os.environ.get("TORCHPRUNER_BATCH_WEIGHT_PACK", "1") != "0"
 
 
+# TORCHPRUNER_BN_BWD_FUSE=0: a bottleneck's backward keeps the separate BN statistics pass and the
+# materialised residual gradient (A/B switch, read once per process)
+_BWD_FUSE = os.environ.get("TORCHPRUNER_BN_BWD_FUSE", "1") != "0"
+# backward passes that took each fusion (tests / diagnostics): tail statistics from a dgrad epilogue,
+# identity gradients handed over unmasked
+FUSE_COUNTS = {"bn_stats_from_dgrad": 0, "raw_residual": 0}
+
+
+class _BNLink:
+    """What a training BN(+ReLU) tail (:class:`_NativeBNAct`) shares with the residual-block entry
+    nodes next to it (:class:`_NativeBlockEntry`), so two of its backward passes over the block
+    output can ride in conv1's data-gradient GEMM epilogue instead:
+
+    * raw residual gradient (``raw_res``, the block's own tail, identity shortcut): the tail's
+      backward hands its incoming gradient to the identity branch unmasked (no masked copy
+      written); the entry's conv1 dgrad epilogue masks it by the tail's ReLU bits ``mk``;
+    * backward statistics (the previous block's tail, whose output is this block's input): the
+      entry's conv1 dgrad epilogue produces that tail's incoming gradient and reduces its BN
+      statistics per tile (``part``); the tail's backward uses them when the gradient it receives
+      is exactly that tensor, unmodified (``g_ptr`` / ``g_ver``: no other consumer added to it),
+      and runs its own statistics pass otherwise."""
+
+    __slots__ = ("xh", "mean", "invstd", "mk", "raw_res", "part", "g_ptr", "g_ver")
+
+    def __init__(self):
+        self.xh = self.mean = self.invstd = self.mk = self.part = None
+        self.raw_res = False
+        self.g_ptr = self.g_ver = None
+
+
 class _PackSet:
     """The zero-padded GEMM operands of the fp32 conv weights (``pack_conv_weight`` modes 0-2),
     cached across uses and repacked TOGETHER by one ``pack_conv_weights_multi`` launch: the
@@ -284,6 +314,37 @@ def _grad_nhwc(gy, meta):
     if g.shape[-1] != cout_p:
         g = F.pad(g, (0, cout_p - g.shape[-1]))
     return g.contiguous()
+
+
+def _conv_dgrad_fused(g, w32, meta, res, res_stride, res_bits, link):
+    """1x1 stride-1 input gradient (conv1 of a residual block) with the bottleneck fusions of
+    ``conv_gen_bwd_bn``: ``res`` masked by ``res_bits`` (a raw residual gradient, see _BNLink)
+    and / or the backward statistics of ``link``'s BN (the producer of this conv's input).
+    Returns (dx NHWC, tile statistics or None); one-pass implicit-GEMM tiles only."""
+    T = ops.require()
+    ks, stride, pad, Cin, Cout, H, W, _, _, _, cin_p, cout_p = meta[:12]
+    B = g.shape[0]
+    shared = meta[8] == torch.float32
+    M, K = B * H * W, _kslice(cout_p)
+    cache = {}
+
+    def wt():
+        if "wt" not in cache:
+            cache["wt"] = _pack(T, w32, cin_p, K, K, 1, shared)
+        return cache["wt"]
+
+    def run(cfg, sp):
+        return T.conv_gen_bwd(g, wt(), res, res_stride, None, 1, 1, 0, H, W, False, cfg, sp)
+
+    cands = [c for c in TUNER.candidates(M, cin_p, K) if c[0] >= 0 and c[1] == 1]
+    cands = cands + sk_candidates(T, cands, 1, M, cin_p)
+    if K <= 256:
+        cands = cands + [(CFG_SB | c, 1) for c in (2, 3, 6)]
+    key = ("tdgrad1", tuple(g.shape), cin_p, res is not None and res_stride)
+    cfg, _ = TUNER.choose(key, M, cin_p, K, run, cands=cands)
+    bn = link is not None and link.xh is not None
+    return T.conv_gen_bwd_bn(g, wt(), res, res_stride, res_bits, link.xh if bn else None, link.mean if bn else None,
+                             link.invstd if bn else None, link.mk if bn else None, cfg)
 
 
 def _conv_dgrad(g, w32, meta, res=None, res_stride=1):
@@ -454,10 +515,16 @@ class _NativeBlockEntry(torch.autograd.Function):
     accumulation pass over x (an add kernel per block) disappears."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, wd, bd, ds_stride):
+    def forward(ctx, x, w1, b1, wd, bd, ds_stride, link_in=None, link_res=None):
         # (conv1 output, identity-branch pre-BN, and the two outputs' BN tile statistics or None)
         y1, saved1, ctx.meta1, p1 = _conv_fwd(x, w1, b1, 1, 1, 0, stats=True, keep=True)  # carried width
         ctx.has_ds = wd is not None
+        # bottleneck backward fusions (_BNLink): conv1's dgrad output has the block input's exact width
+        fuse = _BWD_FUSE and ctx.meta1[10] == ctx.meta1[12] and ctx.meta1[10] % 4 == 0
+        ctx.link_in = link_in if fuse else None
+        ctx.link_res = link_res if fuse and wd is None else None
+        if ctx.link_res is not None:
+            link_res.raw_res = True  # read by the block tail's forward (it runs after this node)
         pd = None
         if ctx.has_ds:
             yd, saved_d, ctx.meta_d, pd = _conv_fwd(x, wd, bd, 1, ds_stride, 0, stats=True)
@@ -482,7 +549,7 @@ class _NativeBlockEntry(torch.autograd.Function):
         Cx = m1[12]
         dx = dw1 = db1 = dwd = dbd = None
         g1h = _grad_nhwc(g1, m1) if g1 is not None else None
-        res, res_stride, gdh = None, 1, None
+        res, res_stride, gdh, res_bits = None, 1, None, None
         if gid is not None:
             if ctx.has_ds:
                 md = ctx.meta_d
@@ -498,11 +565,22 @@ class _NativeBlockEntry(torch.autograd.Function):
                 if m1[10] != res.shape[-1]:
                     res = F.pad(res, (0, m1[10] - res.shape[-1]))
                 res = res.contiguous()
+                lr = ctx.link_res
+                if lr is not None and lr.raw_res and lr.mk is not None:
+                    res_bits = lr.mk  # the tail handed its gradient over unmasked
         if ctx.needs_input_grad[0]:
             if g1h is None:  # only the identity branch carries a gradient (rare): dgrad of zeros + res
                 B, H, W = xh.shape[0], xh.shape[1], xh.shape[2]
                 g1h = torch.zeros((B, H, W, m1[11]), dtype=torch.float32, device=xh.device)
-            dx = _dx_nchw(_conv_dgrad(g1h, w1, m1, res, res_stride), m1)
+            li = ctx.link_in
+            li = li if li is not None and li.xh is not None and tuple(li.xh.shape) == tuple(xh.shape) else None
+            if res_bits is not None or li is not None:
+                dxh, part = _conv_dgrad_fused(g1h, w1, m1, res, res_stride, res_bits, li)
+                if li is not None:
+                    li.part, li.g_ptr, li.g_ver = part, dxh.data_ptr(), dxh._version
+                dx = _dx_nchw(dxh, m1)
+            else:
+                dx = _dx_nchw(_conv_dgrad(g1h, w1, m1, res, res_stride), m1)
         if ctx.needs_input_grad[1] and g1 is not None:
             dw1 = _conv_wgrad(g1h, xh, m1)
         if m1[7] and ctx.needs_input_grad[2] and g1 is not None:
@@ -513,7 +591,7 @@ class _NativeBlockEntry(torch.autograd.Function):
                 dwd = _conv_wgrad(gdh, xh, md)
             if md[7] and ctx.needs_input_grad[4]:
                 dbd = gid.sum((0, 2, 3))
-        return dx, dw1, db1, dwd, dbd, None
+        return dx, dw1, db1, dwd, dbd, None, None, None
 
 
 class _NativeBN2d(torch.autograd.Function):
@@ -561,7 +639,8 @@ class _NativeBNAct(torch.autograd.Function):
     ATen ReLU / add / threshold-backward passes of the unfused block disappear."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu, pre=None, nbt=None, cr=0):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, res, relu, pre=None, nbt=None, cr=0,
+                link=None):
         T = ops.require()
         xh = _nhwc(x)
         rh = _nhwc(res) if res is not None else None
@@ -571,6 +650,10 @@ class _NativeBNAct(torch.autograd.Function):
         y, mean, invstd, mk = T.bn_train_fwd(xh, w, b, running_mean, running_var, float(eps), float(momentum), rh,
                                              bool(relu), pre, nbt, int(cr))
         ctx.cr = int(cr)
+        ctx.link = None
+        if link is not None and relu and int(cr) == xh.shape[-1]:
+            link.xh, link.mean, link.invstd, link.mk = xh, mean, invstd, mk
+            ctx.link = link
         if running_mean is not None:
             epochs.bump_stats()
         # the backward masks by the ReLU bit mask (1 byte per 4 channels) instead of re-reading y
@@ -584,12 +667,24 @@ class _NativeBNAct(torch.autograd.Function):
         xh, w, mean, invstd, mk = ctx.saved_tensors
         g = _nhwc(gy)
         want_res = ctx.has_res and ctx.needs_input_grad[7]
+        link, pre = ctx.link, None
+        if link is not None and link.part is not None:
+            # statistics reduced by the consumer's dgrad epilogue, valid if g is that very output
+            # (a second consumer's gradient would have been added in place or into a new tensor)
+            if g.data_ptr() == link.g_ptr and g._version == link.g_ver:
+                pre = link.part
+                FUSE_COUNTS["bn_stats_from_dgrad"] += 1
+            link.part = None
+        raw = want_res and link is not None and link.raw_res  # the entry masks the identity gradient
+        if raw:
+            FUSE_COUNTS["raw_residual"] += 1
         dx, dgamma, dbeta, dres = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
-                                                 ctx.needs_input_grad[0], None, want_res, mk if ctx.relu else None,
-                                                 ctx.cr)
+                                                 ctx.needs_input_grad[0], None, want_res and not raw,
+                                                 mk if ctx.relu else None, ctx.cr, pre)
+        res_grad = (gy if raw else _as_nchw(dres)) if want_res else None
         return (_as_nchw(dx) if ctx.needs_input_grad[0] else None, dgamma if ctx.has_w else None,
-                dbeta if ctx.has_b else None, None, None, None, None, _as_nchw(dres) if want_res else None, None,
-                None, None, None)
+                dbeta if ctx.has_b else None, None, None, None, None, res_grad, None,
+                None, None, None, None)
 
 
 def _bn_counter(bn):
@@ -612,11 +707,11 @@ def _bn_fusable(bn, x, res=None) -> bool:
 
 
 def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: bool = True,
-           pre: torch.Tensor = None) -> torch.Tensor:
+           pre: torch.Tensor = None, link: _BNLink = None) -> torch.Tensor:
     """``relu?(bn(x) + res?)`` — fused on the native kernels in training mode, the module's own
     ops otherwise (eval mode, unsupported inputs). ``pre``: x's batch statistics already reduced
     per tile by the producing conv's epilogue (:func:`conv_stats`), which skips the statistics
-    pass over x."""
+    pass over x. ``link``: a residual block tail's :class:`_BNLink` (bottleneck backward fusions)."""
     if not _bn_fusable(bn, x, res):
         y = bn(_real(x, bn.num_features))
         if res is not None:
@@ -632,7 +727,7 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, res: torch.Tensor = None, relu: 
     if pre is not None and (pre.dim() != 3 or pre.shape[2] != x.shape[1]):
         pre = None
     return _NativeBNAct.apply(x, bn.weight, bn.bias, rm, rv, bn.eps, momentum if momentum is not None else 0.0, res,
-                              relu, pre, nbt, bn.num_features)
+                              relu, pre, nbt, bn.num_features, link)
 
 
 def _block_kind(m) -> str | None:
@@ -669,13 +764,17 @@ def _native_block_forward(self, x):
     if not (self.training and x.is_cuda):
         return type(self).forward(self, x)
     entry = _entry_convs(self, x)
+    link = None
     # block-internal activations (conv1 / conv2 outputs: the widths a structured prune cuts) flow at
     # their carried width (_act_w) from conv to BN to conv; the block output has its real width
     if entry is not None:
         c1, dconv, dbn = entry
+        # the previous block tail's link (its output is x) and this block's tail link
+        link = _BNLink() if _BWD_FUSE and _block_kind(self) == "bottleneck" else None
         y1, idp, p1, pd = _NativeBlockEntry.apply(x, c1.weight, c1.bias, dconv.weight if dconv is not None else None,
                                                   dconv.bias if dconv is not None else None,
-                                                  dconv.stride[0] if dconv is not None else 1)
+                                                  dconv.stride[0] if dconv is not None else 1,
+                                                  getattr(x, "_tp_link", None) if _BWD_FUSE else None, link)
         identity = bn_act(dbn, idp, relu=False, pre=pd) if dbn is not None else idp
         out = bn_act(self.bn1, y1, relu=True, pre=p1)
     else:
@@ -686,7 +785,12 @@ def _native_block_forward(self, x):
         y2, p2 = conv_stats(self.conv2, out, keep=True)
         out = bn_act(self.bn2, y2, relu=True, pre=p2)
         y3, p3 = conv_stats(self.conv3, out)
-        return bn_act(self.bn3, y3, res=identity, relu=True, pre=p3)
+        if link is None and _BWD_FUSE:
+            link = _BNLink()  # (no entry node here: the next block can still fuse this tail's statistics)
+        out = bn_act(self.bn3, y3, res=identity, relu=True, pre=p3, link=link)
+        if link is not None and link.xh is not None:
+            out._tp_link = link  # for the next block's entry node (its conv1 dgrad produces our gradient)
+        return out
     y2, p2 = conv_stats(self.conv2, out)
     return bn_act(self.bn2, y2, res=identity, relu=True, pre=p2)
 
