@@ -195,8 +195,12 @@ def test_vgg_engine_sensitivity_matches_fp64(cuda, prune):
             del os.environ["TORCHPRUNER_BACKEND"]
         for m, a, r in zip(mods, got, ref):
             assert a.shape == r.shape and a.shape[-1] == m.weight.shape[0]
-            err = np.abs(a - r).max() / (np.abs(r).max() + 1e-30)
-            assert err < (5e-3 if red == "mean" else 2e-2), (m, red, err)
+            e = np.abs(a - r) / (np.abs(r).max() + 1e-30)
+            if red == "mean":
+                assert e.max() < 5e-3, (m, red, e.max())
+            else:  # per-sample sums: a ReLU decision flip (fp32 vs fp64, tuner-chosen kernel) moves one
+                # sample's sum by a few %; the bulk must still agree to fp32 accuracy
+                assert e.max() < 5e-2 and np.median(e) < 1e-3, (m, red, e.max(), np.median(e))
 
 
 @pytest.mark.gpu

@@ -596,3 +596,29 @@ def test_bottleneck_backward_fusions(cuda):
         taken = {k: tr.FUSE_COUNTS[k] - before[k] for k in before}
         assert taken["raw_residual"] >= 3, taken  # identity blocks: 1 + 2 + 0 + 0 ... (+ later layers)
         assert taken["bn_stats_from_dgrad"] >= 4, taken
+
+
+def test_bottleneck_fusions_release_the_graph(cuda):
+    """The _BNLink objects must not keep a finished step's graph alive: pruning in place between two
+    steps (new parameter shapes) would then hit the old grad accumulators ("invalid gradient")."""
+    from torchpruner_amd import Pruner, get_resnet_pruning_graph
+    from torchpruner_amd.engine import train as tr
+    from torchpruner_amd.models.resnet import Bottleneck, ResNet
+    torch.manual_seed(4)
+    model = ResNet(Bottleneck, [2, 2, 1, 1], num_classes=10, width=16).to(cuda)
+    model = model.to(memory_format=torch.channels_last).train()
+    x = torch.randn(4, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=cuda)
+    pruner = Pruner(model, (3, 64, 64), cuda)
+    rng = np.random.RandomState(0)
+    for step in range(3):
+        model.zero_grad(set_to_none=True)
+        with tr.native_convs(model):
+            loss = F.cross_entropy(model(x), y)
+            loss.backward()
+        assert torch.isfinite(loss)
+        del loss
+        for module, cascade in get_resnet_pruning_graph(model):  # every prunable conv, in place
+            n = module.weight.shape[0]
+            pruner.prune_model(module, rng.choice(n, max(1, n // 8), replace=False), cascade)
+        model.train()

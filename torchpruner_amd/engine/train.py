@@ -567,7 +567,7 @@ class _NativeBlockEntry(torch.autograd.Function):
                 res = res.contiguous()
                 lr = ctx.link_res
                 if lr is not None and lr.raw_res and lr.mk is not None:
-                    res_bits = lr.mk  # the tail handed its gradient over unmasked
+                    res_bits, lr.mk = lr.mk, None  # the tail handed its gradient over unmasked
         if ctx.needs_input_grad[0]:
             if g1h is None:  # only the identity branch carries a gradient (rare): dgrad of zeros + res
                 B, H, W = xh.shape[0], xh.shape[1], xh.shape[2]
@@ -651,8 +651,10 @@ class _NativeBNAct(torch.autograd.Function):
                                              bool(relu), pre, nbt, int(cr))
         ctx.cr = int(cr)
         ctx.link = None
-        if link is not None and relu and int(cr) == xh.shape[-1]:
-            link.xh, link.mean, link.invstd, link.mk = xh, mean, invstd, mk
+        if link is not None and relu and xh.shape[-1] % 4 == 0:
+            # detached: a link must not reference the graph (a node's ctx holds it: no cycle that would
+            # keep old graphs — and their parameters' grad accumulators — alive)
+            link.xh, link.mean, link.invstd, link.mk = xh.detach(), mean, invstd, mk
             ctx.link = link
         if running_mean is not None:
             epochs.bump_stats()
@@ -675,9 +677,13 @@ class _NativeBNAct(torch.autograd.Function):
                 pre = link.part
                 FUSE_COUNTS["bn_stats_from_dgrad"] += 1
             link.part = None
-        raw = want_res and link is not None and link.raw_res  # the entry masks the identity gradient
+        # the entry masks the identity gradient by link.mk (it clears it after use: a second backward
+        # over a retained graph runs unfused)
+        raw = want_res and link is not None and link.raw_res and link.mk is not None
         if raw:
             FUSE_COUNTS["raw_residual"] += 1
+        if link is not None:  # the next block's entry has run: drop the references to this tail's tensors
+            link.xh = link.mean = link.invstd = None
         dx, dgamma, dbeta, dres = T.bn_train_bwd(g, xh, w if ctx.has_w else None, mean, invstd,
                                                  ctx.needs_input_grad[0], None, want_res and not raw,
                                                  mk if ctx.relu else None, ctx.cr, pre)
