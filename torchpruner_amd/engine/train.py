@@ -472,20 +472,35 @@ class _NativeConv2dStats(torch.autograd.Function):
     None), computed in the GEMM epilogue: the following training BN skips its statistics pass."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, ks, stride, pad, keep=False):
+    def forward(ctx, x, weight, bias, ks, stride, pad, keep=False, link_in=None):
         y, saved, ctx.meta, part = _conv_fwd(x, weight, bias, ks, stride, pad, stats=True, keep=keep)
         ctx.save_for_backward(*saved)
         if part is not None:
             ctx.mark_non_differentiable(part)
         # no zero-filled fp64 gradient for the statistics output (one fill launch per conv otherwise)
         ctx.set_materialize_grads(False)
+        m = ctx.meta  # a 1x1 stride-1 conv reading its input at its exact width: the producing BN's
+        # backward statistics can come from this conv's dgrad epilogue (_BNLink)
+        ctx.link_in = link_in if (_BWD_FUSE and ks == 1 and stride == 1 and m[10] == m[12]) else None
         return _as_nchw(y), part
 
     @staticmethod
     def backward(ctx, gy, _gpart):
         if gy is None:
-            return (None,) * 7
-        return _NativeConv2d.backward(ctx, gy)
+            return (None,) * 8
+        li = ctx.link_in
+        if li is None or li.xh is None or not ctx.needs_input_grad[0]:
+            return _NativeConv2d.backward(ctx, gy) + (None,)
+        xh, w32 = ctx.saved_tensors
+        meta = ctx.meta
+        if tuple(li.xh.shape) != tuple(xh.shape):
+            return _NativeConv2d.backward(ctx, gy) + (None,)
+        g = _grad_nhwc(gy, meta)
+        dxh, part = _conv_dgrad_fused(g, w32, meta, None, 1, None, li)
+        li.part, li.g_ptr, li.g_ver = part, dxh.data_ptr(), dxh._version
+        dw = _conv_wgrad(g, xh, meta) if ctx.needs_input_grad[1] else None
+        db = gy[:, :meta[4]].sum((0, 2, 3)) if meta[7] and ctx.needs_input_grad[2] else None
+        return _dx_nchw(dxh, meta), dw, db, None, None, None, None, None
 
 
 def _real(x: torch.Tensor, c: int) -> torch.Tensor:
@@ -493,7 +508,7 @@ def _real(x: torch.Tensor, c: int) -> torch.Tensor:
     return x if x.shape[1] == c else x[:, :c]
 
 
-def conv_stats(conv: nn.Conv2d, x: torch.Tensor, keep: bool = False):
+def conv_stats(conv: nn.Conv2d, x: torch.Tensor, keep: bool = False, link: _BNLink = None):
     """``(conv(x), tile statistics or None)`` — a native conv whose tuned kernel is a one-pass
     implicit GEMM computes its output's BN statistics in the epilogue (1x1, strided 3x3, the
     packed-tap stem; Winograd picks return None); anything else runs the module (None). ``x`` may
@@ -502,7 +517,7 @@ def conv_stats(conv: nn.Conv2d, x: torch.Tensor, keep: bool = False):
             and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv.weight.dtype == torch.float32 \
             and _fits(conv, x):
         ks, s, p = _geom(conv)
-        return _NativeConv2dStats.apply(x, conv.weight, conv.bias, ks, s, p, keep)
+        return _NativeConv2dStats.apply(x, conv.weight, conv.bias, ks, s, p, keep, link)
     return conv(_real(x, conv.in_channels)), None
 
 
@@ -789,8 +804,9 @@ def _native_block_forward(self, x):
         out = bn_act(self.bn1, y1, relu=True, pre=p1)
     if _block_kind(self) == "bottleneck":
         y2, p2 = conv_stats(self.conv2, out, keep=True)
-        out = bn_act(self.bn2, y2, relu=True, pre=p2)
-        y3, p3 = conv_stats(self.conv3, out)
+        link2 = _BNLink() if _BWD_FUSE else None  # bn2's backward statistics from conv3's dgrad epilogue
+        out = bn_act(self.bn2, y2, relu=True, pre=p2, link=link2)
+        y3, p3 = conv_stats(self.conv3, out, link=link2 if link2 is not None and link2.xh is not None else None)
         if link is None and _BWD_FUSE:
             link = _BNLink()  # (no entry node here: the next block can still fuse this tail's statistics)
         out = bn_act(self.bn3, y3, res=identity, relu=True, pre=p3, link=link)
