@@ -31,6 +31,16 @@ hipError_t tp_conv_gen4(const float* x, const float* w, int B, int H, int W, int
                         float* apoz, float* out, float* ws, double* bnpart, float* tay_part, int tay_mode,
                         hipStream_t st);
 int tp_conv_gen_tay_slots(int cfg, int HWo);
+hipError_t tp_conv_gen5(const float* x, const float* w, int B, int H, int W, int Cin, int Cout, int ks, int stride,
+                        int pad, int transposed, int Ho_t, int Wo_t, int cfg, int splits, const float* scale,
+                        const float* shift, int relu, const float* res, int res_stride, const float* mask,
+                        float* apoz, float* out, float* ws, double* bnpart, float* tay_part, int tay_mode,
+                        const uint8_t* res_bits, const float* bnb_y, const float* bnb_mean, const float* bnb_invstd,
+                        const uint8_t* bnb_bits, hipStream_t st);
+hipError_t tp_bn_bwd_train_pre(const float* g, const float* x, float* dx, int P, int C, int Cr, const float* gamma,
+                               const float* mean, const float* invstd, float* dgamma, float* dbeta, float* a,
+                               float* k1, float* k2, double* ws, const double* pre, int G, const float* ym,
+                               float* dres, const uint8_t* mk, hipStream_t st);
 hipError_t tp_conv_wgrad(const float* g, const float* x, float* dw, float* ws, int B, int H, int W, int Cin, int Cout,
                          int ks, int stride, int pad, int Kpad, int cfg, int splits, hipStream_t st);
 hipError_t tp_conv_wino(const float* x, const uint8_t* x_argmax, const float* u, int B, int H, int W, int C, int K,
@@ -110,6 +120,24 @@ int main() {
          hipErrorInvalidValue);  // cfg 4: no partials
   EXPECT(tp_conv_gen4(n, n, 2, 4, 4, 64, 64, 3, 2, 1, 1, 8, 8, 2, 1, n, n, 0, n, 1, nullptr, n, n, n, nullptr, tp_, 0,
                       0) == hipErrorInvalidValue);  // no mask
+  // bottleneck backward fusions (tp_conv_gen5): residual bit mask needs a stride-1 res, no mask, GEN 1;
+  // BN-backward statistics need bnpart + mean / invstd, no ReLU / mask / partials
+  const uint8_t* bits = reinterpret_cast<const uint8_t*>(16);
+  double* bp = reinterpret_cast<double*>(16);
+  EXPECT(tp_conv_gen5(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 2, 1, n, n, 0, n, 1, n, n, n, n, nullptr, nullptr, 0,
+                      bits, n, n, n, nullptr, 0) == hipErrorInvalidValue);  // res_bits without res
+  EXPECT(tp_conv_gen5(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 2, 1, n, n, 0, mk, 2, n, n, n, n, nullptr, nullptr, 0,
+                      bits, n, n, n, nullptr, 0) == hipErrorInvalidValue);  // res_bits with a strided res
+  EXPECT(tp_conv_gen5(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 2, 1, n, n, 0, n, 1, n, n, n, n, nullptr, nullptr, 0,
+                      nullptr, mk, mk, mk, nullptr, 0) == hipErrorInvalidValue);  // bnb without bnpart
+  EXPECT(tp_conv_gen5(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 2, 1, n, n, 0, n, 1, n, n, n, n, bp, nullptr, 0,
+                      nullptr, mk, nullptr, mk, nullptr, 0) == hipErrorInvalidValue);  // bnb without mean
+  EXPECT(tp_conv_gen5(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 2, 1, n, n, 1, n, 1, n, n, n, n, bp, nullptr, 0,
+                      nullptr, mk, mk, mk, nullptr, 0) == hipErrorInvalidValue);  // bnb with a ReLU epilogue
+  EXPECT(tp_conv_gen5(n, n, 2, 8, 8, 64, 64, 1, 1, 0, 0, 0, 0, 2, 1, n, n, 0, n, 1, n, n, n, n, bp, nullptr, 0,
+                      nullptr, nullptr, nullptr, nullptr, bits, 0) == hipErrorInvalidValue);  // bnb_bits alone
+  EXPECT(tp_bn_bwd_train_pre(n, n, n, 64, 8, 8, n, n, n, n, n, n, n, n, nullptr, nullptr, 0, n, n, nullptr, 0) ==
+         hipErrorInvalidValue);  // no tiles
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 6, 64, 3, 1, 1, 64, 0, 1, 0) == hipErrorInvalidValue);   // Cin % 4
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 96, 0, 1, 0) == hipErrorInvalidValue);  // Kpad small
   EXPECT(tp_conv_wgrad(n, n, n, n, 2, 8, 8, 64, 64, 3, 1, 1, 576, 7, 1, 0) == hipErrorInvalidValue); // bad cfg
