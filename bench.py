@@ -256,7 +256,13 @@ def run(args) -> int:
     }
 
     if not args.no_extras:
-        result.update(extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase, scores))
+        # the extras run after the timed headline: one that raises (on every rank alike) is reported in
+        # the JSON line instead of costing the headline its line
+        try:
+            result.update(extras(args, model, task, convs, dev, world, rank, timed_run, log, value, phase, scores))
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] extras failed: {e!r}")
+            result["extras_error"] = repr(e)[:800]
         if "b100_tuner_choices" in result:
             result["tuner_choices"]["b100"] = result.pop("b100_tuner_choices")
 
@@ -272,6 +278,7 @@ def run(args) -> int:
         nb = args.baseline_batches
         t_eager = time.perf_counter()
         xb, yb = task.sample(nb * B, args.seed + 5)
+        bt = None
         try:
             with _env(TORCHPRUNER_BACKEND="torch"):
                 ev = [find_best_module_for_attributions(model, c) for c in convs]
@@ -281,19 +288,27 @@ def run(args) -> int:
                 reference_taylor_all(model, DeviceLoader(xb, yb, B), F.cross_entropy, dev, ev)
                 torch.cuda.synchronize()
                 bt = time.perf_counter() - t1
+        except Exception as e:  # noqa: BLE001  (rank 0 only, after the timed region: vs_baseline stays null)
+            log(f"[bench] reference-semantics eager run failed: {e!r}")
+            result["eager_reference_error"] = repr(e)[:800]
         finally:
             model.zero_grad(set_to_none=True)
-        eager = nb * B / bt
-        result["eager_reference_img_s_per_gpu"] = round(eager, 1)
-        result["vs_baseline"] = round((value / world) / eager, 2)
-        result["vs_baseline_definition"] = ("per-GPU img/s / reference-semantics eager img/s on the same GPU "
-                                            "(BASELINE.md: the reference publishes no number for this metric)")
+        if bt is not None:
+            eager = nb * B / bt
+            result["eager_reference_img_s_per_gpu"] = round(eager, 1)
+            result["vs_baseline"] = round((value / world) / eager, 2)
+            result["vs_baseline_definition"] = ("per-GPU img/s / reference-semantics eager img/s on the same GPU "
+                                                "(BASELINE.md: the reference publishes no number for this metric)")
+            log(f"[bench] reference-semantics eager: {eager:.0f} img/s per GPU -> vs_baseline {result['vs_baseline']}")
         phase["eager_reference"] = time.perf_counter() - t_eager
-        log(f"[bench] reference-semantics eager: {eager:.0f} img/s per GPU -> vs_baseline {result['vs_baseline']}")
 
     if not args.no_prune:
         t0 = time.perf_counter()
-        result.update(accuracy(args, model, task, convs, scores, cfg, dev, log))
+        try:
+            result.update(accuracy(args, model, task, convs, scores, cfg, dev, log))
+        except Exception as e:  # noqa: BLE001  (rank 0 only, after the timed region)
+            log(f"[bench] accuracy phase failed: {e!r}")
+            result["accuracy_error"] = repr(e)[:800]
         phase["accuracy"] = time.perf_counter() - t0
     phase["total"] = time.perf_counter() - t_run
     result["phase_wall_s"] = {k: round(v, 1) for k, v in phase.items()}
